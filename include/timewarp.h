@@ -1,0 +1,267 @@
+/*
+ * timewarp.h — C ABI of the MI355X batched TimedT emulator (libtimewarp.so).
+ *
+ * Drop-in boundary for time-warp's pure-emulation path.  The reference has no
+ * FFI: its "operator API" is the MonadTimed / MonadTransfer / MonadDialog
+ * type-class dictionary, made concrete by the runner
+ *     runTimedT :: (MonadIO m, MonadCatch m) => TimedT m a -> m a
+ *     (src/Control/TimeWarp/Timed/TimedT.hs:293-304).
+ * A scenario written against that API is lowered (host side) into a handler
+ * table ("thread programs", the tw_insn ISA below) plus per-link delay/drop
+ * tables, and this library runs R independent replicas of it on one GPU.
+ * Each entry point names the reference interface it replaces.
+ *
+ * Conventions: every call returns 0 (TW_OK) or a negative tw_status; nothing
+ * throws across the ABI; a tw_ctx is not thread-safe, distinct contexts may be
+ * used concurrently from different host threads; device buffers are owned by
+ * the library; host buffers passed in are copied before the call returns.
+ * There is NO CPU fallback: on a host without a gfx950 device tw_create fails
+ * with TW_ERR_NO_DEVICE.
+ */
+#ifndef TIMEWARP_H
+#define TIMEWARP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define TW_ABI_VERSION 1u
+/* Async exception payloads (throwTo's value) are carried as int32. */
+
+/* ------------------------------------------------------------------ status */
+typedef enum tw_status {
+    TW_OK = 0,
+    TW_ERR_INVALID = -1,      /* malformed descriptor / argument            */
+    TW_ERR_NO_DEVICE = -2,    /* no HIP device (or not gfx950)              */
+    TW_ERR_HIP = -3,          /* HIP runtime error                          */
+    TW_ERR_OOM = -4,          /* device allocation failed                   */
+    TW_ERR_STATE = -5,        /* call out of order (run before load, ...)   */
+    TW_ERR_REPLICA = -6       /* one or more replicas ended in error status */
+} tw_status;
+
+/* per-replica status (tw_replica_result.status) */
+enum {
+    TW_REP_RUNNING = 0,       /* queue not empty yet (t_end / event budget) */
+    TW_REP_DONE = 1,          /* quiescence: event queue empty (TimedT.hs:239,266-267) */
+    TW_REP_ABORTED = 2,       /* an exception escaped runTimedT's loop: async
+                                 exception delivered to a forked thread before
+                                 its action started (TimedT.hs:252-263, handlers=[]) */
+    TW_REP_ERR_SLOTS = 3,     /* thread-slot capacity exceeded              */
+    TW_REP_ERR_QUEUE = 4,     /* event-queue capacity exceeded              */
+    TW_REP_ERR_FRAMES = 5,    /* catch-frame depth exceeded                 */
+    TW_REP_ERR_INSN = 6       /* bad opcode / pc / link                     */
+};
+
+/* ------------------------------------------------------------- exceptions */
+/* Exception codes (1..15); handler masks are 16-bit sets over these codes. */
+enum {
+    TW_EXC_NONE = 0,
+    TW_EXC_THREAD_KILLED = 1, /* AsyncException ThreadKilled (killThread, MonadTimed.hs:205-206) */
+    TW_EXC_TIMEOUT = 2,       /* MTTimeoutError (MonadTimed.hs:69-73, TimedT.hs:370-376)          */
+    TW_EXC_ARITH = 3,         /* ArithException (Overflow etc., ExceptionSpec.hs)                 */
+    TW_EXC_USER0 = 4          /* first scenario-defined exception (e.g. ValueReceived)           */
+};
+#define TW_MASK_ALL 0xFFFEu   /* catchAll: every code 1..15                     */
+
+/* --------------------------------------------------------------------- ISA
+ * A thread program is a sequence of tw_insn.  Word w0 = op | a<<8 | b<<16,
+ * imm is a signed 32-bit immediate (pc, constant-pool index, value).
+ * Registers r0..r3 are int64 per thread; node vars v0..v3 are int64 per node.
+ * A thread REF (for throwTo/killThread) is held in a register as
+ * slot | (tid << 32) — the engine-specific slot is opaque to programs.
+ *
+ * Yielding ops end the current step (the reference's ContT capture at `wait`,
+ * TimedT.hs:343-355): WAIT_*, FORK (parent waits 1 µs, TimedT.hs:340), SEND
+ * (= schedule, i.e. a fork, unless dropped), DELIVER, TMO_BEGIN, END.
+ */
+enum tw_op {
+    TW_OP_NOP = 0,
+    TW_OP_END = 1,        /* thread finishes                                      */
+    TW_OP_WAIT_REL = 2,   /* wait (for K[imm])    : t = now + K[imm]              */
+    TW_OP_WAIT_ABS = 3,   /* wait (till K[imm])   : t = max(now, K[imm])          */
+    TW_OP_WAIT_REG = 4,   /* wait (for r[a])      : t = now + max(r[a],0)         */
+    TW_OP_FORK = 5,       /* r[a] = ref(child); child pc=imm, regs=copy, node =
+                             (b==0xFFFF ? parent node : r[b]); parent waits 1 µs  */
+    TW_OP_MYTID = 6,      /* r[a] = ref(self)                                     */
+    TW_OP_THROW_TO = 7,   /* throwTo r[a] (code = b&0xFF, value = r[b>>8])        */
+    TW_OP_THROW = 8,      /* throwM (code = b&0xFF, value = r[b>>8]) in this thread */
+    TW_OP_CATCH = 9,      /* push catch frame: mask = b, handler pc = imm          */
+    TW_OP_UNCATCH = 10,   /* pop innermost catch frame (scope left normally)       */
+    TW_OP_SETI = 11,      /* r[a] = imm                                           */
+    TW_OP_SETK = 12,      /* r[a] = K[imm]                                        */
+    TW_OP_ADDI = 13,      /* r[a] += imm                                          */
+    TW_OP_MOV = 14,       /* r[a] = r[b]                                          */
+    TW_OP_ADD = 15,       /* r[a] += r[b]                                         */
+    TW_OP_SUB = 16,       /* r[a] -= r[b]                                         */
+    TW_OP_MODI = 17,      /* r[a] = r[a] mod imm (imm > 0, result in [0,imm))     */
+    TW_OP_JMP = 18,       /* pc = imm                                             */
+    TW_OP_JEQ = 19,       /* if r[a] == r[b&0xFF] pc = imm                        */
+    TW_OP_JNE = 20,       /* if r[a] != r[b&0xFF] pc = imm                        */
+    TW_OP_JLT = 21,       /* if r[a] <  r[b&0xFF] pc = imm                        */
+    TW_OP_JLE = 22,       /* if r[a] <= r[b&0xFF] pc = imm                        */
+    TW_OP_JEQI = 23,      /* if r[a] == (int16)b pc = imm                         */
+    TW_OP_JNEI = 24,      /* if r[a] != (int16)b pc = imm                         */
+    TW_OP_NOW = 25,       /* r[a] = virtualTime (TimedT.hs:322)                   */
+    TW_OP_NODE = 26,      /* r[a] = this thread's node                            */
+    TW_OP_NLOAD = 27,     /* r[a] = v[node][b]                                    */
+    TW_OP_NSTORE = 28,    /* v[node][b] = r[a]                                    */
+    TW_OP_LINK = 29,      /* r[a] = out_off[node] + imm  (k-th out-link)          */
+    TW_OP_RLINK = 30,     /* r[a] = link_rev[r[b]]       (reply link)             */
+    TW_OP_SEND = 31,      /* send over link r[a]: kind = b&0xFF, payload = r[b>>8] */
+    TW_OP_DELIVER = 32,   /* (deliver stub) r0=payload r1=link r3=kind            */
+    TW_OP_LISTEN = 33,    /* bind this node to listener set imm; b=1: owned by
+                             this thread (released when it dies)                 */
+    TW_OP_UNLISTEN = 34,  /* unbind this node                                     */
+    TW_OP_TRACE = 35,     /* node hash += term(now, 0x30000|imm, r[a])            */
+    TW_OP_TMO_BEGIN = 36, /* timeout K[imm] (TimedT.hs:370-376): r[a] = fresh epoch e,
+                             done[e] = False, schedule (after K[imm]) watchdog —
+                             a fork, so the caller yields 1 µs                   */
+    TW_OP_TMO_END = 37,   /* `finally` on normal exit: pop finally frame, done[e]=True */
+    TW_OP_TMO_FIRE = 38,  /* (watchdog stub) unless done[r1]: throwTo r0 MTTimeoutError */
+    TW_OP_MULI = 39,      /* r[a] *= imm                                          */
+    TW_OP_NLOADX = 40,    /* r[a] = v[r[b>>8]][b&0xFF]  (another node's var)      */
+    TW_OP_NSTOREX = 41,   /* v[r[b>>8]][b&0xFF] = r[a]                            */
+    TW_OP_TMO_PUSH = 42,  /* enter `act `finally` done:=True` for epoch r[a]      */
+    TW_OP_COUNT = 43
+};
+
+/* Fixed stubs at the start of every program image (validated by tw_load). */
+#define TW_PC_DELIVER_STUB 0u  /* WAIT_REG r2 ; DELIVER ; END                   */
+#define TW_PC_WATCHDOG_STUB 3u /* WAIT_REG r2 ; TMO_FIRE ; END                  */
+#define TW_PC_USER 6u          /* first user instruction                        */
+#define TW_PC_NONE 0xFFFFFFFFu
+
+typedef struct tw_insn {
+    uint32_t w0;  /* op | a<<8 | b<<16 */
+    int32_t imm;
+} tw_insn;
+
+/* Link-table entry: bits 0..30 delay in µs, bit 31 = drop ("network nastiness").
+ * Entry for a send = table[link][ordinal % link_depth][replica], where ordinal
+ * counts sends already attempted on that link in that replica (replica-minor,
+ * the layout the engine keeps in HBM so lock-stepped lanes coalesce). */
+#define TW_LINK_DROP 0x80000000u
+
+/* --------------------------------------------------------------- scenario */
+typedef struct tw_scenario_desc {
+    uint32_t abi_version;      /* TW_ABI_VERSION */
+    uint32_t n_replicas;
+    uint32_t n_nodes;
+    uint32_t n_insns;
+    const tw_insn* insns;
+    uint32_t n_consts;
+    const int64_t* consts;     /* time constants (µs) and other 64-bit immediates */
+    uint32_t main_pc;          /* main thread entry (runs at t=0 without a pop, TimedT.hs:237) */
+    uint32_t main_node;
+    /* listeners: listener_pc[set * n_msg_kinds + kind] (TW_PC_NONE = no listener) */
+    uint32_t n_listener_sets;
+    uint32_t n_msg_kinds;
+    const uint32_t* listener_pc;
+    /* links, CSR over source nodes */
+    uint32_t n_links;
+    const uint32_t* out_off;   /* n_nodes + 1 */
+    const uint32_t* link_dst;  /* n_links */
+    const uint32_t* link_rev;  /* n_links (TW_PC_NONE if no reverse link) */
+    uint32_t link_depth;       /* >= 1 */
+    const uint32_t* link_table;/* [n_links][link_depth][n_replicas]; NULL = all 0 µs */
+    const int64_t* node_vars;  /* [n_nodes][4] initial node vars (same for all replicas); NULL = 0 */
+    const int64_t* main_regs;  /* [n_replicas][4] initial main-thread registers; NULL = 0 */
+    /* capacities (per replica) */
+    uint32_t max_slots;        /* concurrent threads                              */
+    uint32_t queue_capacity;   /* far-queue entries (live + superseded)          */
+    int64_t near_horizon_us;   /* events due within this horizon use the on-chip queue */
+    uint32_t max_timeouts;     /* timeout epochs per replica (done-flag bitmap size) */
+} tw_scenario_desc;
+
+#define TW_MAX_FRAMES 3        /* catch/finally frames per thread (both engines) */
+
+typedef struct tw_replica_result {
+    int64_t final_t;           /* curTime after the last pop                     */
+    uint64_t events;           /* committed events = PQ.minView pops (TimedT.hs:242) */
+    uint64_t delivered;
+    uint64_t dropped;          /* link drops                                     */
+    uint64_t undeliverable;    /* delivered to an unbound port / unknown kind    */
+    uint32_t status;           /* TW_REP_*                                       */
+    uint32_t main_exc;         /* uncaught main-thread exception code, rethrown by
+                                  runTimedT after quiescence (TimedT.hs:302-304) */
+    uint64_t threads;          /* threads ever created (incl. main)              */
+} tw_replica_result;
+
+typedef struct tw_stats {
+    uint64_t events;           /* sum over replicas of this tw_run call          */
+    uint64_t sends;            /* delivered + dropped + undeliverable attempts    */
+    uint64_t delivered;
+    uint64_t dropped;
+    uint64_t undeliverable;
+    int64_t max_final_t;
+    uint32_t replicas_done;
+    uint32_t replicas_error;
+    uint32_t launches;         /* kernel launches issued by this call            */
+    uint32_t reserved;
+    double kernel_ms;          /* device time of the event kernels (HIP events)  */
+    double wall_ms;            /* host wall time of the call                     */
+} tw_stats;
+
+typedef struct tw_ctx tw_ctx;
+
+/* Create a context on HIP device `device` (no CPU fallback). */
+int tw_create(int device, tw_ctx** out);
+
+/* Copy a lowered scenario into HBM and reset every replica to t=0, queue empty,
+ * main thread about to run (TimedT.hs:120-127, 234-237).  Replaces the
+ * construction of the TimedT value + emptyScenario. */
+int tw_load(tw_ctx* ctx, const tw_scenario_desc* desc);
+
+/* Run every replica's event loop (launchTimedT, TimedT.hs:234-286) until its
+ * queue is empty, the next event is later than t_end_us, or its committed-event
+ * total (since tw_load) reached max_events (UINT64_MAX = no cap).  May be called
+ * repeatedly to advance in pieces.  Blocking.  Replaces runTimedT. */
+int tw_run(tw_ctx* ctx, int64_t t_end_us, uint64_t max_events, tw_stats* out);
+
+/* Per-replica results (final virtual time, counters, status, main exception). */
+int tw_read_results(tw_ctx* ctx, tw_replica_result* out, size_t n_replicas);
+
+/* Per-node trace hashes, layout [replica][node] (n = n_replicas * n_nodes). */
+int tw_read_hashes(tw_ctx* ctx, uint64_t* out, size_t n);
+
+/* Convenience aggregate of tw_read_results. */
+int tw_read_final(tw_ctx* ctx, int64_t* max_final_t, uint64_t* delivered,
+                  uint64_t* dropped, uint64_t* events);
+
+/* Duration (ms) of every event-kernel launch of the last tw_run, measured with
+ * HIP events on the library's stream; returns the count written. */
+int tw_last_launch_ms(tw_ctx* ctx, double* out, size_t cap);
+
+void tw_destroy(tw_ctx* ctx);
+const char* tw_strerror(int code);
+const char* tw_version(void);
+
+/* ---------------------------------------------------------------- hashing
+ * Per-node trace hash (made fully commutative): every
+ * committed event / trace / delivery at node n adds term(t, kind, val) to
+ * H[n] modulo 2^64.  Thread ids never enter a term (they depend on global pop
+ * order, TimedT.hs:288-289).  Shared by the engine and the oracle. */
+static inline uint64_t tw_mix64(uint64_t z) {
+    z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+    z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+    return z ^ (z >> 31);
+}
+static inline uint64_t tw_term(int64_t t, uint32_t kind, int64_t val) {
+    uint64_t h = tw_mix64((uint64_t)t + 0x9e3779b97f4a7c15ull);
+    h = tw_mix64(h ^ ((uint64_t)kind * 0xd6e8feb86659fd93ull));
+    return tw_mix64(h ^ (uint64_t)val);
+}
+#define TW_KIND_RESUME 0x10000u   /* | pc        : a thread resumed at pc       */
+#define TW_KIND_EXC 0x20000u      /* | exc code  : async exception delivered    */
+#define TW_KIND_TRACE 0x30000u    /* | tag       : explicit TRACE               */
+#define TW_KIND_RECV 0x40000u     /* | msg kind  : message delivered to node    */
+#define TW_KIND_DROP 0x50000u     /* | msg kind  : link dropped the message     */
+#define TW_KIND_UNDELIV 0x60000u  /* | msg kind  : no listener at destination   */
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* TIMEWARP_H */

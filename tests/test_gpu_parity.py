@@ -1,0 +1,52 @@
+"""GPU engine vs oracle (canonical mode): bit-exact on every output.
+
+Runs through the C ABI (libtimewarp.so) on cuda:0; no torch involved.  The
+oracle is the CPU restatement of TimedT (oracle/timedt_oracle.cpp)."""
+import numpy as np
+import pytest
+
+from timewarp import scenarios
+from timewarp.abi import RESULT_DTYPE
+
+pytestmark = pytest.mark.gpu
+
+FIELDS = [f for f in RESULT_DTYPE.names]
+
+
+def _compare(scn, engine_mod, oracle_mod, threads=8):
+    st, res, hashes = engine_mod.run_scenario(scn)
+    ores, ohashes = oracle_mod.run_batch(scn, threads=threads)
+    bad = {}
+    for f in FIELDS:
+        m = np.nonzero(res[f] != ores[f])[0]
+        if m.size:
+            bad[f] = (m[:5].tolist(), res[f][m[:5]].tolist(), ores[f][m[:5]].tolist())
+    hm = np.nonzero((hashes != ohashes).any(axis=1))[0]
+    if hm.size:
+        bad["hashes"] = hm[:5].tolist()
+    assert not bad, f"{scn.name}: GPU != oracle: {bad}"
+    assert st.events == int(ores["events"].sum())
+    return st, ores
+
+
+def test_token_ring_small(engine_mod, oracle_mod):
+    scn = scenarios.token_ring(n_nodes=16, n_replicas=256, launch_duration=20_000_000)
+    st, ores = _compare(scn, engine_mod, oracle_mod)
+    assert (ores["status"] == 1).all()
+
+
+def test_token_ring_drop_long(engine_mod, oracle_mod):
+    scn = scenarios.token_ring(n_nodes=12, n_replicas=300, launch_duration=200_000_000, drop_log2=4,
+                               link_depth=8)
+    st, ores = _compare(scn, engine_mod, oracle_mod)
+    assert ores["dropped"].sum() > 0
+
+
+def test_ping_pong(engine_mod, oracle_mod):
+    scn = scenarios.ping_pong(n_replicas=1000, round_trips=50)
+    _compare(scn, engine_mod, oracle_mod)
+
+
+def test_hotspot_small(engine_mod, oracle_mod):
+    scn = scenarios.hotspot(n_senders=8, n_replicas=130, msg_num=40)
+    _compare(scn, engine_mod, oracle_mod)

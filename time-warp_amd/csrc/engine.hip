@@ -1,0 +1,1017 @@
+// engine.hip — MI355X (gfx950) batched TimedT event engine + the C ABI of
+// include/timewarp.h.  Built into time-warp_amd/lib/libtimewarp.so.
+//
+// Replaces the pure-emulation runner of time-warp:
+//   launchTimedT / runTimedT   src/Control/TimeWarp/Timed/TimedT.hs:234-304
+//   fork / wait / throwTo / timeout               TimedT.hs:326-376
+// for R independent replicas of one lowered scenario.
+//
+// Mapping to the hardware:
+//   * one LANE per replica: a replica's event loop is strictly sequential in
+//     TimedT (one pop at a time, TimedT.hs:239-263), replicas are independent,
+//     so lanes never synchronise and the whole chip streams replicas;
+//   * all per-replica HBM state is replica-minor ([index][replica]): while
+//     replicas run in lock-step (scenario start-up, identical programs) a
+//     wavefront's 64 accesses to "the same" slot/node/heap index coalesce into
+//     contiguous 1-4 KiB transactions; when they diverge each lane touches one
+//     64-B line per record;
+//   * TimedT's event queue (a pqueue MinQueue of continuations) becomes, per
+//     replica, an on-chip NEAR heap in LDS (events due within the scenario's
+//     horizon: forks' +1 µs, message deliveries, short waits) plus a 4-ary FAR
+//     heap in HBM (sleepForever timers, killers, long waits).  Every thread has
+//     at most one queued event (a thread is either running or parked at one
+//     `wait`), so throwTo's queue rebuild (TimedT.hs:361-368) becomes an O(1)
+//     re-stamp: a fresh (now, seq) entry is pushed and the old one is dropped
+//     lazily at pop time (slot.wake_seq no longer matches);
+//   * the event order is (t, seq) with seq a per-replica insertion counter —
+//     bit-identical to the oracle's canonical mode.
+#include <hip/hip_runtime.h>
+
+#include <chrono>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <vector>
+
+#include "../../include/timewarp.h"
+
+#ifndef TW_NEAR_CAP
+#define TW_NEAR_CAP 16          // on-chip queue entries per replica (LDS)
+#endif
+#define TW_BLOCK 64             // one wavefront per workgroup
+#define TW_STEP_CAP (1u << 22)  // instructions per thread step (== oracle kStepCap)
+
+namespace {
+
+// ------------------------------------------------------------------ layout
+// Thread slot record: 64 B, [slot][replica].
+//  w0: pc:16 | nfr:2 | flags:6 | exc_code:8      flags bit0 started, bit1 main
+//  w1: node   w2: tid   w3: wake_seq (0 = not queued)
+//  w4..w6: frames (mask:16 << 16 | pc:16; mask 0 = finally frame of epoch pc)
+//  w7: pending exception value
+//  r[4]: int64 registers
+struct Th {
+    uint32_t w0, w1, w2, w3;  // pc|nfr|flags|exc, node, tid, wake_seq
+    uint32_t f0, f1, f2;      // catch / finally frames
+    uint32_t w7;              // pending exception value
+    int64_t r0, r1, r2, r3;
+};
+
+// Registers and frames are selected, never indexed: a runtime index into a
+// private array would spill the record to scratch.
+__device__ __forceinline__ int64_t getr(const Th& t, uint32_t a) {
+    return a == 0 ? t.r0 : a == 1 ? t.r1 : a == 2 ? t.r2 : t.r3;
+}
+__device__ __forceinline__ void setr(Th& t, uint32_t a, int64_t v) {
+    t.r0 = a == 0 ? v : t.r0;
+    t.r1 = a == 1 ? v : t.r1;
+    t.r2 = a == 2 ? v : t.r2;
+    t.r3 = a == 3 ? v : t.r3;
+}
+__device__ __forceinline__ uint32_t getf(const Th& t, uint32_t i) { return i == 0 ? t.f0 : i == 1 ? t.f1 : t.f2; }
+__device__ __forceinline__ void setf(Th& t, uint32_t i, uint32_t v) {
+    t.f0 = i == 0 ? v : t.f0;
+    t.f1 = i == 1 ? v : t.f1;
+    t.f2 = i == 2 ? v : t.f2;
+}
+
+#define F_STARTED 1u
+#define F_MAIN 2u
+
+__device__ __forceinline__ uint32_t th_pc(const Th& t) { return t.w0 & 0xFFFFu; }
+__device__ __forceinline__ void th_set_pc(Th& t, uint32_t pc) { t.w0 = (t.w0 & 0xFFFF0000u) | (pc & 0xFFFFu); }
+__device__ __forceinline__ uint32_t th_nfr(const Th& t) { return (t.w0 >> 16) & 3u; }
+__device__ __forceinline__ void th_set_nfr(Th& t, uint32_t n) { t.w0 = (t.w0 & ~(3u << 16)) | (n << 16); }
+__device__ __forceinline__ uint32_t th_flags(const Th& t) { return (t.w0 >> 18) & 0x3Fu; }
+__device__ __forceinline__ void th_or_flags(Th& t, uint32_t f) { t.w0 |= (f & 0x3Fu) << 18; }
+__device__ __forceinline__ uint32_t th_exc(const Th& t) { return t.w0 >> 24; }
+__device__ __forceinline__ void th_set_exc(Th& t, uint32_t c) { t.w0 = (t.w0 & 0x00FFFFFFu) | (c << 24); }
+
+enum {
+    SC_NOW, SC_FINAL_T, SC_EVENTS, SC_DELIVERED, SC_DROPPED, SC_UNDELIV, SC_THREADS, SC_SEQ, SC_TIDC,
+    SC_LIVE, SC_NEAR_N, SC_FAR_N, SC_STATUS, SC_MAIN_EXC, SC_PENDING_MAIN, SC_FREE_TOP, SC_TMO_CTR, SC_COUNT
+};
+
+struct Dev {
+    // shape
+    uint32_t R, S, Q, N, L, D, T;
+    uint32_t n_insns, n_consts, n_sets, n_kinds;
+    int64_t horizon;
+    // scenario (shared by all replicas)
+    const uint2* insns;
+    const int64_t* consts;
+    const uint32_t* lpc;
+    const uint32_t* out_off;
+    const uint32_t* link_dst;
+    const uint32_t* link_rev;
+    const uint32_t* link_table;   // [L*D][R] or null
+    // per-replica scalars: one [field][replica] block of 64-bit words (SC_*),
+    // a single base pointer keeps the loop's scalar-register set small
+    uint64_t* scal;
+    // per-replica arrays
+    uint4* slots;        // [S][R][4]
+    uint32_t* free_stk;  // [S][R]
+    uint4* far;          // [Q][R]  {t_lo, t_hi, key_lo(slot), key_hi(seq)}
+    uint4* near_spill;   // [NEAR_CAP][R]
+    int64_t* nvars;      // [N*4][R]
+    uint64_t* hash;      // [N][R]
+    uint32_t* bind;      // [N][R] 0 or set+1
+    uint32_t* bind_own;  // [N][R] owner tid or 0xFFFFFFFF
+    uint32_t* link_ord;  // [L][R]
+    uint8_t* tmo_done;   // [T][R]
+    uint32_t* n_active;  // [1]
+};
+
+// ------------------------------------------------------------------ hashing
+__device__ __forceinline__ uint64_t mix64(uint64_t z) {
+    z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+    z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+    return z ^ (z >> 31);
+}
+__device__ __forceinline__ uint64_t term(int64_t t, uint32_t kind, int64_t val) {
+    uint64_t h = mix64((uint64_t)t + 0x9e3779b97f4a7c15ull);
+    h = mix64(h ^ ((uint64_t)kind * 0xd6e8feb86659fd93ull));
+    return mix64(h ^ (uint64_t)val);
+}
+
+// ------------------------------------------------------------ event keys
+// key = (t, seq<<32 | slot): seq is unique per replica, so (t, key) orders by (t, seq).
+__device__ __forceinline__ bool kless(int64_t ta, uint64_t ka, int64_t tb, uint64_t kb) {
+    return ta < tb || (ta == tb && ka < kb);
+}
+
+struct Lane {
+    const Dev* c;
+    uint32_t r;       // replica
+    // LDS near heap of this lane: element j at base[j * TW_BLOCK]
+    int64_t* nt;
+    uint64_t* nk;
+    // cached replica scalars
+    int64_t now;
+    uint32_t seq, tidc, live, near_n, far_n, status, main_exc, free_top, tmo_ctr;
+    uint64_t events, delivered, dropped, undeliv, threads;
+    int64_t final_t;
+    // cached far top
+    int64_t far_t;
+    uint64_t far_k;
+
+    __device__ __forceinline__ size_t ix(size_t i) const { return i * c->R + r; }
+
+    __device__ __forceinline__ void fail(uint32_t st) {
+        if (status == TW_REP_RUNNING) status = st;
+    }
+
+    // ---------------------------------------------------------- near heap (LDS)
+    __device__ __forceinline__ void near_push(int64_t t, uint64_t k) {
+        uint32_t i = near_n++;
+        while (i > 0) {
+            uint32_t p = (i - 1) >> 1;
+            int64_t pt = nt[p * TW_BLOCK];
+            uint64_t pk = nk[p * TW_BLOCK];
+            if (!kless(t, k, pt, pk)) break;
+            nt[i * TW_BLOCK] = pt;
+            nk[i * TW_BLOCK] = pk;
+            i = p;
+        }
+        nt[i * TW_BLOCK] = t;
+        nk[i * TW_BLOCK] = k;
+    }
+    __device__ __forceinline__ void near_pop() {
+        uint32_t n = --near_n;
+        if (n == 0) return;
+        int64_t t = nt[n * TW_BLOCK];
+        uint64_t k = nk[n * TW_BLOCK];
+        uint32_t i = 0;
+        for (;;) {
+            uint32_t c0 = 2 * i + 1;
+            if (c0 >= n) break;
+            int64_t ct = nt[c0 * TW_BLOCK];
+            uint64_t ck = nk[c0 * TW_BLOCK];
+            if (c0 + 1 < n) {
+                int64_t dt = nt[(c0 + 1) * TW_BLOCK];
+                uint64_t dk = nk[(c0 + 1) * TW_BLOCK];
+                if (kless(dt, dk, ct, ck)) { ct = dt; ck = dk; ++c0; }
+            }
+            if (!kless(ct, ck, t, k)) break;
+            nt[i * TW_BLOCK] = ct;
+            nk[i * TW_BLOCK] = ck;
+            i = c0;
+        }
+        nt[i * TW_BLOCK] = t;
+        nk[i * TW_BLOCK] = k;
+    }
+
+    // ------------------------------------------------------ far heap (HBM, 4-ary)
+    __device__ __forceinline__ uint4 far_ld(uint32_t i) const { return c->far[ix(i)]; }
+    __device__ __forceinline__ void far_st(uint32_t i, int64_t t, uint64_t k) const {
+        c->far[ix(i)] = make_uint4((uint32_t)t, (uint32_t)((uint64_t)t >> 32), (uint32_t)k, (uint32_t)(k >> 32));
+    }
+    __device__ __forceinline__ void far_push(int64_t t, uint64_t k) {
+        if (far_n >= c->Q) { fail(TW_REP_ERR_QUEUE); return; }
+        uint32_t i = far_n++;
+        while (i > 0) {
+            uint32_t p = (i - 1) >> 2;
+            uint4 e = far_ld(p);
+            int64_t pt = (int64_t)(((uint64_t)e.y << 32) | e.x);
+            uint64_t pk = ((uint64_t)e.w << 32) | e.z;
+            if (!kless(t, k, pt, pk)) break;
+            c->far[ix(i)] = e;
+            i = p;
+        }
+        far_st(i, t, k);
+        if (i == 0) { far_t = t; far_k = k; }
+    }
+    __device__ __forceinline__ void far_pop() {
+        uint32_t n = --far_n;
+        if (n == 0) return;
+        uint4 le = far_ld(n);
+        int64_t t = (int64_t)(((uint64_t)le.y << 32) | le.x);
+        uint64_t k = ((uint64_t)le.w << 32) | le.z;
+        uint32_t i = 0;
+        for (;;) {
+            uint32_t c0 = 4 * i + 1;
+            if (c0 >= n) break;
+            uint32_t cn = n - c0 < 4 ? n - c0 : 4;
+            // the (up to) four children are independent loads: issue all, then reduce
+            uint4 e0 = far_ld(c0);
+            uint4 e1 = cn > 1 ? far_ld(c0 + 1) : e0;
+            uint4 e2 = cn > 2 ? far_ld(c0 + 2) : e0;
+            uint4 e3 = cn > 3 ? far_ld(c0 + 3) : e0;
+            uint32_t best = 0;
+            int64_t bt = (int64_t)(((uint64_t)e0.y << 32) | e0.x);
+            uint64_t bk = ((uint64_t)e0.w << 32) | e0.z;
+            {
+                int64_t jt = (int64_t)(((uint64_t)e1.y << 32) | e1.x);
+                uint64_t jk = ((uint64_t)e1.w << 32) | e1.z;
+                if (cn > 1 && kless(jt, jk, bt, bk)) { best = 1; bt = jt; bk = jk; }
+                jt = (int64_t)(((uint64_t)e2.y << 32) | e2.x);
+                jk = ((uint64_t)e2.w << 32) | e2.z;
+                if (cn > 2 && kless(jt, jk, bt, bk)) { best = 2; bt = jt; bk = jk; }
+                jt = (int64_t)(((uint64_t)e3.y << 32) | e3.x);
+                jk = ((uint64_t)e3.w << 32) | e3.z;
+                if (cn > 3 && kless(jt, jk, bt, bk)) { best = 3; bt = jt; bk = jk; }
+            }
+            if (!kless(bt, bk, t, k)) break;
+            far_st(i, bt, bk);
+            if (i == 0) { far_t = bt; far_k = bk; }
+            i = c0 + best;
+        }
+        far_st(i, t, k);
+        if (i == 0) { far_t = t; far_k = k; }
+    }
+
+    // ------------------------------------------------------------- queue
+    __device__ __forceinline__ void enqueue(Th& th, uint32_t slot, int64_t t) {
+        uint32_t s = ++seq;
+        if (th.w3 == 0) ++live;
+        th.w3 = s;
+        uint64_t k = ((uint64_t)s << 32) | slot;
+        if (t - now < c->horizon && near_n < TW_NEAR_CAP) near_push(t, k);
+        else far_push(t, k);
+    }
+
+    // ------------------------------------------------------------- slots
+    __device__ __forceinline__ void load_th(uint32_t slot, Th& th) const {
+        const uint4* p = c->slots + ix(slot) * 4;
+        uint4 a = p[0], b = p[1], d = p[2], e = p[3];
+        th.w0 = a.x; th.w1 = a.y; th.w2 = a.z; th.w3 = a.w;
+        th.f0 = b.x; th.f1 = b.y; th.f2 = b.z; th.w7 = b.w;
+        th.r0 = (int64_t)(((uint64_t)d.y << 32) | d.x);
+        th.r1 = (int64_t)(((uint64_t)d.w << 32) | d.z);
+        th.r2 = (int64_t)(((uint64_t)e.y << 32) | e.x);
+        th.r3 = (int64_t)(((uint64_t)e.w << 32) | e.z);
+    }
+    __device__ __forceinline__ void store_th(uint32_t slot, const Th& th) const {
+        uint4* p = c->slots + ix(slot) * 4;
+        p[0] = make_uint4(th.w0, th.w1, th.w2, th.w3);
+        p[1] = make_uint4(th.f0, th.f1, th.f2, th.w7);
+        p[2] = make_uint4((uint32_t)th.r0, (uint32_t)((uint64_t)th.r0 >> 32), (uint32_t)th.r1,
+                          (uint32_t)((uint64_t)th.r1 >> 32));
+        p[3] = make_uint4((uint32_t)th.r2, (uint32_t)((uint64_t)th.r2 >> 32), (uint32_t)th.r3,
+                          (uint32_t)((uint64_t)th.r3 >> 32));
+    }
+    __device__ __forceinline__ uint32_t alloc_slot() {
+        if (free_top == 0) { fail(TW_REP_ERR_SLOTS); return 0xFFFFFFFFu; }
+        return c->free_stk[ix(--free_top)];
+    }
+    __device__ __forceinline__ void free_slot(uint32_t slot) { c->free_stk[ix(free_top++)] = slot; }
+
+    __device__ __forceinline__ void hash(uint32_t node, uint32_t kind, int64_t val) {
+        c->hash[ix(node)] += term(now, kind, val);
+    }
+
+    // Create a thread queued at now (fork, TimedT.hs:326-339).  Returns its ref.
+    __device__ __forceinline__ bool spawn(uint32_t pc, uint32_t node, int64_t q0, int64_t q1, int64_t q2, int64_t q3, int64_t& ref) {
+        uint32_t s = alloc_slot();
+        if (s == 0xFFFFFFFFu) return false;
+        Th ch;
+        uint32_t tid = tidc++;
+        ++threads;
+        ch.w0 = pc & 0xFFFFu;
+        ch.w1 = node;
+        ch.w2 = tid;
+        ch.w3 = 0;
+        ch.f0 = ch.f1 = ch.f2 = ch.w7 = 0;
+        ch.r0 = q0; ch.r1 = q1; ch.r2 = q2; ch.r3 = q3;
+        enqueue(ch, s, now);
+        store_th(s, ch);
+        ref = (int64_t)(((uint64_t)tid << 32) | s);
+        return true;
+    }
+
+    // throwTo (TimedT.hs:357-368): re-stamp target's event to now, first exception wins.
+    __device__ __forceinline__ void throw_to(Th& self, uint32_t self_slot, int64_t ref, uint32_t code, int64_t val) {
+        uint32_t ts = (uint32_t)ref;
+        uint32_t tid = (uint32_t)((uint64_t)ref >> 32);
+        if (ts >= c->S) return;
+        if (ts == self_slot) {  // the running thread: its record lives in registers
+            if (self.w2 != tid) return;
+            if (th_exc(self) == 0) { th_set_exc(self, code); self.w7 = (uint32_t)val; }
+            return;
+        }
+        uint4* p = c->slots + ix(ts) * 4;
+        uint4 a = p[0];
+        if (a.z != tid) return;  // dead (slot free or reused): the map entry is unobservable
+        if (a.w != 0) {         // queued: wake to now with a fresh seq
+            uint32_t s = ++seq;
+            a.w = s;
+            uint64_t k = ((uint64_t)s << 32) | ts;
+            if (near_n < TW_NEAR_CAP) near_push(now, k);
+            else far_push(now, k);
+        }
+        if ((a.x >> 24) == 0) {
+            a.x = (a.x & 0x00FFFFFFu) | (code << 24);
+            p[1].w = (uint32_t)val;
+        }
+        p[0] = a;
+    }
+
+    // Thread ends (END or uncaught exception).
+    __device__ __forceinline__ void die(Th& th, uint32_t slot) {
+        uint32_t node = th.w1;
+        if (c->bind[ix(node)] && c->bind_own[ix(node)] == th.w2) {
+            c->bind[ix(node)] = 0;
+            c->bind_own[ix(node)] = 0xFFFFFFFFu;
+        }
+        th.w2 = 0xFFFFFFFFu;  // invalidate refs to this slot
+        th.w3 = 0;
+        store_th(slot, th);
+        free_slot(slot);
+    }
+
+    // Raise `code` in th; true if a catch frame took it (pc set to handler).
+    __device__ __forceinline__ bool unwind(Th& th, uint32_t slot, uint32_t code, int64_t val) {
+        uint32_t n = th_nfr(th);
+        while (n > 0) {
+            uint32_t f = getf(th, --n);
+            uint32_t mask = f >> 16;
+            if (mask == 0) {
+                uint32_t e = f & 0xFFFFu;
+                if (e < c->T) c->tmo_done[ix(e)] = 1;
+                continue;
+            }
+            if (mask & (1u << code)) {
+                th_set_nfr(th, n);
+                th_set_pc(th, f & 0xFFFFu);
+                th.r0 = val;
+                th.r3 = code;
+                return true;
+            }
+        }
+        th_set_nfr(th, 0);
+        if (th_flags(th) & F_MAIN) main_exc = code;
+        die(th, slot);
+        return false;
+    }
+
+    // Run the thread's continuation until it yields or ends.
+    __device__ __forceinline__ void step(Th& th, uint32_t slot) {
+        th_or_flags(th, F_STARTED);
+        const int64_t* K = c->consts;
+        for (uint32_t n = 0; n < TW_STEP_CAP; ++n) {
+            uint32_t pc = th_pc(th);
+            if (pc >= c->n_insns) { fail(TW_REP_ERR_INSN); store_th(slot, th); return; }
+            uint2 in = c->insns[pc];
+            uint32_t op = in.x & 0xFFu, a = (in.x >> 8) & 3u, b = in.x >> 16;
+            int32_t imm = (int32_t)in.y;
+            th_set_pc(th, pc + 1);
+            switch (op) {
+            case TW_OP_NOP: break;
+            case TW_OP_END: die(th, slot); return;
+            case TW_OP_WAIT_REL: enqueue(th, slot, now + K[imm]); store_th(slot, th); return;
+            case TW_OP_WAIT_ABS: {
+                int64_t t = K[imm];
+                enqueue(th, slot, t > now ? t : now);
+                store_th(slot, th);
+                return;
+            }
+            case TW_OP_WAIT_REG: {
+                int64_t d = getr(th, a);
+                enqueue(th, slot, now + (d > 0 ? d : 0));
+                store_th(slot, th);
+                return;
+            }
+            case TW_OP_FORK: {
+                uint32_t node = b == 0xFFFFu ? th.w1 : (uint32_t)getr(th, b & 3);
+                if (node >= c->N) { fail(TW_REP_ERR_INSN); store_th(slot, th); return; }
+                int64_t ref;
+                if (!spawn((uint32_t)imm, node, th.r0, th.r1, th.r2, th.r3, ref)) { store_th(slot, th); return; }
+                setr(th, a, ref);
+                enqueue(th, slot, now + 1);
+                store_th(slot, th);
+                return;
+            }
+            case TW_OP_MYTID: setr(th, a, (int64_t)(((uint64_t)th.w2 << 32) | slot)); break;
+            case TW_OP_THROW_TO: throw_to(th, slot, getr(th, a), b & 0xFFu, getr(th, (b >> 8) & 3)); break;
+            case TW_OP_THROW:
+                if (!unwind(th, slot, b & 0xFFu, getr(th, (b >> 8) & 3))) return;
+                break;
+            case TW_OP_CATCH: {
+                uint32_t nf = th_nfr(th);
+                if (nf >= TW_MAX_FRAMES) { fail(TW_REP_ERR_FRAMES); store_th(slot, th); return; }
+                setf(th, nf, (b << 16) | ((uint32_t)imm & 0xFFFFu));
+                th_set_nfr(th, nf + 1);
+                break;
+            }
+            case TW_OP_UNCATCH: {
+                uint32_t nf = th_nfr(th);
+                if (nf == 0 || (getf(th, nf - 1) >> 16) == 0) { fail(TW_REP_ERR_INSN); store_th(slot, th); return; }
+                th_set_nfr(th, nf - 1);
+                break;
+            }
+            case TW_OP_SETI: setr(th, a, imm); break;
+            case TW_OP_SETK: setr(th, a, K[imm]); break;
+            case TW_OP_ADDI: setr(th, a, getr(th, a) + imm); break;
+            case TW_OP_MULI: setr(th, a, getr(th, a) * imm); break;
+            case TW_OP_MOV: setr(th, a, getr(th, b & 3)); break;
+            case TW_OP_ADD: setr(th, a, getr(th, a) + getr(th, b & 3)); break;
+            case TW_OP_SUB: setr(th, a, getr(th, a) - getr(th, b & 3)); break;
+            case TW_OP_MODI: {
+                int64_t m = getr(th, a) % imm;
+                setr(th, a, m < 0 ? m + imm : m);
+                break;
+            }
+            case TW_OP_JMP: th_set_pc(th, (uint32_t)imm); break;
+            case TW_OP_JEQ: if (getr(th, a) == getr(th, b & 3)) th_set_pc(th, (uint32_t)imm); break;
+            case TW_OP_JNE: if (getr(th, a) != getr(th, b & 3)) th_set_pc(th, (uint32_t)imm); break;
+            case TW_OP_JLT: if (getr(th, a) < getr(th, b & 3)) th_set_pc(th, (uint32_t)imm); break;
+            case TW_OP_JLE: if (getr(th, a) <= getr(th, b & 3)) th_set_pc(th, (uint32_t)imm); break;
+            case TW_OP_JEQI: if (getr(th, a) == (int64_t)(int16_t)b) th_set_pc(th, (uint32_t)imm); break;
+            case TW_OP_JNEI: if (getr(th, a) != (int64_t)(int16_t)b) th_set_pc(th, (uint32_t)imm); break;
+            case TW_OP_NOW: setr(th, a, now); break;
+            case TW_OP_NODE: setr(th, a, th.w1); break;
+            case TW_OP_NLOAD: setr(th, a, c->nvars[ix((size_t)th.w1 * 4 + (b & 3))]); break;
+            case TW_OP_NSTORE: c->nvars[ix((size_t)th.w1 * 4 + (b & 3))] = getr(th, a); break;
+            case TW_OP_NLOADX:
+            case TW_OP_NSTOREX: {
+                uint64_t node = (uint64_t)getr(th, (b >> 8) & 3);
+                if (node >= c->N) { fail(TW_REP_ERR_INSN); store_th(slot, th); return; }
+                int64_t* v = &c->nvars[ix(node * 4 + (b & 3))];
+                if (op == TW_OP_NLOADX) setr(th, a, *v);
+                else *v = getr(th, a);
+                break;
+            }
+            case TW_OP_LINK: setr(th, a, (int64_t)c->out_off[th.w1] + imm); break;
+            case TW_OP_RLINK: {
+                uint64_t l = (uint64_t)getr(th, b & 3);
+                if (l >= c->L) { fail(TW_REP_ERR_INSN); store_th(slot, th); return; }
+                setr(th, a, (int64_t)c->link_rev[l]);
+                break;
+            }
+            case TW_OP_SEND: {
+                uint64_t link = (uint64_t)getr(th, a);
+                if (link >= c->L) { fail(TW_REP_ERR_INSN); store_th(slot, th); return; }
+                uint32_t kind = b & 0xFFu;
+                int64_t payload = getr(th, (b >> 8) & 3);
+                uint32_t ord = c->link_ord[ix(link)];
+                c->link_ord[ix(link)] = ord + 1;
+                uint32_t e = c->link_table ? c->link_table[ix((size_t)link * c->D + ord % c->D)] : 0u;
+                if (e & TW_LINK_DROP) {
+                    ++dropped;
+                    hash(th.w1, TW_KIND_DROP | kind, payload);
+                    break;
+                }
+                int64_t ref;
+                if (!spawn(TW_PC_DELIVER_STUB, th.w1, payload, (int64_t)link, (int64_t)(e & 0x7FFFFFFFu), (int64_t)kind, ref)) { store_th(slot, th); return; }
+                enqueue(th, slot, now + 1);
+                store_th(slot, th);
+                return;
+            }
+            case TW_OP_DELIVER: {
+                uint64_t link = (uint64_t)getr(th, 1);
+                uint32_t kind = (uint32_t)getr(th, 3);
+                uint32_t dst = c->link_dst[link];
+                uint32_t set = c->bind[ix(dst)];
+                uint32_t lpc = TW_PC_NONE;
+                if (set && kind < c->n_kinds) lpc = c->lpc[(size_t)(set - 1) * c->n_kinds + kind];
+                if (lpc == TW_PC_NONE) {
+                    ++undeliv;
+                    hash(dst, TW_KIND_UNDELIV | kind, getr(th, 0));
+                    break;
+                }
+                ++delivered;
+                hash(dst, TW_KIND_RECV | kind, getr(th, 0));
+                int64_t ref;
+                if (!spawn(lpc, dst, getr(th, 0), (int64_t)link, (int64_t)th.w1, (int64_t)kind, ref)) { store_th(slot, th); return; }
+                enqueue(th, slot, now + 1);
+                store_th(slot, th);
+                return;
+            }
+            case TW_OP_LISTEN:
+                if ((uint32_t)imm >= c->n_sets) { fail(TW_REP_ERR_INSN); store_th(slot, th); return; }
+                c->bind[ix(th.w1)] = (uint32_t)imm + 1;
+                c->bind_own[ix(th.w1)] = b ? th.w2 : 0xFFFFFFFFu;
+                break;
+            case TW_OP_UNLISTEN:
+                c->bind[ix(th.w1)] = 0;
+                c->bind_own[ix(th.w1)] = 0xFFFFFFFFu;
+                break;
+            case TW_OP_TRACE: hash(th.w1, TW_KIND_TRACE | ((uint32_t)imm & 0xFFFFu), getr(th, a)); break;
+            case TW_OP_TMO_BEGIN: {
+                if (tmo_ctr >= c->T) { fail(TW_REP_ERR_INSN); store_th(slot, th); return; }
+                uint32_t e = tmo_ctr++;
+                c->tmo_done[ix(e)] = 0;
+                setr(th, a, e);
+                int64_t ref;
+                if (!spawn(TW_PC_WATCHDOG_STUB, th.w1, (int64_t)(((uint64_t)th.w2 << 32) | slot), (int64_t)e, K[imm], 0, ref)) { store_th(slot, th); return; }
+                enqueue(th, slot, now + 1);
+                store_th(slot, th);
+                return;
+            }
+            case TW_OP_TMO_PUSH: {
+                uint32_t nf = th_nfr(th);
+                if (nf >= TW_MAX_FRAMES) { fail(TW_REP_ERR_FRAMES); store_th(slot, th); return; }
+                setf(th, nf, (uint32_t)getr(th, a) & 0xFFFFu);
+                th_set_nfr(th, nf + 1);
+                break;
+            }
+            case TW_OP_TMO_END: {
+                uint32_t nf = th_nfr(th);
+                if (nf == 0 || (getf(th, nf - 1) >> 16) != 0) { fail(TW_REP_ERR_INSN); store_th(slot, th); return; }
+                uint32_t ep = getf(th, nf - 1) & 0xFFFFu;
+                th_set_nfr(th, nf - 1);
+                if (ep < c->T) c->tmo_done[ix(ep)] = 1;
+                break;
+            }
+            case TW_OP_TMO_FIRE: {
+                uint64_t e = (uint64_t)getr(th, 1);
+                if (e < c->T && !c->tmo_done[ix(e)]) throw_to(th, slot, getr(th, 0), TW_EXC_TIMEOUT, 0);
+                break;
+            }
+            default:
+                fail(TW_REP_ERR_INSN);
+                store_th(slot, th);
+                return;
+            }
+            if (status != TW_REP_RUNNING) { store_th(slot, th); return; }
+        }
+        fail(TW_REP_ERR_INSN);
+        store_th(slot, th);
+    }
+};
+
+// ------------------------------------------------------------------ kernels
+__global__ void __launch_bounds__(TW_BLOCK) tw_init_kernel(Dev c, uint32_t main_pc, uint32_t main_node,
+                                                          const int64_t* main_regs, const int64_t* nv_init) {
+    uint32_t r = blockIdx.x * TW_BLOCK + threadIdx.x;
+    if (r >= c.R) return;
+    for (uint32_t f = 0; f < SC_COUNT; ++f) c.scal[(size_t)f * c.R + r] = 0;
+    c.scal[(size_t)SC_THREADS * c.R + r] = 1;
+    c.scal[(size_t)SC_TIDC * c.R + r] = 1;
+    c.scal[(size_t)SC_STATUS * c.R + r] = TW_REP_RUNNING;
+    c.scal[(size_t)SC_PENDING_MAIN * c.R + r] = 1;
+    // free stack: slots S-1 .. 1 (slot 0 = main), pops hand out 1, 2, 3, ...
+    for (uint32_t k = 0; k + 1 < c.S; ++k) c.free_stk[(size_t)k * c.R + r] = c.S - 1 - k;
+    c.scal[(size_t)SC_FREE_TOP * c.R + r] = c.S - 1;
+    uint4* p = c.slots + (size_t)r * 4;  // slot 0
+    uint32_t w0 = (main_pc & 0xFFFFu) | (F_MAIN << 18);
+    p[0] = make_uint4(w0, main_node, 0u, 0u);
+    p[1] = make_uint4(0u, 0u, 0u, 0u);
+    int64_t m[4] = {0, 0, 0, 0};
+    if (main_regs)
+        for (int i = 0; i < 4; ++i) m[i] = main_regs[(size_t)r * 4 + i];
+    p[2] = make_uint4((uint32_t)m[0], (uint32_t)((uint64_t)m[0] >> 32), (uint32_t)m[1], (uint32_t)((uint64_t)m[1] >> 32));
+    p[3] = make_uint4((uint32_t)m[2], (uint32_t)((uint64_t)m[2] >> 32), (uint32_t)m[3], (uint32_t)((uint64_t)m[3] >> 32));
+    if (nv_init)
+        for (uint32_t i = 0; i < c.N * 4; ++i) c.nvars[(size_t)i * c.R + r] = nv_init[i];
+    for (uint32_t n = 0; n < c.N; ++n) c.bind_own[(size_t)n * c.R + r] = 0xFFFFFFFFu;
+}
+
+__global__ void __launch_bounds__(TW_BLOCK) tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events,
+                                                         uint32_t budget) {
+    __shared__ int64_t s_t[TW_NEAR_CAP * TW_BLOCK];
+    __shared__ uint64_t s_k[TW_NEAR_CAP * TW_BLOCK];
+    uint32_t r = blockIdx.x * TW_BLOCK + threadIdx.x;
+    if (r >= c.R) return;
+    uint64_t* sc = c.scal + r;
+    const size_t R = c.R;
+    if (sc[SC_STATUS * R] != TW_REP_RUNNING) return;
+
+    Lane L;
+    L.c = &c;
+    L.r = r;
+    L.nt = s_t + threadIdx.x;
+    L.nk = s_k + threadIdx.x;
+    L.now = (int64_t)sc[SC_NOW * R]; L.final_t = (int64_t)sc[SC_FINAL_T * R];
+    L.seq = (uint32_t)sc[SC_SEQ * R]; L.tidc = (uint32_t)sc[SC_TIDC * R]; L.live = (uint32_t)sc[SC_LIVE * R];
+    L.near_n = (uint32_t)sc[SC_NEAR_N * R]; L.far_n = (uint32_t)sc[SC_FAR_N * R];
+    L.status = (uint32_t)sc[SC_STATUS * R]; L.main_exc = (uint32_t)sc[SC_MAIN_EXC * R];
+    L.free_top = (uint32_t)sc[SC_FREE_TOP * R]; L.tmo_ctr = (uint32_t)sc[SC_TMO_CTR * R];
+    L.events = sc[SC_EVENTS * R]; L.delivered = sc[SC_DELIVERED * R]; L.dropped = sc[SC_DROPPED * R];
+    L.undeliv = sc[SC_UNDELIV * R]; L.threads = sc[SC_THREADS * R];
+    for (uint32_t j = 0; j < L.near_n; ++j) {
+        uint4 e = c.near_spill[(size_t)j * c.R + r];
+        L.nt[j * TW_BLOCK] = (int64_t)(((uint64_t)e.y << 32) | e.x);
+        L.nk[j * TW_BLOCK] = ((uint64_t)e.w << 32) | e.z;
+    }
+    if (L.far_n) {
+        uint4 e = L.far_ld(0);
+        L.far_t = (int64_t)(((uint64_t)e.y << 32) | e.x);
+        L.far_k = ((uint64_t)e.w << 32) | e.z;
+    }
+
+    uint32_t pending_main = (uint32_t)sc[SC_PENDING_MAIN * R];
+    for (uint32_t it = 0; it < budget; ++it) {
+        if (L.status != TW_REP_RUNNING) break;
+        Th th;
+        uint32_t slot;
+        bool run = false;
+        if (pending_main) {  // runInSandbox main (TimedT.hs:237): runs at t=0, not a pop
+            pending_main = 0;
+            slot = 0;
+            L.load_th(0, th);
+            run = true;
+        } else {
+            if (L.live == 0) { L.status = TW_REP_DONE; break; }  // whileM_ notDone
+            if (L.events >= max_events) break;
+            bool use_near;
+            int64_t t;
+            uint64_t k;
+            if (L.near_n && (!L.far_n || kless(L.nt[0], L.nk[0], L.far_t, L.far_k))) {
+                use_near = true; t = L.nt[0]; k = L.nk[0];
+            } else {
+                use_near = false; t = L.far_t; k = L.far_k;
+            }
+            if (t > t_end) break;
+            if (use_near) L.near_pop();
+            else L.far_pop();
+            slot = (uint32_t)k;
+            L.load_th(slot, th);
+            if (th.w3 != (uint32_t)(k >> 32)) continue;  // superseded by a throwTo re-stamp
+            // PQ.minView; curTime .= timestamp (TimedT.hs:241-247)
+            th.w3 = 0;
+            --L.live;
+            L.now = t;
+            L.final_t = t;
+            ++L.events;
+            uint32_t exc = th_exc(th);  // asyncExceptions . at tid <<.= Nothing (:252)
+            if (exc) {
+                int64_t val = (int64_t)(int32_t)th.w7;
+                th_set_exc(th, 0);
+                th.w7 = 0;
+                L.hash(th.w1, TW_KIND_EXC | exc, 0);
+                if (!(th_flags(th) & (F_STARTED | F_MAIN))) {  // escapes launchTimedT (:252-263)
+                    L.status = TW_REP_ABORTED;
+                    L.main_exc = exc;
+                    L.store_th(slot, th);
+                    break;
+                }
+                run = L.unwind(th, slot, exc, val);
+            } else {
+                L.hash(th.w1, TW_KIND_RESUME | th_pc(th), 0);
+                run = true;
+            }
+        }
+        if (run) L.step(th, slot);
+    }
+    sc[SC_PENDING_MAIN * R] = pending_main;
+    if (L.status == TW_REP_RUNNING && L.live == 0) L.status = TW_REP_DONE;
+
+    sc[SC_NOW * R] = (uint64_t)L.now; sc[SC_FINAL_T * R] = (uint64_t)L.final_t;
+    sc[SC_SEQ * R] = L.seq; sc[SC_TIDC * R] = L.tidc; sc[SC_LIVE * R] = L.live;
+    sc[SC_NEAR_N * R] = L.near_n; sc[SC_FAR_N * R] = L.far_n;
+    sc[SC_STATUS * R] = L.status; sc[SC_MAIN_EXC * R] = L.main_exc;
+    sc[SC_FREE_TOP * R] = L.free_top; sc[SC_TMO_CTR * R] = L.tmo_ctr;
+    sc[SC_EVENTS * R] = L.events; sc[SC_DELIVERED * R] = L.delivered; sc[SC_DROPPED * R] = L.dropped;
+    sc[SC_UNDELIV * R] = L.undeliv; sc[SC_THREADS * R] = L.threads;
+    for (uint32_t j = 0; j < L.near_n; ++j) {
+        int64_t t = L.nt[j * TW_BLOCK];
+        uint64_t k = L.nk[j * TW_BLOCK];
+        c.near_spill[(size_t)j * c.R + r] =
+            make_uint4((uint32_t)t, (uint32_t)((uint64_t)t >> 32), (uint32_t)k, (uint32_t)(k >> 32));
+    }
+    bool active = L.status == TW_REP_RUNNING && L.events < max_events;
+    if (active) {
+        // next event beyond t_end?  then this replica is parked, not active
+        int64_t nt = INT64_MAX;
+        if (L.near_n) nt = L.nt[0];
+        if (L.far_n && L.far_t < nt) nt = L.far_t;
+        if (nt > t_end) active = false;
+    }
+    if (active) atomicAdd(c.n_active, 1u);
+}
+
+}  // namespace
+
+// ======================================================================= C ABI
+struct tw_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    Dev d{};
+    bool loaded = false;
+    std::vector<void*> allocs;
+    uint32_t* h_active = nullptr;  // pinned
+    std::vector<double> launch_ms;
+    std::vector<hipEvent_t> ev_pool;
+};
+
+namespace {
+
+int hip_fail(hipError_t e) {
+    (void)e;
+    return TW_ERR_HIP;
+}
+
+#define HIPCHK(x)                                     \
+    do {                                              \
+        hipError_t _e = (x);                          \
+        if (_e != hipSuccess) {                       \
+            fprintf(stderr, "timewarp: %s failed: %s\n", #x, hipGetErrorString(_e)); \
+            return _e == hipErrorOutOfMemory ? TW_ERR_OOM : hip_fail(_e); \
+        }                                             \
+    } while (0)
+
+template <class T>
+int dalloc(tw_ctx* c, T** p, size_t n) {
+    void* q = nullptr;
+    if (n == 0) n = 1;
+    HIPCHK(hipMalloc(&q, n * sizeof(T)));
+    c->allocs.push_back(q);
+    *p = (T*)q;
+    return TW_OK;
+}
+
+void free_all(tw_ctx* c) {
+    for (void* p : c->allocs) (void)hipFree(p);
+    c->allocs.clear();
+    c->loaded = false;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* tw_version(void) { return "timewarp-mi355x 0.1 (gfx950, lane-per-replica, near-cap " "16)"; }
+
+const char* tw_strerror(int code) {
+    switch (code) {
+    case TW_OK: return "ok";
+    case TW_ERR_INVALID: return "invalid argument or scenario descriptor";
+    case TW_ERR_NO_DEVICE: return "no HIP device";
+    case TW_ERR_HIP: return "HIP runtime error";
+    case TW_ERR_OOM: return "device out of memory";
+    case TW_ERR_STATE: return "call out of order";
+    case TW_ERR_REPLICA: return "replica error";
+    default: return "unknown error";
+    }
+}
+
+int tw_create(int device, tw_ctx** out) {
+    if (!out) return TW_ERR_INVALID;
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0 || device < 0 || device >= n) return TW_ERR_NO_DEVICE;
+    tw_ctx* c = new (std::nothrow) tw_ctx;
+    if (!c) return TW_ERR_OOM;
+    c->device = device;
+    if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipHostMalloc((void**)&c->h_active, sizeof(uint32_t)) != hipSuccess) {
+        delete c;
+        return TW_ERR_HIP;
+    }
+    *out = c;
+    return TW_OK;
+}
+
+void tw_destroy(tw_ctx* c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    free_all(c);
+    for (hipEvent_t e : c->ev_pool) (void)hipEventDestroy(e);
+    if (c->h_active) (void)hipHostFree(c->h_active);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+}
+
+static int validate(const tw_scenario_desc* s) {
+    if (!s || s->abi_version != TW_ABI_VERSION) return TW_ERR_INVALID;
+    if (s->n_replicas == 0 || s->n_nodes == 0 || !s->insns || s->n_insns < TW_PC_USER || s->n_insns > 0xFFFF)
+        return TW_ERR_INVALID;
+    if (s->max_slots < 1 || s->queue_capacity < 1 || s->link_depth < 1 || !s->out_off) return TW_ERR_INVALID;
+    if (s->main_pc >= s->n_insns || s->main_node >= s->n_nodes || s->max_timeouts > 65536) return TW_ERR_INVALID;
+    if (s->n_links && (!s->link_dst || !s->link_rev)) return TW_ERR_INVALID;
+    if (s->n_listener_sets && (!s->listener_pc || !s->n_msg_kinds)) return TW_ERR_INVALID;
+    // fixed stubs
+    const uint32_t stub_ops[6] = {TW_OP_WAIT_REG, TW_OP_DELIVER, TW_OP_END, TW_OP_WAIT_REG, TW_OP_TMO_FIRE, TW_OP_END};
+    for (int i = 0; i < 6; ++i)
+        if ((s->insns[i].w0 & 0xFF) != stub_ops[i]) return TW_ERR_INVALID;
+    for (uint32_t l = 0; l < s->n_links; ++l)
+        if (s->link_dst[l] >= s->n_nodes) return TW_ERR_INVALID;
+    if (s->out_off[s->n_nodes] != s->n_links) return TW_ERR_INVALID;
+    return TW_OK;
+}
+
+int tw_load(tw_ctx* c, const tw_scenario_desc* s) {
+    if (!c) return TW_ERR_INVALID;
+    int v = validate(s);
+    if (v) return v;
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    free_all(c);
+    Dev& d = c->d;
+    d = Dev{};
+    d.R = s->n_replicas; d.S = s->max_slots; d.Q = s->queue_capacity; d.N = s->n_nodes;
+    d.L = s->n_links; d.D = s->link_depth; d.T = s->max_timeouts;
+    d.n_insns = s->n_insns; d.n_consts = s->n_consts; d.n_sets = s->n_listener_sets; d.n_kinds = s->n_msg_kinds;
+    d.horizon = s->near_horizon_us;
+    const size_t R = d.R;
+    int e;
+#define ALLOC(p, n) if ((e = dalloc(c, &p, (n))) != TW_OK) { free_all(c); return e; }
+    uint2* insns; int64_t* consts; uint32_t *lpc, *out_off, *ldst, *lrev, *ltab = nullptr;
+    ALLOC(insns, d.n_insns);
+    ALLOC(consts, d.n_consts);
+    ALLOC(lpc, (size_t)d.n_sets * d.n_kinds);
+    ALLOC(out_off, (size_t)d.N + 1);
+    ALLOC(ldst, d.L);
+    ALLOC(lrev, d.L);
+    if (s->link_table) ALLOC(ltab, (size_t)d.L * d.D * R);
+    ALLOC(d.scal, (size_t)SC_COUNT * R);
+    ALLOC(d.slots, (size_t)d.S * R * 4);
+    ALLOC(d.free_stk, (size_t)d.S * R);
+    ALLOC(d.far, (size_t)d.Q * R);
+    ALLOC(d.near_spill, (size_t)TW_NEAR_CAP * R);
+    ALLOC(d.nvars, (size_t)d.N * 4 * R);
+    ALLOC(d.hash, (size_t)d.N * R);
+    ALLOC(d.bind, (size_t)d.N * R);
+    ALLOC(d.bind_own, (size_t)d.N * R);
+    ALLOC(d.link_ord, (size_t)(d.L ? d.L : 1) * R);
+    ALLOC(d.tmo_done, (size_t)(d.T ? d.T : 1) * R);
+    ALLOC(d.n_active, 1);
+    int64_t *mregs = nullptr, *nvi = nullptr;
+    if (s->main_regs) ALLOC(mregs, R * 4);
+    if (s->node_vars) ALLOC(nvi, (size_t)d.N * 4);
+#undef ALLOC
+    hipStream_t st = c->stream;
+    HIPCHK(hipMemcpyAsync(insns, s->insns, sizeof(tw_insn) * d.n_insns, hipMemcpyHostToDevice, st));
+    if (d.n_consts) HIPCHK(hipMemcpyAsync(consts, s->consts, 8 * d.n_consts, hipMemcpyHostToDevice, st));
+    if (d.n_sets) HIPCHK(hipMemcpyAsync(lpc, s->listener_pc, 4ull * d.n_sets * d.n_kinds, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(out_off, s->out_off, 4ull * (d.N + 1), hipMemcpyHostToDevice, st));
+    if (d.L) {
+        HIPCHK(hipMemcpyAsync(ldst, s->link_dst, 4ull * d.L, hipMemcpyHostToDevice, st));
+        HIPCHK(hipMemcpyAsync(lrev, s->link_rev, 4ull * d.L, hipMemcpyHostToDevice, st));
+    }
+    if (ltab) HIPCHK(hipMemcpyAsync(ltab, s->link_table, 4ull * d.L * d.D * R, hipMemcpyHostToDevice, st));
+    if (mregs) HIPCHK(hipMemcpyAsync(mregs, s->main_regs, 32ull * R, hipMemcpyHostToDevice, st));
+    if (nvi) HIPCHK(hipMemcpyAsync(nvi, s->node_vars, 32ull * d.N, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemsetAsync(d.nvars, 0, 32ull * d.N * R, st));
+    HIPCHK(hipMemsetAsync(d.hash, 0, 8ull * d.N * R, st));
+    HIPCHK(hipMemsetAsync(d.bind, 0, 4ull * d.N * R, st));
+    HIPCHK(hipMemsetAsync(d.link_ord, 0, 4ull * (d.L ? d.L : 1) * R, st));
+    HIPCHK(hipMemsetAsync(d.tmo_done, 0, (size_t)(d.T ? d.T : 1) * R, st));
+    d.insns = insns; d.consts = consts; d.lpc = lpc; d.out_off = out_off; d.link_dst = ldst; d.link_rev = lrev;
+    d.link_table = ltab;
+    uint32_t blocks = (uint32_t)((R + TW_BLOCK - 1) / TW_BLOCK);
+    hipLaunchKernelGGL(tw_init_kernel, dim3(blocks), dim3(TW_BLOCK), 0, st, d, s->main_pc, s->main_node,
+                       (const int64_t*)mregs, (const int64_t*)nvi);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(st));
+    c->loaded = true;
+    return TW_OK;
+}
+
+int tw_run(tw_ctx* c, int64_t t_end_us, uint64_t max_events, tw_stats* out) {
+    if (!c) return TW_ERR_INVALID;
+    if (!c->loaded) return TW_ERR_STATE;
+    auto w0 = std::chrono::steady_clock::now();
+    HIPCHK(hipSetDevice(c->device));
+    hipStream_t st = c->stream;
+    const Dev& d = c->d;
+    uint32_t blocks = (d.R + TW_BLOCK - 1) / TW_BLOCK;
+    // events before this call (to report per-call deltas)
+    std::vector<uint64_t> ev0(d.R);
+    HIPCHK(hipMemcpyAsync(ev0.data(), d.scal + (size_t)SC_EVENTS * d.R, 8ull * d.R, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    const uint64_t limit = max_events;  // cumulative per-replica cap
+    c->launch_ms.clear();
+    const uint32_t budget = 1u << 14;  // pops per lane per launch: bounded kernel time
+    const int per_check = 4;           // launches between host checks
+    uint32_t launches = 0;
+    double kms = 0.0;
+    for (int round = 0; round < (1 << 20); ++round) {
+        size_t need = 2 * per_check;
+        while (c->ev_pool.size() < need) {
+            hipEvent_t e;
+            HIPCHK(hipEventCreate(&e));
+            c->ev_pool.push_back(e);
+        }
+        for (int i = 0; i < per_check; ++i) {
+            HIPCHK(hipMemsetAsync(d.n_active, 0, 4, st));
+            HIPCHK(hipEventRecord(c->ev_pool[2 * i], st));
+            hipLaunchKernelGGL(tw_run_kernel, dim3(blocks), dim3(TW_BLOCK), 0, st, d, t_end_us, limit, budget);
+            HIPCHK(hipGetLastError());
+            HIPCHK(hipEventRecord(c->ev_pool[2 * i + 1], st));
+            ++launches;
+        }
+        HIPCHK(hipMemcpyAsync(c->h_active, d.n_active, 4, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+        for (int i = 0; i < per_check; ++i) {
+            float ms = 0.f;
+            HIPCHK(hipEventElapsedTime(&ms, c->ev_pool[2 * i], c->ev_pool[2 * i + 1]));
+            c->launch_ms.push_back(ms);
+            kms += ms;
+        }
+        if (*c->h_active == 0) break;
+    }
+    if (out) {
+        std::memset(out, 0, sizeof(*out));
+        std::vector<tw_replica_result> rr(d.R);
+        int rc = tw_read_results(c, rr.data(), d.R);
+        if (rc) return rc;
+        for (uint32_t i = 0; i < d.R; ++i) {
+            out->events += rr[i].events - ev0[i];
+            out->delivered += rr[i].delivered;
+            out->dropped += rr[i].dropped;
+            out->undeliverable += rr[i].undeliverable;
+            if (rr[i].final_t > out->max_final_t) out->max_final_t = rr[i].final_t;
+            if (rr[i].status == TW_REP_DONE) ++out->replicas_done;
+            if (rr[i].status >= TW_REP_ERR_SLOTS) ++out->replicas_error;
+        }
+        out->sends = out->delivered + out->dropped + out->undeliverable;
+        out->launches = launches;
+        out->kernel_ms = kms;
+        out->wall_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - w0).count();
+    }
+    return TW_OK;
+}
+
+int tw_read_results(tw_ctx* c, tw_replica_result* out, size_t n) {
+    if (!c || !out) return TW_ERR_INVALID;
+    if (!c->loaded) return TW_ERR_STATE;
+    const Dev& d = c->d;
+    if (n < d.R) return TW_ERR_INVALID;
+    HIPCHK(hipSetDevice(c->device));
+    std::vector<uint64_t> sc((size_t)SC_COUNT * d.R);
+    HIPCHK(hipMemcpyAsync(sc.data(), d.scal, 8ull * SC_COUNT * d.R, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    auto F = [&](int f, uint32_t i) { return sc[(size_t)f * d.R + i]; };
+    for (uint32_t i = 0; i < d.R; ++i) {
+        out[i].final_t = (int64_t)F(SC_FINAL_T, i); out[i].events = F(SC_EVENTS, i);
+        out[i].delivered = F(SC_DELIVERED, i); out[i].dropped = F(SC_DROPPED, i);
+        out[i].undeliverable = F(SC_UNDELIV, i); out[i].status = (uint32_t)F(SC_STATUS, i);
+        out[i].main_exc = (uint32_t)F(SC_MAIN_EXC, i); out[i].threads = F(SC_THREADS, i);
+    }
+    return TW_OK;
+}
+
+int tw_read_hashes(tw_ctx* c, uint64_t* out, size_t n) {
+    if (!c || !out) return TW_ERR_INVALID;
+    if (!c->loaded) return TW_ERR_STATE;
+    const Dev& d = c->d;
+    if (n < (size_t)d.R * d.N) return TW_ERR_INVALID;
+    HIPCHK(hipSetDevice(c->device));
+    std::vector<uint64_t> tmp((size_t)d.R * d.N);  // device layout [node][replica]
+    HIPCHK(hipMemcpyAsync(tmp.data(), d.hash, 8ull * d.R * d.N, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    for (uint32_t node = 0; node < d.N; ++node)
+        for (uint32_t r = 0; r < d.R; ++r) out[(size_t)r * d.N + node] = tmp[(size_t)node * d.R + r];
+    return TW_OK;
+}
+
+int tw_read_final(tw_ctx* c, int64_t* max_final_t, uint64_t* delivered, uint64_t* dropped, uint64_t* events) {
+    if (!c) return TW_ERR_INVALID;
+    if (!c->loaded) return TW_ERR_STATE;
+    std::vector<tw_replica_result> rr(c->d.R);
+    int rc = tw_read_results(c, rr.data(), rr.size());
+    if (rc) return rc;
+    int64_t ft = 0;
+    uint64_t dl = 0, dr = 0, ev = 0;
+    for (auto& x : rr) {
+        ft = x.final_t > ft ? x.final_t : ft;
+        dl += x.delivered; dr += x.dropped; ev += x.events;
+    }
+    if (max_final_t) *max_final_t = ft;
+    if (delivered) *delivered = dl;
+    if (dropped) *dropped = dr;
+    if (events) *events = ev;
+    return TW_OK;
+}
+
+int tw_last_launch_ms(tw_ctx* c, double* out, size_t cap) {
+    if (!c || !out) return TW_ERR_INVALID;
+    size_t n = c->launch_ms.size() < cap ? c->launch_ms.size() : cap;
+    for (size_t i = 0; i < n; ++i) out[i] = c->launch_ms[i];
+    return (int)n;
+}
+
+}  // extern "C"

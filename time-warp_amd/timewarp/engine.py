@@ -1,0 +1,147 @@
+"""Host binding of libtimewarp.so (the HIP engine) — the product path.
+
+``Engine`` mirrors the reference runner ``runTimedT`` (TimedT.hs:293-304) for a
+batch of replicas: ``load`` = build the TimedT value + ``emptyScenario``,
+``run`` = ``launchTimedT`` to quiescence, results = final virtual time,
+counters and per-node trace hashes.  Calls go through the C ABI of
+include/timewarp.h with plain pointers (ctypes); there is no CPU fallback —
+if the library or a GPU is missing this raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from dataclasses import dataclass
+from typing import Optional
+
+import numpy as np
+
+from .abi import RESULT_DTYPE, TwStats
+from .scenario import Scenario
+
+_PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(_PKG_ROOT, "lib", "libtimewarp.so")
+UNLIMITED = (1 << 64) - 1
+T_INF = (1 << 63) - 1
+
+EXPORTS = ["tw_create", "tw_load", "tw_run", "tw_read_results", "tw_read_hashes", "tw_read_final",
+           "tw_last_launch_ms", "tw_destroy", "tw_strerror", "tw_version"]
+
+
+class EngineError(RuntimeError):
+    pass
+
+
+_lib = None
+
+
+def load_library(path: Optional[str] = None):
+    """dlopen libtimewarp.so and declare the C signatures (no device call)."""
+    global _lib
+    if _lib is not None and path is None:
+        return _lib
+    p = path or LIB_PATH
+    if not os.path.exists(p):
+        raise EngineError(f"HIP engine library missing: {p} (run __graft_entry__.build())")
+    lib = C.CDLL(p)
+    lib.tw_create.argtypes = [C.c_int, C.POINTER(C.c_void_p)]
+    lib.tw_load.argtypes = [C.c_void_p, C.c_void_p]
+    lib.tw_run.argtypes = [C.c_void_p, C.c_int64, C.c_uint64, C.POINTER(TwStats)]
+    lib.tw_read_results.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t]
+    lib.tw_read_hashes.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t]
+    lib.tw_read_final.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
+    lib.tw_last_launch_ms.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t]
+    lib.tw_destroy.argtypes = [C.c_void_p]
+    lib.tw_strerror.argtypes = [C.c_int]
+    lib.tw_strerror.restype = C.c_char_p
+    lib.tw_version.restype = C.c_char_p
+    for name in ("tw_create", "tw_load", "tw_run", "tw_read_results", "tw_read_hashes", "tw_read_final",
+                 "tw_last_launch_ms"):
+        getattr(lib, name).restype = C.c_int
+    if path is None:
+        _lib = lib
+    return lib
+
+
+def _check(rc: int, what: str):
+    if rc < 0:
+        msg = load_library().tw_strerror(rc).decode()
+        raise EngineError(f"{what} failed: {rc} ({msg})")
+
+
+@dataclass
+class RunStats:
+    events: int
+    sends: int
+    delivered: int
+    dropped: int
+    undeliverable: int
+    max_final_t: int
+    replicas_done: int
+    replicas_error: int
+    launches: int
+    kernel_ms: float
+    wall_ms: float
+
+
+class Engine:
+    """A tw_ctx on one GPU holding one loaded scenario."""
+
+    def __init__(self, device: int = 0):
+        self.lib = load_library()
+        ctx = C.c_void_p()
+        _check(self.lib.tw_create(device, C.byref(ctx)), "tw_create")
+        self.ctx = ctx
+        self.scn: Optional[Scenario] = None
+
+    def close(self):
+        if self.ctx:
+            self.lib.tw_destroy(self.ctx)
+            self.ctx = C.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def load(self, scn: Scenario) -> "Engine":
+        d = scn.desc()
+        _check(self.lib.tw_load(self.ctx, C.addressof(d)), "tw_load")
+        self.scn = scn
+        return self
+
+    def run(self, t_end: int = T_INF, max_events: int = UNLIMITED) -> RunStats:
+        st = TwStats()
+        _check(self.lib.tw_run(self.ctx, t_end, max_events, C.byref(st)), "tw_run")
+        return RunStats(**{f: getattr(st, f) for f, _ in TwStats._fields_ if f != "reserved"})
+
+    def results(self) -> np.ndarray:
+        out = np.zeros(self.scn.n_replicas, RESULT_DTYPE)
+        _check(self.lib.tw_read_results(self.ctx, out.ctypes.data, out.shape[0]), "tw_read_results")
+        return out
+
+    def hashes(self) -> np.ndarray:
+        out = np.zeros((self.scn.n_replicas, self.scn.n_nodes), np.uint64)
+        _check(self.lib.tw_read_hashes(self.ctx, out.ctypes.data, out.size), "tw_read_hashes")
+        return out
+
+    def launch_ms(self) -> np.ndarray:
+        buf = np.zeros(1 << 16, np.float64)
+        n = self.lib.tw_last_launch_ms(self.ctx, buf.ctypes.data, buf.shape[0])
+        _check(n, "tw_last_launch_ms")
+        return buf[:n].copy()
+
+
+def run_scenario(scn: Scenario, device: int = 0, t_end: int = T_INF, max_events: int = UNLIMITED):
+    """Load + run to quiescence; returns (stats, results, hashes)."""
+    with Engine(device) as e:
+        e.load(scn)
+        st = e.run(t_end, max_events)
+        return st, e.results(), e.hashes()

@@ -1,0 +1,374 @@
+"""Lowering of MonadTimed / MonadDialog scenarios to thread programs.
+
+A scenario of the reference is Haskell code polymorphic in ``m`` under
+``MonadTimed``/``MonadDialog`` constraints (e.g. ``WorkMode``,
+examples/token-ring/Main.hs:93-98).  Here the same scenario is written as
+per-node handler state machines against a small assembler whose methods keep
+the reference's names and meaning:
+
+===============================  ==============================================
+reference (file:line)            lowering
+===============================  ==============================================
+``wait (for t)`` / ``till``      ``Code.wait(for_(t))`` -> WAIT_REL / WAIT_ABS
+  (MonadTimed.hs:125, TimedT.hs:343-355)
+``fork act`` (TimedT.hs:326-342) ``Code.fork(entry, ref=r)`` -> FORK (+1 µs)
+``fork_``  (MonadTimed.hs:194)   ``Code.fork_(entry)``
+``schedule t act`` (:162-163)    ``Code.schedule(t, entry)`` = fork_ of a stub
+                                 ``wait t; jmp entry``
+``invoke t act`` (:182-183)      ``Code.invoke(t)`` = wait
+``work t act`` (:201-202)        ``Code.work(t, entry)``
+``killThread`` (:205-206)        ``Code.kill_thread(ref)``
+``throwTo`` (TimedT.hs:357-368)  ``Code.throw_to(ref, exc, val)``
+``throwM`` / ``catch``           ``Code.throw`` / ``Code.catch_(mask, handler)``
+``timeout t act`` (:370-376)     ``Code.timeout_begin(t)`` ... ``timeout_end()``
+``virtualTime`` / ``myThreadId`` ``Code.now(r)`` / ``Code.my_thread_id(r)``
+``send addr msg`` (MonadDialog.hs:154-156)  ``Code.send(link, kind, payload)``
+``listen (AtPort p) [..]`` (:204-211)       ``Code.listen(set)``
+``reply`` (:177-180)             ``Code.reply_link(r, r_in)`` + ``send``
+===============================  ==============================================
+
+Registers r0..r3 are per-thread int64 and are copied into forked children
+(the closure a forked action captures).  A thread ref (``fork``'s result) is an
+opaque register value usable only by throw_to / kill_thread.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+from typing import Callable, Dict, List, Optional, Union
+
+import numpy as np
+
+from . import isa
+from .timeunits import TimeSpec
+
+
+class Label:
+    __slots__ = ("name", "pc")
+
+    def __init__(self, name: str):
+        self.name = name
+        self.pc: Optional[int] = None
+
+    def __repr__(self):
+        return f"Label({self.name}@{self.pc})"
+
+
+Imm = Union[int, Label]
+
+
+def _enc(op: int, a: int = 0, b: int = 0) -> int:
+    return (op & 0xFF) | ((a & 0xFF) << 8) | ((b & 0xFFFF) << 16)
+
+
+class Program:
+    """Program image: insns + constant pool + listener sets + message kinds."""
+
+    def __init__(self):
+        self._insns: List[list] = []
+        self.consts: List[int] = []
+        self._cidx: Dict[int, int] = {}
+        self._labels: Dict[str, Label] = {}
+        self._deferred: List[Callable[[], None]] = []
+        self.msg_kinds: Dict[str, int] = {}
+        self.listener_sets: List[Dict[int, Label]] = []
+        self._nfresh = 0
+        # fixed stubs (include/timewarp.h TW_PC_*): deliverer and timeout watchdog
+        self._emit(isa.OP_WAIT_REG, 2)
+        self._emit(isa.OP_DELIVER)
+        self._emit(isa.OP_END)
+        self._emit(isa.OP_WAIT_REG, 2)
+        self._emit(isa.OP_TMO_FIRE)
+        self._emit(isa.OP_END)
+        assert self.pc == isa.PC_USER
+
+    # ---------------------------------------------------------------- basics
+    @property
+    def pc(self) -> int:
+        return len(self._insns)
+
+    def _emit(self, op: int, a: int = 0, b: int = 0, imm: Imm = 0) -> None:
+        self._insns.append([_enc(op, a, b), imm])
+
+    def const(self, v: int) -> int:
+        v = int(v)
+        if v not in self._cidx:
+            self._cidx[v] = len(self.consts)
+            self.consts.append(v)
+        return self._cidx[v]
+
+    def label(self, name: Optional[str] = None) -> Label:
+        if name is None:
+            self._nfresh += 1
+            name = f"_L{self._nfresh}"
+        if name in self._labels:
+            return self._labels[name]
+        lab = Label(name)
+        self._labels[name] = lab
+        return lab
+
+    def bind(self, lab: Label) -> Label:
+        if lab.pc is not None:
+            raise ValueError(f"label {lab.name} bound twice")
+        lab.pc = self.pc
+        return lab
+
+    def function(self, name: str) -> "Code":
+        """Start a code block at a (new or forward-declared) label."""
+        self.bind(self.label(name))
+        return Code(self)
+
+    def kind(self, name: str) -> int:
+        """Message kind id (the reference dispatches by message name, MonadDialog.hs:240)."""
+        if name not in self.msg_kinds:
+            self.msg_kinds[name] = len(self.msg_kinds)
+        return self.msg_kinds[name]
+
+    def listener_set(self, listeners: Dict[str, Union[str, Label]]) -> int:
+        """A `listen` binding's listener list: message name -> handler entry."""
+        s = {self.kind(k): (v if isinstance(v, Label) else self.label(v)) for k, v in listeners.items()}
+        self.listener_sets.append(s)
+        return len(self.listener_sets) - 1
+
+    def defer(self, fn: Callable[[], None]) -> None:
+        self._deferred.append(fn)
+
+    # -------------------------------------------------------------- finalize
+    def finalize(self):
+        while self._deferred:
+            fns, self._deferred = self._deferred, []
+            for fn in fns:
+                fn()
+        insns = np.zeros((len(self._insns), 2), dtype=np.uint32)
+        for i, (w0, imm) in enumerate(self._insns):
+            if isinstance(imm, Label):
+                if imm.pc is None:
+                    raise ValueError(f"unbound label {imm.name}")
+                imm = imm.pc
+            insns[i, 0] = w0
+            insns[i, 1] = np.uint32(int(imm) & 0xFFFFFFFF)
+        nk = max(1, len(self.msg_kinds))
+        ls = np.full((max(1, len(self.listener_sets)), nk), isa.PC_NONE, dtype=np.uint32)
+        for si, s in enumerate(self.listener_sets):
+            for k, lab in s.items():
+                if lab.pc is None:
+                    raise ValueError(f"unbound listener {lab.name}")
+                ls[si, k] = lab.pc
+        consts = np.array(self.consts if self.consts else [0], dtype=np.int64)
+        return Image(insns=insns, consts=consts, listener_pc=ls, n_msg_kinds=nk,
+                     n_listener_sets=len(self.listener_sets), labels=dict(self._labels))
+
+
+@dataclass
+class Image:
+    insns: np.ndarray          # [n, 2] uint32 (w0, imm)
+    consts: np.ndarray         # int64
+    listener_pc: np.ndarray    # [sets, kinds] uint32
+    n_msg_kinds: int
+    n_listener_sets: int
+    labels: Dict[str, Label] = field(default_factory=dict)
+
+    def pc_of(self, name: str) -> int:
+        return self.labels[name].pc
+
+
+class Code:
+    """Emitter for one code block (MonadTimed/MonadDialog vocabulary)."""
+
+    def __init__(self, prog: Program):
+        self.p = prog
+
+    def _e(self, op, a=0, b=0, imm: Imm = 0):
+        self.p._emit(op, a, b, imm)
+        return self
+
+    def _lab(self, x) -> Label:
+        return x if isinstance(x, Label) else self.p.label(x)
+
+    # ------------------------------------------------------------ control
+    def label(self, name=None) -> Label:
+        return self.p.label(name)
+
+    def bind(self, lab) -> Label:
+        return self.p.bind(self._lab(lab))
+
+    def here(self, name=None) -> Label:
+        return self.p.bind(self.p.label(name))
+
+    def jmp(self, target):
+        return self._e(isa.OP_JMP, imm=self._lab(target))
+
+    def end(self):
+        return self._e(isa.OP_END)
+
+    # ------------------------------------------------------------- timing
+    def wait(self, spec: TimeSpec):
+        """``wait`` (TimedT.hs:343-355)."""
+        if spec.relative:
+            return self._e(isa.OP_WAIT_REL, imm=self.p.const(spec.us))
+        return self._e(isa.OP_WAIT_ABS, imm=self.p.const(spec.us))
+
+    def wait_reg(self, r: int):
+        return self._e(isa.OP_WAIT_REG, r)
+
+    invoke = wait  # invoke t act = wait t >> act (MonadTimed.hs:182-183)
+
+    def sleep_forever(self):
+        """``sleepForever = forever (wait (for 100500 minute))`` (Misc.hs:50-51)."""
+        top = self.here()
+        self._e(isa.OP_WAIT_REL, imm=self.p.const(100500 * 60_000_000))
+        return self.jmp(top)
+
+    def now(self, r: int):
+        return self._e(isa.OP_NOW, r)
+
+    # ------------------------------------------------------------ threads
+    def fork(self, entry, ref: int = 0, node_reg: Optional[int] = None):
+        """``fork`` (TimedT.hs:326-342); child gets a copy of r0..r3."""
+        b = 0xFFFF if node_reg is None else node_reg
+        return self._e(isa.OP_FORK, ref, b, self._lab(entry))
+
+    def fork_(self, entry, node_reg: Optional[int] = None, scratch: int = 3):
+        return self.fork(entry, ref=scratch, node_reg=node_reg)
+
+    def schedule(self, spec: TimeSpec, entry, scratch: int = 3):
+        """``schedule t act = fork_ (invoke t act)`` (MonadTimed.hs:162-163)."""
+        stub = self.p.label()
+        target = self._lab(entry)
+
+        def emit():
+            self.p.bind(stub)
+            c = Code(self.p)
+            c.wait(spec)
+            c.jmp(target)
+
+        self.p.defer(emit)
+        return self.fork_(stub, scratch=scratch)
+
+    def work(self, spec: TimeSpec, entry, ref: int = 2):
+        """``work rel act = fork act >>= schedule rel . killThread`` (MonadTimed.hs:201-202)."""
+        self.fork(entry, ref=ref)
+        killer = self.p.label()
+
+        def emit():
+            self.p.bind(killer)
+            c = Code(self.p)
+            c.kill_thread(ref)
+            c.end()
+
+        self.p.defer(emit)
+        return self.schedule(spec, killer, scratch=3 if ref != 3 else 1)
+
+    def my_thread_id(self, r: int):
+        return self._e(isa.OP_MYTID, r)
+
+    def throw_to(self, ref: int, exc: int, val_reg: int = 0):
+        """``throwTo`` (TimedT.hs:357-368): target woken to now, first exception wins."""
+        return self._e(isa.OP_THROW_TO, ref, (exc & 0xFF) | ((val_reg & 3) << 8))
+
+    def kill_thread(self, ref: int):
+        """``killThread = flip throwTo ThreadKilled`` (MonadTimed.hs:205-206)."""
+        return self.throw_to(ref, isa.EXC_THREAD_KILLED)
+
+    def throw(self, exc: int, val_reg: int = 0):
+        """``throwM`` in the current thread."""
+        return self._e(isa.OP_THROW, 0, (exc & 0xFF) | ((val_reg & 3) << 8))
+
+    def catch_(self, mask: int, handler):
+        """Enter ``act `catch` handler``; handler runs outside the frame with
+        r0 = exception value, r3 = exception code (TimedT.hs:183-204)."""
+        return self._e(isa.OP_CATCH, 0, mask, self._lab(handler))
+
+    def uncatch(self):
+        return self._e(isa.OP_UNCATCH)
+
+    def timeout_begin(self, t_us: int, epoch_reg: int = 3):
+        """``timeout t act`` (TimedT.hs:370-376): schedule the watchdog (a fork,
+        +1 µs), then enter ``act `finally` done := True``."""
+        self._e(isa.OP_TMO_BEGIN, epoch_reg, 0, self.p.const(t_us))
+        return self._e(isa.OP_TMO_PUSH, epoch_reg)
+
+    def timeout_end(self):
+        return self._e(isa.OP_TMO_END)
+
+    # ----------------------------------------------------------- registers
+    def seti(self, r: int, v: int):
+        if -(1 << 31) <= v < (1 << 31):
+            return self._e(isa.OP_SETI, r, 0, v)
+        return self._e(isa.OP_SETK, r, 0, self.p.const(v))
+
+    def addi(self, r: int, v: int):
+        return self._e(isa.OP_ADDI, r, 0, v)
+
+    def muli(self, r: int, v: int):
+        return self._e(isa.OP_MULI, r, 0, v)
+
+    def modi(self, r: int, v: int):
+        return self._e(isa.OP_MODI, r, 0, v)
+
+    def mov(self, r: int, s: int):
+        return self._e(isa.OP_MOV, r, s)
+
+    def add(self, r: int, s: int):
+        return self._e(isa.OP_ADD, r, s)
+
+    def sub(self, r: int, s: int):
+        return self._e(isa.OP_SUB, r, s)
+
+    def jeq(self, r, s, target):
+        return self._e(isa.OP_JEQ, r, s, self._lab(target))
+
+    def jne(self, r, s, target):
+        return self._e(isa.OP_JNE, r, s, self._lab(target))
+
+    def jlt(self, r, s, target):
+        return self._e(isa.OP_JLT, r, s, self._lab(target))
+
+    def jle(self, r, s, target):
+        return self._e(isa.OP_JLE, r, s, self._lab(target))
+
+    def jeqi(self, r, v, target):
+        return self._e(isa.OP_JEQI, r, v & 0xFFFF, self._lab(target))
+
+    def jnei(self, r, v, target):
+        return self._e(isa.OP_JNEI, r, v & 0xFFFF, self._lab(target))
+
+    def node(self, r: int):
+        return self._e(isa.OP_NODE, r)
+
+    def nload(self, r: int, var: int):
+        return self._e(isa.OP_NLOAD, r, var)
+
+    def nstore(self, r: int, var: int):
+        return self._e(isa.OP_NSTORE, r, var)
+
+    def nloadx(self, r: int, var: int, node_reg: int):
+        return self._e(isa.OP_NLOADX, r, (var & 0xFF) | ((node_reg & 3) << 8))
+
+    def nstorex(self, r: int, var: int, node_reg: int):
+        return self._e(isa.OP_NSTOREX, r, (var & 0xFF) | ((node_reg & 3) << 8))
+
+    def trace(self, tag: int, r: int = 0):
+        """Checkpoint / logMeasure-style trace record into the node hash."""
+        return self._e(isa.OP_TRACE, r, 0, tag)
+
+    # ------------------------------------------------------------ network
+    def link(self, r: int, k: int):
+        """r = id of this node's k-th outgoing link (the NetworkAddress)."""
+        return self._e(isa.OP_LINK, r, 0, k)
+
+    def reply_link(self, r: int, r_in: int = 1):
+        """Link back to the peer of an incoming message (``reply``, MonadDialog.hs:177)."""
+        return self._e(isa.OP_RLINK, r, r_in)
+
+    def send(self, link_reg: int, kind: Union[str, int], payload_reg: int = 0):
+        """``send`` (MonadDialog.hs:154-156) over the emulated transfer:
+        dropped -> nothing; else ``schedule (after d) (deliver ..)``."""
+        k = self.p.kind(kind) if isinstance(kind, str) else kind
+        return self._e(isa.OP_SEND, link_reg, (k & 0xFF) | ((payload_reg & 3) << 8))
+
+    def listen(self, lset: int, owned: bool = False):
+        """``listen (AtPort ..)`` (MonadDialog.hs:204-211): bind this node's port."""
+        return self._e(isa.OP_LISTEN, 0, 1 if owned else 0, lset)
+
+    def unlisten(self):
+        return self._e(isa.OP_UNLISTEN)

@@ -1,0 +1,310 @@
+"""Scenario builders for the BASELINE.json configs, lowered to thread programs.
+
+Each builder restates a reference scenario as per-node handler state machines
+(see program.py for the API mapping) and draws its link tables host-side from
+random-1.1 StdGen (stdgen.py), one generator per replica, so every trace is
+deterministic.
+
+  token_ring  — examples/token-ring/Main.hs (configs 1 and 3)
+  ping_pong   — examples/ping-pong/Main.hs re-hosted on emulation (config 2)
+  hotspot     — bench/Network Sender/Receiver request/response (config 5)
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from . import isa
+from .program import Program
+from .scenario import Scenario, Topology
+from .stdgen import StdGenVec
+from .timeunits import after, at, for_, ms, sec
+
+# trace tags (logInfo / logError / logMeasure points of the reference scenarios)
+TAG_CREATE_TOKEN = 1     # token-ring/Main.hs:134  "Creating token"
+TAG_GOT_TOKEN = 2        # token-ring/Main.hs:138  "Got token with value"
+TAG_NOTE = 3             # token-ring/Main.hs:200-204 noteTokenMethod
+TAG_WRONG_VALUE = 4      # token-ring/Main.hs:206-208 "Wrong token value"
+TAG_NO_PROGRESS = 5      # token-ring/Main.hs:184-187 "Token value hasn't changed"
+TAG_PING = 6             # ping-pong/Main.hs:73-75  "Get Ping"; bench PingReceived
+TAG_PONG = 7             # ping-pong/Main.hs:64-66  "Get Pong"; bench PongReceived
+TAG_PING_SENT = 8        # bench/Network/Sender/Main.hs:60 logMeasure PingSent
+
+EXC_VALUE_RECEIVED = isa.EXC_USER0  # data SignalException = ValueReceived Int (token-ring/Main.hs:156)
+
+
+def _capped(n: int) -> int:
+    return int(min(n, 0xFFFFFFFF))
+
+
+# --------------------------------------------------------------- token ring
+def token_ring(n_nodes: int = 16, n_replicas: int = 1, launch_duration: int = sec(20),
+               token_passing_delay: int = sec(3), allowed_progress_delay: int = sec(5),
+               network_delay=(ms(1), ms(5)), drop_log2: int = 0, seed_base: int = 0,
+               link_depth: int = 1, near_horizon_us: int = sec(10)) -> Scenario:
+    """examples/token-ring/Main.hs lowered.
+
+    Node ids: ring nodes 0..N-1 are the reference's ``no = 1..N``
+    (nodePort = 2000+no, :87-88), node N is the observer (port 5000, :163-164),
+    node N+1 hosts the main thread.  Out-links: ring node i -> [(i+1) mod N,
+    observer].  ``call`` (MonadRpc, absent) is lowered to a one-way send.
+    Delays (:73-77): observer links ConnectedIn 0; ring links U[1 ms, 5 ms];
+    optional drop with probability 2^-drop_log2 per send (config 3 nastiness).
+    """
+    N = int(n_nodes)
+    OBS, SYS = N, N + 1
+    p = Program()
+    K_TOKEN, K_NOTE = p.kind("token"), p.kind("noteToken")
+    ring_set = p.listener_set({"token": "accept_token"})
+    obs_set = p.listener_set({"noteToken": "note_token"})
+
+    # scenario (main thread), :63-72
+    c = p.function("main")
+    c.seti(0, 0).seti(2, N)
+    loop = c.here()
+    c.fork("launch_node", ref=1, node_reg=0)          # fork $ launchNode no
+    c.addi(0, 1).jlt(0, 2, loop)
+    c.seti(0, OBS)
+    c.fork_("launch_observer", node_reg=0)            # fork_ launchObserver
+    c.end()
+
+    # launchNode no, :104-135
+    c = p.function("launch_node")
+    c.fork("worker", ref=1)                           # wtid <- fork worker
+    c.nstore(1, 0)                                    # (acceptToken closes over wtid)
+    c.fork("server", ref=2)                           # stid <- fork server
+    c.schedule(at(launch_duration), "kill_pair")      # schedule (at launchDuration) kill
+    c.node(0)
+    done = c.label()
+    c.jnei(0, 0, done)                                # when (no == 1)
+    c.invoke(after(sec(1)))                           # invoke (after 1 sec)
+    c.trace(TAG_CREATE_TOKEN, 0)
+    c.seti(0, 1)
+    c.link(1, 0).send(1, K_TOKEN, 0)                  # initPassingToken 1
+    c.bind(done)
+    c.end()
+
+    c = p.function("kill_pair")                       # mapM_ killThread [r1, r2]
+    c.kill_thread(1).kill_thread(2).end()
+
+    # worker: forever $ catch sleepForever onValueReceived, :110-112, 137-147
+    c = p.function("worker")
+    c.catch_(1 << EXC_VALUE_RECEIVED, "on_value")
+    c.sleep_forever()
+    c = p.function("on_value")                        # r0 = v
+    c.trace(TAG_GOT_TOKEN, 0)
+    c.link(1, 1).send(1, K_NOTE, 0)                   # execClient observer (noteTokenCall v)
+    c.wait(for_(token_passing_delay))                 # wait (for tokenPassingDelay)
+    c.addi(0, 1)
+    c.link(1, 0).send(1, K_TOKEN, 0)                  # initPassingToken (v + 1)
+    c.jmp("worker")
+
+    # server: serve (no ^. nodePort) [method "token" (acceptToken wtid)], :116-122
+    c = p.function("server")
+    c.listen(ring_set, owned=True)
+    c.sleep_forever()
+    c = p.function("accept_token")                    # acceptToken tid value, :152-154
+    c.nload(2, 0).throw_to(2, EXC_VALUE_RECEIVED, 0).end()
+
+    # launchObserver, :166-194
+    c = p.function("launch_observer")
+    c.fork("obs_server", ref=1)
+    c.fork("checker", ref=2)
+    c.schedule(at(launch_duration), "kill_pair")
+    c.end()
+    c = p.function("obs_server")
+    c.listen(obs_set, owned=True)
+    c.sleep_forever()
+    c = p.function("checker")                         # forever $ wait 1 sec; check progress
+    chk = c.here()
+    c.wait(for_(sec(1)))
+    c.nload(0, 0).now(1).sub(1, 0).seti(2, allowed_progress_delay)
+    c.jle(1, 2, chk)
+    c.nload(3, 1).trace(TAG_NO_PROGRESS, 3)
+    c.jmp(chk)
+    c = p.function("note_token")                      # noteTokenMethod, :197-208
+    c.now(1).nload(2, 1).nstore(1, 0).nstore(0, 1)
+    c.trace(TAG_NOTE, 0)
+    ok = c.label()
+    c.addi(2, 1).jeq(0, 2, ok)
+    c.trace(TAG_WRONG_VALUE, 0)
+    c.bind(ok)
+    c.end()
+
+    img = p.finalize()
+    out = [[(i + 1) % N, OBS] for i in range(N)] + [[], []]
+    topo = Topology.from_out_lists(N + 2, out)
+    L = topo.n_links
+
+    # Delays: ring links (even ids) random, observer links (odd ids) 0
+    live_kind = np.zeros(L, np.uint32)
+    live_lo = np.zeros(L, np.int64)
+    live_hi = np.zeros(L, np.int64)
+    ring_links = np.arange(0, 2 * N, 2)
+    live_kind[ring_links] = 2
+    live_lo[ring_links] = network_delay[0]
+    live_hi[ring_links] = network_delay[1]
+    live_kind[ring_links + 1] = 1
+
+    table = np.zeros((L, link_depth, n_replicas), np.uint32)
+    g = StdGenVec(seed_base + np.arange(n_replicas, dtype=np.int64))
+    for l in ring_links.tolist():
+        for k in range(link_depth):
+            dly = g.range(network_delay[0], network_delay[1]).astype(np.uint32)
+            if drop_log2:
+                u = g.range(0, (1 << drop_log2) - 1)
+                dly = np.where(u == 0, dly | np.uint32(isa.LINK_DROP), dly)
+            table[l, k, :] = dly
+
+    hops = launch_duration // max(1, token_passing_delay) + 2
+    max_slots = 3 * N + 64
+    return Scenario(
+        name=f"token_ring_n{N}",
+        image=img, topo=topo, n_replicas=n_replicas,
+        main_pc=img.pc_of("main"), main_node=SYS,
+        link_table=table, max_slots=_capped(max_slots),
+        queue_capacity=_capped(max_slots + 2 * N + 4 * hops + 256),
+        near_horizon_us=near_horizon_us,
+        meta=dict(config="token_ring", n_nodes=N, launch_duration=launch_duration,
+                  drop_log2=drop_log2, seed_base=seed_base),
+        live_kind=live_kind, live_lo=live_lo, live_hi=live_hi,
+    )
+
+
+# ---------------------------------------------------------------- ping-pong
+def ping_pong(n_replicas: int = 1, round_trips: int = 1, network_delay=(ms(1), ms(5)),
+              seed_base: int = 0, near_horizon_us: int = sec(10)) -> Scenario:
+    """examples/ping-pong/Main.hs re-hosted on the emulated transfer.
+
+    Node 0 = "ping" (listens AtPort 4444), node 1 = "pong" (AtPort 5555),
+    node 2 hosts main.  ping: wait 2 s, send Ping, listen for Pong (:57-67);
+    pong: listen for Ping, reply Pong (:69-77).  ``round_trips`` > 1 re-sends
+    Ping on each Pong (throughput extension; 1 reproduces the example).
+    Per-replica per-link constant delays ~ U[1 ms, 5 ms] from mkStdGen(replica),
+    drawn ping->pong then pong->ping.
+    """
+    p = Program()
+    K_PING, K_PONG = p.kind("Ping"), p.kind("Pong")
+    ping_set = p.listener_set({"Pong": "on_pong"})
+    pong_set = p.listener_set({"Ping": "on_ping"})
+
+    c = p.function("main")
+    c.seti(0, 0).fork_("ping_main", node_reg=0)
+    c.seti(0, 1).fork_("pong_main", node_reg=0)
+    c.end()
+
+    c = p.function("ping_main")
+    c.wait(for_(sec(2)))                              # wait (for 2 sec)
+    c.seti(0, 0).link(1, 0).send(1, K_PING, 0)        # send (localhost, 5555) Ping
+    c.listen(ping_set)                                # listen (AtPort 4444) [...]
+    c.end()
+
+    c = p.function("pong_main")
+    c.listen(pong_set)                                # listen (AtPort 5555) [...]
+    c.end()
+
+    c = p.function("on_ping")                         # \Ping -> log; send (localhost,4444) Pong
+    c.trace(TAG_PING, 0)
+    c.link(2, 0).send(2, K_PONG, 0)
+    c.end()
+
+    c = p.function("on_pong")                         # \Pong -> log
+    c.trace(TAG_PONG, 0)
+    c.addi(0, 1).seti(2, round_trips)
+    fin = c.label()
+    c.jle(2, 0, fin)
+    c.link(1, 0).send(1, K_PING, 0)
+    c.bind(fin)
+    c.end()
+
+    img = p.finalize()
+    topo = Topology.from_out_lists(3, [[1], [0], []])
+    g = StdGenVec(seed_base + np.arange(n_replicas, dtype=np.int64))
+    table = np.zeros((2, 1, n_replicas), np.uint32)
+    table[0, 0, :] = g.range(*network_delay)
+    table[1, 0, :] = g.range(*network_delay)
+    return Scenario(
+        name="ping_pong", image=img, topo=topo, n_replicas=n_replicas,
+        main_pc=img.pc_of("main"), main_node=2, link_table=table,
+        max_slots=16, queue_capacity=64, near_horizon_us=near_horizon_us,
+        meta=dict(config="ping_pong", round_trips=round_trips, seed_base=seed_base),
+    )
+
+
+# ------------------------------------------------------------------ hotspot
+def hotspot(n_senders: int = 256, n_replicas: int = 1, msg_num: int = 1000, msg_rate: int = 1000,
+            duration_s: int = 10, network_delay=(ms(1), ms(5)), seed_base: int = 0,
+            near_horizon_us: int = sec(10)) -> Scenario:
+    """bench/Network many-senders -> one-receiver request/response.
+
+    Sender (Sender/Main.hs:34-64): listen for Pong, then per message
+    ``wait (for sendDelay)`` with sendDelay = 10^6 / msgRate µs (:38-39),
+    stop once the work timer exceeds ``duration`` (:52-53), send Ping msgId;
+    finally ``wait (for 1 sec)`` and close.  Receiver (Receiver/Main.hs:32-41):
+    listen, on Ping reply Pong, stop after ``duration``.  Node i < S = sender i,
+    node S = receiver, node S+1 hosts main.  Links: i -> S (id i), S -> i (id S+i).
+    """
+    S = int(n_senders)
+    RECV, SYS = S, S + 1
+    send_delay = 1_000_000 // msg_rate
+    p = Program()
+    K_PING, K_PONG = p.kind("Ping"), p.kind("Pong")
+    recv_set = p.listener_set({"Ping": "on_ping"})
+    send_set = p.listener_set({"Pong": "on_pong"})
+
+    c = p.function("main")
+    c.seti(0, RECV).fork_("receiver_main", node_reg=0)
+    c.seti(0, 0).seti(2, S)
+    loop = c.here()
+    c.fork("sender_main", ref=1, node_reg=0)
+    c.addi(0, 1).jlt(0, 2, loop)
+    c.end()
+
+    c = p.function("receiver_main")
+    c.listen(recv_set)                                # stopper <- listen (AtPort port) [...]
+    c.wait(for_(sec(duration_s)))                     # wait (for duration sec)
+    c.unlisten()                                      # stopper
+    c.end()
+
+    c = p.function("on_ping")                         # Ping -> logMeasure; reply Pong
+    c.trace(TAG_PING, 0)
+    c.reply_link(2, 1).send(2, K_PONG, 0)
+    c.end()
+
+    c = p.function("sender_main")
+    c.listen(send_set)                                # listen (AtConnTo addr) [Pong -> ...]
+    c.now(1).nstore(1, 0)                             # workTimer <- startTimer
+    c.seti(0, 0)
+    top = c.here()
+    stop = c.label()
+    c.wait(for_(send_delay))                          # wait (for sendDelay)
+    c.now(1).nload(3, 0).sub(1, 3).seti(3, sec(duration_s))
+    c.jlt(3, 1, stop)                                 # when (working > duration) mzero
+    c.trace(TAG_PING_SENT, 0)
+    c.link(1, 0).send(1, K_PING, 0)                   # send addr (Ping sMsgId payload)
+    c.addi(0, 1).seti(2, msg_num)
+    c.jlt(0, 2, top)
+    c.bind(stop)
+    c.wait(for_(sec(1)))                              # wait (for 1 sec)  -- responses
+    c.unlisten()                                      # sequence_ closeConns
+    c.end()
+
+    c = p.function("on_pong")
+    c.trace(TAG_PONG, 0)
+    c.end()
+
+    img = p.finalize()
+    out = [[RECV] for _ in range(S)] + [list(range(S)), []]
+    topo = Topology.from_out_lists(S + 2, out)
+    g = StdGenVec(seed_base + np.arange(n_replicas, dtype=np.int64))
+    table = np.zeros((topo.n_links, 1, n_replicas), np.uint32)
+    for l in range(topo.n_links):
+        table[l, 0, :] = g.range(*network_delay)
+    in_flight = (network_delay[1] // max(1, send_delay) + 2) * 2
+    max_slots = S * (in_flight + 2) + 64
+    return Scenario(
+        name=f"hotspot_s{S}", image=img, topo=topo, n_replicas=n_replicas,
+        main_pc=img.pc_of("main"), main_node=SYS, link_table=table,
+        max_slots=_capped(max_slots), queue_capacity=_capped(2 * max_slots + 256),
+        near_horizon_us=near_horizon_us,
+        meta=dict(config="hotspot", n_senders=S, msg_num=msg_num, msg_rate=msg_rate),
+    )
