@@ -171,9 +171,11 @@ typedef struct tw_scenario_desc {
     const int64_t* main_regs;  /* [n_replicas][4] initial main-thread registers; NULL = 0 */
     /* capacities (per replica) */
     uint32_t max_slots;        /* concurrent threads                              */
-    uint32_t queue_capacity;   /* far-queue entries (live + superseded)          */
+    uint32_t queue_capacity;   /* far-heap entries (live + superseded)           */
     int64_t near_horizon_us;   /* events due within this horizon use the on-chip queue */
     uint32_t max_timeouts;     /* timeout epochs per replica (done-flag bitmap size) */
+    uint32_t run_capacity;     /* entries per monotone far-queue run (4 runs per
+                                  replica); 0 = far events use the heap only */
 } tw_scenario_desc;
 
 #define TW_MAX_FRAMES 3        /* catch/finally frames per thread (both engines) */
@@ -214,6 +216,11 @@ int tw_create(int device, tw_ctx** out);
  * main thread about to run (TimedT.hs:120-127, 234-237).  Replaces the
  * construction of the TimedT value + emptyScenario. */
 int tw_load(tw_ctx* ctx, const tw_scenario_desc* desc);
+
+/* Reset every replica of the loaded scenario to its initial state (t=0, main
+ * about to run) without re-uploading tables: the device-resident equivalent of
+ * evaluating runTimedT again on the same scenario.  Stream-ordered, async. */
+int tw_reset(tw_ctx* ctx);
 
 /* Run every replica's event loop (launchTimedT, TimedT.hs:234-286) until its
  * queue is empty, the next event is later than t_end_us, or its committed-event

@@ -1,0 +1,122 @@
+"""test/Test/Control/TimeWarp/Timed/MonadTimedSpec.hs properties, restated for
+the TimedT oracle with hypothesis (Arbitrary Microsecond = U[0, 600 s],
+test/Test/Control/TimeWarp/Common.hs:27-29)."""
+import hypothesis.strategies as st
+from hypothesis import given, settings
+
+import progs
+from timewarp.program import Program
+from timewarp.timeunits import after, at, for_, now, till
+
+US = st.integers(min_value=0, max_value=600_000_000)
+SMALL = st.integers(min_value=0, max_value=50)
+
+
+def _times(r):
+    return [(t, v) for (t, node, tag, v) in r.traces if tag == progs.TAG_TS]
+
+
+@settings(max_examples=60, deadline=None)
+@given(rel=US, pre=US)
+def test_wait_passing(oracle_mod, rel, pre):
+    """waitPassingTimedProp (:320-324): t1 + rel <= t2."""
+    p = Program()
+    c = p.function("main")
+    c.wait(for_(pre)).now(0).trace(progs.TAG_TS, 0)
+    c.wait(for_(rel)).now(0).trace(progs.TAG_TS, 0).end()
+    r = oracle_mod.run(progs.single(p))
+    (t1, _), (t2, _) = _times(r)
+    assert t1 + rel <= t2 and t2 == t1 + rel
+
+
+@settings(max_examples=60, deadline=None)
+@given(rel=US, pre=US, absolute=st.booleans(), use_schedule=st.booleans())
+def test_schedule_invoke_time_passing(oracle_mod, rel, pre, absolute, use_schedule):
+    """actionTimeSemanticTimedProp for schedule / invoke (:288-318): the action
+    runs, and at a time >= the requested one (relative or absolute spec)."""
+    spec = at(rel) if absolute else after(rel)
+    p = Program()
+    c = p.function("main")
+    c.wait(for_(pre)).now(1)
+    if use_schedule:
+        c.schedule(spec, "act")
+        c.end()
+    else:
+        c.invoke(spec)
+        c.jmp("act")
+    c = p.function("act")
+    c.now(0).trace(progs.TAG_TS, 0).trace(progs.TAG_TS, 1).end()
+    r = oracle_mod.run(progs.single(p))
+    (t_act, _), (_, t1) = _times(r)
+    target = rel if absolute else t1 + rel
+    assert t_act >= target
+    assert t_act == max(target, t1)
+
+
+@settings(max_examples=40, deadline=None)
+@given(pre=US)
+def test_now(oracle_mod, pre):
+    """nowProp (:349-355): invoke now leaves the clock unchanged."""
+    p = Program()
+    c = p.function("main")
+    c.wait(for_(pre)).now(0).trace(progs.TAG_TS, 0)
+    c.invoke(now)
+    c.now(0).trace(progs.TAG_TS, 0).end()
+    r = oracle_mod.run(progs.single(p))
+    (t1, _), (t2, _) = _times(r)
+    assert t1 == t2
+
+
+@settings(max_examples=80, deadline=None)
+@given(tout=st.one_of(US, SMALL), wt=st.one_of(US, SMALL))
+def test_timeout(oracle_mod, tout, wt):
+    """timeoutTimedProp (:275-286).  The watchdog fires at t0+tout, the action
+    ends at t0+1+wt (the watchdog's schedule is a fork).  On the exact tie
+    tout == wt+1 the outcome depends on equal-timestamp pop order: the pqueue
+    transcription completes the action (like the reference), the canonical
+    (t,seq) order fires the watchdog first — either is accepted there, as the
+    reference property accepts both outcomes on a tie."""
+    scn = progs.timeout_prog(tout, wt)
+    for mode in (0, 1):
+        r = oracle_mod.run(scn, mode=mode)
+        (_, outcome), = _times(r)
+        if tout == wt + 1:
+            assert outcome in (1, 2)
+            if mode == 1:
+                assert outcome == 1
+        elif outcome == 1:
+            assert wt <= tout and wt + 1 < tout + 1
+        else:
+            assert tout <= wt
+
+
+@settings(max_examples=60, deadline=None)
+@given(m=US, f1=US, f2=US)
+def test_kill_thread(oracle_mod, m, f1, f2):
+    """killThreadTimedProp (:246-273)."""
+    r = oracle_mod.run(progs.kill_thread_prog(m, f1, f2))
+    (_, res), = _times(r)
+    if res == 0:
+        assert m <= f1 and m <= f2
+    elif res == 2:
+        assert f2 <= m
+    else:
+        assert res == 1
+
+
+def test_exceptions_dont_affect_other_threads(oracle_mod):
+    """exceptionNotAffectOtherThread (:398-402): a scheduled thread's uncaught
+    throw does not stop another scheduled thread."""
+    p = Program()
+    c = p.function("main")
+    c.schedule(after(3_000_000), "ok")
+    c.schedule(after(1_000_000), "bad")
+    c.end()
+    c = p.function("ok")
+    c.seti(0, 1).trace(progs.TAG_TS, 0).end()
+    c = p.function("bad")
+    c.throw(5)
+    c.end()
+    r = oracle_mod.run(progs.single(p))
+    assert [v for _, v in _times(r)] == [1]
+    assert r.result["main_exc"] == 0

@@ -39,6 +39,7 @@
 #define TW_NEAR_CAP 16          // on-chip queue entries per replica (LDS)
 #endif
 #define TW_BLOCK 64             // one wavefront per workgroup
+#define TW_RUNS 4               // monotone far-queue runs per replica
 #define TW_STEP_CAP (1u << 22)  // instructions per thread step (== oracle kStepCap)
 
 namespace {
@@ -89,12 +90,13 @@ __device__ __forceinline__ void th_set_exc(Th& t, uint32_t c) { t.w0 = (t.w0 & 0
 
 enum {
     SC_NOW, SC_FINAL_T, SC_EVENTS, SC_DELIVERED, SC_DROPPED, SC_UNDELIV, SC_THREADS, SC_SEQ, SC_TIDC,
-    SC_LIVE, SC_NEAR_N, SC_FAR_N, SC_STATUS, SC_MAIN_EXC, SC_PENDING_MAIN, SC_FREE_TOP, SC_TMO_CTR, SC_COUNT
+    SC_LIVE, SC_NEAR_N, SC_FAR_N, SC_STATUS, SC_MAIN_EXC, SC_PENDING_MAIN, SC_FREE_TOP, SC_TMO_CTR,
+    SC_RH0, SC_RC0 = SC_RH0 + TW_RUNS, SC_COUNT = SC_RC0 + TW_RUNS
 };
 
 struct Dev {
     // shape
-    uint32_t R, S, Q, N, L, D, T;
+    uint32_t R, S, Q, N, L, D, T, Cr;
     uint32_t n_insns, n_consts, n_sets, n_kinds;
     int64_t horizon;
     // scenario (shared by all replicas)
@@ -112,6 +114,7 @@ struct Dev {
     uint4* slots;        // [S][R][4]
     uint32_t* free_stk;  // [S][R]
     uint4* far;          // [Q][R]  {t_lo, t_hi, key_lo(slot), key_hi(seq)}
+    uint4* runs;         // [TW_RUNS][Cr][R] monotone FIFO runs (ring buffers)
     uint4* near_spill;   // [NEAR_CAP][R]
     int64_t* nvars;      // [N*4][R]
     uint64_t* hash;      // [N][R]
@@ -146,6 +149,14 @@ struct Lane {
     // LDS near heap of this lane: element j at base[j * TW_BLOCK]
     int64_t* nt;
     uint64_t* nk;
+    // program image and constant pool (LDS copy when it fits)
+    const uint2* P;
+    const int64_t* K;
+    // far runs: head index, count, head key, tail key (indexed only by unrolled constants)
+    uint32_t rh[TW_RUNS], rc[TW_RUNS];
+    int64_t rt[TW_RUNS], ut[TW_RUNS];
+    uint64_t rk[TW_RUNS], uk[TW_RUNS];
+    uint32_t next_free;  // cached free_stk[free_top-1] (prefetched)
     // cached replica scalars
     int64_t now;
     uint32_t seq, tidc, live, near_n, far_n, status, main_exc, free_top, tmo_ctr;
@@ -260,6 +271,60 @@ struct Lane {
         if (i == 0) { far_t = t; far_k = k; }
     }
 
+    // ---------------------------------------------------- far runs (HBM FIFOs)
+    // Patience-sorting piles: a far event is appended to the run whose tail is
+    // the largest key <= it, so runs stay sorted and pops are O(1) with the next
+    // head prefetched.  TimedT scenarios park threads in monotone streams
+    // (killers at one absolute time, sleepForever timers, re-stamped victims of
+    // a killer sweep), so the heap sees only stragglers.
+    __device__ __forceinline__ uint4* run_at(uint32_t j, uint32_t pos) const {
+        return c->runs + ((size_t)j * c->Cr + pos) * c->R + r;
+    }
+    __device__ __forceinline__ bool run_push(int64_t t, uint64_t k) {
+        if (c->Cr == 0) return false;
+        int best = -1, empty = -1;
+        int64_t bt = 0;
+        uint64_t bk = 0;
+#pragma unroll
+        for (int j = 0; j < TW_RUNS; ++j) {
+            if (rc[j] == 0) {
+                if (empty < 0) empty = j;
+            } else if (rc[j] < c->Cr && !kless(t, k, ut[j], uk[j])) {
+                if (best < 0 || kless(bt, bk, ut[j], uk[j])) { best = j; bt = ut[j]; bk = uk[j]; }
+            }
+        }
+        int sel = best >= 0 ? best : empty;
+        if (sel < 0) return false;
+#pragma unroll
+        for (int j = 0; j < TW_RUNS; ++j) {
+            if (j == sel) {
+                uint32_t pos = rh[j] + rc[j];
+                if (pos >= c->Cr) pos -= c->Cr;
+                *run_at(j, pos) = make_uint4((uint32_t)t, (uint32_t)((uint64_t)t >> 32), (uint32_t)k, (uint32_t)(k >> 32));
+                if (rc[j] == 0) { rt[j] = t; rk[j] = k; }
+                ut[j] = t; uk[j] = k;
+                ++rc[j];
+            }
+        }
+        return true;
+    }
+    __device__ __forceinline__ void run_pop(int sel) {
+#pragma unroll
+        for (int j = 0; j < TW_RUNS; ++j) {
+            if (j == sel) {
+                rh[j] = rh[j] + 1 == c->Cr ? 0 : rh[j] + 1;
+                if (--rc[j]) {
+                    uint4 e = *run_at(j, rh[j]);
+                    rt[j] = (int64_t)(((uint64_t)e.y << 32) | e.x);
+                    rk[j] = ((uint64_t)e.w << 32) | e.z;
+                }
+            }
+        }
+    }
+    __device__ __forceinline__ void push_far(int64_t t, uint64_t k) {
+        if (!run_push(t, k)) far_push(t, k);
+    }
+
     // ------------------------------------------------------------- queue
     __device__ __forceinline__ void enqueue(Th& th, uint32_t slot, int64_t t) {
         uint32_t s = ++seq;
@@ -267,7 +332,17 @@ struct Lane {
         th.w3 = s;
         uint64_t k = ((uint64_t)s << 32) | slot;
         if (t - now < c->horizon && near_n < TW_NEAR_CAP) near_push(t, k);
-        else far_push(t, k);
+        else push_far(t, k);
+    }
+    // Source of the minimum (t, seq) event: 0..TW_RUNS-1 run, TW_RUNS near, TW_RUNS+1 heap, -1 none.
+    __device__ __forceinline__ int min_source(int64_t& t, uint64_t& k) const {
+        int src = -1;
+        if (near_n) { src = TW_RUNS; t = nt[0]; k = nk[0]; }
+        if (far_n && (src < 0 || kless(far_t, far_k, t, k))) { src = TW_RUNS + 1; t = far_t; k = far_k; }
+#pragma unroll
+        for (int j = 0; j < TW_RUNS; ++j)
+            if (rc[j] && (src < 0 || kless(rt[j], rk[j], t, k))) { src = j; t = rt[j]; k = rk[j]; }
+        return src;
     }
 
     // ------------------------------------------------------------- slots
@@ -290,14 +365,23 @@ struct Lane {
         p[3] = make_uint4((uint32_t)th.r2, (uint32_t)((uint64_t)th.r2 >> 32), (uint32_t)th.r3,
                           (uint32_t)((uint64_t)th.r3 >> 32));
     }
+    // Free-slot stack; its top is cached in a register and the next one is
+    // prefetched at every pop, so a fork never waits on this load.
     __device__ __forceinline__ uint32_t alloc_slot() {
         if (free_top == 0) { fail(TW_REP_ERR_SLOTS); return 0xFFFFFFFFu; }
-        return c->free_stk[ix(--free_top)];
+        uint32_t s = next_free;
+        if (--free_top) next_free = c->free_stk[ix(free_top - 1)];
+        return s;
     }
-    __device__ __forceinline__ void free_slot(uint32_t slot) { c->free_stk[ix(free_top++)] = slot; }
+    __device__ __forceinline__ void free_slot(uint32_t slot) {
+        c->free_stk[ix(free_top++)] = slot;
+        next_free = slot;
+    }
 
+    // Commutative per-node trace hash: a no-return 64-bit atomic add, so the
+    // event's critical path never waits on the node's hash line.
     __device__ __forceinline__ void hash(uint32_t node, uint32_t kind, int64_t val) {
-        c->hash[ix(node)] += term(now, kind, val);
+        atomicAdd((unsigned long long*)(c->hash + ix(node)), (unsigned long long)term(now, kind, val));
     }
 
     // Create a thread queued at now (fork, TimedT.hs:326-339).  Returns its ref.
@@ -337,7 +421,7 @@ struct Lane {
             a.w = s;
             uint64_t k = ((uint64_t)s << 32) | ts;
             if (near_n < TW_NEAR_CAP) near_push(now, k);
-            else far_push(now, k);
+            else push_far(now, k);
         }
         if ((a.x >> 24) == 0) {
             a.x = (a.x & 0x00FFFFFFu) | (code << 24);
@@ -387,11 +471,10 @@ struct Lane {
     // Run the thread's continuation until it yields or ends.
     __device__ __forceinline__ void step(Th& th, uint32_t slot) {
         th_or_flags(th, F_STARTED);
-        const int64_t* K = c->consts;
         for (uint32_t n = 0; n < TW_STEP_CAP; ++n) {
             uint32_t pc = th_pc(th);
             if (pc >= c->n_insns) { fail(TW_REP_ERR_INSN); store_th(slot, th); return; }
-            uint2 in = c->insns[pc];
+            uint2 in = P[pc];
             uint32_t op = in.x & 0xFFu, a = (in.x >> 8) & 3u, b = in.x >> 16;
             int32_t imm = (int32_t)in.y;
             th_set_pc(th, pc + 1);
@@ -597,10 +680,24 @@ __global__ void __launch_bounds__(TW_BLOCK) tw_init_kernel(Dev c, uint32_t main_
     for (uint32_t n = 0; n < c.N; ++n) c.bind_own[(size_t)n * c.R + r] = 0xFFFFFFFFu;
 }
 
+// LDS per workgroup: near heap keys [NEAR_CAP][64] x 2 words, then (when it
+// fits) the program image and constant pool, so instruction fetch and time
+// constants never leave the CU.
+__host__ __device__ constexpr size_t near_lds_bytes() { return (size_t)TW_NEAR_CAP * TW_BLOCK * 16; }
+
+template <bool PLDS>
 __global__ void __launch_bounds__(TW_BLOCK) tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events,
                                                          uint32_t budget) {
-    __shared__ int64_t s_t[TW_NEAR_CAP * TW_BLOCK];
-    __shared__ uint64_t s_k[TW_NEAR_CAP * TW_BLOCK];
+    extern __shared__ __attribute__((aligned(16))) uint64_t lds[];
+    int64_t* s_t = (int64_t*)lds;
+    uint64_t* s_k = lds + TW_NEAR_CAP * TW_BLOCK;
+    uint2* s_p = (uint2*)(lds + 2 * TW_NEAR_CAP * TW_BLOCK);
+    int64_t* s_c = (int64_t*)(s_p + c.n_insns);
+    if (PLDS) {
+        for (uint32_t i = threadIdx.x; i < c.n_insns; i += TW_BLOCK) s_p[i] = c.insns[i];
+        for (uint32_t i = threadIdx.x; i < c.n_consts; i += TW_BLOCK) s_c[i] = c.consts[i];
+        __syncthreads();
+    }
     uint32_t r = blockIdx.x * TW_BLOCK + threadIdx.x;
     if (r >= c.R) return;
     uint64_t* sc = c.scal + r;
@@ -612,6 +709,8 @@ __global__ void __launch_bounds__(TW_BLOCK) tw_run_kernel(Dev c, int64_t t_end, 
     L.r = r;
     L.nt = s_t + threadIdx.x;
     L.nk = s_k + threadIdx.x;
+    L.P = PLDS ? (const uint2*)s_p : c.insns;
+    L.K = PLDS ? (const int64_t*)s_c : c.consts;
     L.now = (int64_t)sc[SC_NOW * R]; L.final_t = (int64_t)sc[SC_FINAL_T * R];
     L.seq = (uint32_t)sc[SC_SEQ * R]; L.tidc = (uint32_t)sc[SC_TIDC * R]; L.live = (uint32_t)sc[SC_LIVE * R];
     L.near_n = (uint32_t)sc[SC_NEAR_N * R]; L.far_n = (uint32_t)sc[SC_FAR_N * R];
@@ -619,15 +718,35 @@ __global__ void __launch_bounds__(TW_BLOCK) tw_run_kernel(Dev c, int64_t t_end, 
     L.free_top = (uint32_t)sc[SC_FREE_TOP * R]; L.tmo_ctr = (uint32_t)sc[SC_TMO_CTR * R];
     L.events = sc[SC_EVENTS * R]; L.delivered = sc[SC_DELIVERED * R]; L.dropped = sc[SC_DROPPED * R];
     L.undeliv = sc[SC_UNDELIV * R]; L.threads = sc[SC_THREADS * R];
+    L.next_free = L.free_top ? c.free_stk[(size_t)(L.free_top - 1) * R + r] : 0u;
     for (uint32_t j = 0; j < L.near_n; ++j) {
-        uint4 e = c.near_spill[(size_t)j * c.R + r];
+        uint4 e = c.near_spill[(size_t)j * R + r];
         L.nt[j * TW_BLOCK] = (int64_t)(((uint64_t)e.y << 32) | e.x);
         L.nk[j * TW_BLOCK] = ((uint64_t)e.w << 32) | e.z;
     }
+    L.far_t = 0;
+    L.far_k = 0;
     if (L.far_n) {
         uint4 e = L.far_ld(0);
         L.far_t = (int64_t)(((uint64_t)e.y << 32) | e.x);
         L.far_k = ((uint64_t)e.w << 32) | e.z;
+    }
+#pragma unroll
+    for (int j = 0; j < TW_RUNS; ++j) {
+        L.rh[j] = (uint32_t)sc[(SC_RH0 + j) * R];
+        L.rc[j] = (uint32_t)sc[(SC_RC0 + j) * R];
+        L.rt[j] = L.ut[j] = 0;
+        L.rk[j] = L.uk[j] = 0;
+        if (L.rc[j]) {
+            uint4 h = *L.run_at(j, L.rh[j]);
+            uint32_t tp = L.rh[j] + L.rc[j] - 1;
+            if (tp >= c.Cr) tp -= c.Cr;
+            uint4 u = *L.run_at(j, tp);
+            L.rt[j] = (int64_t)(((uint64_t)h.y << 32) | h.x);
+            L.rk[j] = ((uint64_t)h.w << 32) | h.z;
+            L.ut[j] = (int64_t)(((uint64_t)u.y << 32) | u.x);
+            L.uk[j] = ((uint64_t)u.w << 32) | u.z;
+        }
     }
 
     uint32_t pending_main = (uint32_t)sc[SC_PENDING_MAIN * R];
@@ -644,17 +763,13 @@ __global__ void __launch_bounds__(TW_BLOCK) tw_run_kernel(Dev c, int64_t t_end, 
         } else {
             if (L.live == 0) { L.status = TW_REP_DONE; break; }  // whileM_ notDone
             if (L.events >= max_events) break;
-            bool use_near;
-            int64_t t;
-            uint64_t k;
-            if (L.near_n && (!L.far_n || kless(L.nt[0], L.nk[0], L.far_t, L.far_k))) {
-                use_near = true; t = L.nt[0]; k = L.nk[0];
-            } else {
-                use_near = false; t = L.far_t; k = L.far_k;
-            }
-            if (t > t_end) break;
-            if (use_near) L.near_pop();
-            else L.far_pop();
+            int64_t t = 0;
+            uint64_t k = 0;
+            int src = L.min_source(t, k);
+            if (src < 0 || t > t_end) break;
+            if (src == TW_RUNS) L.near_pop();
+            else if (src == TW_RUNS + 1) L.far_pop();
+            else L.run_pop(src);
             slot = (uint32_t)k;
             L.load_th(slot, th);
             if (th.w3 != (uint32_t)(k >> 32)) continue;  // superseded by a throwTo re-stamp
@@ -694,19 +809,22 @@ __global__ void __launch_bounds__(TW_BLOCK) tw_run_kernel(Dev c, int64_t t_end, 
     sc[SC_FREE_TOP * R] = L.free_top; sc[SC_TMO_CTR * R] = L.tmo_ctr;
     sc[SC_EVENTS * R] = L.events; sc[SC_DELIVERED * R] = L.delivered; sc[SC_DROPPED * R] = L.dropped;
     sc[SC_UNDELIV * R] = L.undeliv; sc[SC_THREADS * R] = L.threads;
+#pragma unroll
+    for (int j = 0; j < TW_RUNS; ++j) {
+        sc[(SC_RH0 + j) * R] = L.rh[j];
+        sc[(SC_RC0 + j) * R] = L.rc[j];
+    }
     for (uint32_t j = 0; j < L.near_n; ++j) {
         int64_t t = L.nt[j * TW_BLOCK];
         uint64_t k = L.nk[j * TW_BLOCK];
-        c.near_spill[(size_t)j * c.R + r] =
+        c.near_spill[(size_t)j * R + r] =
             make_uint4((uint32_t)t, (uint32_t)((uint64_t)t >> 32), (uint32_t)k, (uint32_t)(k >> 32));
     }
     bool active = L.status == TW_REP_RUNNING && L.events < max_events;
-    if (active) {
-        // next event beyond t_end?  then this replica is parked, not active
-        int64_t nt = INT64_MAX;
-        if (L.near_n) nt = L.nt[0];
-        if (L.far_n && L.far_t < nt) nt = L.far_t;
-        if (nt > t_end) active = false;
+    if (active) {  // parked beyond t_end => not active
+        int64_t t = 0;
+        uint64_t k = 0;
+        if (L.min_source(t, k) < 0 || t > t_end) active = false;
     }
     if (active) atomicAdd(c.n_active, 1u);
 }
@@ -721,6 +839,11 @@ struct tw_ctx {
     bool loaded = false;
     std::vector<void*> allocs;
     uint32_t* h_active = nullptr;  // pinned
+    uint32_t main_pc = 0, main_node = 0;
+    int64_t* main_regs = nullptr;  // device copies for tw_reset
+    int64_t* nv_init = nullptr;
+    bool prog_lds = false;         // program + constants fit in LDS beside the near heap
+    size_t lds_bytes = 0;
     std::vector<double> launch_ms;
     std::vector<hipEvent_t> ev_pool;
 };
@@ -822,6 +945,8 @@ static int validate(const tw_scenario_desc* s) {
     return TW_OK;
 }
 
+int tw_reset(tw_ctx* c);
+
 int tw_load(tw_ctx* c, const tw_scenario_desc* s) {
     if (!c) return TW_ERR_INVALID;
     int v = validate(s);
@@ -835,7 +960,10 @@ int tw_load(tw_ctx* c, const tw_scenario_desc* s) {
     d.L = s->n_links; d.D = s->link_depth; d.T = s->max_timeouts;
     d.n_insns = s->n_insns; d.n_consts = s->n_consts; d.n_sets = s->n_listener_sets; d.n_kinds = s->n_msg_kinds;
     d.horizon = s->near_horizon_us;
+    d.Cr = s->run_capacity;
     const size_t R = d.R;
+    c->lds_bytes = near_lds_bytes() + 8ull * d.n_insns + 8ull * d.n_consts;
+    c->prog_lds = c->lds_bytes <= 48 * 1024;
     int e;
 #define ALLOC(p, n) if ((e = dalloc(c, &p, (n))) != TW_OK) { free_all(c); return e; }
     uint2* insns; int64_t* consts; uint32_t *lpc, *out_off, *ldst, *lrev, *ltab = nullptr;
@@ -850,6 +978,7 @@ int tw_load(tw_ctx* c, const tw_scenario_desc* s) {
     ALLOC(d.slots, (size_t)d.S * R * 4);
     ALLOC(d.free_stk, (size_t)d.S * R);
     ALLOC(d.far, (size_t)d.Q * R);
+    ALLOC(d.runs, (size_t)(d.Cr ? TW_RUNS * (size_t)d.Cr : 1) * R);
     ALLOC(d.near_spill, (size_t)TW_NEAR_CAP * R);
     ALLOC(d.nvars, (size_t)d.N * 4 * R);
     ALLOC(d.hash, (size_t)d.N * R);
@@ -874,21 +1003,38 @@ int tw_load(tw_ctx* c, const tw_scenario_desc* s) {
     if (ltab) HIPCHK(hipMemcpyAsync(ltab, s->link_table, 4ull * d.L * d.D * R, hipMemcpyHostToDevice, st));
     if (mregs) HIPCHK(hipMemcpyAsync(mregs, s->main_regs, 32ull * R, hipMemcpyHostToDevice, st));
     if (nvi) HIPCHK(hipMemcpyAsync(nvi, s->node_vars, 32ull * d.N, hipMemcpyHostToDevice, st));
+    d.insns = insns; d.consts = consts; d.lpc = lpc; d.out_off = out_off; d.link_dst = ldst; d.link_rev = lrev;
+    d.link_table = ltab;
+    c->main_pc = s->main_pc;
+    c->main_node = s->main_node;
+    c->main_regs = mregs;
+    c->nv_init = nvi;
+    c->loaded = true;
+    int rc = tw_reset(c);
+    if (rc) return rc;
+    HIPCHK(hipStreamSynchronize(st));
+    return TW_OK;
+}
+
+int tw_reset(tw_ctx* c) {
+    if (!c) return TW_ERR_INVALID;
+    if (!c->loaded) return TW_ERR_STATE;
+    HIPCHK(hipSetDevice(c->device));
+    const Dev& d = c->d;
+    const size_t R = d.R;
+    hipStream_t st = c->stream;
     HIPCHK(hipMemsetAsync(d.nvars, 0, 32ull * d.N * R, st));
     HIPCHK(hipMemsetAsync(d.hash, 0, 8ull * d.N * R, st));
     HIPCHK(hipMemsetAsync(d.bind, 0, 4ull * d.N * R, st));
     HIPCHK(hipMemsetAsync(d.link_ord, 0, 4ull * (d.L ? d.L : 1) * R, st));
     HIPCHK(hipMemsetAsync(d.tmo_done, 0, (size_t)(d.T ? d.T : 1) * R, st));
-    d.insns = insns; d.consts = consts; d.lpc = lpc; d.out_off = out_off; d.link_dst = ldst; d.link_rev = lrev;
-    d.link_table = ltab;
     uint32_t blocks = (uint32_t)((R + TW_BLOCK - 1) / TW_BLOCK);
-    hipLaunchKernelGGL(tw_init_kernel, dim3(blocks), dim3(TW_BLOCK), 0, st, d, s->main_pc, s->main_node,
-                       (const int64_t*)mregs, (const int64_t*)nvi);
+    hipLaunchKernelGGL(tw_init_kernel, dim3(blocks), dim3(TW_BLOCK), 0, st, d, c->main_pc, c->main_node,
+                       (const int64_t*)c->main_regs, (const int64_t*)c->nv_init);
     HIPCHK(hipGetLastError());
-    HIPCHK(hipStreamSynchronize(st));
-    c->loaded = true;
     return TW_OK;
 }
+
 
 int tw_run(tw_ctx* c, int64_t t_end_us, uint64_t max_events, tw_stats* out) {
     if (!c) return TW_ERR_INVALID;
@@ -918,7 +1064,12 @@ int tw_run(tw_ctx* c, int64_t t_end_us, uint64_t max_events, tw_stats* out) {
         for (int i = 0; i < per_check; ++i) {
             HIPCHK(hipMemsetAsync(d.n_active, 0, 4, st));
             HIPCHK(hipEventRecord(c->ev_pool[2 * i], st));
-            hipLaunchKernelGGL(tw_run_kernel, dim3(blocks), dim3(TW_BLOCK), 0, st, d, t_end_us, limit, budget);
+            if (c->prog_lds)
+                hipLaunchKernelGGL(tw_run_kernel<true>, dim3(blocks), dim3(TW_BLOCK), c->lds_bytes, st, d, t_end_us,
+                                   limit, budget);
+            else
+                hipLaunchKernelGGL(tw_run_kernel<false>, dim3(blocks), dim3(TW_BLOCK), near_lds_bytes(), st, d,
+                                   t_end_us, limit, budget);
             HIPCHK(hipGetLastError());
             HIPCHK(hipEventRecord(c->ev_pool[2 * i + 1], st));
             ++launches;

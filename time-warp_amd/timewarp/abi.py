@@ -32,6 +32,7 @@ class TwScenarioDesc(C.Structure):
         ("queue_capacity", C.c_uint32),
         ("near_horizon_us", C.c_int64),
         ("max_timeouts", C.c_uint32),
+        ("run_capacity", C.c_uint32),
     ]
 
 

@@ -24,7 +24,7 @@ LIB_PATH = os.path.join(_PKG_ROOT, "lib", "libtimewarp.so")
 UNLIMITED = (1 << 64) - 1
 T_INF = (1 << 63) - 1
 
-EXPORTS = ["tw_create", "tw_load", "tw_run", "tw_read_results", "tw_read_hashes", "tw_read_final",
+EXPORTS = ["tw_create", "tw_load", "tw_reset", "tw_run", "tw_read_results", "tw_read_hashes", "tw_read_final",
            "tw_last_launch_ms", "tw_destroy", "tw_strerror", "tw_version"]
 
 
@@ -46,6 +46,7 @@ def load_library(path: Optional[str] = None):
     lib = C.CDLL(p)
     lib.tw_create.argtypes = [C.c_int, C.POINTER(C.c_void_p)]
     lib.tw_load.argtypes = [C.c_void_p, C.c_void_p]
+    lib.tw_reset.argtypes = [C.c_void_p]
     lib.tw_run.argtypes = [C.c_void_p, C.c_int64, C.c_uint64, C.POINTER(TwStats)]
     lib.tw_read_results.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t]
     lib.tw_read_hashes.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t]
@@ -55,7 +56,7 @@ def load_library(path: Optional[str] = None):
     lib.tw_strerror.argtypes = [C.c_int]
     lib.tw_strerror.restype = C.c_char_p
     lib.tw_version.restype = C.c_char_p
-    for name in ("tw_create", "tw_load", "tw_run", "tw_read_results", "tw_read_hashes", "tw_read_final",
+    for name in ("tw_create", "tw_load", "tw_reset", "tw_run", "tw_read_results", "tw_read_hashes", "tw_read_final",
                  "tw_last_launch_ms"):
         getattr(lib, name).restype = C.c_int
     if path is None:
@@ -115,6 +116,11 @@ class Engine:
         d = scn.desc()
         _check(self.lib.tw_load(self.ctx, C.addressof(d)), "tw_load")
         self.scn = scn
+        return self
+
+    def reset(self) -> "Engine":
+        """Back to t=0 on the device-resident tables (no host upload)."""
+        _check(self.lib.tw_reset(self.ctx), "tw_reset")
         return self
 
     def run(self, t_end: int = T_INF, max_events: int = UNLIMITED) -> RunStats:

@@ -67,6 +67,7 @@ class Scenario:
     queue_capacity: int = 256
     near_horizon_us: int = 10_000_000
     max_timeouts: int = 0
+    run_capacity: int = 0
     meta: dict = field(default_factory=dict)
     # oracle-only: the reference's live Delays function (kind/lo/hi per link)
     live_kind: Optional[np.ndarray] = None
@@ -127,5 +128,6 @@ class Scenario:
         d.queue_capacity = self.queue_capacity
         d.near_horizon_us = self.near_horizon_us
         d.max_timeouts = self.max_timeouts
+        d.run_capacity = self.run_capacity
         d._keep = keep  # type: ignore[attr-defined]
         return d

@@ -163,6 +163,7 @@ def token_ring(n_nodes: int = 16, n_replicas: int = 1, launch_duration: int = se
         main_pc=img.pc_of("main"), main_node=SYS,
         link_table=table, max_slots=_capped(max_slots),
         queue_capacity=_capped(max_slots + 2 * N + 4 * hops + 256),
+        run_capacity=_capped(2 * N + 4 * hops + 256),
         near_horizon_us=near_horizon_us,
         meta=dict(config="token_ring", n_nodes=N, launch_duration=launch_duration,
                   drop_log2=drop_log2, seed_base=seed_base),
@@ -305,6 +306,6 @@ def hotspot(n_senders: int = 256, n_replicas: int = 1, msg_num: int = 1000, msg_
         name=f"hotspot_s{S}", image=img, topo=topo, n_replicas=n_replicas,
         main_pc=img.pc_of("main"), main_node=SYS, link_table=table,
         max_slots=_capped(max_slots), queue_capacity=_capped(2 * max_slots + 256),
-        near_horizon_us=near_horizon_us,
+        run_capacity=_capped(2 * S + 64), near_horizon_us=near_horizon_us,
         meta=dict(config="hotspot", n_senders=S, msg_num=msg_num, msg_rate=msg_rate),
     )
