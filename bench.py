@@ -34,8 +34,9 @@ BYTES_PER_SEND = 8              # link-table entry + ordinal
 def build_scenario(args, rank: int):
     from timewarp import scenarios
 
-    R = args.replicas
-    base = rank * R
+    from timewarp.dist import weak_block
+
+    base, R = weak_block(rank, args.replicas)
     if args.config == "token_ring":
         return scenarios.token_ring(n_nodes=args.nodes, n_replicas=R, launch_duration=args.duration_s * 1_000_000,
                                     drop_log2=args.drop_log2, seed_base=base), (
@@ -107,13 +108,7 @@ def main():
         if dist_on:
             dist.barrier()
 
-    def allreduce(vals, op):
-        if not dist_on:
-            return vals
-        t = torch.tensor(vals, dtype=torch.float64, device=f"cuda:{local}")
-        dist.all_reduce(t, op=op)
-        return t.tolist()
-
+    from timewarp import dist as twd
     from timewarp.engine import Engine
 
     scn, workload = build_scenario(args, rank)
@@ -145,8 +140,9 @@ def main():
 
     res = eng.results()
     hashes = eng.hashes()
-    tot_events, tot_sends = allreduce([float(events), float(sends)], dist.ReduceOp.SUM if dist_on else None)
-    (max_elapsed,) = allreduce([elapsed], dist.ReduceOp.MAX if dist_on else None)
+    tot = twd.reduce_stats({"events": events, "sends": sends, "elapsed_s": elapsed},
+                           device=f"cuda:{local}" if dist_on else None)
+    tot_events, max_elapsed = tot["events"], tot["elapsed_s"]
 
     if rank == 0:
         value = tot_events / max_elapsed

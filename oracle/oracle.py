@@ -70,6 +70,7 @@ def lib():
         _lib.two_stdgen_draws.argtypes = [C.c_int64, C.c_int64, C.c_int64, C.c_void_p, C.c_size_t]
         _lib.two_stdgen_next.argtypes = [C.c_int64, C.c_void_p, C.c_size_t, C.c_void_p]
         _lib.two_pqueue_order.argtypes = [C.c_void_p, C.c_size_t, C.c_void_p]
+        _lib.two_pqueue_order.restype = C.c_size_t
     return _lib
 
 
@@ -158,8 +159,9 @@ def stdgen_next(seed: int, n: int):
     return (int(s[0]), int(s[1])), out
 
 
-def pqueue_order(keys) -> np.ndarray:
-    k = np.ascontiguousarray(keys, dtype=np.int64)
+def pqueue_order(ops) -> np.ndarray:
+    """ops[i] >= 0: insert key ops[i] (payload i); -1: minView.  Returns popped payloads."""
+    k = np.ascontiguousarray(ops, dtype=np.int64)
     out = np.zeros(len(k), np.int64)
-    lib().two_pqueue_order(k.ctypes.data, len(k), out.ctypes.data)
-    return out
+    m = lib().two_pqueue_order(k.ctypes.data, len(k), out.ctypes.data)
+    return out[:m]

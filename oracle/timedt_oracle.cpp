@@ -612,14 +612,19 @@ void two_stdgen_next(int64_t seed, int32_t* out, size_t n, int32_t* s1s2) {
     for (size_t i = 0; i < n; ++i) out[i] = stdgen_next(g);
 }
 
-// pqueue transcription self-test hook: insert keys (ties carry a payload id),
-// return pop order of payload ids.
-void two_pqueue_order(const int64_t* keys, size_t n, int64_t* out_ids) {
+// pqueue transcription self-test hook: ops[i] >= 0 inserts key ops[i] with
+// payload id i, ops[i] == -1 pops (minView) and records the payload id.
+// Returns the number of ids written.
+size_t two_pqueue_order(const int64_t* ops, size_t n, int64_t* out_ids) {
     struct KV { int64_t k; int64_t id; };
     struct LE { bool operator()(const KV& a, const KV& b) const { return a.k <= b.k; } };
     PQueueMin<KV, LE> q;
-    for (size_t i = 0; i < n; ++i) q.insert(KV{keys[i], (int64_t)i});
-    for (size_t i = 0; i < n; ++i) out_ids[i] = q.pop().id;
+    size_t m = 0;
+    for (size_t i = 0; i < n; ++i) {
+        if (ops[i] >= 0) q.insert(KV{ops[i], (int64_t)i});
+        else if (!q.empty()) out_ids[m++] = q.pop().id;
+    }
+    return m;
 }
 
 }  // extern "C"

@@ -1,0 +1,67 @@
+"""Multi-rank replica sharding with world_size 2 over gloo (CPU).
+
+Each rank owns a weak-scaling block of replicas; the per-rank run (here the
+oracle, standing in for the per-GPU engine which needs a device) is reduced
+with timewarp.dist exactly as bench.py does over RCCL.  The union must equal a
+single-process run of all replicas, replica for replica."""
+import os
+import socket
+
+import numpy as np
+import torch.multiprocessing as mp
+
+R_PER_RANK = 12
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, out_path):
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [os.path.join(root, "time-warp_amd"), os.path.join(root, "oracle")]
+    import torch.distributed as dist
+
+    import oracle
+    from timewarp import dist as twd
+    from timewarp import scenarios
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    seed_base, n = twd.weak_block(rank, R_PER_RANK)
+    scn = scenarios.token_ring(n_nodes=9, n_replicas=n, launch_duration=30_000_000, drop_log2=3,
+                               link_depth=4, seed_base=seed_base)
+    res, hashes = oracle.run_batch(scn, threads=2)
+    stats = twd.reduce_stats({"events": int(res["events"].sum()), "dropped": int(res["dropped"].sum()),
+                              "max_final_t": int(res["final_t"].max()), "elapsed_s": 0.1 * (rank + 1)})
+    allres, allh = twd.gather_results(res, hashes)
+    if rank == 0:
+        np.savez(out_path, res=allres, hashes=allh, events=stats["events"], dropped=stats["dropped"],
+                 max_final_t=stats["max_final_t"], elapsed=stats["elapsed_s"])
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_rank_sharding_equals_single_process(tmp_path, oracle_mod):
+    from timewarp import dist as twd
+    from timewarp import scenarios
+
+    out = str(tmp_path / "r.npz")
+    mp.spawn(_worker, args=(2, _free_port(), out), nprocs=2, join=True)
+    got = np.load(out)
+    scn = scenarios.token_ring(n_nodes=9, n_replicas=2 * R_PER_RANK, launch_duration=30_000_000, drop_log2=3,
+                               link_depth=4, seed_base=0)
+    res, hashes = oracle_mod.run_batch(scn, threads=4)
+    for f in res.dtype.names:
+        assert np.array_equal(got["res"][f], res[f]), f
+    assert np.array_equal(got["hashes"], hashes)
+    assert got["events"] == res["events"].sum() and got["dropped"] == res["dropped"].sum()
+    assert got["max_final_t"] == res["final_t"].max()
+    assert abs(float(got["elapsed"]) - 0.2) < 1e-12  # max over ranks
+    assert twd.strong_block(10, 3, 0) == (0, 4) and twd.strong_block(10, 3, 2) == (7, 10)

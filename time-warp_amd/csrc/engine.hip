@@ -173,8 +173,7 @@ struct Lane {
     }
 
     // ---------------------------------------------------------- near heap (LDS)
-    __device__ __forceinline__ void near_push(int64_t t, uint64_t k) {
-        uint32_t i = near_n++;
+    __device__ __forceinline__ void near_sift_up(uint32_t i, int64_t t, uint64_t k) {
         while (i > 0) {
             uint32_t p = (i - 1) >> 1;
             int64_t pt = nt[p * TW_BLOCK];
@@ -187,12 +186,8 @@ struct Lane {
         nt[i * TW_BLOCK] = t;
         nk[i * TW_BLOCK] = k;
     }
-    __device__ __forceinline__ void near_pop() {
-        uint32_t n = --near_n;
-        if (n == 0) return;
-        int64_t t = nt[n * TW_BLOCK];
-        uint64_t k = nk[n * TW_BLOCK];
-        uint32_t i = 0;
+    __device__ __forceinline__ void near_sift_down(uint32_t i, int64_t t, uint64_t k) {
+        const uint32_t n = near_n;
         for (;;) {
             uint32_t c0 = 2 * i + 1;
             if (c0 >= n) break;
@@ -210,6 +205,27 @@ struct Lane {
         }
         nt[i * TW_BLOCK] = t;
         nk[i * TW_BLOCK] = k;
+    }
+    __device__ __forceinline__ void near_push(int64_t t, uint64_t k) { near_sift_up(near_n++, t, k); }
+    __device__ __forceinline__ void near_pop() {
+        uint32_t n = --near_n;
+        if (n == 0) return;
+        near_sift_down(0, nt[n * TW_BLOCK], nk[n * TW_BLOCK]);
+    }
+    // Re-key the live near entry of `slot` (queued with seq `old_seq`) in place;
+    // false if that entry is not on chip.  Keeps repeated throwTo of one thread
+    // from piling up superseded entries.
+    __device__ __forceinline__ bool near_rekey(uint32_t slot, uint32_t old_seq, int64_t t, uint64_t k) {
+        const uint64_t old = ((uint64_t)old_seq << 32) | slot;
+        for (uint32_t i = 0; i < near_n; ++i) {
+            if (nk[i * TW_BLOCK] == old) {
+                int64_t ot = nt[i * TW_BLOCK];
+                if (kless(t, k, ot, old)) near_sift_up(i, t, k);
+                else near_sift_down(i, t, k);
+                return true;
+            }
+        }
+        return false;
     }
 
     // ------------------------------------------------------ far heap (HBM, 4-ary)
@@ -418,10 +434,12 @@ struct Lane {
         if (a.z != tid) return;  // dead (slot free or reused): the map entry is unobservable
         if (a.w != 0) {         // queued: wake to now with a fresh seq
             uint32_t s = ++seq;
-            a.w = s;
             uint64_t k = ((uint64_t)s << 32) | ts;
-            if (near_n < TW_NEAR_CAP) near_push(now, k);
-            else push_far(now, k);
+            if (!near_rekey(ts, a.w, now, k)) {
+                if (near_n < TW_NEAR_CAP) near_push(now, k);
+                else push_far(now, k);
+            }
+            a.w = s;
         }
         if ((a.x >> 24) == 0) {
             a.x = (a.x & 0x00FFFFFFu) | (code << 24);
@@ -468,57 +486,76 @@ struct Lane {
         return false;
     }
 
-    // Run the thread's continuation until it yields or ends.
+    // Run the thread's continuation until it yields or ends (the ContT
+    // continuation of TimedT.hs:343-355).  Dispatch is a waterfall over the
+    // opcodes present in the wave: readfirstlane picks one, the lanes holding it
+    // execute it under a wave-uniform (scalar) switch, the others wait for their
+    // turn — lanes in lock-step take one pass per instruction.  Every yielding
+    // op funnels into one shared spawn + enqueue tail, which keeps the kernel
+    // small enough to stay resident in the instruction cache.
     __device__ __forceinline__ void step(Th& th, uint32_t slot) {
+        enum { GO, YIELD, SPAWN, THROWTO, EXIT, STOP };
         th_or_flags(th, F_STARTED);
-        for (uint32_t n = 0; n < TW_STEP_CAP; ++n) {
+        uint32_t n = 0;
+        for (;;) {
             uint32_t pc = th_pc(th);
-            if (pc >= c->n_insns) { fail(TW_REP_ERR_INSN); store_th(slot, th); return; }
+            if (pc >= c->n_insns || n >= TW_STEP_CAP) { fail(TW_REP_ERR_INSN); break; }
             uint2 in = P[pc];
-            uint32_t op = in.x & 0xFFu, a = (in.x >> 8) & 3u, b = in.x >> 16;
+            uint32_t op = in.x & 0xFFu;
+            uint32_t uop = __builtin_amdgcn_readfirstlane(op);
+            if (op != uop) continue;
+            ++n;
+            uint32_t a = (in.x >> 8) & 3u, b = in.x >> 16;
             int32_t imm = (int32_t)in.y;
             th_set_pc(th, pc + 1);
-            switch (op) {
+            int act = GO;
+            int64_t yt = 0;                               // YIELD: wake time
+            uint32_t cpc = 0, cnode = 0;                  // SPAWN: child entry + node
+            int64_t q0 = 0, q1 = 0, q2 = 0, q3 = 0;       //        child registers
+            int64_t tref = 0, tval = 0;                   // THROWTO target + payload
+            uint32_t tcode = 0;
+            switch (uop) {
             case TW_OP_NOP: break;
-            case TW_OP_END: die(th, slot); return;
-            case TW_OP_WAIT_REL: enqueue(th, slot, now + K[imm]); store_th(slot, th); return;
+            case TW_OP_END: die(th, slot); act = EXIT; break;
+            case TW_OP_WAIT_REL: yt = now + K[imm]; act = YIELD; break;
             case TW_OP_WAIT_ABS: {
                 int64_t t = K[imm];
-                enqueue(th, slot, t > now ? t : now);
-                store_th(slot, th);
-                return;
+                yt = t > now ? t : now;
+                act = YIELD;
+                break;
             }
             case TW_OP_WAIT_REG: {
                 int64_t d = getr(th, a);
-                enqueue(th, slot, now + (d > 0 ? d : 0));
-                store_th(slot, th);
-                return;
+                yt = now + (d > 0 ? d : 0);
+                act = YIELD;
+                break;
             }
             case TW_OP_FORK: {
                 uint32_t node = b == 0xFFFFu ? th.w1 : (uint32_t)getr(th, b & 3);
-                if (node >= c->N) { fail(TW_REP_ERR_INSN); store_th(slot, th); return; }
-                int64_t ref;
-                if (!spawn((uint32_t)imm, node, th.r0, th.r1, th.r2, th.r3, ref)) { store_th(slot, th); return; }
-                setr(th, a, ref);
-                enqueue(th, slot, now + 1);
-                store_th(slot, th);
-                return;
+                if (node >= c->N) { fail(TW_REP_ERR_INSN); act = STOP; break; }
+                cpc = (uint32_t)imm; cnode = node;
+                q0 = th.r0; q1 = th.r1; q2 = th.r2; q3 = th.r3;
+                act = SPAWN;
+                break;
             }
             case TW_OP_MYTID: setr(th, a, (int64_t)(((uint64_t)th.w2 << 32) | slot)); break;
-            case TW_OP_THROW_TO: throw_to(th, slot, getr(th, a), b & 0xFFu, getr(th, (b >> 8) & 3)); break;
+            case TW_OP_THROW_TO:
+                tref = getr(th, a); tcode = b & 0xFFu; tval = getr(th, (b >> 8) & 3);
+                act = THROWTO;
+                break;
             case TW_OP_THROW:
-                if (!unwind(th, slot, b & 0xFFu, getr(th, (b >> 8) & 3))) return;
+                if (!unwind(th, slot, b & 0xFFu, getr(th, (b >> 8) & 3))) act = EXIT;
                 break;
             case TW_OP_CATCH: {
                 uint32_t nf = th_nfr(th);
-                if (nf >= TW_MAX_FRAMES) { fail(TW_REP_ERR_FRAMES); store_th(slot, th); return; }
+                if (nf >= TW_MAX_FRAMES) { fail(TW_REP_ERR_FRAMES); act = STOP; break; }
                 setf(th, nf, (b << 16) | ((uint32_t)imm & 0xFFFFu));
                 th_set_nfr(th, nf + 1);
                 break;
             }
             case TW_OP_UNCATCH: {
                 uint32_t nf = th_nfr(th);
-                if (nf == 0 || (getf(th, nf - 1) >> 16) == 0) { fail(TW_REP_ERR_INSN); store_th(slot, th); return; }
+                if (nf == 0 || (getf(th, nf - 1) >> 16) == 0) { fail(TW_REP_ERR_INSN); act = STOP; break; }
                 th_set_nfr(th, nf - 1);
                 break;
             }
@@ -548,22 +585,22 @@ struct Lane {
             case TW_OP_NLOADX:
             case TW_OP_NSTOREX: {
                 uint64_t node = (uint64_t)getr(th, (b >> 8) & 3);
-                if (node >= c->N) { fail(TW_REP_ERR_INSN); store_th(slot, th); return; }
+                if (node >= c->N) { fail(TW_REP_ERR_INSN); act = STOP; break; }
                 int64_t* v = &c->nvars[ix(node * 4 + (b & 3))];
-                if (op == TW_OP_NLOADX) setr(th, a, *v);
+                if (uop == TW_OP_NLOADX) setr(th, a, *v);
                 else *v = getr(th, a);
                 break;
             }
             case TW_OP_LINK: setr(th, a, (int64_t)c->out_off[th.w1] + imm); break;
             case TW_OP_RLINK: {
                 uint64_t l = (uint64_t)getr(th, b & 3);
-                if (l >= c->L) { fail(TW_REP_ERR_INSN); store_th(slot, th); return; }
+                if (l >= c->L) { fail(TW_REP_ERR_INSN); act = STOP; break; }
                 setr(th, a, (int64_t)c->link_rev[l]);
                 break;
             }
-            case TW_OP_SEND: {
+            case TW_OP_SEND: {  // schedule (after d) (deliver ..) unless the link drops it
                 uint64_t link = (uint64_t)getr(th, a);
-                if (link >= c->L) { fail(TW_REP_ERR_INSN); store_th(slot, th); return; }
+                if (link >= c->L) { fail(TW_REP_ERR_INSN); act = STOP; break; }
                 uint32_t kind = b & 0xFFu;
                 int64_t payload = getr(th, (b >> 8) & 3);
                 uint32_t ord = c->link_ord[ix(link)];
@@ -574,34 +611,32 @@ struct Lane {
                     hash(th.w1, TW_KIND_DROP | kind, payload);
                     break;
                 }
-                int64_t ref;
-                if (!spawn(TW_PC_DELIVER_STUB, th.w1, payload, (int64_t)link, (int64_t)(e & 0x7FFFFFFFu), (int64_t)kind, ref)) { store_th(slot, th); return; }
-                enqueue(th, slot, now + 1);
-                store_th(slot, th);
-                return;
+                cpc = TW_PC_DELIVER_STUB; cnode = th.w1;
+                q0 = payload; q1 = (int64_t)link; q2 = (int64_t)(e & 0x7FFFFFFFu); q3 = (int64_t)kind;
+                act = SPAWN;
+                break;
             }
-            case TW_OP_DELIVER: {
-                uint64_t link = (uint64_t)getr(th, 1);
-                uint32_t kind = (uint32_t)getr(th, 3);
+            case TW_OP_DELIVER: {  // listener dispatch, ForkStrategy fork_ (MonadDialog.hs:232-256,317)
+                uint64_t link = (uint64_t)th.r1;
+                uint32_t kind = (uint32_t)th.r3;
                 uint32_t dst = c->link_dst[link];
                 uint32_t set = c->bind[ix(dst)];
                 uint32_t lpc = TW_PC_NONE;
                 if (set && kind < c->n_kinds) lpc = c->lpc[(size_t)(set - 1) * c->n_kinds + kind];
                 if (lpc == TW_PC_NONE) {
                     ++undeliv;
-                    hash(dst, TW_KIND_UNDELIV | kind, getr(th, 0));
+                    hash(dst, TW_KIND_UNDELIV | kind, th.r0);
                     break;
                 }
                 ++delivered;
-                hash(dst, TW_KIND_RECV | kind, getr(th, 0));
-                int64_t ref;
-                if (!spawn(lpc, dst, getr(th, 0), (int64_t)link, (int64_t)th.w1, (int64_t)kind, ref)) { store_th(slot, th); return; }
-                enqueue(th, slot, now + 1);
-                store_th(slot, th);
-                return;
+                hash(dst, TW_KIND_RECV | kind, th.r0);
+                cpc = lpc; cnode = dst;
+                q0 = th.r0; q1 = (int64_t)link; q2 = (int64_t)th.w1; q3 = (int64_t)kind;
+                act = SPAWN;
+                break;
             }
             case TW_OP_LISTEN:
-                if ((uint32_t)imm >= c->n_sets) { fail(TW_REP_ERR_INSN); store_th(slot, th); return; }
+                if ((uint32_t)imm >= c->n_sets) { fail(TW_REP_ERR_INSN); act = STOP; break; }
                 c->bind[ix(th.w1)] = (uint32_t)imm + 1;
                 c->bind_own[ix(th.w1)] = b ? th.w2 : 0xFFFFFFFFu;
                 break;
@@ -610,45 +645,62 @@ struct Lane {
                 c->bind_own[ix(th.w1)] = 0xFFFFFFFFu;
                 break;
             case TW_OP_TRACE: hash(th.w1, TW_KIND_TRACE | ((uint32_t)imm & 0xFFFFu), getr(th, a)); break;
-            case TW_OP_TMO_BEGIN: {
-                if (tmo_ctr >= c->T) { fail(TW_REP_ERR_INSN); store_th(slot, th); return; }
+            case TW_OP_TMO_BEGIN: {  // schedule (after t) watchdog (TimedT.hs:373-375)
+                if (tmo_ctr >= c->T) { fail(TW_REP_ERR_INSN); act = STOP; break; }
                 uint32_t e = tmo_ctr++;
                 c->tmo_done[ix(e)] = 0;
                 setr(th, a, e);
-                int64_t ref;
-                if (!spawn(TW_PC_WATCHDOG_STUB, th.w1, (int64_t)(((uint64_t)th.w2 << 32) | slot), (int64_t)e, K[imm], 0, ref)) { store_th(slot, th); return; }
-                enqueue(th, slot, now + 1);
-                store_th(slot, th);
-                return;
+                cpc = TW_PC_WATCHDOG_STUB; cnode = th.w1;
+                q0 = (int64_t)(((uint64_t)th.w2 << 32) | slot); q1 = (int64_t)e; q2 = K[imm]; q3 = 0;
+                act = SPAWN;
+                break;
             }
             case TW_OP_TMO_PUSH: {
                 uint32_t nf = th_nfr(th);
-                if (nf >= TW_MAX_FRAMES) { fail(TW_REP_ERR_FRAMES); store_th(slot, th); return; }
+                if (nf >= TW_MAX_FRAMES) { fail(TW_REP_ERR_FRAMES); act = STOP; break; }
                 setf(th, nf, (uint32_t)getr(th, a) & 0xFFFFu);
                 th_set_nfr(th, nf + 1);
                 break;
             }
             case TW_OP_TMO_END: {
                 uint32_t nf = th_nfr(th);
-                if (nf == 0 || (getf(th, nf - 1) >> 16) != 0) { fail(TW_REP_ERR_INSN); store_th(slot, th); return; }
+                if (nf == 0 || (getf(th, nf - 1) >> 16) != 0) { fail(TW_REP_ERR_INSN); act = STOP; break; }
                 uint32_t ep = getf(th, nf - 1) & 0xFFFFu;
                 th_set_nfr(th, nf - 1);
                 if (ep < c->T) c->tmo_done[ix(ep)] = 1;
                 break;
             }
             case TW_OP_TMO_FIRE: {
-                uint64_t e = (uint64_t)getr(th, 1);
-                if (e < c->T && !c->tmo_done[ix(e)]) throw_to(th, slot, getr(th, 0), TW_EXC_TIMEOUT, 0);
+                uint64_t e = (uint64_t)th.r1;
+                if (e < c->T && !c->tmo_done[ix(e)]) {
+                    tref = th.r0; tcode = TW_EXC_TIMEOUT; tval = 0;
+                    act = THROWTO;
+                }
                 break;
             }
             default:
                 fail(TW_REP_ERR_INSN);
-                store_th(slot, th);
-                return;
+                act = STOP;
+                break;
             }
-            if (status != TW_REP_RUNNING) { store_th(slot, th); return; }
+            if (act == THROWTO) {
+                throw_to(th, slot, tref, tcode, tval);
+                act = GO;
+            }
+            if (act == SPAWN) {  // fork (TimedT.hs:326-342): child at now, parent waits 1 µs
+                int64_t ref;
+                if (!spawn(cpc, cnode, q0, q1, q2, q3, ref)) break;
+                if (uop == TW_OP_FORK) setr(th, a, ref);
+                yt = now + 1;
+                act = YIELD;
+            }
+            if (act == YIELD) {
+                enqueue(th, slot, yt);
+                break;
+            }
+            if (act == EXIT) return;
+            if (act == STOP || status != TW_REP_RUNNING) break;
         }
-        fail(TW_REP_ERR_INSN);
         store_th(slot, th);
     }
 };
