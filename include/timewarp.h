@@ -256,10 +256,11 @@ static inline uint64_t tw_mix64(uint64_t z) {
     z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
     return z ^ (z >> 31);
 }
+/* (t, kind) packs injectively into 64 bits for t < 2^44 µs (~203 days) and
+ * kind < 2^20; val enters through its own mix (mix64(0) = 0). */
 static inline uint64_t tw_term(int64_t t, uint32_t kind, int64_t val) {
-    uint64_t h = tw_mix64((uint64_t)t + 0x9e3779b97f4a7c15ull);
-    h = tw_mix64(h ^ ((uint64_t)kind * 0xd6e8feb86659fd93ull));
-    return tw_mix64(h ^ (uint64_t)val);
+    uint64_t v = val ? tw_mix64((uint64_t)val ^ 0x9e3779b97f4a7c15ull) : 0ull;
+    return tw_mix64((((uint64_t)t << 20) | kind) ^ v);
 }
 #define TW_KIND_RESUME 0x10000u   /* | pc        : a thread resumed at pc       */
 #define TW_KIND_EXC 0x20000u      /* | exc code  : async exception delivered    */

@@ -40,9 +40,25 @@
 #endif
 #define TW_BLOCK 64             // one wavefront per workgroup
 #define TW_RUNS 4               // monotone far-queue runs per replica
+#define TW_RCACHE 4             // write-through thread-record cache entries per lane (LDS)
 #define TW_STEP_CAP (1u << 22)  // instructions per thread step (== oracle kStepCap)
 
+// Explicit address spaces: generic (flat) pointers would make every HBM and
+// LDS access a flat_* instruction that waits on both memory counters.
+#if defined(__HIP_DEVICE_COMPILE__)
+#define GAS __attribute__((address_space(1)))
+#define LAS __attribute__((address_space(3)))
+#else
+#define GAS
+#define LAS
+#endif
+
 namespace {
+
+template <class T>
+__device__ __forceinline__ T GAS* gp(T* p) {
+    return (T GAS*)p;
+}
 
 // ------------------------------------------------------------------ layout
 // Thread slot record: 64 B, [slot][replica].
@@ -58,22 +74,29 @@ struct Th {
     int64_t r0, r1, r2, r3;
 };
 
-// Registers and frames are selected, never indexed: a runtime index into a
-// private array would spill the record to scratch.
+// Registers and frames are selected with mask arithmetic, never indexed: a
+// select chain over the fields gets folded into an indexed load, which pins
+// the whole record in scratch memory.
 __device__ __forceinline__ int64_t getr(const Th& t, uint32_t a) {
-    return a == 0 ? t.r0 : a == 1 ? t.r1 : a == 2 ? t.r2 : t.r3;
+    const int64_t m0 = -(int64_t)(a == 0), m1 = -(int64_t)(a == 1), m2 = -(int64_t)(a == 2), m3 = -(int64_t)(a == 3);
+    return (t.r0 & m0) | (t.r1 & m1) | (t.r2 & m2) | (t.r3 & m3);
 }
 __device__ __forceinline__ void setr(Th& t, uint32_t a, int64_t v) {
-    t.r0 = a == 0 ? v : t.r0;
-    t.r1 = a == 1 ? v : t.r1;
-    t.r2 = a == 2 ? v : t.r2;
-    t.r3 = a == 3 ? v : t.r3;
+    const int64_t m0 = -(int64_t)(a == 0), m1 = -(int64_t)(a == 1), m2 = -(int64_t)(a == 2), m3 = -(int64_t)(a == 3);
+    t.r0 = (v & m0) | (t.r0 & ~m0);
+    t.r1 = (v & m1) | (t.r1 & ~m1);
+    t.r2 = (v & m2) | (t.r2 & ~m2);
+    t.r3 = (v & m3) | (t.r3 & ~m3);
 }
-__device__ __forceinline__ uint32_t getf(const Th& t, uint32_t i) { return i == 0 ? t.f0 : i == 1 ? t.f1 : t.f2; }
+__device__ __forceinline__ uint32_t getf(const Th& t, uint32_t i) {
+    const uint32_t m0 = 0u - (i == 0), m1 = 0u - (i == 1), m2 = 0u - (i == 2);
+    return (t.f0 & m0) | (t.f1 & m1) | (t.f2 & m2);
+}
 __device__ __forceinline__ void setf(Th& t, uint32_t i, uint32_t v) {
-    t.f0 = i == 0 ? v : t.f0;
-    t.f1 = i == 1 ? v : t.f1;
-    t.f2 = i == 2 ? v : t.f2;
+    const uint32_t m0 = 0u - (i == 0), m1 = 0u - (i == 1), m2 = 0u - (i == 2);
+    t.f0 = (v & m0) | (t.f0 & ~m0);
+    t.f1 = (v & m1) | (t.f1 & ~m1);
+    t.f2 = (v & m2) | (t.f2 & ~m2);
 }
 
 #define F_STARTED 1u
@@ -131,10 +154,10 @@ __device__ __forceinline__ uint64_t mix64(uint64_t z) {
     z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
     return z ^ (z >> 31);
 }
+// == tw_term of include/timewarp.h (one mix64 for the common val == 0 case)
 __device__ __forceinline__ uint64_t term(int64_t t, uint32_t kind, int64_t val) {
-    uint64_t h = mix64((uint64_t)t + 0x9e3779b97f4a7c15ull);
-    h = mix64(h ^ ((uint64_t)kind * 0xd6e8feb86659fd93ull));
-    return mix64(h ^ (uint64_t)val);
+    uint64_t v = val ? mix64((uint64_t)val ^ 0x9e3779b97f4a7c15ull) : 0ull;
+    return mix64((((uint64_t)t << 20) | kind) ^ v);
 }
 
 // ------------------------------------------------------------ event keys
@@ -147,16 +170,20 @@ struct Lane {
     const Dev* c;
     uint32_t r;       // replica
     // LDS near heap of this lane: element j at base[j * TW_BLOCK]
-    int64_t* nt;
-    uint64_t* nk;
-    // program image and constant pool (LDS copy when it fits)
-    const uint2* P;
-    const int64_t* K;
+    int64_t LAS* nt;
+    uint64_t LAS* nk;
+    // program image and constant pool (LDS copy)
+    const uint2 LAS* P;
+    const int64_t LAS* K;
     // far runs: head index, count, head key, tail key (indexed only by unrolled constants)
     uint32_t rh[TW_RUNS], rc[TW_RUNS];
     int64_t rt[TW_RUNS], ut[TW_RUNS];
     uint64_t rk[TW_RUNS], uk[TW_RUNS];
     uint32_t next_free;  // cached free_stk[free_top-1] (prefetched)
+    // write-through record cache in LDS: entry e quad q at rcache[(e*4+q)*TW_BLOCK]
+    uint4 LAS* rcache;
+    uint32_t ctag[TW_RCACHE];
+    uint32_t cptr;
     // cached replica scalars
     int64_t now;
     uint32_t seq, tidc, live, near_n, far_n, status, main_exc, free_top, tmo_ctr;
@@ -229,9 +256,9 @@ struct Lane {
     }
 
     // ------------------------------------------------------ far heap (HBM, 4-ary)
-    __device__ __forceinline__ uint4 far_ld(uint32_t i) const { return c->far[ix(i)]; }
+    __device__ __forceinline__ uint4 far_ld(uint32_t i) const { return gp(c->far)[ix(i)]; }
     __device__ __forceinline__ void far_st(uint32_t i, int64_t t, uint64_t k) const {
-        c->far[ix(i)] = make_uint4((uint32_t)t, (uint32_t)((uint64_t)t >> 32), (uint32_t)k, (uint32_t)(k >> 32));
+        gp(c->far)[ix(i)] = make_uint4((uint32_t)t, (uint32_t)((uint64_t)t >> 32), (uint32_t)k, (uint32_t)(k >> 32));
     }
     __device__ __forceinline__ void far_push(int64_t t, uint64_t k) {
         if (far_n >= c->Q) { fail(TW_REP_ERR_QUEUE); return; }
@@ -242,7 +269,7 @@ struct Lane {
             int64_t pt = (int64_t)(((uint64_t)e.y << 32) | e.x);
             uint64_t pk = ((uint64_t)e.w << 32) | e.z;
             if (!kless(t, k, pt, pk)) break;
-            c->far[ix(i)] = e;
+            gp(c->far)[ix(i)] = e;
             i = p;
         }
         far_st(i, t, k);
@@ -293,8 +320,8 @@ struct Lane {
     // head prefetched.  TimedT scenarios park threads in monotone streams
     // (killers at one absolute time, sleepForever timers, re-stamped victims of
     // a killer sweep), so the heap sees only stragglers.
-    __device__ __forceinline__ uint4* run_at(uint32_t j, uint32_t pos) const {
-        return c->runs + ((size_t)j * c->Cr + pos) * c->R + r;
+    __device__ __forceinline__ uint4 GAS* run_at(uint32_t j, uint32_t pos) const {
+        return gp(c->runs) + ((size_t)j * c->Cr + pos) * c->R + r;
     }
     __device__ __forceinline__ bool run_push(int64_t t, uint64_t k) {
         if (c->Cr == 0) return false;
@@ -362,9 +389,7 @@ struct Lane {
     }
 
     // ------------------------------------------------------------- slots
-    __device__ __forceinline__ void load_th(uint32_t slot, Th& th) const {
-        const uint4* p = c->slots + ix(slot) * 4;
-        uint4 a = p[0], b = p[1], d = p[2], e = p[3];
+    __device__ __forceinline__ static void unpack(Th& th, uint4 a, uint4 b, uint4 d, uint4 e) {
         th.w0 = a.x; th.w1 = a.y; th.w2 = a.z; th.w3 = a.w;
         th.f0 = b.x; th.f1 = b.y; th.f2 = b.z; th.w7 = b.w;
         th.r0 = (int64_t)(((uint64_t)d.y << 32) | d.x);
@@ -372,32 +397,68 @@ struct Lane {
         th.r2 = (int64_t)(((uint64_t)e.y << 32) | e.x);
         th.r3 = (int64_t)(((uint64_t)e.w << 32) | e.z);
     }
-    __device__ __forceinline__ void store_th(uint32_t slot, const Th& th) const {
-        uint4* p = c->slots + ix(slot) * 4;
-        p[0] = make_uint4(th.w0, th.w1, th.w2, th.w3);
-        p[1] = make_uint4(th.f0, th.f1, th.f2, th.w7);
-        p[2] = make_uint4((uint32_t)th.r0, (uint32_t)((uint64_t)th.r0 >> 32), (uint32_t)th.r1,
-                          (uint32_t)((uint64_t)th.r1 >> 32));
-        p[3] = make_uint4((uint32_t)th.r2, (uint32_t)((uint64_t)th.r2 >> 32), (uint32_t)th.r3,
-                          (uint32_t)((uint64_t)th.r3 >> 32));
+    __device__ __forceinline__ static void pack(const Th& th, uint4& a, uint4& b, uint4& d, uint4& e) {
+        a = make_uint4(th.w0, th.w1, th.w2, th.w3);
+        b = make_uint4(th.f0, th.f1, th.f2, th.w7);
+        d = make_uint4((uint32_t)th.r0, (uint32_t)((uint64_t)th.r0 >> 32), (uint32_t)th.r1,
+                       (uint32_t)((uint64_t)th.r1 >> 32));
+        e = make_uint4((uint32_t)th.r2, (uint32_t)((uint64_t)th.r2 >> 32), (uint32_t)th.r3,
+                       (uint32_t)((uint64_t)th.r3 >> 32));
+    }
+    __device__ __forceinline__ int cache_find(uint32_t slot) const {
+        int h = -1;
+#pragma unroll
+        for (int e = 0; e < TW_RCACHE; ++e)
+            if (ctag[e] == slot) h = e;
+        return h;
+    }
+    // Thread records: HBM is authoritative (write-through); the LDS cache
+    // serves the common case of popping a thread whose record this lane wrote
+    // a few events earlier (a fork child, the forking parent, a throwTo victim).
+    __device__ __forceinline__ void load_th(uint32_t slot, Th& th) const {
+        int e = cache_find(slot);
+        if (e >= 0) {
+            const uint4 LAS* q = rcache + (size_t)e * 4 * TW_BLOCK;
+            unpack(th, q[0], q[TW_BLOCK], q[2 * TW_BLOCK], q[3 * TW_BLOCK]);
+            return;
+        }
+        const uint4 GAS* p = gp(c->slots) + ix(slot) * 4;
+        unpack(th, p[0], p[1], p[2], p[3]);
+    }
+    __device__ __forceinline__ void store_th(uint32_t slot, const Th& th) {
+        uint4 a, b, d, f;
+        pack(th, a, b, d, f);
+        uint4 GAS* p = gp(c->slots) + ix(slot) * 4;
+        p[0] = a; p[1] = b; p[2] = d; p[3] = f;
+        int e = cache_find(slot);
+        if (e < 0) {
+            e = (int)cptr;
+            cptr = (cptr + 1) & (TW_RCACHE - 1);
+#pragma unroll
+            for (int j = 0; j < TW_RCACHE; ++j)
+                if (j == e) ctag[j] = slot;
+        }
+        uint4 LAS* q = rcache + (size_t)e * 4 * TW_BLOCK;
+        q[0] = a; q[TW_BLOCK] = b; q[2 * TW_BLOCK] = d; q[3 * TW_BLOCK] = f;
     }
     // Free-slot stack; its top is cached in a register and the next one is
     // prefetched at every pop, so a fork never waits on this load.
     __device__ __forceinline__ uint32_t alloc_slot() {
         if (free_top == 0) { fail(TW_REP_ERR_SLOTS); return 0xFFFFFFFFu; }
         uint32_t s = next_free;
-        if (--free_top) next_free = c->free_stk[ix(free_top - 1)];
+        if (--free_top) next_free = gp(c->free_stk)[ix(free_top - 1)];
         return s;
     }
     __device__ __forceinline__ void free_slot(uint32_t slot) {
-        c->free_stk[ix(free_top++)] = slot;
+        gp(c->free_stk)[ix(free_top++)] = slot;
         next_free = slot;
     }
 
     // Commutative per-node trace hash: a no-return 64-bit atomic add, so the
     // event's critical path never waits on the node's hash line.
     __device__ __forceinline__ void hash(uint32_t node, uint32_t kind, int64_t val) {
-        atomicAdd((unsigned long long*)(c->hash + ix(node)), (unsigned long long)term(now, kind, val));
+        __hip_atomic_fetch_add((unsigned long long GAS*)(gp(c->hash) + ix(node)), (unsigned long long)term(now, kind, val),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 
     // Create a thread queued at now (fork, TimedT.hs:326-339).  Returns its ref.
@@ -429,31 +490,31 @@ struct Lane {
             if (th_exc(self) == 0) { th_set_exc(self, code); self.w7 = (uint32_t)val; }
             return;
         }
-        uint4* p = c->slots + ix(ts) * 4;
-        uint4 a = p[0];
-        if (a.z != tid) return;  // dead (slot free or reused): the map entry is unobservable
-        if (a.w != 0) {         // queued: wake to now with a fresh seq
+        Th t;
+        load_th(ts, t);
+        if (t.w2 != tid) return;  // dead (slot free or reused): the map entry is unobservable
+        if (t.w3 != 0) {         // queued: wake to now with a fresh seq
             uint32_t s = ++seq;
             uint64_t k = ((uint64_t)s << 32) | ts;
-            if (!near_rekey(ts, a.w, now, k)) {
+            if (!near_rekey(ts, t.w3, now, k)) {
                 if (near_n < TW_NEAR_CAP) near_push(now, k);
                 else push_far(now, k);
             }
-            a.w = s;
+            t.w3 = s;
         }
-        if ((a.x >> 24) == 0) {
-            a.x = (a.x & 0x00FFFFFFu) | (code << 24);
-            p[1].w = (uint32_t)val;
+        if (th_exc(t) == 0) {
+            th_set_exc(t, code);
+            t.w7 = (uint32_t)val;
         }
-        p[0] = a;
+        store_th(ts, t);
     }
 
     // Thread ends (END or uncaught exception).
     __device__ __forceinline__ void die(Th& th, uint32_t slot) {
         uint32_t node = th.w1;
-        if (c->bind[ix(node)] && c->bind_own[ix(node)] == th.w2) {
-            c->bind[ix(node)] = 0;
-            c->bind_own[ix(node)] = 0xFFFFFFFFu;
+        if (gp(c->bind)[ix(node)] && gp(c->bind_own)[ix(node)] == th.w2) {
+            gp(c->bind)[ix(node)] = 0;
+            gp(c->bind_own)[ix(node)] = 0xFFFFFFFFu;
         }
         th.w2 = 0xFFFFFFFFu;  // invalidate refs to this slot
         th.w3 = 0;
@@ -463,21 +524,23 @@ struct Lane {
 
     // Raise `code` in th; true if a catch frame took it (pc set to handler).
     __device__ __forceinline__ bool unwind(Th& th, uint32_t slot, uint32_t code, int64_t val) {
-        uint32_t n = th_nfr(th);
-        while (n > 0) {
-            uint32_t f = getf(th, --n);
-            uint32_t mask = f >> 16;
-            if (mask == 0) {
-                uint32_t e = f & 0xFFFFu;
-                if (e < c->T) c->tmo_done[ix(e)] = 1;
-                continue;
-            }
-            if (mask & (1u << code)) {
-                th_set_nfr(th, n);
-                th_set_pc(th, f & 0xFFFFu);
-                th.r0 = val;
-                th.r3 = code;
-                return true;
+        const uint32_t n = th_nfr(th);
+        // innermost frame first; constant indices keep the record in registers
+#pragma unroll
+        for (int i = TW_MAX_FRAMES - 1; i >= 0; --i) {
+            if ((uint32_t)i < n) {
+                uint32_t f = i == 0 ? th.f0 : i == 1 ? th.f1 : th.f2;
+                uint32_t mask = f >> 16;
+                if (mask == 0) {
+                    uint32_t e = f & 0xFFFFu;
+                    if (e < c->T) gp(c->tmo_done)[ix(e)] = 1;
+                } else if (mask & (1u << code)) {
+                    th_set_nfr(th, (uint32_t)i);
+                    th_set_pc(th, f & 0xFFFFu);
+                    th.r0 = val;
+                    th.r3 = code;
+                    return true;
+                }
             }
         }
         th_set_nfr(th, 0);
@@ -497,14 +560,15 @@ struct Lane {
         enum { GO, YIELD, SPAWN, THROWTO, EXIT, STOP };
         th_or_flags(th, F_STARTED);
         uint32_t n = 0;
+        uint32_t pc = th_pc(th);
+        if (pc >= c->n_insns) { fail(TW_REP_ERR_INSN); store_th(slot, th); return; }
+        uint2 in = P[pc];
         for (;;) {
-            uint32_t pc = th_pc(th);
-            if (pc >= c->n_insns || n >= TW_STEP_CAP) { fail(TW_REP_ERR_INSN); break; }
-            uint2 in = P[pc];
             uint32_t op = in.x & 0xFFu;
             uint32_t uop = __builtin_amdgcn_readfirstlane(op);
             if (op != uop) continue;
-            ++n;
+            if (++n > TW_STEP_CAP) { fail(TW_REP_ERR_INSN); break; }
+            uint2 nx = P[pc + 1];  // prefetch the fall-through instruction (image padded by one)
             uint32_t a = (in.x >> 8) & 3u, b = in.x >> 16;
             int32_t imm = (int32_t)in.y;
             th_set_pc(th, pc + 1);
@@ -580,22 +644,22 @@ struct Lane {
             case TW_OP_JNEI: if (getr(th, a) != (int64_t)(int16_t)b) th_set_pc(th, (uint32_t)imm); break;
             case TW_OP_NOW: setr(th, a, now); break;
             case TW_OP_NODE: setr(th, a, th.w1); break;
-            case TW_OP_NLOAD: setr(th, a, c->nvars[ix((size_t)th.w1 * 4 + (b & 3))]); break;
-            case TW_OP_NSTORE: c->nvars[ix((size_t)th.w1 * 4 + (b & 3))] = getr(th, a); break;
+            case TW_OP_NLOAD: setr(th, a, gp(c->nvars)[ix((size_t)th.w1 * 4 + (b & 3))]); break;
+            case TW_OP_NSTORE: gp(c->nvars)[ix((size_t)th.w1 * 4 + (b & 3))] = getr(th, a); break;
             case TW_OP_NLOADX:
             case TW_OP_NSTOREX: {
                 uint64_t node = (uint64_t)getr(th, (b >> 8) & 3);
                 if (node >= c->N) { fail(TW_REP_ERR_INSN); act = STOP; break; }
-                int64_t* v = &c->nvars[ix(node * 4 + (b & 3))];
+                int64_t GAS* v = &gp(c->nvars)[ix(node * 4 + (b & 3))];
                 if (uop == TW_OP_NLOADX) setr(th, a, *v);
                 else *v = getr(th, a);
                 break;
             }
-            case TW_OP_LINK: setr(th, a, (int64_t)c->out_off[th.w1] + imm); break;
+            case TW_OP_LINK: setr(th, a, (int64_t)gp(c->out_off)[th.w1] + imm); break;
             case TW_OP_RLINK: {
                 uint64_t l = (uint64_t)getr(th, b & 3);
                 if (l >= c->L) { fail(TW_REP_ERR_INSN); act = STOP; break; }
-                setr(th, a, (int64_t)c->link_rev[l]);
+                setr(th, a, (int64_t)gp(c->link_rev)[l]);
                 break;
             }
             case TW_OP_SEND: {  // schedule (after d) (deliver ..) unless the link drops it
@@ -603,9 +667,9 @@ struct Lane {
                 if (link >= c->L) { fail(TW_REP_ERR_INSN); act = STOP; break; }
                 uint32_t kind = b & 0xFFu;
                 int64_t payload = getr(th, (b >> 8) & 3);
-                uint32_t ord = c->link_ord[ix(link)];
-                c->link_ord[ix(link)] = ord + 1;
-                uint32_t e = c->link_table ? c->link_table[ix((size_t)link * c->D + ord % c->D)] : 0u;
+                uint32_t ord = gp(c->link_ord)[ix(link)];
+                gp(c->link_ord)[ix(link)] = ord + 1;
+                uint32_t e = c->link_table ? gp(c->link_table)[ix((size_t)link * c->D + ord % c->D)] : 0u;
                 if (e & TW_LINK_DROP) {
                     ++dropped;
                     hash(th.w1, TW_KIND_DROP | kind, payload);
@@ -619,10 +683,10 @@ struct Lane {
             case TW_OP_DELIVER: {  // listener dispatch, ForkStrategy fork_ (MonadDialog.hs:232-256,317)
                 uint64_t link = (uint64_t)th.r1;
                 uint32_t kind = (uint32_t)th.r3;
-                uint32_t dst = c->link_dst[link];
-                uint32_t set = c->bind[ix(dst)];
+                uint32_t dst = gp(c->link_dst)[link];
+                uint32_t set = gp(c->bind)[ix(dst)];
                 uint32_t lpc = TW_PC_NONE;
-                if (set && kind < c->n_kinds) lpc = c->lpc[(size_t)(set - 1) * c->n_kinds + kind];
+                if (set && kind < c->n_kinds) lpc = gp(c->lpc)[(size_t)(set - 1) * c->n_kinds + kind];
                 if (lpc == TW_PC_NONE) {
                     ++undeliv;
                     hash(dst, TW_KIND_UNDELIV | kind, th.r0);
@@ -637,18 +701,18 @@ struct Lane {
             }
             case TW_OP_LISTEN:
                 if ((uint32_t)imm >= c->n_sets) { fail(TW_REP_ERR_INSN); act = STOP; break; }
-                c->bind[ix(th.w1)] = (uint32_t)imm + 1;
-                c->bind_own[ix(th.w1)] = b ? th.w2 : 0xFFFFFFFFu;
+                gp(c->bind)[ix(th.w1)] = (uint32_t)imm + 1;
+                gp(c->bind_own)[ix(th.w1)] = b ? th.w2 : 0xFFFFFFFFu;
                 break;
             case TW_OP_UNLISTEN:
-                c->bind[ix(th.w1)] = 0;
-                c->bind_own[ix(th.w1)] = 0xFFFFFFFFu;
+                gp(c->bind)[ix(th.w1)] = 0;
+                gp(c->bind_own)[ix(th.w1)] = 0xFFFFFFFFu;
                 break;
             case TW_OP_TRACE: hash(th.w1, TW_KIND_TRACE | ((uint32_t)imm & 0xFFFFu), getr(th, a)); break;
             case TW_OP_TMO_BEGIN: {  // schedule (after t) watchdog (TimedT.hs:373-375)
                 if (tmo_ctr >= c->T) { fail(TW_REP_ERR_INSN); act = STOP; break; }
                 uint32_t e = tmo_ctr++;
-                c->tmo_done[ix(e)] = 0;
+                gp(c->tmo_done)[ix(e)] = 0;
                 setr(th, a, e);
                 cpc = TW_PC_WATCHDOG_STUB; cnode = th.w1;
                 q0 = (int64_t)(((uint64_t)th.w2 << 32) | slot); q1 = (int64_t)e; q2 = K[imm]; q3 = 0;
@@ -667,12 +731,12 @@ struct Lane {
                 if (nf == 0 || (getf(th, nf - 1) >> 16) != 0) { fail(TW_REP_ERR_INSN); act = STOP; break; }
                 uint32_t ep = getf(th, nf - 1) & 0xFFFFu;
                 th_set_nfr(th, nf - 1);
-                if (ep < c->T) c->tmo_done[ix(ep)] = 1;
+                if (ep < c->T) gp(c->tmo_done)[ix(ep)] = 1;
                 break;
             }
             case TW_OP_TMO_FIRE: {
                 uint64_t e = (uint64_t)th.r1;
-                if (e < c->T && !c->tmo_done[ix(e)]) {
+                if (e < c->T && !gp(c->tmo_done)[ix(e)]) {
                     tref = th.r0; tcode = TW_EXC_TIMEOUT; tval = 0;
                     act = THROWTO;
                 }
@@ -700,6 +764,11 @@ struct Lane {
             }
             if (act == EXIT) return;
             if (act == STOP || status != TW_REP_RUNNING) break;
+            uint32_t npc = th_pc(th);
+            if (npc >= c->n_insns) { fail(TW_REP_ERR_INSN); break; }
+            if (npc == pc + 1) in = nx;
+            else in = P[npc];
+            pc = npc;
         }
         store_th(slot, th);
     }
@@ -710,15 +779,15 @@ __global__ void __launch_bounds__(TW_BLOCK) tw_init_kernel(Dev c, uint32_t main_
                                                           const int64_t* main_regs, const int64_t* nv_init) {
     uint32_t r = blockIdx.x * TW_BLOCK + threadIdx.x;
     if (r >= c.R) return;
-    for (uint32_t f = 0; f < SC_COUNT; ++f) c.scal[(size_t)f * c.R + r] = 0;
-    c.scal[(size_t)SC_THREADS * c.R + r] = 1;
-    c.scal[(size_t)SC_TIDC * c.R + r] = 1;
-    c.scal[(size_t)SC_STATUS * c.R + r] = TW_REP_RUNNING;
-    c.scal[(size_t)SC_PENDING_MAIN * c.R + r] = 1;
+    for (uint32_t f = 0; f < SC_COUNT; ++f) gp(c.scal)[(size_t)f * c.R + r] = 0;
+    gp(c.scal)[(size_t)SC_THREADS * c.R + r] = 1;
+    gp(c.scal)[(size_t)SC_TIDC * c.R + r] = 1;
+    gp(c.scal)[(size_t)SC_STATUS * c.R + r] = TW_REP_RUNNING;
+    gp(c.scal)[(size_t)SC_PENDING_MAIN * c.R + r] = 1;
     // free stack: slots S-1 .. 1 (slot 0 = main), pops hand out 1, 2, 3, ...
-    for (uint32_t k = 0; k + 1 < c.S; ++k) c.free_stk[(size_t)k * c.R + r] = c.S - 1 - k;
-    c.scal[(size_t)SC_FREE_TOP * c.R + r] = c.S - 1;
-    uint4* p = c.slots + (size_t)r * 4;  // slot 0
+    for (uint32_t k = 0; k + 1 < c.S; ++k) gp(c.free_stk)[(size_t)k * c.R + r] = c.S - 1 - k;
+    gp(c.scal)[(size_t)SC_FREE_TOP * c.R + r] = c.S - 1;
+    uint4* p = gp(c.slots) + (size_t)r * 4;  // slot 0
     uint32_t w0 = (main_pc & 0xFFFFu) | (F_MAIN << 18);
     p[0] = make_uint4(w0, main_node, 0u, 0u);
     p[1] = make_uint4(0u, 0u, 0u, 0u);
@@ -728,31 +797,34 @@ __global__ void __launch_bounds__(TW_BLOCK) tw_init_kernel(Dev c, uint32_t main_
     p[2] = make_uint4((uint32_t)m[0], (uint32_t)((uint64_t)m[0] >> 32), (uint32_t)m[1], (uint32_t)((uint64_t)m[1] >> 32));
     p[3] = make_uint4((uint32_t)m[2], (uint32_t)((uint64_t)m[2] >> 32), (uint32_t)m[3], (uint32_t)((uint64_t)m[3] >> 32));
     if (nv_init)
-        for (uint32_t i = 0; i < c.N * 4; ++i) c.nvars[(size_t)i * c.R + r] = nv_init[i];
-    for (uint32_t n = 0; n < c.N; ++n) c.bind_own[(size_t)n * c.R + r] = 0xFFFFFFFFu;
+        for (uint32_t i = 0; i < c.N * 4; ++i) gp(c.nvars)[(size_t)i * c.R + r] = nv_init[i];
+    for (uint32_t n = 0; n < c.N; ++n) gp(c.bind_own)[(size_t)n * c.R + r] = 0xFFFFFFFFu;
 }
 
 // LDS per workgroup: near heap keys [NEAR_CAP][64] x 2 words, then (when it
 // fits) the program image and constant pool, so instruction fetch and time
 // constants never leave the CU.
-__host__ __device__ constexpr size_t near_lds_bytes() { return (size_t)TW_NEAR_CAP * TW_BLOCK * 16; }
+__host__ __device__ constexpr size_t near_lds_bytes() {
+    return (size_t)TW_NEAR_CAP * TW_BLOCK * 16 + (size_t)TW_RCACHE * 4 * TW_BLOCK * 16;
+}
 
-template <bool PLDS>
-__global__ void __launch_bounds__(TW_BLOCK) tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events,
+__global__ void __launch_bounds__(TW_BLOCK) __attribute__((amdgpu_waves_per_eu(1, 2))) tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events,
                                                          uint32_t budget) {
-    extern __shared__ __attribute__((aligned(16))) uint64_t lds[];
-    int64_t* s_t = (int64_t*)lds;
-    uint64_t* s_k = lds + TW_NEAR_CAP * TW_BLOCK;
-    uint2* s_p = (uint2*)(lds + 2 * TW_NEAR_CAP * TW_BLOCK);
-    int64_t* s_c = (int64_t*)(s_p + c.n_insns);
-    if (PLDS) {
-        for (uint32_t i = threadIdx.x; i < c.n_insns; i += TW_BLOCK) s_p[i] = c.insns[i];
-        for (uint32_t i = threadIdx.x; i < c.n_consts; i += TW_BLOCK) s_c[i] = c.consts[i];
+    extern __shared__ __attribute__((aligned(16))) uint64_t lds_raw[];
+    uint64_t LAS* lds = (uint64_t LAS*)lds_raw;
+    int64_t LAS* s_t = (int64_t LAS*)lds;
+    uint64_t LAS* s_k = lds + TW_NEAR_CAP * TW_BLOCK;
+    uint4 LAS* s_rc = (uint4 LAS*)(lds + 2 * TW_NEAR_CAP * TW_BLOCK);
+    uint2 LAS* s_p = (uint2 LAS*)(s_rc + TW_RCACHE * 4 * TW_BLOCK);
+    int64_t LAS* s_c = (int64_t LAS*)(s_p + c.n_insns + 1);
+    {
+        for (uint32_t i = threadIdx.x; i <= c.n_insns; i += TW_BLOCK) s_p[i] = gp(c.insns)[i];
+        for (uint32_t i = threadIdx.x; i < c.n_consts; i += TW_BLOCK) s_c[i] = gp(c.consts)[i];
         __syncthreads();
     }
     uint32_t r = blockIdx.x * TW_BLOCK + threadIdx.x;
     if (r >= c.R) return;
-    uint64_t* sc = c.scal + r;
+    uint64_t* sc = gp(c.scal) + r;
     const size_t R = c.R;
     if (sc[SC_STATUS * R] != TW_REP_RUNNING) return;
 
@@ -761,8 +833,12 @@ __global__ void __launch_bounds__(TW_BLOCK) tw_run_kernel(Dev c, int64_t t_end, 
     L.r = r;
     L.nt = s_t + threadIdx.x;
     L.nk = s_k + threadIdx.x;
-    L.P = PLDS ? (const uint2*)s_p : c.insns;
-    L.K = PLDS ? (const int64_t*)s_c : c.consts;
+    L.P = s_p;
+    L.rcache = s_rc + threadIdx.x;
+    L.cptr = 0;
+#pragma unroll
+    for (int e = 0; e < TW_RCACHE; ++e) L.ctag[e] = 0xFFFFFFFFu;
+    L.K = s_c;
     L.now = (int64_t)sc[SC_NOW * R]; L.final_t = (int64_t)sc[SC_FINAL_T * R];
     L.seq = (uint32_t)sc[SC_SEQ * R]; L.tidc = (uint32_t)sc[SC_TIDC * R]; L.live = (uint32_t)sc[SC_LIVE * R];
     L.near_n = (uint32_t)sc[SC_NEAR_N * R]; L.far_n = (uint32_t)sc[SC_FAR_N * R];
@@ -770,9 +846,9 @@ __global__ void __launch_bounds__(TW_BLOCK) tw_run_kernel(Dev c, int64_t t_end, 
     L.free_top = (uint32_t)sc[SC_FREE_TOP * R]; L.tmo_ctr = (uint32_t)sc[SC_TMO_CTR * R];
     L.events = sc[SC_EVENTS * R]; L.delivered = sc[SC_DELIVERED * R]; L.dropped = sc[SC_DROPPED * R];
     L.undeliv = sc[SC_UNDELIV * R]; L.threads = sc[SC_THREADS * R];
-    L.next_free = L.free_top ? c.free_stk[(size_t)(L.free_top - 1) * R + r] : 0u;
+    L.next_free = L.free_top ? gp(c.free_stk)[(size_t)(L.free_top - 1) * R + r] : 0u;
     for (uint32_t j = 0; j < L.near_n; ++j) {
-        uint4 e = c.near_spill[(size_t)j * R + r];
+        uint4 e = gp(c.near_spill)[(size_t)j * R + r];
         L.nt[j * TW_BLOCK] = (int64_t)(((uint64_t)e.y << 32) | e.x);
         L.nk[j * TW_BLOCK] = ((uint64_t)e.w << 32) | e.z;
     }
@@ -869,7 +945,7 @@ __global__ void __launch_bounds__(TW_BLOCK) tw_run_kernel(Dev c, int64_t t_end, 
     for (uint32_t j = 0; j < L.near_n; ++j) {
         int64_t t = L.nt[j * TW_BLOCK];
         uint64_t k = L.nk[j * TW_BLOCK];
-        c.near_spill[(size_t)j * R + r] =
+        gp(c.near_spill)[(size_t)j * R + r] =
             make_uint4((uint32_t)t, (uint32_t)((uint64_t)t >> 32), (uint32_t)k, (uint32_t)(k >> 32));
     }
     bool active = L.status == TW_REP_RUNNING && L.events < max_events;
@@ -878,7 +954,7 @@ __global__ void __launch_bounds__(TW_BLOCK) tw_run_kernel(Dev c, int64_t t_end, 
         uint64_t k = 0;
         if (L.min_source(t, k) < 0 || t > t_end) active = false;
     }
-    if (active) atomicAdd(c.n_active, 1u);
+    if (active) __hip_atomic_fetch_add(gp(c.n_active), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 }  // namespace
@@ -894,7 +970,6 @@ struct tw_ctx {
     uint32_t main_pc = 0, main_node = 0;
     int64_t* main_regs = nullptr;  // device copies for tw_reset
     int64_t* nv_init = nullptr;
-    bool prog_lds = false;         // program + constants fit in LDS beside the near heap
     size_t lds_bytes = 0;
     std::vector<double> launch_ms;
     std::vector<hipEvent_t> ev_pool;
@@ -1014,12 +1089,12 @@ int tw_load(tw_ctx* c, const tw_scenario_desc* s) {
     d.horizon = s->near_horizon_us;
     d.Cr = s->run_capacity;
     const size_t R = d.R;
-    c->lds_bytes = near_lds_bytes() + 8ull * d.n_insns + 8ull * d.n_consts;
-    c->prog_lds = c->lds_bytes <= 48 * 1024;
+    c->lds_bytes = near_lds_bytes() + 8ull * (d.n_insns + 1) + 8ull * d.n_consts;
+    if (c->lds_bytes > 64 * 1024) { free_all(c); return TW_ERR_INVALID; }  // program + constants must fit in LDS
     int e;
 #define ALLOC(p, n) if ((e = dalloc(c, &p, (n))) != TW_OK) { free_all(c); return e; }
     uint2* insns; int64_t* consts; uint32_t *lpc, *out_off, *ldst, *lrev, *ltab = nullptr;
-    ALLOC(insns, d.n_insns);
+    ALLOC(insns, (size_t)d.n_insns + 1);  // +1 NOP: the fall-through prefetch may read one past
     ALLOC(consts, d.n_consts);
     ALLOC(lpc, (size_t)d.n_sets * d.n_kinds);
     ALLOC(out_off, (size_t)d.N + 1);
@@ -1044,6 +1119,7 @@ int tw_load(tw_ctx* c, const tw_scenario_desc* s) {
     if (s->node_vars) ALLOC(nvi, (size_t)d.N * 4);
 #undef ALLOC
     hipStream_t st = c->stream;
+    HIPCHK(hipMemsetAsync(insns, 0, sizeof(tw_insn) * (d.n_insns + 1), st));
     HIPCHK(hipMemcpyAsync(insns, s->insns, sizeof(tw_insn) * d.n_insns, hipMemcpyHostToDevice, st));
     if (d.n_consts) HIPCHK(hipMemcpyAsync(consts, s->consts, 8 * d.n_consts, hipMemcpyHostToDevice, st));
     if (d.n_sets) HIPCHK(hipMemcpyAsync(lpc, s->listener_pc, 4ull * d.n_sets * d.n_kinds, hipMemcpyHostToDevice, st));
@@ -1116,12 +1192,8 @@ int tw_run(tw_ctx* c, int64_t t_end_us, uint64_t max_events, tw_stats* out) {
         for (int i = 0; i < per_check; ++i) {
             HIPCHK(hipMemsetAsync(d.n_active, 0, 4, st));
             HIPCHK(hipEventRecord(c->ev_pool[2 * i], st));
-            if (c->prog_lds)
-                hipLaunchKernelGGL(tw_run_kernel<true>, dim3(blocks), dim3(TW_BLOCK), c->lds_bytes, st, d, t_end_us,
-                                   limit, budget);
-            else
-                hipLaunchKernelGGL(tw_run_kernel<false>, dim3(blocks), dim3(TW_BLOCK), near_lds_bytes(), st, d,
-                                   t_end_us, limit, budget);
+            hipLaunchKernelGGL(tw_run_kernel, dim3(blocks), dim3(TW_BLOCK), c->lds_bytes, st, d, t_end_us, limit,
+                               budget);
             HIPCHK(hipGetLastError());
             HIPCHK(hipEventRecord(c->ev_pool[2 * i + 1], st));
             ++launches;
