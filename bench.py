@@ -50,6 +50,10 @@ def build_scenario(args, rank: int):
         return scenarios.hotspot(n_senders=args.nodes, n_replicas=R, msg_num=args.msg_num, seed_base=base), (
             f"hotspot (bench/Network) {args.nodes} senders -> 1 receiver x {R} replicas/GPU, "
             f"{args.msg_num} msgs @1000/s")
+    if args.config == "gossip":
+        return scenarios.gossip(n_nodes=args.nodes, seed=0), (
+            f"gossip (config 4) one scenario of {args.nodes} nodes, fanout 4, delay U[1,5] ms, "
+            f"node-partitioned over the GPUs, lookahead 1 ms windows")
     raise SystemExit(f"unknown config {args.config}")
 
 
@@ -76,14 +80,80 @@ def cpu_baseline(scn, gpu_res, gpu_hashes, seconds: float):
     }, parity, n
 
 
+def bench_gossip(args, scn, workload, world, rank, local, dist_on, barrier):
+    """Config 4: ONE scenario partitioned by node over the GPUs (strong scaling)."""
+    import torch
+
+    from timewarp import dist as twd
+    from timewarp.engine import LPEngine, lp_scenario
+
+    L = int(scn.meta["lookahead_us"])
+    N = scn.n_nodes
+    b0, b1 = twd.strong_block(N, world, rank)
+    starts = np.array([twd.strong_block(N, world, r)[0] for r in range(world)])
+    dev = f"cuda:{local}" if dist_on else None
+    eng = LPEngine(lp_scenario(scn), b0, b1 - b0, L, local)
+    for _ in range(args.warmup):
+        eng.reset()
+        twd.lp_loop(eng, starts, L, dev, dist_on)
+    elapsed, kms, windows = 0.0, 0.0, 0
+    for _ in range(args.steps):
+        eng.reset()
+        barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        w, k = twd.lp_loop(eng, starts, L, dev, dist_on)
+        torch.cuda.synchronize()
+        barrier()
+        elapsed += time.perf_counter() - t0
+        kms += k
+        windows = w
+    agg, h = eng.lp_results()
+    if dist_on:
+        tot, hashes = twd.reduce_lp(agg, h, dev)
+        (max_elapsed,) = [twd.reduce_stats({"elapsed_s": elapsed}, device=dev)["elapsed_s"]]
+    else:
+        tot, hashes, max_elapsed = {f: int(agg[f]) for f in agg.dtype.names}, h, elapsed
+    if rank == 0:
+        ev = int(tot["events"])
+        sends = int(tot["delivered"]) + int(tot["dropped"]) + int(tot["undeliverable"])
+        achieved = (64 * ev + 8 * sends) / max(kms / args.steps / 1e3, 1e-12) / 1e9
+        out = {
+            "metric": "committed events/sec (whole node), gossip 1M nodes node-partitioned",
+            "value": ev * args.steps / max_elapsed, "unit": "events/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": max_elapsed * 1e3 / args.steps, "higher_is_better": True,
+            "scaling": "strong", "vs_baseline": None, "dtype": "int64",
+            "data": "synthetic (peers and link delays drawn from random-1.1 StdGen)",
+            "config": {"workload": workload, "nodes": N, "events_per_step": ev, "windows": windows,
+                       "parallelism": f"node-partitioned x{world}, RCCL all-to-all per window"},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": None, "kernel": "tw_run_kernel<LP>",
+                         "kernel_ms_per_step": kms / args.steps},
+        }
+        if not args.no_cpu_baseline:
+            sys.path.insert(0, os.path.join(ROOT, "oracle"))
+            import oracle
+
+            t0 = time.perf_counter()
+            o = oracle.run(scn, trace_cap=0)
+            dt = time.perf_counter() - t0
+            out["cpu_baseline"] = {"value": o.result["events"] / dt, "unit": "events/s", "cores": 1, "kind": "port",
+                                   "sample": f"the whole scenario, sequential oracle (canonical), {dt:.1f} s"}
+            out["parity_sample"] = {"scenario": "whole", "bit_exact": bool(
+                all(int(tot[f]) == int(o.result[f]) for f in ("final_t", "events", "delivered", "dropped", "undeliverable", "threads"))
+                and np.array_equal(hashes, o.hashes))}
+        print(json.dumps(out), flush=True)
+    eng.close()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--config", default="token_ring", choices=["token_ring", "ping_pong", "hotspot"])
+    ap.add_argument("--config", default="token_ring", choices=["token_ring", "ping_pong", "hotspot", "gossip"])
     ap.add_argument("--replicas", type=int, default=65536, help="replicas per GPU")
-    ap.add_argument("--nodes", type=int, default=4096)
+    ap.add_argument("--nodes", type=int, default=None, help="4096 (token_ring), 256 senders (hotspot), 1M (gossip)")
     ap.add_argument("--duration-s", type=int, default=120)
     ap.add_argument("--drop-log2", type=int, default=10)
     ap.add_argument("--round-trips", type=int, default=1000)
@@ -91,6 +161,8 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
+    if args.nodes is None:
+        args.nodes = {"token_ring": 4096, "hotspot": 256, "gossip": 1 << 20}.get(args.config, 2)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -112,6 +184,8 @@ def main():
     from timewarp.engine import Engine
 
     scn, workload = build_scenario(args, rank)
+    if args.config == "gossip":
+        return bench_gossip(args, scn, workload, world, rank, local, dist_on, barrier)
     eng = Engine(local).load(scn)
 
     for _ in range(args.warmup):

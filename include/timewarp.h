@@ -169,6 +169,9 @@ typedef struct tw_scenario_desc {
     const uint32_t* link_table;/* [n_links][link_depth][n_replicas]; NULL = all 0 µs */
     const int64_t* node_vars;  /* [n_nodes][4] initial node vars (same for all replicas); NULL = 0 */
     const int64_t* main_regs;  /* [n_replicas][4] initial main-thread registers; NULL = 0 */
+    const uint32_t* node_listen; /* [n_nodes] listener set + 1 bound (persistently) at t=0,
+                                  0 = unbound; NULL = none (daemons already listening
+                                  when the emulation starts) */
     /* capacities (per replica) */
     uint32_t max_slots;        /* concurrent threads                              */
     uint32_t queue_capacity;   /* far-heap entries (live + superseded)           */
@@ -245,6 +248,45 @@ int tw_last_launch_ms(tw_ctx* ctx, double* out, size_t cap);
 void tw_destroy(tw_ctx* ctx);
 const char* tw_strerror(int code);
 const char* tw_version(void);
+
+/* ------------------------------------------------- node-partitioned (LP) mode
+ * One huge scenario (n_replicas = 1) split by node across contexts / GPUs
+ * (BASELINE config 4).  Each lane runs one node as a logical process with its
+ * own queue; a send whose delay is >= the lookahead becomes a delivery record
+ * for the destination node, and time advances in conservative windows
+ * [T, T + lookahead) with T = the minimum next-event time over all contexts.
+ * Counts and trace hashes equal a sequential TimedT run of the same scenario
+ * for any scenario whose outputs do not depend on equal-timestamp order (the
+ * oracle's tie audit); the deliverer thread's three pops (TimedT.hs:339-355 via
+ * `schedule`) are accounted at the sender (start, wake) and at the receiver
+ * (resume after the handler fork). */
+typedef struct tw_lp_record {
+    int64_t t_arr;     /* delivery time (send time + link delay)         */
+    int64_t payload;
+    uint32_t link;
+    uint32_t kind;
+    uint32_t src;      /* sending node                                   */
+    uint32_t dst;      /* receiving node (global id)                     */
+} tw_lp_record;
+
+/* Load the whole scenario (desc->n_replicas must be 1) and own nodes
+ * [lp_begin, lp_begin + lp_count).  lookahead_us must not exceed any link delay
+ * (a shorter send is a TW_REP_ERR_INSN status).  Replaces runTimedT for one
+ * scenario partitioned by node. */
+int tw_lp_load(tw_ctx* ctx, const tw_scenario_desc* desc, uint32_t lp_begin, uint32_t lp_count,
+               int64_t lookahead_us, uint32_t inbox_cap, uint32_t outbox_cap);
+/* Process every local event with t < t_end_excl; deliver records addressed to
+ * local nodes; *next_t = earliest pending local event (INT64_MAX if none);
+ * *n_foreign = records waiting for tw_lp_take_outbox. */
+int tw_lp_window(tw_ctx* ctx, int64_t t_end_excl, int64_t* next_t, uint64_t* n_foreign);
+/* Move the foreign records out (host buffer), for an exchange (RCCL all-to-all). */
+int tw_lp_take_outbox(tw_ctx* ctx, tw_lp_record* out, size_t cap, size_t* n);
+/* Hand records addressed to local nodes in; updates *next_t. */
+int tw_lp_inject(tw_ctx* ctx, const tw_lp_record* recs, size_t n, int64_t* next_t);
+/* Aggregate counters of the local nodes (final_t = max, counts = sums, status =
+ * worst) and this context's additions to every node's hash (length n_nodes;
+ * the scenario's hashes are the sum over contexts mod 2^64). */
+int tw_lp_results(tw_ctx* ctx, tw_replica_result* agg, uint64_t* node_hashes, size_t n_nodes);
 
 /* ---------------------------------------------------------------- hashing
  * Per-node trace hash (made fully commutative): every

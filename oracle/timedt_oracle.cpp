@@ -215,6 +215,8 @@ struct Sim {
         if (d->node_vars) std::memcpy(node_vars.data(), d->node_vars, node_vars.size() * 8);
         bind.assign(d->n_nodes, 0);
         bind_owner.assign(d->n_nodes, UINT64_MAX);
+        if (d->node_listen)
+            for (uint32_t n = 0; n < d->n_nodes; ++n) bind[n] = d->node_listen[n];
         link_ord.assign(d->n_links, 0);
         tmo_done.assign(d->max_timeouts, 0);
         for (uint32_t n = 0; n < d->n_nodes; ++n) hashes[n] = 0;

@@ -65,3 +65,46 @@ def test_two_rank_sharding_equals_single_process(tmp_path, oracle_mod):
     assert got["max_final_t"] == res["final_t"].max()
     assert abs(float(got["elapsed"]) - 0.2) < 1e-12  # max over ranks
     assert twd.strong_block(10, 3, 0) == (0, 4) and twd.strong_block(10, 3, 2) == (7, 10)
+
+
+def _xchg_worker(rank, world, port, out_path):
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [os.path.join(root, "time-warp_amd")]
+    import torch.distributed as dist
+
+    from timewarp import dist as twd
+    from timewarp.engine import LP_RECORD_DTYPE
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    rng = np.random.default_rng(rank)
+    n = 50 + 30 * rank
+    recs = np.zeros(n, LP_RECORD_DTYPE)
+    recs["t_arr"] = rng.integers(0, 1 << 40, n)
+    recs["payload"] = rank * 1000 + np.arange(n)
+    recs["dst"] = rng.integers(0, 100, n)
+    recs["src"] = rank
+    starts = np.array([0, 37])
+    owner = np.searchsorted(starts, recs["dst"], side="right") - 1
+    got = twd.exchange_records(recs, owner)
+    m = twd.allreduce_min(int(recs["t_arr"].min()))
+    np.savez(out_path + f".{rank}", got=got, sent=recs, m=m)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_record_exchange_all_to_all(tmp_path):
+    """The C4 exchange step (counts + uneven all_to_all_single) over gloo."""
+    out = str(tmp_path / "x")
+    mp.spawn(_xchg_worker, args=(2, _free_port(), out), nprocs=2, join=True)
+    r = [np.load(out + f".{i}.npz") for i in range(2)]
+    sent = np.concatenate([r[0]["sent"], r[1]["sent"]])
+    starts = np.array([0, 37])
+    for rank in range(2):
+        owner = np.searchsorted(starts, sent["dst"], side="right") - 1
+        exp = np.sort(sent[owner == rank], order=["src", "payload"])
+        got = np.sort(r[rank]["got"], order=["src", "payload"])
+        assert np.array_equal(exp, got)
+        assert int(r[rank]["m"]) == int(sent["t_arr"].min())

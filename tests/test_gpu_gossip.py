@@ -1,0 +1,33 @@
+"""Config 4 (single gossip scenario, node-partitioned, lookahead windows):
+the LP engine with P contexts must equal the sequential TimedT oracle on every
+counter and every node hash ("run the node-partitioned engine with P
+logical shards on 1 GPU and require the results to equal the P=1 run")."""
+import numpy as np
+import pytest
+
+from timewarp import scenarios
+
+pytestmark = pytest.mark.gpu
+
+FIELDS = ["final_t", "events", "delivered", "dropped", "undeliverable", "status", "main_exc", "threads"]
+
+
+@pytest.mark.parametrize("n,parts,drop", [(64, 1, 0), (1000, 1, 0), (1000, 4, 0), (5000, 3, 4), (50000, 8, 0)])
+def test_gossip_partitioned_equals_oracle(engine_mod, oracle_mod, n, parts, drop):
+    scn = scenarios.gossip(n, drop_log2=drop, seed=n)
+    agg, hashes, windows = engine_mod.run_partitioned(scn, parts=parts)
+    o = oracle_mod.run(scn, trace_cap=0)
+    for f in FIELDS:
+        assert int(agg[f]) == int(o.result[f]), (f, int(agg[f]), o.result[f])
+    assert np.array_equal(hashes, o.hashes)
+    assert windows > 1
+
+
+def test_gossip_replica_engine(engine_mod, oracle_mod):
+    """The same scenario as one replica on the replica engine."""
+    scn = scenarios.gossip(2000, seed=5)
+    st, res, h = engine_mod.run_scenario(scn)
+    o = oracle_mod.run(scn, trace_cap=0)
+    for f in FIELDS:
+        assert int(res[f][0]) == int(o.result[f]), f
+    assert np.array_equal(h[0], o.hashes)

@@ -58,3 +58,15 @@ def test_random_programs_report(oracle_mod):
             div += 1
     print(f"random programs tie-sensitive under pqueue vs (t,seq): {div}/40")
     assert 0 <= div <= 40
+
+
+def test_gossip_tie_insensitive(oracle_mod):
+    """Config 4 must not depend on equal-timestamp order (the partitioned engine relies on it)."""
+    from timewarp import scenarios
+
+    for n, drop in [(500, 0), (3000, 3)]:
+        scn = scenarios.gossip(n, drop_log2=drop, seed=11)
+        a = oracle_mod.run(scn, mode=0, trace_cap=0)
+        b = oracle_mod.run(scn, mode=1, trace_cap=0)
+        assert a.result == b.result
+        assert np.array_equal(a.hashes, b.hashes)

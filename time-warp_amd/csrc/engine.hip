@@ -101,6 +101,7 @@ __device__ __forceinline__ void setf(Th& t, uint32_t i, uint32_t v) {
 
 #define F_STARTED 1u
 #define F_MAIN 2u
+#define F_PHANTOM 4u   // LP mode: a delivery record's stand-in for the deliverer's wake pop
 
 __device__ __forceinline__ uint32_t th_pc(const Th& t) { return t.w0 & 0xFFFFu; }
 __device__ __forceinline__ void th_set_pc(Th& t, uint32_t pc) { t.w0 = (t.w0 & 0xFFFF0000u) | (pc & 0xFFFFu); }
@@ -146,6 +147,16 @@ struct Dev {
     uint32_t* link_ord;  // [L][R]
     uint8_t* tmo_done;   // [T][R]
     uint32_t* n_active;  // [1]
+    // node-partitioned (LP) mode: lane r = global node lp0 + r
+    uint32_t lp0, Ntot, IB, out_cap;
+    int64_t lookahead;
+    uint64_t* hash_g;    // [Ntot] this context's additions to every node's hash
+    uint4* inbox;        // [IB][R][2] delivery records addressed to local nodes
+    uint32_t* inbox_n;   // [R]
+    uint4* outbox;       // [out_cap][2] records produced this window
+    uint32_t* out_n;     // [1]
+    uint64_t* next_t;    // [1] min next-event time (atomicMin)
+    uint32_t* lp_err;    // [1] inbox/outbox overflow
 };
 
 // ------------------------------------------------------------------ hashing
@@ -166,6 +177,7 @@ __device__ __forceinline__ bool kless(int64_t ta, uint64_t ka, int64_t tb, uint6
     return ta < tb || (ta == tb && ka < kb);
 }
 
+template <bool LP>
 struct Lane {
     const Dev* c;
     uint32_t r;       // replica
@@ -194,6 +206,16 @@ struct Lane {
     uint64_t far_k;
 
     __device__ __forceinline__ size_t ix(size_t i) const { return i * c->R + r; }
+    // per-node arrays: replica mode [node][R]; LP mode a lane owns exactly one node
+    __device__ __forceinline__ size_t nix(uint32_t node, uint32_t var) const {
+        return LP ? ix(var) : ix((size_t)node * 4 + var);
+    }
+    __device__ __forceinline__ size_t bix(uint32_t node) const { return LP ? ix(0) : ix(node); }
+    __device__ __forceinline__ size_t lix(uint64_t link) const { return LP ? (size_t)link : ix(link); }
+    __device__ __forceinline__ size_t tix(uint64_t link, uint32_t ord) const {
+        size_t i = (size_t)link * c->D + ord % c->D;
+        return LP ? i : ix(i);
+    }
 
     __device__ __forceinline__ void fail(uint32_t st) {
         if (status == TW_REP_RUNNING) status = st;
@@ -456,9 +478,24 @@ struct Lane {
 
     // Commutative per-node trace hash: a no-return 64-bit atomic add, so the
     // event's critical path never waits on the node's hash line.
-    __device__ __forceinline__ void hash(uint32_t node, uint32_t kind, int64_t val) {
-        __hip_atomic_fetch_add((unsigned long long GAS*)(gp(c->hash) + ix(node)), (unsigned long long)term(now, kind, val),
-                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __device__ __forceinline__ void hash_t(int64_t t, uint32_t node, uint32_t kind, int64_t val) {
+        unsigned long long GAS* h = LP ? (unsigned long long GAS*)(gp(c->hash_g) + node)
+                                       : (unsigned long long GAS*)(gp(c->hash) + ix(node));
+        __hip_atomic_fetch_add(h, (unsigned long long)term(t, kind, val), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __device__ __forceinline__ void hash(uint32_t node, uint32_t kind, int64_t val) { hash_t(now, node, kind, val); }
+    // LP mode: append a delivery record for another logical process
+    __device__ __forceinline__ void emit(int64_t ta, int64_t payload, uint32_t link, uint32_t kind, uint32_t src,
+                                         uint32_t dst) {
+        uint32_t i = __hip_atomic_fetch_add(gp(c->out_n), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (i >= c->out_cap) {
+            __hip_atomic_fetch_or(gp(c->lp_err), 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            return;
+        }
+        uint4 GAS* o = gp(c->outbox) + (size_t)i * 2;
+        o[0] = make_uint4((uint32_t)ta, (uint32_t)((uint64_t)ta >> 32), (uint32_t)payload,
+                          (uint32_t)((uint64_t)payload >> 32));
+        o[1] = make_uint4(link, kind, src, dst);
     }
 
     // Create a thread queued at now (fork, TimedT.hs:326-339).  Returns its ref.
@@ -512,9 +549,9 @@ struct Lane {
     // Thread ends (END or uncaught exception).
     __device__ __forceinline__ void die(Th& th, uint32_t slot) {
         uint32_t node = th.w1;
-        if (gp(c->bind)[ix(node)] && gp(c->bind_own)[ix(node)] == th.w2) {
-            gp(c->bind)[ix(node)] = 0;
-            gp(c->bind_own)[ix(node)] = 0xFFFFFFFFu;
+        if (gp(c->bind)[bix(node)] && gp(c->bind_own)[bix(node)] == th.w2) {
+            gp(c->bind)[bix(node)] = 0;
+            gp(c->bind_own)[bix(node)] = 0xFFFFFFFFu;
         }
         th.w2 = 0xFFFFFFFFu;  // invalidate refs to this slot
         th.w3 = 0;
@@ -596,7 +633,7 @@ struct Lane {
             }
             case TW_OP_FORK: {
                 uint32_t node = b == 0xFFFFu ? th.w1 : (uint32_t)getr(th, b & 3);
-                if (node >= c->N) { fail(TW_REP_ERR_INSN); act = STOP; break; }
+                if (LP ? node != th.w1 : node >= c->N) { fail(TW_REP_ERR_INSN); act = STOP; break; }
                 cpc = (uint32_t)imm; cnode = node;
                 q0 = th.r0; q1 = th.r1; q2 = th.r2; q3 = th.r3;
                 act = SPAWN;
@@ -644,13 +681,13 @@ struct Lane {
             case TW_OP_JNEI: if (getr(th, a) != (int64_t)(int16_t)b) th_set_pc(th, (uint32_t)imm); break;
             case TW_OP_NOW: setr(th, a, now); break;
             case TW_OP_NODE: setr(th, a, th.w1); break;
-            case TW_OP_NLOAD: setr(th, a, gp(c->nvars)[ix((size_t)th.w1 * 4 + (b & 3))]); break;
-            case TW_OP_NSTORE: gp(c->nvars)[ix((size_t)th.w1 * 4 + (b & 3))] = getr(th, a); break;
+            case TW_OP_NLOAD: setr(th, a, gp(c->nvars)[nix(th.w1, b & 3)]); break;
+            case TW_OP_NSTORE: gp(c->nvars)[nix(th.w1, b & 3)] = getr(th, a); break;
             case TW_OP_NLOADX:
             case TW_OP_NSTOREX: {
                 uint64_t node = (uint64_t)getr(th, (b >> 8) & 3);
-                if (node >= c->N) { fail(TW_REP_ERR_INSN); act = STOP; break; }
-                int64_t GAS* v = &gp(c->nvars)[ix(node * 4 + (b & 3))];
+                if (LP ? node != th.w1 : node >= c->N) { fail(TW_REP_ERR_INSN); act = STOP; break; }
+                int64_t GAS* v = &gp(c->nvars)[nix((uint32_t)node, b & 3)];
                 if (uop == TW_OP_NLOADX) setr(th, a, *v);
                 else *v = getr(th, a);
                 break;
@@ -667,12 +704,29 @@ struct Lane {
                 if (link >= c->L) { fail(TW_REP_ERR_INSN); act = STOP; break; }
                 uint32_t kind = b & 0xFFu;
                 int64_t payload = getr(th, (b >> 8) & 3);
-                uint32_t ord = gp(c->link_ord)[ix(link)];
-                gp(c->link_ord)[ix(link)] = ord + 1;
-                uint32_t e = c->link_table ? gp(c->link_table)[ix((size_t)link * c->D + ord % c->D)] : 0u;
+                uint32_t ord = gp(c->link_ord)[lix(link)];
+                gp(c->link_ord)[lix(link)] = ord + 1;
+                uint32_t e = c->link_table ? gp(c->link_table)[tix(link, ord)] : 0u;
                 if (e & TW_LINK_DROP) {
                     ++dropped;
                     hash(th.w1, TW_KIND_DROP | kind, payload);
+                    break;
+                }
+                if (LP) {
+                    // the deliverer `schedule (after d) deliver` is accounted here (start pop
+                    // at now, wake pop at now+d, both at this node) and its delivery travels
+                    // as a record: the receiver checks its binding at now+d
+                    int64_t dly = (int64_t)(e & 0x7FFFFFFFu);
+                    if (dly < c->lookahead) { fail(TW_REP_ERR_INSN); act = STOP; break; }
+                    int64_t ta = now + dly;
+                    hash_t(now, th.w1, TW_KIND_RESUME | TW_PC_DELIVER_STUB, 0);
+                    hash_t(ta, th.w1, TW_KIND_RESUME | (TW_PC_DELIVER_STUB + 1), 0);
+                    events += 2;
+                    ++threads;
+                    final_t = ta > final_t ? ta : final_t;
+                    emit(ta, payload, (uint32_t)link, kind, th.w1, gp(c->link_dst)[link]);
+                    yt = now + 1;
+                    act = YIELD;
                     break;
                 }
                 cpc = TW_PC_DELIVER_STUB; cnode = th.w1;
@@ -684,29 +738,30 @@ struct Lane {
                 uint64_t link = (uint64_t)th.r1;
                 uint32_t kind = (uint32_t)th.r3;
                 uint32_t dst = gp(c->link_dst)[link];
-                uint32_t set = gp(c->bind)[ix(dst)];
+                uint32_t set = gp(c->bind)[bix(dst)];
                 uint32_t lpc = TW_PC_NONE;
                 if (set && kind < c->n_kinds) lpc = gp(c->lpc)[(size_t)(set - 1) * c->n_kinds + kind];
                 if (lpc == TW_PC_NONE) {
                     ++undeliv;
                     hash(dst, TW_KIND_UNDELIV | kind, th.r0);
+                    if (LP) { die(th, slot); act = EXIT; }  // the phantom deliverer ends here
                     break;
                 }
                 ++delivered;
                 hash(dst, TW_KIND_RECV | kind, th.r0);
                 cpc = lpc; cnode = dst;
-                q0 = th.r0; q1 = (int64_t)link; q2 = (int64_t)th.w1; q3 = (int64_t)kind;
+                q0 = th.r0; q1 = (int64_t)link; q2 = LP ? th.r2 : (int64_t)th.w1; q3 = (int64_t)kind;
                 act = SPAWN;
                 break;
             }
             case TW_OP_LISTEN:
                 if ((uint32_t)imm >= c->n_sets) { fail(TW_REP_ERR_INSN); act = STOP; break; }
-                gp(c->bind)[ix(th.w1)] = (uint32_t)imm + 1;
-                gp(c->bind_own)[ix(th.w1)] = b ? th.w2 : 0xFFFFFFFFu;
+                gp(c->bind)[bix(th.w1)] = (uint32_t)imm + 1;
+                gp(c->bind_own)[bix(th.w1)] = b ? th.w2 : 0xFFFFFFFFu;
                 break;
             case TW_OP_UNLISTEN:
-                gp(c->bind)[ix(th.w1)] = 0;
-                gp(c->bind_own)[ix(th.w1)] = 0xFFFFFFFFu;
+                gp(c->bind)[bix(th.w1)] = 0;
+                gp(c->bind_own)[bix(th.w1)] = 0xFFFFFFFFu;
                 break;
             case TW_OP_TRACE: hash(th.w1, TW_KIND_TRACE | ((uint32_t)imm & 0xFFFFu), getr(th, a)); break;
             case TW_OP_TMO_BEGIN: {  // schedule (after t) watchdog (TimedT.hs:373-375)
@@ -755,6 +810,14 @@ struct Lane {
                 int64_t ref;
                 if (!spawn(cpc, cnode, q0, q1, q2, q3, ref)) break;
                 if (uop == TW_OP_FORK) setr(th, a, ref);
+                if (LP && uop == TW_OP_DELIVER) {
+                    // the deliverer's resume pop (at now+1, on the sending node), then it ends
+                    hash_t(now + 1, (uint32_t)th.r2, TW_KIND_RESUME | (TW_PC_DELIVER_STUB + 2), 0);
+                    ++events;
+                    final_t = now + 1 > final_t ? now + 1 : final_t;
+                    die(th, slot);
+                    return;
+                }
                 yt = now + 1;
                 act = YIELD;
             }
@@ -776,29 +839,47 @@ struct Lane {
 
 // ------------------------------------------------------------------ kernels
 __global__ void __launch_bounds__(TW_BLOCK) tw_init_kernel(Dev c, uint32_t main_pc, uint32_t main_node,
-                                                          const int64_t* main_regs, const int64_t* nv_init) {
+                                                          const int64_t* main_regs, const int64_t* nv_init,
+                                                          const uint32_t* listen_init, int lp_mode) {
     uint32_t r = blockIdx.x * TW_BLOCK + threadIdx.x;
     if (r >= c.R) return;
+    // LP mode: lane r is global node g; only the main node's lane holds the main thread
+    const uint32_t g = lp_mode ? c.lp0 + r : 0u;
+    const bool has_main = !lp_mode || g == main_node;
     for (uint32_t f = 0; f < SC_COUNT; ++f) gp(c.scal)[(size_t)f * c.R + r] = 0;
-    gp(c.scal)[(size_t)SC_THREADS * c.R + r] = 1;
+    gp(c.scal)[(size_t)SC_THREADS * c.R + r] = has_main ? 1 : 0;
     gp(c.scal)[(size_t)SC_TIDC * c.R + r] = 1;
     gp(c.scal)[(size_t)SC_STATUS * c.R + r] = TW_REP_RUNNING;
-    gp(c.scal)[(size_t)SC_PENDING_MAIN * c.R + r] = 1;
+    gp(c.scal)[(size_t)SC_PENDING_MAIN * c.R + r] = has_main ? 1 : 0;
     // free stack: slots S-1 .. 1 (slot 0 = main), pops hand out 1, 2, 3, ...
     for (uint32_t k = 0; k + 1 < c.S; ++k) gp(c.free_stk)[(size_t)k * c.R + r] = c.S - 1 - k;
     gp(c.scal)[(size_t)SC_FREE_TOP * c.R + r] = c.S - 1;
-    uint4* p = gp(c.slots) + (size_t)r * 4;  // slot 0
+    uint4 GAS* p = gp(c.slots) + (size_t)r * 4;  // slot 0
     uint32_t w0 = (main_pc & 0xFFFFu) | (F_MAIN << 18);
-    p[0] = make_uint4(w0, main_node, 0u, 0u);
+    p[0] = make_uint4(w0, main_node, has_main ? 0u : 0xFFFFFFFFu, 0u);
     p[1] = make_uint4(0u, 0u, 0u, 0u);
     int64_t m[4] = {0, 0, 0, 0};
-    if (main_regs)
+    if (main_regs && !lp_mode)
         for (int i = 0; i < 4; ++i) m[i] = main_regs[(size_t)r * 4 + i];
     p[2] = make_uint4((uint32_t)m[0], (uint32_t)((uint64_t)m[0] >> 32), (uint32_t)m[1], (uint32_t)((uint64_t)m[1] >> 32));
     p[3] = make_uint4((uint32_t)m[2], (uint32_t)((uint64_t)m[2] >> 32), (uint32_t)m[3], (uint32_t)((uint64_t)m[3] >> 32));
+    if (lp_mode) {
+        if (nv_init)
+            for (uint32_t i = 0; i < 4; ++i) gp(c.nvars)[(size_t)i * c.R + r] = nv_init[(size_t)g * 4 + i];
+        gp(c.bind_own)[r] = 0xFFFFFFFFu;
+        if (listen_init) gp(c.bind)[r] = listen_init[g];
+        gp(c.inbox_n)[r] = 0;
+        if (!has_main) {  // slot 0 is an ordinary free slot on non-main nodes
+            gp(c.free_stk)[(size_t)(c.S - 1) * c.R + r] = 0;
+            gp(c.scal)[(size_t)SC_FREE_TOP * c.R + r] = c.S;
+        }
+        return;
+    }
     if (nv_init)
         for (uint32_t i = 0; i < c.N * 4; ++i) gp(c.nvars)[(size_t)i * c.R + r] = nv_init[i];
     for (uint32_t n = 0; n < c.N; ++n) gp(c.bind_own)[(size_t)n * c.R + r] = 0xFFFFFFFFu;
+    if (listen_init)
+        for (uint32_t n = 0; n < c.N; ++n) gp(c.bind)[(size_t)n * c.R + r] = listen_init[n];
 }
 
 // LDS per workgroup: near heap keys [NEAR_CAP][64] x 2 words, then (when it
@@ -808,8 +889,9 @@ __host__ __device__ constexpr size_t near_lds_bytes() {
     return (size_t)TW_NEAR_CAP * TW_BLOCK * 16 + (size_t)TW_RCACHE * 4 * TW_BLOCK * 16;
 }
 
-__global__ void __launch_bounds__(TW_BLOCK) __attribute__((amdgpu_waves_per_eu(1, 2))) tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events,
-                                                         uint32_t budget) {
+template <bool LP>
+__global__ void __launch_bounds__(TW_BLOCK) __attribute__((amdgpu_waves_per_eu(1, 2)))
+tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
     extern __shared__ __attribute__((aligned(16))) uint64_t lds_raw[];
     uint64_t LAS* lds = (uint64_t LAS*)lds_raw;
     int64_t LAS* s_t = (int64_t LAS*)lds;
@@ -828,7 +910,7 @@ __global__ void __launch_bounds__(TW_BLOCK) __attribute__((amdgpu_waves_per_eu(1
     const size_t R = c.R;
     if (sc[SC_STATUS * R] != TW_REP_RUNNING) return;
 
-    Lane L;
+    Lane<LP> L;
     L.c = &c;
     L.r = r;
     L.nt = s_t + threadIdx.x;
@@ -877,6 +959,51 @@ __global__ void __launch_bounds__(TW_BLOCK) __attribute__((amdgpu_waves_per_eu(1
         }
     }
 
+    if (LP) {
+        // delivery records addressed to this node become phantom deliverer
+        // threads, inserted in (t, link, payload, src) order so queue seqs are
+        // deterministic whatever order the records arrived in
+        uint32_t n_in = gp(c.inbox_n)[r];
+        if (n_in > c.IB) {
+            L.fail(TW_REP_ERR_QUEUE);
+            n_in = c.IB;
+        }
+        uint32_t used = 0;  // bitmask, IB <= 32
+        for (uint32_t k = 0; k < n_in && L.status == TW_REP_RUNNING; ++k) {
+            int best = -1;
+            uint4 ba = make_uint4(0, 0, 0, 0), bb = ba;
+            for (uint32_t j = 0; j < n_in; ++j) {
+                if (used & (1u << j)) continue;
+                const uint4 GAS* q = gp(c.inbox) + ((size_t)j * R + r) * 2;
+                uint4 ea = q[0], eb = q[1];
+                bool less = best < 0;
+                if (!less) {
+                    int64_t t1 = (int64_t)(((uint64_t)ea.y << 32) | ea.x), t2 = (int64_t)(((uint64_t)ba.y << 32) | ba.x);
+                    uint64_t p1 = ((uint64_t)ea.w << 32) | ea.z, p2 = ((uint64_t)ba.w << 32) | ba.z;
+                    less = t1 < t2 || (t1 == t2 && (eb.x < bb.x || (eb.x == bb.x && (p1 < p2 || (p1 == p2 && eb.z < bb.z)))));
+                }
+                if (less) { best = (int)j; ba = ea; bb = eb; }
+            }
+            used |= 1u << best;
+            int64_t ta = (int64_t)(((uint64_t)ba.y << 32) | ba.x);
+            uint32_t s = L.alloc_slot();
+            if (s == 0xFFFFFFFFu) break;
+            Th ph;
+            ph.w0 = ((TW_PC_DELIVER_STUB + 1) & 0xFFFFu) | ((F_STARTED | F_PHANTOM) << 18);
+            ph.w1 = c.lp0 + r;
+            ph.w2 = 0xFFFFFFFEu;  // never a throwTo target
+            ph.w3 = 0;
+            ph.f0 = ph.f1 = ph.f2 = ph.w7 = 0;
+            ph.r0 = (int64_t)(((uint64_t)ba.w << 32) | ba.z);  // payload
+            ph.r1 = bb.x;                                     // link
+            ph.r2 = bb.z;                                     // sending node
+            ph.r3 = bb.y;                                     // kind
+            L.enqueue(ph, s, ta);
+            L.store_th(s, ph);
+        }
+        gp(c.inbox_n)[r] = 0;
+    }
+
     uint32_t pending_main = (uint32_t)sc[SC_PENDING_MAIN * R];
     for (uint32_t it = 0; it < budget; ++it) {
         if (L.status != TW_REP_RUNNING) break;
@@ -889,7 +1016,10 @@ __global__ void __launch_bounds__(TW_BLOCK) __attribute__((amdgpu_waves_per_eu(1
             L.load_th(0, th);
             run = true;
         } else {
-            if (L.live == 0) { L.status = TW_REP_DONE; break; }  // whileM_ notDone
+            if (L.live == 0) {  // whileM_ notDone
+                if (!LP) L.status = TW_REP_DONE;  // an LP may still receive records
+                break;
+            }
             if (L.events >= max_events) break;
             int64_t t = 0;
             uint64_t k = 0;
@@ -905,8 +1035,12 @@ __global__ void __launch_bounds__(TW_BLOCK) __attribute__((amdgpu_waves_per_eu(1
             th.w3 = 0;
             --L.live;
             L.now = t;
-            L.final_t = t;
-            ++L.events;
+            // LP phantom = the deliverer's wake, already counted and hashed by the sender
+            const bool phantom = LP && (th_flags(th) & F_PHANTOM);
+            if (!phantom) {
+                L.final_t = LP ? (t > L.final_t ? t : L.final_t) : t;
+                ++L.events;
+            }
             uint32_t exc = th_exc(th);  // asyncExceptions . at tid <<.= Nothing (:252)
             if (exc) {
                 int64_t val = (int64_t)(int32_t)th.w7;
@@ -921,14 +1055,14 @@ __global__ void __launch_bounds__(TW_BLOCK) __attribute__((amdgpu_waves_per_eu(1
                 }
                 run = L.unwind(th, slot, exc, val);
             } else {
-                L.hash(th.w1, TW_KIND_RESUME | th_pc(th), 0);
+                if (!phantom) L.hash(th.w1, TW_KIND_RESUME | th_pc(th), 0);
                 run = true;
             }
         }
         if (run) L.step(th, slot);
     }
     sc[SC_PENDING_MAIN * R] = pending_main;
-    if (L.status == TW_REP_RUNNING && L.live == 0) L.status = TW_REP_DONE;
+    if (!LP && L.status == TW_REP_RUNNING && L.live == 0) L.status = TW_REP_DONE;
 
     sc[SC_NOW * R] = (uint64_t)L.now; sc[SC_FINAL_T * R] = (uint64_t)L.final_t;
     sc[SC_SEQ * R] = L.seq; sc[SC_TIDC * R] = L.tidc; sc[SC_LIVE * R] = L.live;
@@ -949,12 +1083,50 @@ __global__ void __launch_bounds__(TW_BLOCK) __attribute__((amdgpu_waves_per_eu(1
             make_uint4((uint32_t)t, (uint32_t)((uint64_t)t >> 32), (uint32_t)k, (uint32_t)(k >> 32));
     }
     bool active = L.status == TW_REP_RUNNING && L.events < max_events;
-    if (active) {  // parked beyond t_end => not active
-        int64_t t = 0;
+    int64_t tn = INT64_MAX;
+    {
         uint64_t k = 0;
-        if (L.min_source(t, k) < 0 || t > t_end) active = false;
+        if (L.min_source(tn, k) < 0) tn = INT64_MAX;
     }
+    if (active && (tn == INT64_MAX || tn > t_end) && !pending_main) active = false;  // parked beyond t_end
+    if (LP && L.status == TW_REP_RUNNING && tn != INT64_MAX)
+        __hip_atomic_fetch_min(gp(c.next_t), (uint64_t)tn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (active) __hip_atomic_fetch_add(gp(c.n_active), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+
+// Delivery records -> inboxes of local nodes (or the foreign buffer for the
+// host exchange).  One thread per record; the per-node inbox slot is claimed
+// with an atomic, and the drain at the next window start sorts them.
+__global__ void __launch_bounds__(256) tw_lp_scatter(Dev c, const uint4* recs, uint32_t n, uint4* foreign,
+                                                     uint32_t* n_foreign, uint32_t foreign_cap) {
+    uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    uint4 a = gp(recs)[(size_t)i * 2], b = gp(recs)[(size_t)i * 2 + 1];
+    uint32_t dst = b.w;
+    if (dst >= c.lp0 && dst < c.lp0 + c.R) {
+        uint32_t lp = dst - c.lp0;
+        uint32_t k = __hip_atomic_fetch_add(gp(c.inbox_n) + lp, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (k >= c.IB) {
+            __hip_atomic_fetch_or(gp(c.lp_err), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            return;
+        }
+        uint4 GAS* q = gp(c.inbox) + ((size_t)k * c.R + lp) * 2;
+        q[0] = a;
+        q[1] = b;
+        int64_t ta = (int64_t)(((uint64_t)a.y << 32) | a.x);
+        __hip_atomic_fetch_min(gp(c.next_t), (uint64_t)ta, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else if (foreign) {
+        uint32_t k = __hip_atomic_fetch_add(gp(n_foreign), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (k >= foreign_cap) {
+            __hip_atomic_fetch_or(gp(c.lp_err), 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            return;
+        }
+        gp(foreign)[(size_t)k * 2] = a;
+        gp(foreign)[(size_t)k * 2 + 1] = b;
+    } else {
+        __hip_atomic_fetch_or(gp(c.lp_err), 4u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
 }
 
 }  // namespace
@@ -970,7 +1142,13 @@ struct tw_ctx {
     uint32_t main_pc = 0, main_node = 0;
     int64_t* main_regs = nullptr;  // device copies for tw_reset
     int64_t* nv_init = nullptr;
+    uint32_t* listen_init = nullptr;
     size_t lds_bytes = 0;
+    // LP mode
+    bool lp = false;
+    uint4* foreign = nullptr;      // [out_cap][2]
+    uint32_t* n_foreign = nullptr;
+    uint4* staging = nullptr;      // inject staging [out_cap][2]
     std::vector<double> launch_ms;
     std::vector<hipEvent_t> ev_pool;
 };
@@ -1074,21 +1252,34 @@ static int validate(const tw_scenario_desc* s) {
 
 int tw_reset(tw_ctx* c);
 
-int tw_load(tw_ctx* c, const tw_scenario_desc* s) {
+static int load_common(tw_ctx* c, const tw_scenario_desc* s, bool lp, uint32_t lp_begin, uint32_t lp_count,
+                       int64_t lookahead, uint32_t inbox_cap, uint32_t outbox_cap) {
     if (!c) return TW_ERR_INVALID;
     int v = validate(s);
     if (v) return v;
+    if (lp && (s->n_replicas != 1 || lp_count == 0 || (uint64_t)lp_begin + lp_count > s->n_nodes ||
+               inbox_cap == 0 || inbox_cap > 32 || outbox_cap == 0 || lookahead < 1))
+        return TW_ERR_INVALID;
     HIPCHK(hipSetDevice(c->device));
     HIPCHK(hipStreamSynchronize(c->stream));
     free_all(c);
     Dev& d = c->d;
     d = Dev{};
-    d.R = s->n_replicas; d.S = s->max_slots; d.Q = s->queue_capacity; d.N = s->n_nodes;
+    c->lp = lp;
+    d.R = lp ? lp_count : s->n_replicas;
+    d.S = s->max_slots; d.Q = s->queue_capacity;
+    d.N = lp ? 1 : s->n_nodes;  // per-lane node arrays
+    d.Ntot = s->n_nodes;
+    d.lp0 = lp ? lp_begin : 0;
+    d.IB = inbox_cap;
+    d.out_cap = outbox_cap;
+    d.lookahead = lookahead;
     d.L = s->n_links; d.D = s->link_depth; d.T = s->max_timeouts;
     d.n_insns = s->n_insns; d.n_consts = s->n_consts; d.n_sets = s->n_listener_sets; d.n_kinds = s->n_msg_kinds;
     d.horizon = s->near_horizon_us;
     d.Cr = s->run_capacity;
     const size_t R = d.R;
+    const size_t Rt = s->n_replicas;  // replica dimension of the host tables
     c->lds_bytes = near_lds_bytes() + 8ull * (d.n_insns + 1) + 8ull * d.n_consts;
     if (c->lds_bytes > 64 * 1024) { free_all(c); return TW_ERR_INVALID; }  // program + constants must fit in LDS
     int e;
@@ -1097,10 +1288,10 @@ int tw_load(tw_ctx* c, const tw_scenario_desc* s) {
     ALLOC(insns, (size_t)d.n_insns + 1);  // +1 NOP: the fall-through prefetch may read one past
     ALLOC(consts, d.n_consts);
     ALLOC(lpc, (size_t)d.n_sets * d.n_kinds);
-    ALLOC(out_off, (size_t)d.N + 1);
+    ALLOC(out_off, (size_t)d.Ntot + 1);
     ALLOC(ldst, d.L);
     ALLOC(lrev, d.L);
-    if (s->link_table) ALLOC(ltab, (size_t)d.L * d.D * R);
+    if (s->link_table) ALLOC(ltab, (size_t)d.L * d.D * Rt);
     ALLOC(d.scal, (size_t)SC_COUNT * R);
     ALLOC(d.slots, (size_t)d.S * R * 4);
     ALLOC(d.free_stk, (size_t)d.S * R);
@@ -1111,37 +1302,60 @@ int tw_load(tw_ctx* c, const tw_scenario_desc* s) {
     ALLOC(d.hash, (size_t)d.N * R);
     ALLOC(d.bind, (size_t)d.N * R);
     ALLOC(d.bind_own, (size_t)d.N * R);
-    ALLOC(d.link_ord, (size_t)(d.L ? d.L : 1) * R);
+    ALLOC(d.link_ord, (size_t)(d.L ? d.L : 1) * (lp ? 1 : R));
     ALLOC(d.tmo_done, (size_t)(d.T ? d.T : 1) * R);
     ALLOC(d.n_active, 1);
+    if (lp) {
+        ALLOC(d.hash_g, (size_t)d.Ntot);
+        ALLOC(d.inbox, (size_t)d.IB * R * 2);
+        ALLOC(d.inbox_n, R);
+        ALLOC(d.outbox, (size_t)d.out_cap * 2);
+        ALLOC(d.out_n, 1);
+        ALLOC(d.next_t, 1);
+        ALLOC(d.lp_err, 1);
+        ALLOC(c->foreign, (size_t)d.out_cap * 2);
+        ALLOC(c->n_foreign, 1);
+        ALLOC(c->staging, (size_t)d.out_cap * 2);
+    }
     int64_t *mregs = nullptr, *nvi = nullptr;
-    if (s->main_regs) ALLOC(mregs, R * 4);
-    if (s->node_vars) ALLOC(nvi, (size_t)d.N * 4);
+    if (s->main_regs && !lp) ALLOC(mregs, R * 4);
+    if (s->node_vars) ALLOC(nvi, (size_t)d.Ntot * 4);
+    uint32_t* lsi = nullptr;
+    if (s->node_listen) ALLOC(lsi, (size_t)d.Ntot);
 #undef ALLOC
     hipStream_t st = c->stream;
     HIPCHK(hipMemsetAsync(insns, 0, sizeof(tw_insn) * (d.n_insns + 1), st));
     HIPCHK(hipMemcpyAsync(insns, s->insns, sizeof(tw_insn) * d.n_insns, hipMemcpyHostToDevice, st));
     if (d.n_consts) HIPCHK(hipMemcpyAsync(consts, s->consts, 8 * d.n_consts, hipMemcpyHostToDevice, st));
     if (d.n_sets) HIPCHK(hipMemcpyAsync(lpc, s->listener_pc, 4ull * d.n_sets * d.n_kinds, hipMemcpyHostToDevice, st));
-    HIPCHK(hipMemcpyAsync(out_off, s->out_off, 4ull * (d.N + 1), hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(out_off, s->out_off, 4ull * (d.Ntot + 1), hipMemcpyHostToDevice, st));
     if (d.L) {
         HIPCHK(hipMemcpyAsync(ldst, s->link_dst, 4ull * d.L, hipMemcpyHostToDevice, st));
         HIPCHK(hipMemcpyAsync(lrev, s->link_rev, 4ull * d.L, hipMemcpyHostToDevice, st));
     }
-    if (ltab) HIPCHK(hipMemcpyAsync(ltab, s->link_table, 4ull * d.L * d.D * R, hipMemcpyHostToDevice, st));
+    if (ltab) HIPCHK(hipMemcpyAsync(ltab, s->link_table, 4ull * d.L * d.D * Rt, hipMemcpyHostToDevice, st));
     if (mregs) HIPCHK(hipMemcpyAsync(mregs, s->main_regs, 32ull * R, hipMemcpyHostToDevice, st));
-    if (nvi) HIPCHK(hipMemcpyAsync(nvi, s->node_vars, 32ull * d.N, hipMemcpyHostToDevice, st));
+    if (nvi) HIPCHK(hipMemcpyAsync(nvi, s->node_vars, 32ull * d.Ntot, hipMemcpyHostToDevice, st));
+    if (lsi) HIPCHK(hipMemcpyAsync(lsi, s->node_listen, 4ull * d.Ntot, hipMemcpyHostToDevice, st));
     d.insns = insns; d.consts = consts; d.lpc = lpc; d.out_off = out_off; d.link_dst = ldst; d.link_rev = lrev;
     d.link_table = ltab;
     c->main_pc = s->main_pc;
     c->main_node = s->main_node;
     c->main_regs = mregs;
     c->nv_init = nvi;
+    c->listen_init = lsi;
     c->loaded = true;
     int rc = tw_reset(c);
     if (rc) return rc;
     HIPCHK(hipStreamSynchronize(st));
     return TW_OK;
+}
+
+int tw_load(tw_ctx* c, const tw_scenario_desc* s) { return load_common(c, s, false, 0, 0, 0, 0, 0); }
+
+int tw_lp_load(tw_ctx* c, const tw_scenario_desc* s, uint32_t lp_begin, uint32_t lp_count, int64_t lookahead_us,
+               uint32_t inbox_cap, uint32_t outbox_cap) {
+    return load_common(c, s, true, lp_begin, lp_count, lookahead_us, inbox_cap, outbox_cap);
 }
 
 int tw_reset(tw_ctx* c) {
@@ -1154,11 +1368,18 @@ int tw_reset(tw_ctx* c) {
     HIPCHK(hipMemsetAsync(d.nvars, 0, 32ull * d.N * R, st));
     HIPCHK(hipMemsetAsync(d.hash, 0, 8ull * d.N * R, st));
     HIPCHK(hipMemsetAsync(d.bind, 0, 4ull * d.N * R, st));
-    HIPCHK(hipMemsetAsync(d.link_ord, 0, 4ull * (d.L ? d.L : 1) * R, st));
+    HIPCHK(hipMemsetAsync(d.link_ord, 0, 4ull * (d.L ? d.L : 1) * (c->lp ? 1 : R), st));
     HIPCHK(hipMemsetAsync(d.tmo_done, 0, (size_t)(d.T ? d.T : 1) * R, st));
+    if (c->lp) {
+        HIPCHK(hipMemsetAsync(d.hash_g, 0, 8ull * d.Ntot, st));
+        HIPCHK(hipMemsetAsync(d.out_n, 0, 4, st));
+        HIPCHK(hipMemsetAsync(d.lp_err, 0, 4, st));
+        HIPCHK(hipMemsetAsync(c->n_foreign, 0, 4, st));
+    }
     uint32_t blocks = (uint32_t)((R + TW_BLOCK - 1) / TW_BLOCK);
     hipLaunchKernelGGL(tw_init_kernel, dim3(blocks), dim3(TW_BLOCK), 0, st, d, c->main_pc, c->main_node,
-                       (const int64_t*)c->main_regs, (const int64_t*)c->nv_init);
+                       (const int64_t*)c->main_regs, (const int64_t*)c->nv_init, (const uint32_t*)c->listen_init,
+                       c->lp ? 1 : 0);
     HIPCHK(hipGetLastError());
     return TW_OK;
 }
@@ -1191,9 +1412,14 @@ int tw_run(tw_ctx* c, int64_t t_end_us, uint64_t max_events, tw_stats* out) {
         }
         for (int i = 0; i < per_check; ++i) {
             HIPCHK(hipMemsetAsync(d.n_active, 0, 4, st));
+            if (c->lp) HIPCHK(hipMemsetAsync(d.next_t, 0xFF, 8, st));
             HIPCHK(hipEventRecord(c->ev_pool[2 * i], st));
-            hipLaunchKernelGGL(tw_run_kernel, dim3(blocks), dim3(TW_BLOCK), c->lds_bytes, st, d, t_end_us, limit,
-                               budget);
+            if (c->lp)
+                hipLaunchKernelGGL(tw_run_kernel<true>, dim3(blocks), dim3(TW_BLOCK), c->lds_bytes, st, d, t_end_us,
+                                   limit, budget);
+            else
+                hipLaunchKernelGGL(tw_run_kernel<false>, dim3(blocks), dim3(TW_BLOCK), c->lds_bytes, st, d, t_end_us,
+                                   limit, budget);
             HIPCHK(hipGetLastError());
             HIPCHK(hipEventRecord(c->ev_pool[2 * i + 1], st));
             ++launches;
@@ -1279,6 +1505,104 @@ int tw_read_final(tw_ctx* c, int64_t* max_final_t, uint64_t* delivered, uint64_t
     if (delivered) *delivered = dl;
     if (dropped) *dropped = dr;
     if (events) *events = ev;
+    return TW_OK;
+}
+
+static int lp_scatter(tw_ctx* c, const uint4* recs, uint32_t n, bool to_foreign) {
+    const Dev& d = c->d;
+    if (n == 0) return TW_OK;
+    uint32_t blocks = (n + 255) / 256;
+    hipLaunchKernelGGL(tw_lp_scatter, dim3(blocks), dim3(256), 0, c->stream, d, recs, n,
+                       to_foreign ? c->foreign : nullptr, c->n_foreign, d.out_cap);
+    HIPCHK(hipGetLastError());
+    return TW_OK;
+}
+
+int tw_lp_window(tw_ctx* c, int64_t t_end_excl, int64_t* next_t, uint64_t* n_foreign) {
+    if (!c || !next_t) return TW_ERR_INVALID;
+    if (!c->loaded || !c->lp) return TW_ERR_STATE;
+    tw_stats st{};
+    int rc = tw_run(c, t_end_excl - 1, UINT64_MAX, nullptr);
+    if (rc) return rc;
+    (void)st;
+    const Dev& d = c->d;
+    hipStream_t s = c->stream;
+    uint32_t nout = 0;
+    HIPCHK(hipMemcpyAsync(&nout, d.out_n, 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    if (nout > d.out_cap) nout = d.out_cap;
+    rc = lp_scatter(c, d.outbox, nout, true);
+    if (rc) return rc;
+    HIPCHK(hipMemsetAsync(d.out_n, 0, 4, s));
+    uint64_t nt = 0;
+    uint32_t nf = 0, err = 0;
+    HIPCHK(hipMemcpyAsync(&nt, d.next_t, 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(&nf, c->n_foreign, 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(&err, d.lp_err, 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    if (err) return TW_ERR_REPLICA;
+    *next_t = nt > (uint64_t)INT64_MAX ? INT64_MAX : (int64_t)nt;
+    if (n_foreign) *n_foreign = nf;
+    return TW_OK;
+}
+
+int tw_lp_take_outbox(tw_ctx* c, tw_lp_record* out, size_t cap, size_t* n) {
+    if (!c || !n) return TW_ERR_INVALID;
+    if (!c->loaded || !c->lp) return TW_ERR_STATE;
+    hipStream_t s = c->stream;
+    uint32_t nf = 0;
+    HIPCHK(hipMemcpyAsync(&nf, c->n_foreign, 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    if (nf > cap || !out) { *n = nf; return nf > cap ? TW_ERR_INVALID : TW_OK; }
+    if (nf) HIPCHK(hipMemcpyAsync(out, c->foreign, 32ull * nf, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemsetAsync(c->n_foreign, 0, 4, s));
+    HIPCHK(hipStreamSynchronize(s));
+    *n = nf;
+    return TW_OK;
+}
+
+int tw_lp_inject(tw_ctx* c, const tw_lp_record* recs, size_t n, int64_t* next_t) {
+    if (!c || (n && !recs)) return TW_ERR_INVALID;
+    if (!c->loaded || !c->lp) return TW_ERR_STATE;
+    const Dev& d = c->d;
+    if (n > d.out_cap) return TW_ERR_INVALID;
+    hipStream_t s = c->stream;
+    if (n) {
+        HIPCHK(hipMemcpyAsync(c->staging, recs, 32ull * n, hipMemcpyHostToDevice, s));
+        int rc = lp_scatter(c, c->staging, (uint32_t)n, false);
+        if (rc) return rc;
+    }
+    uint64_t nt = 0;
+    uint32_t err = 0;
+    HIPCHK(hipMemcpyAsync(&nt, d.next_t, 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(&err, d.lp_err, 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    if (err) return TW_ERR_REPLICA;
+    if (next_t) *next_t = nt > (uint64_t)INT64_MAX ? INT64_MAX : (int64_t)nt;
+    return TW_OK;
+}
+
+int tw_lp_results(tw_ctx* c, tw_replica_result* agg, uint64_t* node_hashes, size_t n_nodes) {
+    if (!c || !agg) return TW_ERR_INVALID;
+    if (!c->loaded || !c->lp) return TW_ERR_STATE;
+    const Dev& d = c->d;
+    std::vector<tw_replica_result> rr(d.R);
+    int rc = tw_read_results(c, rr.data(), rr.size());
+    if (rc) return rc;
+    std::memset(agg, 0, sizeof(*agg));
+    agg->status = TW_REP_DONE;
+    for (auto& x : rr) {
+        agg->final_t = x.final_t > agg->final_t ? x.final_t : agg->final_t;
+        agg->events += x.events; agg->delivered += x.delivered; agg->dropped += x.dropped;
+        agg->undeliverable += x.undeliverable; agg->threads += x.threads;
+        if (x.main_exc) agg->main_exc = x.main_exc;
+        if (x.status >= TW_REP_ABORTED) agg->status = x.status;
+    }
+    if (node_hashes) {
+        if (n_nodes < d.Ntot) return TW_ERR_INVALID;
+        HIPCHK(hipMemcpyAsync(node_hashes, d.hash_g, 8ull * d.Ntot, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+    }
     return TW_OK;
 }
 

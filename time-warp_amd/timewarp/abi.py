@@ -28,6 +28,7 @@ class TwScenarioDesc(C.Structure):
         ("link_table", C.c_void_p),
         ("node_vars", C.c_void_p),
         ("main_regs", C.c_void_p),
+        ("node_listen", C.c_void_p),
         ("max_slots", C.c_uint32),
         ("queue_capacity", C.c_uint32),
         ("near_horizon_us", C.c_int64),

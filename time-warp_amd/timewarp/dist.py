@@ -56,3 +56,112 @@ def gather_results(res: np.ndarray, hashes: np.ndarray):
     objs = [None] * dist.get_world_size()
     dist.all_gather_object(objs, (res, hashes))
     return np.concatenate([o[0] for o in objs]), np.concatenate([o[1] for o in objs])
+
+
+# ------------------------------------------------------ node-partitioned (C4)
+INT64_MAX = (1 << 63) - 1
+
+
+def exchange_records(recs: np.ndarray, owner: np.ndarray, device=None) -> np.ndarray:
+    """All-to-all of delivery records (tw_lp_record, 32 B each) to their owning
+    ranks: counts first, then the payload with uneven splits.  Over the "nccl"
+    backend this is RCCL's all-to-all on xGMI; over gloo it runs on CPU."""
+    import torch
+    import torch.distributed as dist
+
+    from .engine import LP_RECORD_DTYPE
+
+    world = dist.get_world_size()
+    order = np.argsort(owner, kind="stable")
+    recs = np.ascontiguousarray(recs[order])
+    send_counts = np.bincount(owner, minlength=world).astype(np.int64)
+    sc = torch.from_numpy(send_counts).to(device) if device else torch.from_numpy(send_counts)
+    rc = torch.empty_like(sc)
+    dist.all_to_all_single(rc, sc)
+    recv_counts = rc.cpu().numpy()
+    raw = recs.view(np.uint8).reshape(-1)
+    send_t = torch.from_numpy(raw.copy())
+    if device:
+        send_t = send_t.to(device)
+    recv_t = torch.empty(int(recv_counts.sum()) * LP_RECORD_DTYPE.itemsize, dtype=torch.uint8,
+                         device=send_t.device)
+    dist.all_to_all_single(recv_t, send_t,
+                           output_split_sizes=(recv_counts * LP_RECORD_DTYPE.itemsize).tolist(),
+                           input_split_sizes=(send_counts * LP_RECORD_DTYPE.itemsize).tolist())
+    return recv_t.cpu().numpy().view(LP_RECORD_DTYPE).copy()
+
+
+def allreduce_min(v: int, device=None) -> int:
+    import torch
+    import torch.distributed as dist
+
+    t = torch.tensor([v], dtype=torch.int64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN)
+    return int(t.item())
+
+
+def reduce_lp(agg, hashes: np.ndarray, device=None):
+    """Sum counters / max times / sum node hashes (mod 2^64) over ranks."""
+    import torch
+    import torch.distributed as dist
+
+    sums = torch.tensor([int(agg[f]) for f in ("events", "delivered", "dropped", "undeliverable", "threads")],
+                        dtype=torch.int64, device=device)
+    maxs = torch.tensor([int(agg[f]) for f in ("final_t", "status", "main_exc")], dtype=torch.int64, device=device)
+    h = torch.from_numpy(hashes.view(np.int64).copy())
+    if device:
+        h = h.to(device)
+    dist.all_reduce(sums, op=dist.ReduceOp.SUM)
+    dist.all_reduce(maxs, op=dist.ReduceOp.MAX)
+    dist.all_reduce(h, op=dist.ReduceOp.SUM)  # two's-complement wrap == sum mod 2^64
+    out = dict(zip(("events", "delivered", "dropped", "undeliverable", "threads"), sums.tolist()))
+    out.update(zip(("final_t", "status", "main_exc"), maxs.tolist()))
+    return out, h.cpu().numpy().view(np.uint64).copy()
+
+
+def lp_loop(eng, starts: np.ndarray, lookahead_us: int, device=None, distributed: bool = True,
+            max_windows: int = 1 << 20):
+    """Conservative window loop of one rank's LPEngine; returns (windows, kernel_ms)."""
+    from .engine import LP_RECORD_DTYPE
+
+    T, windows, kms = 0, 0, 0.0
+    while T < INT64_MAX and windows < max_windows:
+        nt, nf = eng.window(T + lookahead_us)
+        kms += float(eng.launch_ms().sum())
+        out = eng.take_outbox() if nf else np.zeros(0, LP_RECORD_DTYPE)
+        if distributed:
+            owner = np.searchsorted(starts, out["dst"], side="right") - 1
+            inc = exchange_records(out, owner.astype(np.int64), device)
+            if inc.size:
+                nt = min(nt, eng.inject(inc))
+            T = allreduce_min(nt, device)
+        else:
+            if out.size:
+                nt = min(nt, eng.inject(out))
+            T = nt
+        windows += 1
+    return windows, kms
+
+
+def run_partitioned_dist(scn, lookahead_us=None, device_index: int = 0, max_windows: int = 1 << 20):
+    """One scenario partitioned by node over all ranks (one GPU each):
+    conservative windows [T, T+L), records exchanged by all-to-all, next T by
+    an all-reduce(min) of the ranks' next-event times (GVT)."""
+    import torch.distributed as dist
+
+    from .engine import LPEngine, lp_scenario
+
+    L = int(lookahead_us if lookahead_us is not None else scn.meta["lookahead_us"])
+    world, rank = dist.get_world_size(), dist.get_rank()
+    N = scn.n_nodes
+    b0, b1 = strong_block(N, world, rank)
+    starts = np.array([strong_block(N, world, r)[0] for r in range(world)])
+    dev = f"cuda:{device_index}" if dist.get_backend() == "nccl" else None
+    eng = LPEngine(lp_scenario(scn), b0, b1 - b0, L, device_index)
+    try:
+        windows, _ = lp_loop(eng, starts, L, dev, True, max_windows)
+        agg, h = eng.lp_results()
+        tot, hashes = reduce_lp(agg, h, dev)
+        return tot, hashes, windows
+    finally:
+        eng.close()

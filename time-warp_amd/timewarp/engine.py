@@ -25,7 +25,12 @@ UNLIMITED = (1 << 64) - 1
 T_INF = (1 << 63) - 1
 
 EXPORTS = ["tw_create", "tw_load", "tw_reset", "tw_run", "tw_read_results", "tw_read_hashes", "tw_read_final",
-           "tw_last_launch_ms", "tw_destroy", "tw_strerror", "tw_version"]
+           "tw_last_launch_ms", "tw_destroy", "tw_strerror", "tw_version",
+           "tw_lp_load", "tw_lp_window", "tw_lp_take_outbox", "tw_lp_inject", "tw_lp_results"]
+
+# tw_lp_record (include/timewarp.h)
+LP_RECORD_DTYPE = np.dtype([("t_arr", np.int64), ("payload", np.int64), ("link", np.uint32),
+                            ("kind", np.uint32), ("src", np.uint32), ("dst", np.uint32)])
 
 
 class EngineError(RuntimeError):
@@ -56,8 +61,14 @@ def load_library(path: Optional[str] = None):
     lib.tw_strerror.argtypes = [C.c_int]
     lib.tw_strerror.restype = C.c_char_p
     lib.tw_version.restype = C.c_char_p
+    lib.tw_lp_load.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_int64, C.c_uint32, C.c_uint32]
+    lib.tw_lp_window.argtypes = [C.c_void_p, C.c_int64, C.POINTER(C.c_int64), C.POINTER(C.c_uint64)]
+    lib.tw_lp_take_outbox.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.POINTER(C.c_size_t)]
+    lib.tw_lp_inject.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.POINTER(C.c_int64)]
+    lib.tw_lp_results.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t]
     for name in ("tw_create", "tw_load", "tw_reset", "tw_run", "tw_read_results", "tw_read_hashes", "tw_read_final",
-                 "tw_last_launch_ms"):
+                 "tw_last_launch_ms", "tw_lp_load", "tw_lp_window", "tw_lp_take_outbox", "tw_lp_inject",
+                 "tw_lp_results"):
         getattr(lib, name).restype = C.c_int
     if path is None:
         _lib = lib
@@ -151,3 +162,98 @@ def run_scenario(scn: Scenario, device: int = 0, t_end: int = T_INF, max_events:
         e.load(scn)
         st = e.run(t_end, max_events)
         return st, e.results(), e.hashes()
+
+
+class LPEngine(Engine):
+    """One context of a node-partitioned run (config 4): owns nodes
+    [lp_begin, lp_begin + lp_count) of a single scenario."""
+
+    def __init__(self, scn: Scenario, lp_begin: int, lp_count: int, lookahead_us: int, device: int = 0,
+                 inbox_cap: int = 16, outbox_cap: int = 1 << 22):
+        super().__init__(device)
+        d = scn.desc()
+        _check(self.lib.tw_lp_load(self.ctx, C.addressof(d), lp_begin, lp_count, lookahead_us, inbox_cap,
+                                   outbox_cap), "tw_lp_load")
+        self.scn, self.lp_begin, self.lp_count = scn, lp_begin, lp_count
+        self.outbox_cap = outbox_cap
+
+    def window(self, t_end_excl: int):
+        nt, nf = C.c_int64(), C.c_uint64()
+        _check(self.lib.tw_lp_window(self.ctx, t_end_excl, C.byref(nt), C.byref(nf)), "tw_lp_window")
+        return nt.value, nf.value
+
+    def take_outbox(self) -> np.ndarray:
+        n = C.c_size_t()
+        buf = np.zeros(self.outbox_cap, LP_RECORD_DTYPE)
+        _check(self.lib.tw_lp_take_outbox(self.ctx, buf.ctypes.data, buf.shape[0], C.byref(n)), "tw_lp_take_outbox")
+        return buf[: n.value].copy()
+
+    def inject(self, recs: np.ndarray) -> int:
+        recs = np.ascontiguousarray(recs, dtype=LP_RECORD_DTYPE)
+        nt = C.c_int64()
+        _check(self.lib.tw_lp_inject(self.ctx, recs.ctypes.data if recs.size else None, recs.shape[0],
+                                     C.byref(nt)), "tw_lp_inject")
+        return nt.value
+
+    def lp_results(self):
+        agg = np.zeros(1, RESULT_DTYPE)
+        h = np.zeros(self.scn.n_nodes, np.uint64)
+        _check(self.lib.tw_lp_results(self.ctx, agg.ctypes.data, h.ctypes.data, h.shape[0]), "tw_lp_results")
+        return agg[0], h
+
+
+def lp_scenario(scn: Scenario, max_slots: int = 32, queue_capacity: int = 64) -> Scenario:
+    """Per-logical-process capacities (each lane holds one node's threads)."""
+    import copy
+
+    s = copy.copy(scn)
+    s.max_slots, s.queue_capacity, s.run_capacity = max_slots, queue_capacity, 0
+    return s
+
+
+def run_partitioned(scn: Scenario, parts: int = 1, lookahead_us: Optional[int] = None, device: int = 0,
+                    max_windows: int = 1 << 20):
+    """Run one scenario node-partitioned over `parts` contexts in this process
+    (records between contexts are routed on the host, exactly what the RCCL
+    all-to-all does between GPUs).  Returns (aggregate result, node hashes,
+    windows)."""
+    L = int(lookahead_us if lookahead_us is not None else scn.meta["lookahead_us"])
+    s = lp_scenario(scn)
+    N = scn.n_nodes
+    bounds = [(i * N // parts, (i + 1) * N // parts) for i in range(parts)]
+    engines = [LPEngine(s, b0, b1 - b0, L, device) for b0, b1 in bounds]
+    starts = np.array([b0 for b0, _ in bounds])
+    try:
+        T, windows = 0, 0
+        while T < T_INF and windows < max_windows:
+            nexts, outs = [], []
+            for e in engines:
+                nt, nf = e.window(T + L)
+                nexts.append(nt)
+                outs.append(e.take_outbox() if nf else None)
+            allrec = [o for o in outs if o is not None and o.size]
+            if allrec:
+                recs = np.concatenate(allrec)
+                owner = np.searchsorted(starts, recs["dst"], side="right") - 1
+                for i, e in enumerate(engines):
+                    mine = recs[owner == i]
+                    if mine.size:
+                        nexts[i] = min(nexts[i], e.inject(mine))
+            T = min(nexts)
+            windows += 1
+        agg, hashes = None, np.zeros(N, np.uint64)
+        for e in engines:
+            a, h = e.lp_results()
+            hashes += h
+            if agg is None:
+                agg = a.copy()
+            else:
+                agg["final_t"] = max(agg["final_t"], a["final_t"])
+                for f in ("events", "delivered", "dropped", "undeliverable", "threads"):
+                    agg[f] += a[f]
+                agg["main_exc"] = max(agg["main_exc"], a["main_exc"])
+                agg["status"] = max(agg["status"], a["status"])
+        return agg, hashes, windows
+    finally:
+        for e in engines:
+            e.close()

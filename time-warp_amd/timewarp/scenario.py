@@ -63,6 +63,7 @@ class Scenario:
     link_table: Optional[np.ndarray] = None   # uint32 [n_links, depth, n_replicas]
     node_vars: Optional[np.ndarray] = None    # int64 [n_nodes, 4]
     main_regs: Optional[np.ndarray] = None    # int64 [n_replicas, 4]
+    node_listen: Optional[np.ndarray] = None  # uint32 [n_nodes]: listener set + 1 bound at t=0
     max_slots: int = 64
     queue_capacity: int = 256
     near_horizon_us: int = 10_000_000
@@ -124,6 +125,7 @@ class Scenario:
         d.link_table = ptr(self.link_table, np.uint32)
         d.node_vars = ptr(self.node_vars, np.int64)
         d.main_regs = ptr(self.main_regs, np.int64)
+        d.node_listen = ptr(self.node_listen, np.uint32)
         d.max_slots = self.max_slots
         d.queue_capacity = self.queue_capacity
         d.near_horizon_us = self.near_horizon_us

@@ -309,3 +309,98 @@ def hotspot(n_senders: int = 256, n_replicas: int = 1, msg_num: int = 1000, msg_
         run_capacity=_capped(2 * S + 64), near_horizon_us=near_horizon_us,
         meta=dict(config="hotspot", n_senders=S, msg_num=msg_num, msg_rate=msg_rate),
     )
+
+
+# ------------------------------------------------------------------- gossip
+TAG_RUMOR_FIRST = 9      # first receipt of the rumor at a node
+K_RUMOR_PAYLOAD = 7      # forwarding is payload-independent (tie-insensitive by design)
+
+
+def gossip(n_nodes: int = 1024, fanout: int = 4, n_replicas: int = 1, network_delay=(ms(1), ms(5)),
+           seed: int = 0, start_us: int = sec(1), origin: int = 0, drop_log2: int = 0,
+           near_horizon_us: int = sec(10)) -> Scenario:
+    """Config 4: one gossip/broadcast scenario (build-defined; the reference has
+    no gossip example — it composes MonadDialog `listen`/`send`, MonadDialog.hs
+    :149-271, exactly like examples/ping-pong).
+
+    Every node is a daemon already listening when the emulation starts
+    (``node_listen``).  The main thread, on the origin node, waits
+    ``start_us`` and sends the rumor to its ``fanout`` peers.  A node that
+    receives the rumor for the first time records the time and forwards it to
+    its own peers; later copies are ignored.  The forwarded payload is a
+    constant, so the outcome does not depend on the order of equal-time
+    deliveries.  Peers (distinct, != self) and per-link delays U[1 ms, 5 ms] are
+    drawn from mkStdGen(seed); the minimum link delay (1 ms) is the lookahead
+    of the node-partitioned engine.
+    """
+    N, F = int(n_nodes), int(fanout)
+    p = Program()
+    K = p.kind("rumor")
+    lset = p.listener_set({"rumor": "on_rumor"})
+
+    c = p.function("main")
+    c.wait(for_(start_us))
+    c.seti(0, K_RUMOR_PAYLOAD)
+    c.nstore(0, 0)                                     # the origin knows the rumor
+    c.now(3).nstore(3, 1)
+    for k in range(F):
+        c.link(1, k).send(1, K, 0)
+    c.end()
+
+    c = p.function("on_rumor")                        # listener: r0 = payload
+    dup = c.label()
+    c.nload(2, 0).jnei(2, 0, dup)                      # already seen -> ignore
+    c.seti(2, 1).nstore(2, 0).now(3).nstore(3, 1)
+    c.trace(TAG_RUMOR_FIRST, 0)
+    for k in range(F):
+        c.link(1, k).send(1, K, 0)
+    c.bind(dup)
+    c.end()
+
+    img = p.finalize()
+    g = StdGenVec(np.array([seed], dtype=np.int64))
+    peers = np.zeros((N, F), np.int64)
+    # host draw, vectorised over nodes with one generator per node (seed*N + node)
+    gn = StdGenVec(np.int64(seed) * N + np.arange(N, dtype=np.int64))
+    for k in range(F):
+        while True:
+            cand = gn.range(0, N - 2)
+            cand = cand + (cand >= np.arange(N))       # skip self
+            clash = np.zeros(N, bool)
+            for j in range(k):
+                clash |= cand == peers[:, j]
+            if not clash.any() or N <= F:
+                peers[:, k] = cand
+                break
+            # redraw only clashing nodes: keep others, loop over the mask
+            peers[~clash, k] = cand[~clash]
+            keep = ~clash
+            while clash.any():
+                c2 = gn.range(0, N - 2)
+                c2 = c2 + (c2 >= np.arange(N))
+                bad = np.zeros(N, bool)
+                for j in range(k):
+                    bad |= c2 == peers[:, j]
+                take = clash & ~bad
+                peers[take, k] = c2[take]
+                clash &= ~take
+            break
+    del g
+    out_off = np.arange(N + 1, dtype=np.uint32) * F
+    dst = peers.reshape(-1).astype(np.uint32)
+    topo = Topology(N, out_off, dst, np.full(N * F, isa.PC_NONE, np.uint32))
+    gd = StdGenVec(np.int64(seed) * N + 7919 + np.arange(N, dtype=np.int64))
+    table = np.zeros((N * F, 1, n_replicas), np.uint32)
+    delays = np.stack([gd.range(*network_delay) for _ in range(F)], axis=1).reshape(-1).astype(np.uint32)
+    if drop_log2:
+        u = np.stack([gd.range(0, (1 << drop_log2) - 1) for _ in range(F)], axis=1).reshape(-1)
+        delays = np.where(u == 0, delays | np.uint32(isa.LINK_DROP), delays)
+    table[:, 0, :] = delays[:, None]
+    listen = np.full(N, lset + 1, np.uint32)
+    return Scenario(
+        name=f"gossip_n{N}", image=img, topo=topo, n_replicas=n_replicas,
+        main_pc=img.pc_of("main"), main_node=origin, link_table=table, node_listen=listen,
+        max_slots=_capped(8 * N + 64), queue_capacity=_capped(8 * N + 256), run_capacity=_capped(4 * N + 64),
+        near_horizon_us=near_horizon_us,
+        meta=dict(config="gossip", n_nodes=N, fanout=F, seed=seed, lookahead_us=int(network_delay[0])),
+    )
