@@ -255,6 +255,15 @@ def main():
                 "algorithmic_bytes": "64 B/event + 8 B/send (SURVEY.md 8d)",
             },
         }
+        prof = os.path.join(ROOT, "profiles", "pmc_summary.json")
+        if os.path.exists(prof) and args.config == "token_ring" and args.replicas == 65536 and args.nodes == 4096:
+            pm = json.load(open(prof))
+            if pm.get("bench_args", "").strip() == "" and "hbm_bytes_total" in pm:
+                per_step = float(pm["hbm_bytes_total"])
+                out["roofline"]["traffic"] = per_step
+                out["roofline"]["traffic_unit"] = ("HBM bytes per step, rocprofv3 (2*FETCH_SIZE + WRITE_SIZE)*1024 "
+                                                   "over the step's tw_run_kernel dispatches (profiles/pmc_summary.json)")
+                out["roofline"]["traffic_per_event"] = per_step / max(1, events / args.steps)
         if not args.no_cpu_baseline:
             cb, parity, n = cpu_baseline(scn, res, hashes, args.cpu_seconds)
             out["cpu_baseline"] = cb

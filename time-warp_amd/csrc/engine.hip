@@ -222,9 +222,11 @@ struct Lane {
     }
 
     // ---------------------------------------------------------- near heap (LDS)
+    // 4-ary heap: 16 entries are two levels, and the four children of a node
+    // are independent LDS loads, so a sift costs at most two LDS round trips.
     __device__ __forceinline__ void near_sift_up(uint32_t i, int64_t t, uint64_t k) {
         while (i > 0) {
-            uint32_t p = (i - 1) >> 1;
+            uint32_t p = (i - 1) >> 2;
             int64_t pt = nt[p * TW_BLOCK];
             uint64_t pk = nk[p * TW_BLOCK];
             if (!kless(t, k, pt, pk)) break;
@@ -238,19 +240,24 @@ struct Lane {
     __device__ __forceinline__ void near_sift_down(uint32_t i, int64_t t, uint64_t k) {
         const uint32_t n = near_n;
         for (;;) {
-            uint32_t c0 = 2 * i + 1;
+            uint32_t c0 = 4 * i + 1;
             if (c0 >= n) break;
-            int64_t ct = nt[c0 * TW_BLOCK];
-            uint64_t ck = nk[c0 * TW_BLOCK];
-            if (c0 + 1 < n) {
-                int64_t dt = nt[(c0 + 1) * TW_BLOCK];
-                uint64_t dk = nk[(c0 + 1) * TW_BLOCK];
-                if (kless(dt, dk, ct, ck)) { ct = dt; ck = dk; ++c0; }
+            uint32_t cn = n - c0 < 4 ? n - c0 : 4;
+            int64_t bt = nt[c0 * TW_BLOCK];
+            uint64_t bk = nk[c0 * TW_BLOCK];
+            uint32_t bi = c0;
+#pragma unroll
+            for (uint32_t j = 1; j < 4; ++j) {
+                if (j < cn) {
+                    int64_t jt = nt[(c0 + j) * TW_BLOCK];
+                    uint64_t jk = nk[(c0 + j) * TW_BLOCK];
+                    if (kless(jt, jk, bt, bk)) { bt = jt; bk = jk; bi = c0 + j; }
+                }
             }
-            if (!kless(ct, ck, t, k)) break;
-            nt[i * TW_BLOCK] = ct;
-            nk[i * TW_BLOCK] = ck;
-            i = c0;
+            if (!kless(bt, bk, t, k)) break;
+            nt[i * TW_BLOCK] = bt;
+            nk[i * TW_BLOCK] = bk;
+            i = bi;
         }
         nt[i * TW_BLOCK] = t;
         nk[i * TW_BLOCK] = k;
@@ -1025,11 +1032,11 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
             uint64_t k = 0;
             int src = L.min_source(t, k);
             if (src < 0 || t > t_end) break;
+            slot = (uint32_t)k;
+            L.load_th(slot, th);  // issued first: its latency overlaps the queue maintenance
             if (src == TW_RUNS) L.near_pop();
             else if (src == TW_RUNS + 1) L.far_pop();
             else L.run_pop(src);
-            slot = (uint32_t)k;
-            L.load_th(slot, th);
             if (th.w3 != (uint32_t)(k >> 32)) continue;  // superseded by a throwTo re-stamp
             // PQ.minView; curTime .= timestamp (TimedT.hs:241-247)
             th.w3 = 0;

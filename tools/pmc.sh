@@ -14,3 +14,10 @@ for P in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_
   timeout -k 10 300 rocprofv3 --pmc $P --kernel-trace --output-format csv -d $OUT/pass$i -o run -- python3 bench.py $ARGS > $OUT/pass$i.log 2>&1
   echo "pass $i rc=$?"
 done
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/stats -o run -- python3 bench.py $ARGS > $OUT/stats.log 2>&1
+echo "stats rc=$?"
+python3 tools/pmc_summary.py $OUT/summary.json $OUT/stats $OUT/pass1 $OUT/pass2 $OUT/pass3 $OUT/pass4 $OUT/pass5 > $OUT/summary.log 2>&1
+python3 - "$OUT/summary.json" "$*" <<'PY'
+import json, sys
+s = json.load(open(sys.argv[1])); s["bench_args"] = sys.argv[2]; json.dump(s, open(sys.argv[1], "w"), indent=1)
+PY
