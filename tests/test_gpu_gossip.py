@@ -31,3 +31,14 @@ def test_gossip_replica_engine(engine_mod, oracle_mod):
     for f in FIELDS:
         assert int(res[f][0]) == int(o.result[f]), f
     assert np.array_equal(h[0], o.hashes)
+
+
+def test_lookahead_violation_is_an_error(engine_mod):
+    """token-ring's observer links have 0 µs delay (examples/token-ring/Main.hs:75-76):
+    no conservative window exists, and the LP engine must say so instead of
+    producing a wrong trace."""
+    from timewarp import isa
+
+    scn = scenarios.token_ring(n_nodes=8, n_replicas=1, launch_duration=20_000_000)
+    agg, hashes, windows = engine_mod.run_partitioned(scn, parts=2, lookahead_us=1000, max_windows=100000)
+    assert int(agg["status"]) == isa.REP_ERR_INSN

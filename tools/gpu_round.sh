@@ -1,0 +1,25 @@
+#!/bin/bash
+# One GPU session: each step under its own time limit; stop at the first step
+# that aborted, faulted, hung or timed out (exit codes other than 0/1).
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+step() {  # step NAME SECONDS CMD...
+  local name=$1 secs=$2; shift 2
+  timeout -k 10 "$secs" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "$name=$rc"
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
+  return 0
+}
+for s in "$@"; do
+  case $s in
+    pytest) step pytest_gpu 600 python -m pytest tests/ -q -m gpu -x ;;
+    smoke)  step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    phase)  step phase 300 python tools/phase_probe.py 65536 4096 ;;
+    bench)  step bench 500 python bench.py ;;
+    bench_c2) step bench_c2 400 python bench.py --config ping_pong ;;
+    bench_c4) step bench_c4 500 python bench.py --config gossip ;;
+    bench_c5) step bench_c5 400 python bench.py --config hotspot ;;
+    *) echo "unknown step $s"; exit 2 ;;
+  esac
+done
