@@ -45,7 +45,9 @@ def load_library(path: Optional[str] = None):
     global _lib
     if _lib is not None and path is None:
         return _lib
-    p = path or LIB_PATH
+    # TW_LIB selects an alternative in-tree build of the same ABI (A/B runs of
+    # kernel variants on one GPU box); default lib/libtimewarp.so
+    p = path or os.environ.get("TW_LIB") or LIB_PATH
     if not os.path.exists(p):
         raise EngineError(f"HIP engine library missing: {p} (run __graft_entry__.build())")
     lib = C.CDLL(p)

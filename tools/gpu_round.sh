@@ -3,8 +3,9 @@
 # that aborted, faulted, hung or timed out (exit codes other than 0/1).
 export TMPDIR=/tmp
 mkdir -p gpurun_out
+SFX=""
 step() {  # step NAME SECONDS CMD...
-  local name=$1 secs=$2; shift 2
+  local name=$1$SFX secs=$2; shift 2
   timeout -k 10 "$secs" "$@" > "gpurun_out/$name.log" 2>&1
   local rc=$?
   echo "$name=$rc"
@@ -16,10 +17,13 @@ for s in "$@"; do
     pytest) step pytest_gpu 600 python -m pytest tests/ -q -m gpu -x ;;
     smoke)  step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     phase)  step phase 300 python tools/phase_probe.py 65536 4096 ;;
+    probe)  step probe 300 env TW_LIB=$PWD/time-warp_amd/lib/libtimewarp_prof.so python tools/kernel_probe.py 65536 4096 ;;
     bench)  step bench 500 python bench.py ;;
     bench_c2) step bench_c2 400 python bench.py --config ping_pong ;;
     bench_c4) step bench_c4 500 python bench.py --config gossip ;;
     bench_c5) step bench_c5 400 python bench.py --config hotspot ;;
+    lib=*) export TW_LIB=$PWD/time-warp_amd/lib/libtimewarp_${s#lib=}.so; SFX=_${s#lib=} ;;
+    pmc) bash tools/pmc.sh gpurun_out/pmc$SFX > gpurun_out/pmc$SFX.log 2>&1; rc=$?; echo "pmc=$rc"; [ $rc -eq 0 ] || exit $rc ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
