@@ -53,6 +53,30 @@
 #define LAS
 #endif
 
+// Diagnostic build (-DTW_PROF=1, lib/libtimewarp_prof.so): per-lane counters
+// and s_memtime cycle splits summed into Dev::prof at kernel end.  The product
+// build compiles every PROF_* to nothing.
+#ifdef TW_PROF_LITE  // cycle splits + iteration/pop counts only (32-bit, no forced waits)
+#define LITE_T(v) uint64_t v = __builtin_amdgcn_s_memtime()
+#define LITE_ACC(i, v) (lite[(i)] += (uint32_t)(v))
+#else
+#define LITE_T(v) ((void)0)
+#define LITE_ACC(i, v) ((void)0)
+#endif
+#ifdef TW_PROF
+#define PROF_N 32
+#define PROF_INC(i, v) (L_prof[(i)] += (v))
+#define KPROF_INC(i, v) (L.L_prof[(i)] += (v))
+#define PROF_T(v) uint64_t v = __builtin_amdgcn_s_memtime()
+#else
+#define KPROF_INC(i, v) ((void)0)
+#define PROF_INC(i, v) ((void)0)
+#define PROF_T(v) ((void)0)
+#endif
+enum { P_SEL, P_WAIT, P_PRE, P_STEP, P_ITERS, P_POPS, P_SUPER, P_SRC_NEAR, P_SRC_FAR, P_SRC_RUN, P_HIT, P_MISS,
+       P_INSNS, P_PASSES, P_NEAR_PUSH, P_RUN_PUSH, P_FAR_PUSH, P_HASH, P_STORE, P_THROWTO, P_ALLOC, P_DIE,
+       P_LOOP, P_TAIL, P_STCYC, P_COUNT };
+
 namespace {
 
 template <class T>
@@ -157,6 +181,7 @@ struct Dev {
     uint32_t* out_n;     // [1]
     uint64_t* next_t;    // [1] min next-event time (atomicMin)
     uint32_t* lp_err;    // [1] inbox/outbox overflow
+    unsigned long long* prof;  // [P_COUNT] diagnostic build only
 };
 
 // ------------------------------------------------------------------ hashing
@@ -204,6 +229,9 @@ struct Lane {
     // cached far top
     int64_t far_t;
     uint64_t far_k;
+#ifdef TW_PROF
+    uint64_t L_prof[P_COUNT];
+#endif
 
     __device__ __forceinline__ size_t ix(size_t i) const { return i * c->R + r; }
     // per-node arrays: replica mode [node][R]; LP mode a lane owns exactly one node
@@ -262,7 +290,10 @@ struct Lane {
         nt[i * TW_BLOCK] = t;
         nk[i * TW_BLOCK] = k;
     }
-    __device__ __forceinline__ void near_push(int64_t t, uint64_t k) { near_sift_up(near_n++, t, k); }
+    __device__ __forceinline__ void near_push(int64_t t, uint64_t k) {
+        PROF_INC(P_NEAR_PUSH, 1);
+        near_sift_up(near_n++, t, k);
+    }
     __device__ __forceinline__ void near_pop() {
         uint32_t n = --near_n;
         if (n == 0) return;
@@ -291,6 +322,7 @@ struct Lane {
     }
     __device__ __forceinline__ void far_push(int64_t t, uint64_t k) {
         if (far_n >= c->Q) { fail(TW_REP_ERR_QUEUE); return; }
+        PROF_INC(P_FAR_PUSH, 1);
         uint32_t i = far_n++;
         while (i > 0) {
             uint32_t p = (i - 1) >> 2;
@@ -367,6 +399,7 @@ struct Lane {
         }
         int sel = best >= 0 ? best : empty;
         if (sel < 0) return false;
+        PROF_INC(P_RUN_PUSH, 1);
 #pragma unroll
         for (int j = 0; j < TW_RUNS; ++j) {
             if (j == sel) {
@@ -444,19 +477,22 @@ struct Lane {
     // Thread records: HBM is authoritative (write-through); the LDS cache
     // serves the common case of popping a thread whose record this lane wrote
     // a few events earlier (a fork child, the forking parent, a throwTo victim).
-    __device__ __forceinline__ void load_th(uint32_t slot, Th& th) const {
+    __device__ __forceinline__ void load_th(uint32_t slot, Th& th) {
         int e = cache_find(slot);
         if (e >= 0) {
             const uint4 LAS* q = rcache + (size_t)e * 4 * TW_BLOCK;
             unpack(th, q[0], q[TW_BLOCK], q[2 * TW_BLOCK], q[3 * TW_BLOCK]);
+            PROF_INC(P_HIT, 1);
             return;
         }
+        PROF_INC(P_MISS, 1);
         const uint4 GAS* p = gp(c->slots) + ix(slot) * 4;
         unpack(th, p[0], p[1], p[2], p[3]);
     }
     __device__ __forceinline__ void store_th(uint32_t slot, const Th& th) {
         uint4 a, b, d, f;
         pack(th, a, b, d, f);
+        PROF_INC(P_STORE, 1);
         uint4 GAS* p = gp(c->slots) + ix(slot) * 4;
         p[0] = a; p[1] = b; p[2] = d; p[3] = f;
         int e = cache_find(slot);
@@ -474,6 +510,7 @@ struct Lane {
     // prefetched at every pop, so a fork never waits on this load.
     __device__ __forceinline__ uint32_t alloc_slot() {
         if (free_top == 0) { fail(TW_REP_ERR_SLOTS); return 0xFFFFFFFFu; }
+        PROF_INC(P_ALLOC, 1);
         uint32_t s = next_free;
         if (--free_top) next_free = gp(c->free_stk)[ix(free_top - 1)];
         return s;
@@ -488,6 +525,10 @@ struct Lane {
     __device__ __forceinline__ void hash_t(int64_t t, uint32_t node, uint32_t kind, int64_t val) {
         unsigned long long GAS* h = LP ? (unsigned long long GAS*)(gp(c->hash_g) + node)
                                        : (unsigned long long GAS*)(gp(c->hash) + ix(node));
+        PROF_INC(P_HASH, 1);
+#ifdef TW_EXP_NOHASH  // A/B experiment only: breaks parity
+        return;
+#endif
         __hip_atomic_fetch_add(h, (unsigned long long)term(t, kind, val), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     __device__ __forceinline__ void hash(uint32_t node, uint32_t kind, int64_t val) { hash_t(now, node, kind, val); }
@@ -528,6 +569,7 @@ struct Lane {
     __device__ __forceinline__ void throw_to(Th& self, uint32_t self_slot, int64_t ref, uint32_t code, int64_t val) {
         uint32_t ts = (uint32_t)ref;
         uint32_t tid = (uint32_t)((uint64_t)ref >> 32);
+        PROF_INC(P_THROWTO, 1);
         if (ts >= c->S) return;
         if (ts == self_slot) {  // the running thread: its record lives in registers
             if (self.w2 != tid) return;
@@ -556,6 +598,7 @@ struct Lane {
     // Thread ends (END or uncaught exception).
     __device__ __forceinline__ void die(Th& th, uint32_t slot) {
         uint32_t node = th.w1;
+        PROF_INC(P_DIE, 1);
         if (gp(c->bind)[bix(node)] && gp(c->bind_own)[bix(node)] == th.w2) {
             gp(c->bind)[bix(node)] = 0;
             gp(c->bind_own)[bix(node)] = 0xFFFFFFFFu;
@@ -610,7 +653,13 @@ struct Lane {
         for (;;) {
             uint32_t op = in.x & 0xFFu;
             uint32_t uop = __builtin_amdgcn_readfirstlane(op);
+            PROF_INC(P_PASSES, 1);
             if (op != uop) continue;
+            // keep the dispatch scalar: without this the compiler substitutes the
+            // per-lane `op` (known equal here) and lowers the switch to a vector
+            // binary search with an exec-mask save/restore per level
+            asm volatile("v_readfirstlane_b32 %0, %1" : "=s"(uop) : "v"(op));
+            PROF_INC(P_INSNS, 1);
             if (++n > TW_STEP_CAP) { fail(TW_REP_ERR_INSN); break; }
             uint2 nx = P[pc + 1];  // prefetch the fall-through instruction (image padded by one)
             uint32_t a = (in.x >> 8) & 3u, b = in.x >> 16;
@@ -809,6 +858,9 @@ struct Lane {
                 act = STOP;
                 break;
             }
+#ifdef TW_PROF
+            uint64_t ta0 = __builtin_amdgcn_s_memtime();
+#endif
             if (act == THROWTO) {
                 throw_to(th, slot, tref, tcode, tval);
                 act = GO;
@@ -830,8 +882,10 @@ struct Lane {
             }
             if (act == YIELD) {
                 enqueue(th, slot, yt);
+                PROF_INC(P_TAIL, __builtin_amdgcn_s_memtime() - ta0);
                 break;
             }
+            PROF_INC(P_TAIL, __builtin_amdgcn_s_memtime() - ta0);
             if (act == EXIT) return;
             if (act == STOP || status != TW_REP_RUNNING) break;
             uint32_t npc = th_pc(th);
@@ -840,7 +894,11 @@ struct Lane {
             else in = P[npc];
             pc = npc;
         }
+#ifdef TW_PROF
+        uint64_t ts0 = __builtin_amdgcn_s_memtime();
+#endif
         store_th(slot, th);
+        PROF_INC(P_STCYC, __builtin_amdgcn_s_memtime() - ts0);
     }
 };
 
@@ -1011,9 +1069,27 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
         gp(c.inbox_n)[r] = 0;
     }
 
+#ifdef TW_PROF
+    for (int i = 0; i < P_COUNT; ++i) L.L_prof[i] = 0;
+    PROF_T(tk0);
+#endif
+#ifdef TW_PROF_LITE
+    uint32_t lite[6] = {0, 0, 0, 0, 0, 0};  // sel, pre, step, loop, iters, pops
+    LITE_T(lk0);
+#endif
     uint32_t pending_main = (uint32_t)sc[SC_PENDING_MAIN * R];
     for (uint32_t it = 0; it < budget; ++it) {
         if (L.status != TW_REP_RUNNING) break;
+        PROF_T(t0);
+        LITE_T(l0);
+#ifdef TW_PROF_LITE
+        uint64_t l1 = l0;
+        LITE_ACC(4, 1);
+#endif
+#ifdef TW_PROF
+        uint64_t t2 = t0;
+#endif
+        KPROF_INC(P_ITERS, 1);
         Th th;
         uint32_t slot;
         bool run = false;
@@ -1037,7 +1113,24 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
             if (src == TW_RUNS) L.near_pop();
             else if (src == TW_RUNS + 1) L.far_pop();
             else L.run_pop(src);
+#ifdef TW_PROF
+            PROF_T(t1);
+#ifndef TW_PROF_NOWAIT
+            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+#endif
+            t2 = __builtin_amdgcn_s_memtime();
+            KPROF_INC(P_SEL, t1 - t0);
+            KPROF_INC(P_WAIT, t2 - t1);
+            KPROF_INC(src == TW_RUNS ? P_SRC_NEAR : src == TW_RUNS + 1 ? P_SRC_FAR : P_SRC_RUN, 1);
+            if (th.w3 != (uint32_t)(k >> 32)) KPROF_INC(P_SUPER, 1);
+#endif
+#ifdef TW_PROF_LITE
+            l1 = __builtin_amdgcn_s_memtime();
+            LITE_ACC(0, l1 - l0);
+#endif
             if (th.w3 != (uint32_t)(k >> 32)) continue;  // superseded by a throwTo re-stamp
+            KPROF_INC(P_POPS, 1);
+            LITE_ACC(5, 1);
             // PQ.minView; curTime .= timestamp (TimedT.hs:241-247)
             th.w3 = 0;
             --L.live;
@@ -1066,8 +1159,40 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
                 run = true;
             }
         }
+#ifdef TW_PROF
+        PROF_T(t3);
+        if (!pending_main) KPROF_INC(P_PRE, t3 - t2);
+#endif
+#ifdef TW_PROF_LITE
+        LITE_T(l2);
+        LITE_ACC(1, l2 - l1);
+#endif
         if (run) L.step(th, slot);
+#ifdef TW_PROF_LITE
+        LITE_ACC(2, __builtin_amdgcn_s_memtime() - l2);
+#endif
+#ifdef TW_PROF
+        PROF_T(t4);
+        KPROF_INC(P_STEP, t4 - t3);
+#endif
     }
+#ifdef TW_PROF_LITE
+    LITE_ACC(3, __builtin_amdgcn_s_memtime() - lk0);
+    if (c.prof)
+        for (int i = 0; i < 6; ++i)
+            __hip_atomic_fetch_add(gp(c.prof) + i, (unsigned long long)lite[i], __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+#endif
+#ifdef TW_PROF
+    {
+        PROF_T(tk1);
+        KPROF_INC(P_LOOP, tk1 - tk0);
+        if (c.prof)
+            for (int i = 0; i < P_COUNT; ++i)
+                __hip_atomic_fetch_add(gp(c.prof) + i, (unsigned long long)L.L_prof[i], __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+    }
+#endif
     sc[SC_PENDING_MAIN * R] = pending_main;
     if (!LP && L.status == TW_REP_RUNNING && L.live == 0) L.status = TW_REP_DONE;
 
@@ -1312,6 +1437,10 @@ static int load_common(tw_ctx* c, const tw_scenario_desc* s, bool lp, uint32_t l
     ALLOC(d.link_ord, (size_t)(d.L ? d.L : 1) * (lp ? 1 : R));
     ALLOC(d.tmo_done, (size_t)(d.T ? d.T : 1) * R);
     ALLOC(d.n_active, 1);
+#if defined(TW_PROF) || defined(TW_PROF_LITE)
+    ALLOC(d.prof, P_COUNT);
+    HIPCHK(hipMemsetAsync(d.prof, 0, 8 * P_COUNT, c->stream));
+#endif
     if (lp) {
         ALLOC(d.hash_g, (size_t)d.Ntot);
         ALLOC(d.inbox, (size_t)d.IB * R * 2);
@@ -1612,6 +1741,17 @@ int tw_lp_results(tw_ctx* c, tw_replica_result* agg, uint64_t* node_hashes, size
     }
     return TW_OK;
 }
+
+#if defined(TW_PROF) || defined(TW_PROF_LITE)
+// Diagnostic build only: copy the P_COUNT counters out, optionally zeroing them.
+int tw_prof_read(tw_ctx* c, unsigned long long* out, size_t cap, int reset) {
+    if (!c || !out || !c->loaded || !c->d.prof) return TW_ERR_STATE;
+    size_t n = cap < (size_t)P_COUNT ? cap : (size_t)P_COUNT;
+    HIPCHK(hipMemcpy(out, c->d.prof, 8 * n, hipMemcpyDeviceToHost));
+    if (reset) HIPCHK(hipMemset(c->d.prof, 0, 8 * P_COUNT));
+    return (int)n;
+}
+#endif
 
 int tw_last_launch_ms(tw_ctx* c, double* out, size_t cap) {
     if (!c || !out) return TW_ERR_INVALID;

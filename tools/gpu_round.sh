@@ -14,11 +14,14 @@ step() {  # step NAME SECONDS CMD...
 }
 for s in "$@"; do
   case $s in
-    pytest) step pytest_gpu 600 python -m pytest tests/ -q -m gpu -x ;;
+    pytest) step pytest_gpu 600 python -u -m pytest tests/ -q -m gpu -x --timeout 120 --timeout-method thread ;;
     smoke)  step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     phase)  step phase 300 python tools/phase_probe.py 65536 4096 ;;
     probe)  step probe 300 env TW_LIB=$PWD/time-warp_amd/lib/libtimewarp_prof.so python tools/kernel_probe.py 65536 4096 ;;
+    lite) step lite 300 env TW_PROBE_LITE=1 TW_LIB=$PWD/time-warp_amd/lib/libtimewarp_lite.so python tools/kernel_probe.py 65536 4096 ;;
+    probe2) step probe2 300 env TW_LIB=$PWD/time-warp_amd/lib/libtimewarp_prof2.so python tools/kernel_probe.py 65536 4096 ;;
     bench)  step bench 500 python bench.py ;;
+    benchq) step benchq 300 python bench.py --steps 2 --no-cpu-baseline ;;
     bench_c2) step bench_c2 400 python bench.py --config ping_pong ;;
     bench_c4) step bench_c4 500 python bench.py --config gossip ;;
     bench_c5) step bench_c5 400 python bench.py --config hotspot ;;

@@ -20,40 +20,53 @@ sys.path.insert(0, os.path.join(ROOT, "time-warp_amd"))
 from timewarp import isa, scenarios  # noqa: E402
 from timewarp.engine import Engine  # noqa: E402
 
-NAMES = ["loop_cyc", "sel_cyc", "wait_cyc", "step_cyc", "iters", "pops", "superseded", "src_near", "src_far",
-         "src_run", "hit", "miss", "writeback", "hash_flush", "near_push", "run_push", "far_push", "insns",
-         "passes", "active_lanes", "kernel_cyc", "prolog_cyc", "epilog_cyc", "hash_terms"]
-OPS = {v: k[3:] for k, v in vars(isa).items() if k.startswith("OP_") and isinstance(v, int) and k != "OP_COUNT"}
+NAMES = ["sel_cyc", "wait_cyc", "pre_cyc", "step_cyc", "iters", "pops", "superseded", "src_near", "src_far",
+         "src_run", "hit", "miss", "insns", "passes", "near_push", "run_push", "far_push", "hash", "store",
+         "throwto", "alloc", "die", "loop_cyc", "tail_cyc", "store_cyc"]
+
+
+
+LITE = ["sel_cyc", "pre_cyc", "step_cyc", "loop_cyc", "iters", "pops"]
 
 
 def read(eng):
-    buf = (C.c_ulonglong * 128)()
+    buf = (C.c_ulonglong * 32)()
     fn = eng.lib.tw_prof_read
     fn.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]
-    n = fn(eng.ctx, buf, 128, 1)
+    n = fn(eng.ctx, buf, 32, 1)
     if n < 0:
         raise RuntimeError(f"tw_prof_read: {n}")
-    v = list(buf)
-    out = {k: v[i] for i, k in enumerate(NAMES)}
-    out["ops"] = {OPS.get(o, str(o)): {"passes": v[32 + o], "cyc": v[80 + o]} for o in range(43)
-                  if v[32 + o] or v[80 + o]}
-    return out
+    if os.environ.get("TW_PROBE_LITE"):
+        return {k: buf[i] for i, k in enumerate(LITE)}
+    return {k: buf[i] for i, k in enumerate(NAMES)}
 
 
-def derived(d, waves):
-    it = max(d["iters"], 1)
+def derived_lite(d):
+    pops, it = max(d["pops"], 1), max(d["iters"], 1)
+    return {"loop_per_pop": d["loop_cyc"] / pops, "sel_per_iter": d["sel_cyc"] / it,
+            "pre_per_pop": d["pre_cyc"] / pops, "step_per_pop": d["step_cyc"] / pops,
+            "iters_per_pop": it / pops}
+
+
+def derived(d):
+    """Counters are summed over lanes, cycles weighted by the lanes active in each
+    iteration: x / pops = wave cycles (or counts) per committed event."""
     pops = max(d["pops"], 1)
+    it = max(d["iters"], 1)
     return {
-        "cyc_per_iter": d["loop_cyc"] / it,
+        "cyc_per_pop": d["loop_cyc"] / pops,
         "sel_per_iter": d["sel_cyc"] / it,
         "wait_per_iter": d["wait_cyc"] / it,
-        "step_per_iter": d["step_cyc"] / it,
-        "lanes_per_iter": d["active_lanes"] / it,
+        "pre_per_pop": d["pre_cyc"] / pops,
+        "step_per_pop": d["step_cyc"] / pops,
+        "tail_per_pop": d["tail_cyc"] / pops,
+        "store_per_pop": d["store_cyc"] / pops,
         "hit_rate": d["hit"] / max(d["hit"] + d["miss"], 1),
-        "passes_per_iter": d["passes"] / it,
+        "passes_per_pop": d["passes"] / pops,
         "insns_per_pop": d["insns"] / pops,
-        "src_mix": [d["src_near"] / pops, d["src_run"] / pops, d["src_far"] / pops],
-        "kernel_cyc_per_wave": d["kernel_cyc"] / max(waves, 1),
+        "src_mix_near_run_far": [d["src_near"] / it, d["src_run"] / it, d["src_far"] / it],
+        "per_pop": {k: d[k] / pops for k in ("hash", "store", "throwto", "alloc", "die", "near_push", "run_push",
+                                             "far_push", "superseded", "miss")},
     }
 
 
@@ -65,7 +78,6 @@ def main():
     eng = Engine(0).load(scn)
     if not hasattr(eng.lib, "tw_prof_read"):
         raise SystemExit("TW_LIB is not the diagnostic build (tw_prof_read missing)")
-    waves = (R + 63) // 64
     read(eng)
     eng.reset()
     for name, t_end in [("startup<1s", 999_999), ("token<L", Ld - 1), ("teardown", (1 << 63) - 1)]:
@@ -73,7 +85,8 @@ def main():
         d = read(eng)
         ms = float(eng.launch_ms().sum())
         rec = {"phase": name, "events": st.events, "kernel_ms": ms, "launches": st.launches,
-               "derived": derived(d, waves * st.launches), "counters": d}
+               "ev_per_s": st.events / max(ms, 1e-9) * 1e3, "derived": derived_lite(d) if os.environ.get("TW_PROBE_LITE") else derived(d),
+               "counters": d}
         print(json.dumps(rec), flush=True)
 
 
