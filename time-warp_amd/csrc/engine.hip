@@ -12,17 +12,20 @@
 //     so lanes never synchronise and the whole chip streams replicas;
 //   * all per-replica HBM state is replica-minor ([index][replica]): while
 //     replicas run in lock-step (scenario start-up, identical programs) a
-//     wavefront's 64 accesses to "the same" slot/node/heap index coalesce into
+//     wavefront's 64 accesses to "the same" slot/node/queue index coalesce into
 //     contiguous 1-4 KiB transactions; when they diverge each lane touches one
 //     64-B line per record;
-//   * TimedT's event queue (a pqueue MinQueue of continuations) becomes, per
-//     replica, an on-chip NEAR heap in LDS (events due within the scenario's
-//     horizon: forks' +1 µs, message deliveries, short waits) plus a 4-ary FAR
-//     heap in HBM (sleepForever timers, killers, long waits).  Every thread has
-//     at most one queued event (a thread is either running or parked at one
-//     `wait`), so throwTo's queue rebuild (TimedT.hs:361-368) becomes an O(1)
-//     re-stamp: a fresh (now, seq) entry is pushed and the old one is dropped
-//     lazily at pop time (slot.wake_seq no longer matches);
+//   * at one wave per SIMD nothing hides latency, so the event loop keeps its
+//     working set on chip: TimedT's event queue (a pqueue MinQueue of
+//     continuations) becomes an LDS NEAR heap of 64-bit keys (events due within
+//     the scenario's horizon) with its root cached in registers, plus monotone
+//     FIFO runs and a 4-ary heap in HBM for far events; thread records of
+//     near-queued threads live in a write-back LDS cache (LRU), so the common
+//     pop -> run -> re-queue cycle never waits on HBM;
+//   * every thread has at most one queued event, so throwTo's queue rebuild
+//     (TimedT.hs:361-368) becomes an O(1) re-stamp: a fresh (now, seq) entry is
+//     pushed (or the near entry re-keyed in place) and a superseded entry is
+//     dropped lazily at pop time (slot.wake_seq no longer matches);
 //   * the event order is (t, seq) with seq a per-replica insertion counter —
 //     bit-identical to the oracle's canonical mode.
 #include <hip/hip_runtime.h>
@@ -35,12 +38,10 @@
 
 #include "../../include/timewarp.h"
 
-#ifndef TW_NEAR_CAP
 #define TW_NEAR_CAP 16          // on-chip queue entries per replica (LDS)
-#endif
-#define TW_BLOCK 64             // one wavefront per workgroup
+#define TW_WG 256               // lanes per workgroup (4 waves share one program image)
 #define TW_RUNS 4               // monotone far-queue runs per replica
-#define TW_RCACHE 4             // write-through thread-record cache entries per lane (LDS)
+#define TW_RC 6                 // write-back thread-record cache entries per lane (LDS)
 #define TW_STEP_CAP (1u << 22)  // instructions per thread step (== oracle kStepCap)
 
 // Explicit address spaces: generic (flat) pointers would make every HBM and
@@ -53,29 +54,23 @@
 #define LAS
 #endif
 
-// Diagnostic build (-DTW_PROF=1, lib/libtimewarp_prof.so): per-lane counters
-// and s_memtime cycle splits summed into Dev::prof at kernel end.  The product
-// build compiles every PROF_* to nothing.
-#ifdef TW_PROF_LITE  // cycle splits + iteration/pop counts only (32-bit, no forced waits)
+// Diagnostic build (-DTW_PROF_LITE, lib/libtimewarp_lite.so): s_memtime cycle
+// splits summed into Dev::prof at kernel end (tools/kernel_probe.py).  The
+// product build compiles every LITE_* to nothing.
+#ifdef TW_PROF_LITE
 #define LITE_T(v) uint64_t v = __builtin_amdgcn_s_memtime()
-#define LITE_ACC(i, v) (lite[(i)] += (uint32_t)(v))
+#define LITE_ACC(i, v) (L.lite[(i)] += (uint32_t)(v))
+#define LITE_ACCM(i, v) (lite[(i)] += (uint32_t)(v))
+#define LITE_WRAP(i, stmt) do { uint64_t _w0 = __builtin_amdgcn_s_memtime(); stmt; LITE_ACCM(i, __builtin_amdgcn_s_memtime() - _w0); } while (0)
+#define KLITE_WRAP(i, stmt) do { uint64_t _w0 = __builtin_amdgcn_s_memtime(); stmt; LITE_ACC(i, __builtin_amdgcn_s_memtime() - _w0); } while (0)
 #else
 #define LITE_T(v) ((void)0)
 #define LITE_ACC(i, v) ((void)0)
+#define LITE_ACCM(i, v) ((void)0)
+#define LITE_WRAP(i, stmt) do { stmt; } while (0)
+#define KLITE_WRAP(i, stmt) do { stmt; } while (0)
 #endif
-#ifdef TW_PROF
-#define PROF_N 32
-#define PROF_INC(i, v) (L_prof[(i)] += (v))
-#define KPROF_INC(i, v) (L.L_prof[(i)] += (v))
-#define PROF_T(v) uint64_t v = __builtin_amdgcn_s_memtime()
-#else
-#define KPROF_INC(i, v) ((void)0)
-#define PROF_INC(i, v) ((void)0)
-#define PROF_T(v) ((void)0)
-#endif
-enum { P_SEL, P_WAIT, P_PRE, P_STEP, P_ITERS, P_POPS, P_SUPER, P_SRC_NEAR, P_SRC_FAR, P_SRC_RUN, P_HIT, P_MISS,
-       P_INSNS, P_PASSES, P_NEAR_PUSH, P_RUN_PUSH, P_FAR_PUSH, P_HASH, P_STORE, P_THROWTO, P_ALLOC, P_DIE,
-       P_LOOP, P_TAIL, P_STCYC, P_COUNT };
+#define P_COUNT 16
 
 namespace {
 
@@ -86,21 +81,38 @@ __device__ __forceinline__ T GAS* gp(T* p) {
 
 // ------------------------------------------------------------------ layout
 // Thread slot record: 64 B, [slot][replica].
-//  w0: pc:16 | nfr:2 | flags:6 | exc_code:8      flags bit0 started, bit1 main
+//  w0: pc:16 | nfr:2 | flags:6 | exc_code:8
 //  w1: node   w2: tid   w3: wake_seq (0 = not queued)
-//  w4..w6: frames (mask:16 << 16 | pc:16; mask 0 = finally frame of epoch pc)
+//  f0..f2: frames (mask:16 << 16 | pc:16; mask 0 = finally frame of epoch pc)
 //  w7: pending exception value
-//  r[4]: int64 registers
+//  r0..r3: int64 registers
 struct Th {
-    uint32_t w0, w1, w2, w3;  // pc|nfr|flags|exc, node, tid, wake_seq
-    uint32_t f0, f1, f2;      // catch / finally frames
-    uint32_t w7;              // pending exception value
+    uint32_t w0, w1, w2, w3;
+    uint32_t f0, f1, f2;
+    uint32_t w7;
     int64_t r0, r1, r2, r3;
 };
 
-// Registers and frames are selected with mask arithmetic, never indexed: a
+#define F_STARTED 1u
+#define F_MAIN 2u
+#define F_PHANTOM 4u   // LP mode: a delivery record's stand-in for the deliverer's wake pop
+#define F_OWNS 8u      // has bound its node with an owned listener (checked at death)
+#define F_NEARQ 16u    // its live queue entry is in the on-chip near heap
+
+__device__ __forceinline__ uint32_t th_pc(const Th& t) { return t.w0 & 0xFFFFu; }
+__device__ __forceinline__ void th_set_pc(Th& t, uint32_t pc) { t.w0 = (t.w0 & 0xFFFF0000u) | (pc & 0xFFFFu); }
+__device__ __forceinline__ uint32_t th_nfr(const Th& t) { return (t.w0 >> 16) & 3u; }
+__device__ __forceinline__ void th_set_nfr(Th& t, uint32_t n) { t.w0 = (t.w0 & ~(3u << 16)) | (n << 16); }
+__device__ __forceinline__ uint32_t th_flags(const Th& t) { return (t.w0 >> 18) & 0x3Fu; }
+__device__ __forceinline__ void th_or_flags(Th& t, uint32_t f) { t.w0 |= (f & 0x3Fu) << 18; }
+__device__ __forceinline__ void th_clr_flags(Th& t, uint32_t f) { t.w0 &= ~((f & 0x3Fu) << 18); }
+__device__ __forceinline__ uint32_t th_exc(const Th& t) { return t.w0 >> 24; }
+__device__ __forceinline__ void th_set_exc(Th& t, uint32_t c) { t.w0 = (t.w0 & 0x00FFFFFFu) | (c << 24); }
+
+// Registers and frames are selected with mask arithmetic, never indexing: a
 // select chain over the fields gets folded into an indexed load, which pins
-// the whole record in scratch memory.
+// the whole record in scratch memory.  Register operands are wave-uniform
+// (the dispatch is on the whole instruction word), so the masks are scalar.
 __device__ __forceinline__ int64_t getr(const Th& t, uint32_t a) {
     const int64_t m0 = -(int64_t)(a == 0), m1 = -(int64_t)(a == 1), m2 = -(int64_t)(a == 2), m3 = -(int64_t)(a == 3);
     return (t.r0 & m0) | (t.r1 & m1) | (t.r2 & m2) | (t.r3 & m3);
@@ -123,23 +135,10 @@ __device__ __forceinline__ void setf(Th& t, uint32_t i, uint32_t v) {
     t.f2 = (v & m2) | (t.f2 & ~m2);
 }
 
-#define F_STARTED 1u
-#define F_MAIN 2u
-#define F_PHANTOM 4u   // LP mode: a delivery record's stand-in for the deliverer's wake pop
-
-__device__ __forceinline__ uint32_t th_pc(const Th& t) { return t.w0 & 0xFFFFu; }
-__device__ __forceinline__ void th_set_pc(Th& t, uint32_t pc) { t.w0 = (t.w0 & 0xFFFF0000u) | (pc & 0xFFFFu); }
-__device__ __forceinline__ uint32_t th_nfr(const Th& t) { return (t.w0 >> 16) & 3u; }
-__device__ __forceinline__ void th_set_nfr(Th& t, uint32_t n) { t.w0 = (t.w0 & ~(3u << 16)) | (n << 16); }
-__device__ __forceinline__ uint32_t th_flags(const Th& t) { return (t.w0 >> 18) & 0x3Fu; }
-__device__ __forceinline__ void th_or_flags(Th& t, uint32_t f) { t.w0 |= (f & 0x3Fu) << 18; }
-__device__ __forceinline__ uint32_t th_exc(const Th& t) { return t.w0 >> 24; }
-__device__ __forceinline__ void th_set_exc(Th& t, uint32_t c) { t.w0 = (t.w0 & 0x00FFFFFFu) | (c << 24); }
-
 enum {
     SC_NOW, SC_FINAL_T, SC_EVENTS, SC_DELIVERED, SC_DROPPED, SC_UNDELIV, SC_THREADS, SC_SEQ, SC_TIDC,
-    SC_LIVE, SC_NEAR_N, SC_FAR_N, SC_STATUS, SC_MAIN_EXC, SC_PENDING_MAIN, SC_FREE_TOP, SC_TMO_CTR,
-    SC_RH0, SC_RC0 = SC_RH0 + TW_RUNS, SC_COUNT = SC_RC0 + TW_RUNS
+    SC_LIVE, SC_NEAR_N, SC_FAR_N, SC_STATUS, SC_MAIN_EXC, SC_PENDING_MAIN, SC_FREE_N, SC_FTOP, SC_BUMP,
+    SC_TMO_CTR, SC_RH0, SC_RC0 = SC_RH0 + TW_RUNS, SC_COUNT = SC_RC0 + TW_RUNS
 };
 
 struct Dev {
@@ -155,15 +154,14 @@ struct Dev {
     const uint32_t* link_dst;
     const uint32_t* link_rev;
     const uint32_t* link_table;   // [L*D][R] or null
-    // per-replica scalars: one [field][replica] block of 64-bit words (SC_*),
-    // a single base pointer keeps the loop's scalar-register set small
+    // per-replica scalars: one [field][replica] block of 64-bit words (SC_*)
     uint64_t* scal;
     // per-replica arrays
     uint4* slots;        // [S][R][4]
-    uint32_t* free_stk;  // [S][R]
-    uint4* far;          // [Q][R]  {t_lo, t_hi, key_lo(slot), key_hi(seq)}
+    uint32_t* free_stk;  // [S][R] (entries below the register-cached top)
+    uint4* far;          // [Q][R]  {t_lo, t_hi, slot, seq}
     uint4* runs;         // [TW_RUNS][Cr][R] monotone FIFO runs (ring buffers)
-    uint4* near_spill;   // [NEAR_CAP][R]
+    uint4* near_spill;   // [NEAR_CAP][R]  near heap between launches
     int64_t* nvars;      // [N*4][R]
     uint64_t* hash;      // [N][R]
     uint32_t* bind;      // [N][R] 0 or set+1
@@ -190,50 +188,108 @@ __device__ __forceinline__ uint64_t mix64(uint64_t z) {
     z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
     return z ^ (z >> 31);
 }
-// == tw_term of include/timewarp.h (one mix64 for the common val == 0 case)
+// == tw_term of include/timewarp.h
 __device__ __forceinline__ uint64_t term(int64_t t, uint32_t kind, int64_t val) {
     uint64_t v = val ? mix64((uint64_t)val ^ 0x9e3779b97f4a7c15ull) : 0ull;
     return mix64((((uint64_t)t << 20) | kind) ^ v);
 }
+__device__ __forceinline__ uint64_t term0(int64_t t, uint32_t kind) { return mix64(((uint64_t)t << 20) | kind); }
 
-// ------------------------------------------------------------ event keys
-// key = (t, seq<<32 | slot): seq is unique per replica, so (t, key) orders by (t, seq).
-__device__ __forceinline__ bool kless(int64_t ta, uint64_t ka, int64_t tb, uint64_t kb) {
-    return ta < tb || (ta == tb && ka < kb);
+__device__ __forceinline__ bool tless(int64_t ta, uint32_t sa, int64_t tb, uint32_t sb) {
+    return ta < tb || (ta == tb && sa < sb);
 }
+__device__ __forceinline__ uint4 ent(int64_t t, uint32_t slot, uint32_t seq) {
+    return make_uint4((uint32_t)t, (uint32_t)((uint64_t)t >> 32), slot, seq);
+}
+__device__ __forceinline__ int64_t ent_t(uint4 e) { return (int64_t)(((uint64_t)e.y << 32) | e.x); }
+
+enum { ST_CACHE, ST_THROUGH, ST_DEAD };  // store_rec modes
+
+// Six per-lane words with no array behind them: an array written at a per-lane
+// index (the LRU victim) is re-rolled by the compiler into scratch stores.
+static_assert(TW_RC == 6, "RegVec6 holds the record-cache metadata");
+struct RegVec6 {
+    uint32_t v0, v1, v2, v3, v4, v5;
+    __device__ __forceinline__ void fill(uint32_t x) { v0 = v1 = v2 = v3 = v4 = v5 = x; }
+    // per-lane h: mask arithmetic (a select chain would be folded into an
+    // indexed load and pin the whole lane state in scratch)
+    __device__ __forceinline__ uint32_t at(int h) const {
+        return (v0 & (0u - (h == 0))) | (v1 & (0u - (h == 1))) | (v2 & (0u - (h == 2))) |
+               (v3 & (0u - (h == 3))) | (v4 & (0u - (h == 4))) | (v5 & (0u - (h == 5)));
+    }
+    __device__ __forceinline__ void put(int h, uint32_t x) {
+        uint32_t m;
+        m = 0u - (h == 0); v0 = (x & m) | (v0 & ~m);
+        m = 0u - (h == 1); v1 = (x & m) | (v1 & ~m);
+        m = 0u - (h == 2); v2 = (x & m) | (v2 & ~m);
+        m = 0u - (h == 3); v3 = (x & m) | (v3 & ~m);
+        m = 0u - (h == 4); v4 = (x & m) | (v4 & ~m);
+        m = 0u - (h == 5); v5 = (x & m) | (v5 & ~m);
+    }
+    __device__ __forceinline__ int find(uint32_t x) const {
+        int h = -1;
+        h = v0 == x ? 0 : h;
+        h = v1 == x ? 1 : h;
+        h = v2 == x ? 2 : h;
+        h = v3 == x ? 3 : h;
+        h = v4 == x ? 4 : h;
+        h = v5 == x ? 5 : h;
+        return h;
+    }
+    __device__ __forceinline__ int argmin() const {
+        int h = 0;
+        uint32_t b = v0;
+        if (v1 < b) { b = v1; h = 1; }
+        if (v2 < b) { b = v2; h = 2; }
+        if (v3 < b) { b = v3; h = 3; }
+        if (v4 < b) { b = v4; h = 4; }
+        if (v5 < b) { b = v5; h = 5; }
+        return h;
+    }
+};
 
 template <bool LP>
 struct Lane {
-    const Dev* c;
+    Dev c;  // by value: kernel arguments stay in SGPRs
     uint32_t r;       // replica
-    // LDS near heap of this lane: element j at base[j * TW_BLOCK]
-    int64_t LAS* nt;
-    uint64_t LAS* nk;
-    // program image and constant pool (LDS copy)
-    const uint2 LAS* P;
-    const int64_t LAS* K;
-    // far runs: head index, count, head key, tail key (indexed only by unrolled constants)
-    uint32_t rh[TW_RUNS], rc[TW_RUNS];
+    // LDS (lane-offset pointers; element j at [j * TW_WG])
+    uint64_t LAS* nk;     // near heap keys: (t - nbase) << 32 | seq
+    uint32_t LAS* ns;     // near heap slots
+    uint4 LAS* rcd;       // record cache: entry e quad q at [(e*4+q) * TW_WG]
+    const uint2 LAS* P;   // program image
+    const int64_t LAS* K; // constant pool
+    // near heap
+    uint32_t near_n;
+    int64_t nbase;
+    uint64_t nrk;  // cached root key
+    uint32_t nrs;  // cached root slot
+    // far runs: head index, count, head (t, seq, slot), tail (t, seq)
+    uint32_t rh[TW_RUNS], rn[TW_RUNS];
     int64_t rt[TW_RUNS], ut[TW_RUNS];
-    uint64_t rk[TW_RUNS], uk[TW_RUNS];
-    uint32_t next_free;  // cached free_stk[free_top-1] (prefetched)
-    // write-through record cache in LDS: entry e quad q at rcache[(e*4+q)*TW_BLOCK]
-    uint4 LAS* rcache;
-    uint32_t ctag[TW_RCACHE];
-    uint32_t cptr;
-    // cached replica scalars
-    int64_t now;
-    uint32_t seq, tidc, live, near_n, far_n, status, main_exc, free_top, tmo_ctr;
-    uint64_t events, delivered, dropped, undeliv, threads;
-    int64_t final_t;
-    // cached far top
-    int64_t far_t;
-    uint64_t far_k;
-#ifdef TW_PROF
-    uint64_t L_prof[P_COUNT];
+    uint32_t rs[TW_RUNS], rsl[TW_RUNS], us[TW_RUNS];
+    // far heap top
+    uint32_t far_n;
+    int64_t ft;
+    uint32_t fs, fsl;
+    // min over far sources (lazily recomputed: a run head reload overlaps the step)
+    bool far_dirty;
+    int fsrc;  // -1 none, 0..TW_RUNS-1 run, TW_RUNS heap
+    int64_t fmt;
+    uint32_t fms, fmsl;
+    // write-back record cache: tags, LRU stamps, dirty bits
+    RegVec6 ctag, cst;
+    uint32_t cdirty, clk;
+    // free slots: bump pointer + stack with its top in a register
+    uint32_t free_n, ftop, bump;
+    // replica scalars
+    int64_t now, final_t;
+    uint32_t seq, tidc, live, status, main_exc, tmo_ctr;
+    uint32_t d_ev, d_dl, d_dr, d_ud, d_th;  // this launch's counter increments
+#ifdef TW_PROF_LITE
+    uint32_t lite[16];  // sel, pre, step, loop, iters, pops, dispatch, tail, store, spawn, yield-enq, throw, die, selmin, load, pop
 #endif
 
-    __device__ __forceinline__ size_t ix(size_t i) const { return i * c->R + r; }
+    __device__ __forceinline__ size_t ix(size_t i) const { return i * c.R + r; }
     // per-node arrays: replica mode [node][R]; LP mode a lane owns exactly one node
     __device__ __forceinline__ size_t nix(uint32_t node, uint32_t var) const {
         return LP ? ix(var) : ix((size_t)node * 4 + var);
@@ -241,7 +297,7 @@ struct Lane {
     __device__ __forceinline__ size_t bix(uint32_t node) const { return LP ? ix(0) : ix(node); }
     __device__ __forceinline__ size_t lix(uint64_t link) const { return LP ? (size_t)link : ix(link); }
     __device__ __forceinline__ size_t tix(uint64_t link, uint32_t ord) const {
-        size_t i = (size_t)link * c->D + ord % c->D;
+        size_t i = (size_t)link * c.D + ord % c.D;
         return LP ? i : ix(i);
     }
 
@@ -250,129 +306,125 @@ struct Lane {
     }
 
     // ---------------------------------------------------------- near heap (LDS)
-    // 4-ary heap: 16 entries are two levels, and the four children of a node
-    // are independent LDS loads, so a sift costs at most two LDS round trips.
-    __device__ __forceinline__ void near_sift_up(uint32_t i, int64_t t, uint64_t k) {
+    // 4-ary heap of unique 64-bit keys: 16 entries are two levels, the four
+    // children of a node are read together (one LDS round trip per level).
+    __device__ __forceinline__ uint64_t nkey(int64_t t, uint32_t s) const {
+        return ((uint64_t)(t - nbase) << 32) | s;
+    }
+    __device__ __forceinline__ bool near_fits(int64_t t) const {
+        return near_n < TW_NEAR_CAP && t - now < c.horizon && (uint64_t)(t - nbase) < 0xFFFFFFFFull;
+    }
+    __device__ __forceinline__ void near_sift_up(uint32_t i, uint64_t k, uint32_t s) {
         while (i > 0) {
             uint32_t p = (i - 1) >> 2;
-            int64_t pt = nt[p * TW_BLOCK];
-            uint64_t pk = nk[p * TW_BLOCK];
-            if (!kless(t, k, pt, pk)) break;
-            nt[i * TW_BLOCK] = pt;
-            nk[i * TW_BLOCK] = pk;
+            uint64_t pk = nk[p * TW_WG];
+            uint32_t ps = ns[p * TW_WG];
+            if (k > pk) break;
+            nk[i * TW_WG] = pk;
+            ns[i * TW_WG] = ps;
             i = p;
         }
-        nt[i * TW_BLOCK] = t;
-        nk[i * TW_BLOCK] = k;
+        nk[i * TW_WG] = k;
+        ns[i * TW_WG] = s;
+        if (i == 0) { nrk = k; nrs = s; }
     }
-    __device__ __forceinline__ void near_sift_down(uint32_t i, int64_t t, uint64_t k) {
+    __device__ __forceinline__ void near_sift_down(uint32_t i, uint64_t k, uint32_t s) {
         const uint32_t n = near_n;
         for (;;) {
             uint32_t c0 = 4 * i + 1;
             if (c0 >= n) break;
-            uint32_t cn = n - c0 < 4 ? n - c0 : 4;
-            int64_t bt = nt[c0 * TW_BLOCK];
-            uint64_t bk = nk[c0 * TW_BLOCK];
-            uint32_t bi = c0;
-#pragma unroll
-            for (uint32_t j = 1; j < 4; ++j) {
-                if (j < cn) {
-                    int64_t jt = nt[(c0 + j) * TW_BLOCK];
-                    uint64_t jk = nk[(c0 + j) * TW_BLOCK];
-                    if (kless(jt, jk, bt, bk)) { bt = jt; bk = jk; bi = c0 + j; }
-                }
-            }
-            if (!kless(bt, bk, t, k)) break;
-            nt[i * TW_BLOCK] = bt;
-            nk[i * TW_BLOCK] = bk;
+            uint64_t k0 = nk[c0 * TW_WG], k1 = ~0ull, k2 = ~0ull, k3 = ~0ull;
+            uint32_t s0 = ns[c0 * TW_WG], s1 = 0, s2 = 0, s3 = 0;
+            if (c0 + 1 < n) { k1 = nk[(c0 + 1) * TW_WG]; s1 = ns[(c0 + 1) * TW_WG]; }
+            if (c0 + 2 < n) { k2 = nk[(c0 + 2) * TW_WG]; s2 = ns[(c0 + 2) * TW_WG]; }
+            if (c0 + 3 < n) { k3 = nk[(c0 + 3) * TW_WG]; s3 = ns[(c0 + 3) * TW_WG]; }
+            uint64_t bk = k0;
+            uint32_t bs = s0, bi = c0;
+            if (k1 < bk) { bk = k1; bs = s1; bi = c0 + 1; }
+            if (k2 < bk) { bk = k2; bs = s2; bi = c0 + 2; }
+            if (k3 < bk) { bk = k3; bs = s3; bi = c0 + 3; }
+            if (k < bk) break;
+            nk[i * TW_WG] = bk;
+            ns[i * TW_WG] = bs;
+            if (i == 0) { nrk = bk; nrs = bs; }
             i = bi;
         }
-        nt[i * TW_BLOCK] = t;
-        nk[i * TW_BLOCK] = k;
+        nk[i * TW_WG] = k;
+        ns[i * TW_WG] = s;
+        if (i == 0) { nrk = k; nrs = s; }
     }
-    __device__ __forceinline__ void near_push(int64_t t, uint64_t k) {
-        PROF_INC(P_NEAR_PUSH, 1);
-        near_sift_up(near_n++, t, k);
+    __device__ __forceinline__ void near_push(int64_t t, uint32_t sq, uint32_t slot) {
+        near_sift_up(near_n++, nkey(t, sq), slot);
     }
     __device__ __forceinline__ void near_pop() {
         uint32_t n = --near_n;
         if (n == 0) return;
-        near_sift_down(0, nt[n * TW_BLOCK], nk[n * TW_BLOCK]);
+        near_sift_down(0, nk[n * TW_WG], ns[n * TW_WG]);
     }
-    // Re-key the live near entry of `slot` (queued with seq `old_seq`) in place;
-    // false if that entry is not on chip.  Keeps repeated throwTo of one thread
-    // from piling up superseded entries.
-    __device__ __forceinline__ bool near_rekey(uint32_t slot, uint32_t old_seq, int64_t t, uint64_t k) {
-        const uint64_t old = ((uint64_t)old_seq << 32) | slot;
+    // Re-key the live near entry with seq `old_seq` (seqs are unique) to (t, sq).
+    __device__ __forceinline__ bool near_rekey(uint32_t old_seq, int64_t t, uint32_t sq, uint32_t slot) {
         for (uint32_t i = 0; i < near_n; ++i) {
-            if (nk[i * TW_BLOCK] == old) {
-                int64_t ot = nt[i * TW_BLOCK];
-                if (kless(t, k, ot, old)) near_sift_up(i, t, k);
-                else near_sift_down(i, t, k);
+            uint64_t ok = nk[i * TW_WG];
+            if ((uint32_t)ok == old_seq) {
+                uint64_t k = nkey(t, sq);
+                if (k < ok) near_sift_up(i, k, slot);
+                else near_sift_down(i, k, slot);
                 return true;
             }
         }
         return false;
     }
+    // Move the near heap to a new time base (keeps (t - nbase) inside 32 bits).
+    __device__ void near_rebase(int64_t nb) {
+        uint64_t d = (uint64_t)(nb - nbase) << 32;
+        for (uint32_t i = 0; i < near_n; ++i) nk[i * TW_WG] -= d;
+        nrk -= d;
+        nbase = nb;
+    }
 
     // ------------------------------------------------------ far heap (HBM, 4-ary)
-    __device__ __forceinline__ uint4 far_ld(uint32_t i) const { return gp(c->far)[ix(i)]; }
-    __device__ __forceinline__ void far_st(uint32_t i, int64_t t, uint64_t k) const {
-        gp(c->far)[ix(i)] = make_uint4((uint32_t)t, (uint32_t)((uint64_t)t >> 32), (uint32_t)k, (uint32_t)(k >> 32));
-    }
-    __device__ __forceinline__ void far_push(int64_t t, uint64_t k) {
-        if (far_n >= c->Q) { fail(TW_REP_ERR_QUEUE); return; }
-        PROF_INC(P_FAR_PUSH, 1);
+    __device__ __forceinline__ uint4 far_ld(uint32_t i) const { return gp(c.far)[ix(i)]; }
+    __device__ __forceinline__ void far_st(uint32_t i, uint4 e) const { gp(c.far)[ix(i)] = e; }
+    __device__ __forceinline__ void far_push(int64_t t, uint32_t sq, uint32_t slot) {
+        if (far_n >= c.Q) { fail(TW_REP_ERR_QUEUE); return; }
         uint32_t i = far_n++;
         while (i > 0) {
             uint32_t p = (i - 1) >> 2;
             uint4 e = far_ld(p);
-            int64_t pt = (int64_t)(((uint64_t)e.y << 32) | e.x);
-            uint64_t pk = ((uint64_t)e.w << 32) | e.z;
-            if (!kless(t, k, pt, pk)) break;
-            gp(c->far)[ix(i)] = e;
+            if (!tless(t, sq, ent_t(e), e.w)) break;
+            far_st(i, e);
             i = p;
         }
-        far_st(i, t, k);
-        if (i == 0) { far_t = t; far_k = k; }
+        far_st(i, ent(t, slot, sq));
+        if (i == 0) { ft = t; fs = sq; fsl = slot; far_dirty = true; }
     }
     __device__ __forceinline__ void far_pop() {
         uint32_t n = --far_n;
+        far_dirty = true;
         if (n == 0) return;
         uint4 le = far_ld(n);
-        int64_t t = (int64_t)(((uint64_t)le.y << 32) | le.x);
-        uint64_t k = ((uint64_t)le.w << 32) | le.z;
+        int64_t t = ent_t(le);
         uint32_t i = 0;
         for (;;) {
             uint32_t c0 = 4 * i + 1;
             if (c0 >= n) break;
             uint32_t cn = n - c0 < 4 ? n - c0 : 4;
-            // the (up to) four children are independent loads: issue all, then reduce
             uint4 e0 = far_ld(c0);
             uint4 e1 = cn > 1 ? far_ld(c0 + 1) : e0;
             uint4 e2 = cn > 2 ? far_ld(c0 + 2) : e0;
             uint4 e3 = cn > 3 ? far_ld(c0 + 3) : e0;
+            uint4 b = e0;
             uint32_t best = 0;
-            int64_t bt = (int64_t)(((uint64_t)e0.y << 32) | e0.x);
-            uint64_t bk = ((uint64_t)e0.w << 32) | e0.z;
-            {
-                int64_t jt = (int64_t)(((uint64_t)e1.y << 32) | e1.x);
-                uint64_t jk = ((uint64_t)e1.w << 32) | e1.z;
-                if (cn > 1 && kless(jt, jk, bt, bk)) { best = 1; bt = jt; bk = jk; }
-                jt = (int64_t)(((uint64_t)e2.y << 32) | e2.x);
-                jk = ((uint64_t)e2.w << 32) | e2.z;
-                if (cn > 2 && kless(jt, jk, bt, bk)) { best = 2; bt = jt; bk = jk; }
-                jt = (int64_t)(((uint64_t)e3.y << 32) | e3.x);
-                jk = ((uint64_t)e3.w << 32) | e3.z;
-                if (cn > 3 && kless(jt, jk, bt, bk)) { best = 3; bt = jt; bk = jk; }
-            }
-            if (!kless(bt, bk, t, k)) break;
-            far_st(i, bt, bk);
-            if (i == 0) { far_t = bt; far_k = bk; }
+            if (cn > 1 && tless(ent_t(e1), e1.w, ent_t(b), b.w)) { b = e1; best = 1; }
+            if (cn > 2 && tless(ent_t(e2), e2.w, ent_t(b), b.w)) { b = e2; best = 2; }
+            if (cn > 3 && tless(ent_t(e3), e3.w, ent_t(b), b.w)) { b = e3; best = 3; }
+            if (!tless(ent_t(b), b.w, t, le.w)) break;
+            far_st(i, b);
+            if (i == 0) { ft = ent_t(b); fs = b.w; fsl = b.z; }
             i = c0 + best;
         }
-        far_st(i, t, k);
-        if (i == 0) { far_t = t; far_k = k; }
+        far_st(i, le);
+        if (i == 0) { ft = t; fs = le.w; fsl = le.z; }
     }
 
     // ---------------------------------------------------- far runs (HBM FIFOs)
@@ -382,75 +434,78 @@ struct Lane {
     // (killers at one absolute time, sleepForever timers, re-stamped victims of
     // a killer sweep), so the heap sees only stragglers.
     __device__ __forceinline__ uint4 GAS* run_at(uint32_t j, uint32_t pos) const {
-        return gp(c->runs) + ((size_t)j * c->Cr + pos) * c->R + r;
+        return gp(c.runs) + ((size_t)j * c.Cr + pos) * c.R + r;
     }
-    __device__ __forceinline__ bool run_push(int64_t t, uint64_t k) {
-        if (c->Cr == 0) return false;
+    __device__ __forceinline__ bool run_push(int64_t t, uint32_t sq, uint32_t slot) {
+        if (c.Cr == 0) return false;
         int best = -1, empty = -1;
         int64_t bt = 0;
-        uint64_t bk = 0;
+        uint32_t bs = 0;
 #pragma unroll
         for (int j = 0; j < TW_RUNS; ++j) {
-            if (rc[j] == 0) {
+            if (rn[j] == 0) {
                 if (empty < 0) empty = j;
-            } else if (rc[j] < c->Cr && !kless(t, k, ut[j], uk[j])) {
-                if (best < 0 || kless(bt, bk, ut[j], uk[j])) { best = j; bt = ut[j]; bk = uk[j]; }
+            } else if (rn[j] < c.Cr && !tless(t, sq, ut[j], us[j])) {
+                if (best < 0 || tless(bt, bs, ut[j], us[j])) { best = j; bt = ut[j]; bs = us[j]; }
             }
         }
         int sel = best >= 0 ? best : empty;
         if (sel < 0) return false;
-        PROF_INC(P_RUN_PUSH, 1);
 #pragma unroll
         for (int j = 0; j < TW_RUNS; ++j) {
             if (j == sel) {
-                uint32_t pos = rh[j] + rc[j];
-                if (pos >= c->Cr) pos -= c->Cr;
-                *run_at(j, pos) = make_uint4((uint32_t)t, (uint32_t)((uint64_t)t >> 32), (uint32_t)k, (uint32_t)(k >> 32));
-                if (rc[j] == 0) { rt[j] = t; rk[j] = k; }
-                ut[j] = t; uk[j] = k;
-                ++rc[j];
+                uint32_t pos = rh[j] + rn[j];
+                if (pos >= c.Cr) pos -= c.Cr;
+                *run_at(j, pos) = ent(t, slot, sq);
+                if (rn[j] == 0) { rt[j] = t; rs[j] = sq; rsl[j] = slot; far_dirty = true; }
+                ut[j] = t; us[j] = sq;
+                ++rn[j];
             }
         }
         return true;
     }
     __device__ __forceinline__ void run_pop(int sel) {
+        far_dirty = true;
 #pragma unroll
         for (int j = 0; j < TW_RUNS; ++j) {
             if (j == sel) {
-                rh[j] = rh[j] + 1 == c->Cr ? 0 : rh[j] + 1;
-                if (--rc[j]) {
+                rh[j] = rh[j] + 1 == c.Cr ? 0 : rh[j] + 1;
+                if (--rn[j]) {  // next head: its latency overlaps this event's step
                     uint4 e = *run_at(j, rh[j]);
-                    rt[j] = (int64_t)(((uint64_t)e.y << 32) | e.x);
-                    rk[j] = ((uint64_t)e.w << 32) | e.z;
+                    rt[j] = ent_t(e); rs[j] = e.w; rsl[j] = e.z;
                 }
             }
         }
     }
-    __device__ __forceinline__ void push_far(int64_t t, uint64_t k) {
-        if (!run_push(t, k)) far_push(t, k);
+    __device__ __forceinline__ void far_min() {
+        far_dirty = false;
+        fsrc = -1;
+        if (far_n) { fsrc = TW_RUNS; fmt = ft; fms = fs; fmsl = fsl; }
+#pragma unroll
+        for (int j = 0; j < TW_RUNS; ++j)
+            if (rn[j] && (fsrc < 0 || tless(rt[j], rs[j], fmt, fms))) { fsrc = j; fmt = rt[j]; fms = rs[j]; fmsl = rsl[j]; }
+    }
+    __device__ __forceinline__ void push_far(int64_t t, uint32_t sq, uint32_t slot) {
+        if (!run_push(t, sq, slot)) far_push(t, sq, slot);
     }
 
     // ------------------------------------------------------------- queue
-    __device__ __forceinline__ void enqueue(Th& th, uint32_t slot, int64_t t) {
+    // Queue the thread at t with a fresh seq; returns true if the entry is on chip.
+    __device__ __forceinline__ bool enqueue(Th& th, uint32_t slot, int64_t t) {
         uint32_t s = ++seq;
         if (th.w3 == 0) ++live;
         th.w3 = s;
-        uint64_t k = ((uint64_t)s << 32) | slot;
-        if (t - now < c->horizon && near_n < TW_NEAR_CAP) near_push(t, k);
-        else push_far(t, k);
-    }
-    // Source of the minimum (t, seq) event: 0..TW_RUNS-1 run, TW_RUNS near, TW_RUNS+1 heap, -1 none.
-    __device__ __forceinline__ int min_source(int64_t& t, uint64_t& k) const {
-        int src = -1;
-        if (near_n) { src = TW_RUNS; t = nt[0]; k = nk[0]; }
-        if (far_n && (src < 0 || kless(far_t, far_k, t, k))) { src = TW_RUNS + 1; t = far_t; k = far_k; }
-#pragma unroll
-        for (int j = 0; j < TW_RUNS; ++j)
-            if (rc[j] && (src < 0 || kless(rt[j], rk[j], t, k))) { src = j; t = rt[j]; k = rk[j]; }
-        return src;
+        if (near_fits(t)) {
+            near_push(t, s, slot);
+            th_or_flags(th, F_NEARQ);
+            return true;
+        }
+        push_far(t, s, slot);
+        th_clr_flags(th, F_NEARQ);
+        return false;
     }
 
-    // ------------------------------------------------------------- slots
+    // ------------------------------------------------- thread records (cache)
     __device__ __forceinline__ static void unpack(Th& th, uint4 a, uint4 b, uint4 d, uint4 e) {
         th.w0 = a.x; th.w1 = a.y; th.w2 = a.z; th.w3 = a.w;
         th.f0 = b.x; th.f1 = b.y; th.f2 = b.z; th.w7 = b.w;
@@ -467,100 +522,122 @@ struct Lane {
         e = make_uint4((uint32_t)th.r2, (uint32_t)((uint64_t)th.r2 >> 32), (uint32_t)th.r3,
                        (uint32_t)((uint64_t)th.r3 >> 32));
     }
-    __device__ __forceinline__ int cache_find(uint32_t slot) const {
-        int h = -1;
-#pragma unroll
-        for (int e = 0; e < TW_RCACHE; ++e)
-            if (ctag[e] == slot) h = e;
-        return h;
-    }
-    // Thread records: HBM is authoritative (write-through); the LDS cache
-    // serves the common case of popping a thread whose record this lane wrote
-    // a few events earlier (a fork child, the forking parent, a throwTo victim).
-    __device__ __forceinline__ void load_th(uint32_t slot, Th& th) {
-        int e = cache_find(slot);
-        if (e >= 0) {
-            const uint4 LAS* q = rcache + (size_t)e * 4 * TW_BLOCK;
-            unpack(th, q[0], q[TW_BLOCK], q[2 * TW_BLOCK], q[3 * TW_BLOCK]);
-            PROF_INC(P_HIT, 1);
+    __device__ __forceinline__ int cfind(uint32_t slot) const { return ctag.find(slot); }
+    __device__ __forceinline__ void ctouch(int h) { cst.put(h, ++clk); }
+    __device__ __forceinline__ uint4 GAS* hrec(uint32_t slot) const { return gp(c.slots) + ix(slot) * 4; }
+    __device__ __forceinline__ uint4 LAS* crec(int e) const { return rcd + (size_t)e * 4 * TW_WG; }
+    // HBM holds a record unless the cache has a (newer) copy.
+    __device__ __forceinline__ void load_rec(uint32_t slot, Th& th) {
+        int h = cfind(slot);
+        if (h >= 0) {
+            const uint4 LAS* q = crec(h);
+            unpack(th, q[0], q[TW_WG], q[2 * TW_WG], q[3 * TW_WG]);
+            ctouch(h);
             return;
         }
-        PROF_INC(P_MISS, 1);
-        const uint4 GAS* p = gp(c->slots) + ix(slot) * 4;
+        const uint4 GAS* p = hrec(slot);
         unpack(th, p[0], p[1], p[2], p[3]);
     }
-    __device__ __forceinline__ void store_th(uint32_t slot, const Th& th) {
+    __device__ __forceinline__ void writeback(int e) {
+        const uint4 LAS* q = crec(e);
+        uint4 a = q[0], b = q[TW_WG], d = q[2 * TW_WG], f = q[3 * TW_WG];
+        uint4 GAS* p = hrec(ctag.at(e));
+        p[0] = a; p[1] = b; p[2] = d; p[3] = f;
+    }
+    // ST_CACHE: the thread is queued on chip (it runs again soon) -> keep the
+    // record in the cache, dirty; ST_THROUGH: queued far -> write it to HBM and
+    // drop any cached copy; ST_DEAD: only the header quad (the tid that
+    // invalidates stale refs) is written.
+    __device__ __forceinline__ void store_rec(uint32_t slot, const Th& th, int mode) {
         uint4 a, b, d, f;
         pack(th, a, b, d, f);
-        PROF_INC(P_STORE, 1);
-        uint4 GAS* p = gp(c->slots) + ix(slot) * 4;
-        p[0] = a; p[1] = b; p[2] = d; p[3] = f;
-        int e = cache_find(slot);
-        if (e < 0) {
-            e = (int)cptr;
-            cptr = (cptr + 1) & (TW_RCACHE - 1);
-#pragma unroll
-            for (int j = 0; j < TW_RCACHE; ++j)
-                if (j == e) ctag[j] = slot;
+        int h = cfind(slot);
+        if (mode == ST_CACHE) {
+            if (h < 0) {  // LRU victim (invalid entries carry stamp 0)
+                h = cst.argmin();
+                if (cdirty & (1u << h)) writeback(h);
+                ctag.put(h, slot);
+            }
+            uint4 LAS* q = crec(h);
+            q[0] = a; q[TW_WG] = b; q[2 * TW_WG] = d; q[3 * TW_WG] = f;
+            cdirty |= 1u << h;
+            ctouch(h);
+            return;
         }
-        uint4 LAS* q = rcache + (size_t)e * 4 * TW_BLOCK;
-        q[0] = a; q[TW_BLOCK] = b; q[2 * TW_BLOCK] = d; q[3 * TW_BLOCK] = f;
+        if (h >= 0) {
+            ctag.put(h, 0xFFFFFFFFu);
+            cst.put(h, 0);
+            cdirty &= ~(1u << h);
+        }
+        uint4 GAS* p = hrec(slot);
+        p[0] = a;
+        if (mode == ST_THROUGH) { p[1] = b; p[2] = d; p[3] = f; }
     }
-    // Free-slot stack; its top is cached in a register and the next one is
-    // prefetched at every pop, so a fork never waits on this load.
+    __device__ __forceinline__ void flush_cache() {
+#pragma unroll
+        for (int e = 0; e < TW_RC; ++e)
+            if (cdirty & (1u << e)) writeback(e);
+        cdirty = 0;
+    }
+
+    // Free slots: never-used slots come from a bump pointer (no memory read);
+    // freed slots form a LIFO stack whose top lives in a register.
     __device__ __forceinline__ uint32_t alloc_slot() {
-        if (free_top == 0) { fail(TW_REP_ERR_SLOTS); return 0xFFFFFFFFu; }
-        PROF_INC(P_ALLOC, 1);
-        uint32_t s = next_free;
-        if (--free_top) next_free = gp(c->free_stk)[ix(free_top - 1)];
-        return s;
+        if (free_n) {
+            uint32_t s = ftop;
+            if (--free_n) ftop = gp(c.free_stk)[ix(free_n - 1)];
+            return s;
+        }
+        if (bump < c.S) return bump++;
+        fail(TW_REP_ERR_SLOTS);
+        return 0xFFFFFFFFu;
     }
     __device__ __forceinline__ void free_slot(uint32_t slot) {
-        gp(c->free_stk)[ix(free_top++)] = slot;
-        next_free = slot;
+        if (free_n) gp(c.free_stk)[ix(free_n - 1)] = ftop;
+        ftop = slot;
+        ++free_n;
     }
 
     // Commutative per-node trace hash: a no-return 64-bit atomic add, so the
     // event's critical path never waits on the node's hash line.
-    __device__ __forceinline__ void hash_t(int64_t t, uint32_t node, uint32_t kind, int64_t val) {
-        unsigned long long GAS* h = LP ? (unsigned long long GAS*)(gp(c->hash_g) + node)
-                                       : (unsigned long long GAS*)(gp(c->hash) + ix(node));
-        PROF_INC(P_HASH, 1);
-#ifdef TW_EXP_NOHASH  // A/B experiment only: breaks parity
-        return;
-#endif
-        __hip_atomic_fetch_add(h, (unsigned long long)term(t, kind, val), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __device__ __forceinline__ void hash_add(uint32_t node, uint64_t v) {
+        unsigned long long GAS* h = LP ? (unsigned long long GAS*)(gp(c.hash_g) + node)
+                                       : (unsigned long long GAS*)(gp(c.hash) + ix(node));
+        __hip_atomic_fetch_add(h, (unsigned long long)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    __device__ __forceinline__ void hash(uint32_t node, uint32_t kind, int64_t val) { hash_t(now, node, kind, val); }
+    __device__ __forceinline__ void hash(uint32_t node, uint32_t kind, int64_t val) {
+        hash_add(node, term(now, kind, val));
+    }
     // LP mode: append a delivery record for another logical process
     __device__ __forceinline__ void emit(int64_t ta, int64_t payload, uint32_t link, uint32_t kind, uint32_t src,
                                          uint32_t dst) {
-        uint32_t i = __hip_atomic_fetch_add(gp(c->out_n), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (i >= c->out_cap) {
-            __hip_atomic_fetch_or(gp(c->lp_err), 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        uint32_t i = __hip_atomic_fetch_add(gp(c.out_n), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (i >= c.out_cap) {
+            __hip_atomic_fetch_or(gp(c.lp_err), 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             return;
         }
-        uint4 GAS* o = gp(c->outbox) + (size_t)i * 2;
+        uint4 GAS* o = gp(c.outbox) + (size_t)i * 2;
         o[0] = make_uint4((uint32_t)ta, (uint32_t)((uint64_t)ta >> 32), (uint32_t)payload,
                           (uint32_t)((uint64_t)payload >> 32));
         o[1] = make_uint4(link, kind, src, dst);
     }
 
     // Create a thread queued at now (fork, TimedT.hs:326-339).  Returns its ref.
-    __device__ __forceinline__ bool spawn(uint32_t pc, uint32_t node, int64_t q0, int64_t q1, int64_t q2, int64_t q3, int64_t& ref) {
+    __device__ __forceinline__ bool spawn(uint32_t pc, uint32_t node, int64_t q0, int64_t q1, int64_t q2, int64_t q3,
+                                          int64_t& ref) {
         uint32_t s = alloc_slot();
         if (s == 0xFFFFFFFFu) return false;
         Th ch;
         uint32_t tid = tidc++;
-        ++threads;
+        ++d_th;
         ch.w0 = pc & 0xFFFFu;
         ch.w1 = node;
         ch.w2 = tid;
         ch.w3 = 0;
         ch.f0 = ch.f1 = ch.f2 = ch.w7 = 0;
         ch.r0 = q0; ch.r1 = q1; ch.r2 = q2; ch.r3 = q3;
-        enqueue(ch, s, now);
-        store_th(s, ch);
+        bool on_chip = enqueue(ch, s, now);
+        store_rec(s, ch, on_chip ? ST_CACHE : ST_THROUGH);
         ref = (int64_t)(((uint64_t)tid << 32) | s);
         return true;
     }
@@ -569,50 +646,52 @@ struct Lane {
     __device__ __forceinline__ void throw_to(Th& self, uint32_t self_slot, int64_t ref, uint32_t code, int64_t val) {
         uint32_t ts = (uint32_t)ref;
         uint32_t tid = (uint32_t)((uint64_t)ref >> 32);
-        PROF_INC(P_THROWTO, 1);
-        if (ts >= c->S) return;
+        if (ts >= c.S) return;
         if (ts == self_slot) {  // the running thread: its record lives in registers
             if (self.w2 != tid) return;
             if (th_exc(self) == 0) { th_set_exc(self, code); self.w7 = (uint32_t)val; }
             return;
         }
         Th t;
-        load_th(ts, t);
+        load_rec(ts, t);
         if (t.w2 != tid) return;  // dead (slot free or reused): the map entry is unobservable
-        if (t.w3 != 0) {         // queued: wake to now with a fresh seq
+        bool on_chip = (th_flags(t) & F_NEARQ) != 0;
+        if (t.w3 != 0) {          // queued: wake to now with a fresh seq
             uint32_t s = ++seq;
-            uint64_t k = ((uint64_t)s << 32) | ts;
-            if (!near_rekey(ts, t.w3, now, k)) {
-                if (near_n < TW_NEAR_CAP) near_push(now, k);
-                else push_far(now, k);
+            if (!(on_chip && near_rekey(t.w3, now, s, ts))) {
+                on_chip = near_fits(now);
+                if (on_chip) near_push(now, s, ts);
+                else push_far(now, s, ts);
             }
+            if (on_chip) th_or_flags(t, F_NEARQ);
+            else th_clr_flags(t, F_NEARQ);
             t.w3 = s;
         }
         if (th_exc(t) == 0) {
             th_set_exc(t, code);
             t.w7 = (uint32_t)val;
         }
-        store_th(ts, t);
+        store_rec(ts, t, on_chip ? ST_CACHE : ST_THROUGH);
     }
 
     // Thread ends (END or uncaught exception).
     __device__ __forceinline__ void die(Th& th, uint32_t slot) {
-        uint32_t node = th.w1;
-        PROF_INC(P_DIE, 1);
-        if (gp(c->bind)[bix(node)] && gp(c->bind_own)[bix(node)] == th.w2) {
-            gp(c->bind)[bix(node)] = 0;
-            gp(c->bind_own)[bix(node)] = 0xFFFFFFFFu;
+        if (th_flags(th) & F_OWNS) {
+            uint32_t node = th.w1;
+            if (gp(c.bind_own)[bix(node)] == th.w2) {
+                gp(c.bind)[bix(node)] = 0;
+                gp(c.bind_own)[bix(node)] = 0xFFFFFFFFu;
+            }
         }
         th.w2 = 0xFFFFFFFFu;  // invalidate refs to this slot
         th.w3 = 0;
-        store_th(slot, th);
+        store_rec(slot, th, ST_DEAD);
         free_slot(slot);
     }
 
     // Raise `code` in th; true if a catch frame took it (pc set to handler).
     __device__ __forceinline__ bool unwind(Th& th, uint32_t slot, uint32_t code, int64_t val) {
         const uint32_t n = th_nfr(th);
-        // innermost frame first; constant indices keep the record in registers
 #pragma unroll
         for (int i = TW_MAX_FRAMES - 1; i >= 0; --i) {
             if ((uint32_t)i < n) {
@@ -620,7 +699,7 @@ struct Lane {
                 uint32_t mask = f >> 16;
                 if (mask == 0) {
                     uint32_t e = f & 0xFFFFu;
-                    if (e < c->T) gp(c->tmo_done)[ix(e)] = 1;
+                    if (e < c.T) gp(c.tmo_done)[ix(e)] = 1;
                 } else if (mask & (1u << code)) {
                     th_set_nfr(th, (uint32_t)i);
                     th_set_pc(th, f & 0xFFFFu);
@@ -638,42 +717,42 @@ struct Lane {
 
     // Run the thread's continuation until it yields or ends (the ContT
     // continuation of TimedT.hs:343-355).  Dispatch is a waterfall over the
-    // opcodes present in the wave: readfirstlane picks one, the lanes holding it
-    // execute it under a wave-uniform (scalar) switch, the others wait for their
-    // turn — lanes in lock-step take one pass per instruction.  Every yielding
-    // op funnels into one shared spawn + enqueue tail, which keeps the kernel
-    // small enough to stay resident in the instruction cache.
+    // instruction words present in the wave: readfirstlane picks one, the lanes
+    // holding it execute it with op and register operands wave-uniform (scalar
+    // branches), the others wait for their turn — lanes in lock-step take one
+    // pass per instruction.  Every yielding op funnels into one shared
+    // spawn + enqueue tail.
     __device__ __forceinline__ void step(Th& th, uint32_t slot) {
         enum { GO, YIELD, SPAWN, THROWTO, EXIT, STOP };
         th_or_flags(th, F_STARTED);
         uint32_t n = 0;
         uint32_t pc = th_pc(th);
-        if (pc >= c->n_insns) { fail(TW_REP_ERR_INSN); store_th(slot, th); return; }
+        if (pc >= c.n_insns) { fail(TW_REP_ERR_INSN); store_rec(slot, th, ST_THROUGH); return; }
         uint2 in = P[pc];
+        int mode = ST_THROUGH;
+        LITE_T(q0t);
+#ifdef TW_PROF_LITE
+        uint64_t q1t = q0t;
+#endif
         for (;;) {
-            uint32_t op = in.x & 0xFFu;
-            uint32_t uop = __builtin_amdgcn_readfirstlane(op);
-            PROF_INC(P_PASSES, 1);
-            if (op != uop) continue;
-            // keep the dispatch scalar: without this the compiler substitutes the
-            // per-lane `op` (known equal here) and lowers the switch to a vector
-            // binary search with an exec-mask save/restore per level
-            asm volatile("v_readfirstlane_b32 %0, %1" : "=s"(uop) : "v"(op));
-            PROF_INC(P_INSNS, 1);
+            const uint32_t w = in.x;
+            if (w != __builtin_amdgcn_readfirstlane(w)) continue;
+            uint32_t uw;  // opaque scalar copy: keeps every decode below on the SALU
+            asm volatile("v_readfirstlane_b32 %0, %1" : "=s"(uw) : "v"(w));
             if (++n > TW_STEP_CAP) { fail(TW_REP_ERR_INSN); break; }
             uint2 nx = P[pc + 1];  // prefetch the fall-through instruction (image padded by one)
-            uint32_t a = (in.x >> 8) & 3u, b = in.x >> 16;
-            int32_t imm = (int32_t)in.y;
-            th_set_pc(th, pc + 1);
+            const uint32_t op = uw & 0xFFu, a = (uw >> 8) & 3u, b = uw >> 16;
+            const int32_t imm = (int32_t)in.y;
+            uint32_t npc = pc + 1;
             int act = GO;
             int64_t yt = 0;                               // YIELD: wake time
             uint32_t cpc = 0, cnode = 0;                  // SPAWN: child entry + node
             int64_t q0 = 0, q1 = 0, q2 = 0, q3 = 0;       //        child registers
             int64_t tref = 0, tval = 0;                   // THROWTO target + payload
             uint32_t tcode = 0;
-            switch (uop) {
+            switch (op) {
             case TW_OP_NOP: break;
-            case TW_OP_END: die(th, slot); act = EXIT; break;
+            case TW_OP_END: act = EXIT; break;
             case TW_OP_WAIT_REL: yt = now + K[imm]; act = YIELD; break;
             case TW_OP_WAIT_ABS: {
                 int64_t t = K[imm];
@@ -689,7 +768,7 @@ struct Lane {
             }
             case TW_OP_FORK: {
                 uint32_t node = b == 0xFFFFu ? th.w1 : (uint32_t)getr(th, b & 3);
-                if (LP ? node != th.w1 : node >= c->N) { fail(TW_REP_ERR_INSN); act = STOP; break; }
+                if (LP ? node != th.w1 : node >= c.N) { fail(TW_REP_ERR_INSN); act = STOP; break; }
                 cpc = (uint32_t)imm; cnode = node;
                 q0 = th.r0; q1 = th.r1; q2 = th.r2; q3 = th.r3;
                 act = SPAWN;
@@ -701,7 +780,9 @@ struct Lane {
                 act = THROWTO;
                 break;
             case TW_OP_THROW:
-                if (!unwind(th, slot, b & 0xFFu, getr(th, (b >> 8) & 3))) act = EXIT;
+                th_set_pc(th, npc);
+                if (!unwind(th, slot, b & 0xFFu, getr(th, (b >> 8) & 3))) return;  // died (record stored)
+                npc = th_pc(th);
                 break;
             case TW_OP_CATCH: {
                 uint32_t nf = th_nfr(th);
@@ -728,43 +809,43 @@ struct Lane {
                 setr(th, a, m < 0 ? m + imm : m);
                 break;
             }
-            case TW_OP_JMP: th_set_pc(th, (uint32_t)imm); break;
-            case TW_OP_JEQ: if (getr(th, a) == getr(th, b & 3)) th_set_pc(th, (uint32_t)imm); break;
-            case TW_OP_JNE: if (getr(th, a) != getr(th, b & 3)) th_set_pc(th, (uint32_t)imm); break;
-            case TW_OP_JLT: if (getr(th, a) < getr(th, b & 3)) th_set_pc(th, (uint32_t)imm); break;
-            case TW_OP_JLE: if (getr(th, a) <= getr(th, b & 3)) th_set_pc(th, (uint32_t)imm); break;
-            case TW_OP_JEQI: if (getr(th, a) == (int64_t)(int16_t)b) th_set_pc(th, (uint32_t)imm); break;
-            case TW_OP_JNEI: if (getr(th, a) != (int64_t)(int16_t)b) th_set_pc(th, (uint32_t)imm); break;
+            case TW_OP_JMP: npc = (uint32_t)imm; break;
+            case TW_OP_JEQ: if (getr(th, a) == getr(th, b & 3)) npc = (uint32_t)imm; break;
+            case TW_OP_JNE: if (getr(th, a) != getr(th, b & 3)) npc = (uint32_t)imm; break;
+            case TW_OP_JLT: if (getr(th, a) < getr(th, b & 3)) npc = (uint32_t)imm; break;
+            case TW_OP_JLE: if (getr(th, a) <= getr(th, b & 3)) npc = (uint32_t)imm; break;
+            case TW_OP_JEQI: if (getr(th, a) == (int64_t)(int16_t)b) npc = (uint32_t)imm; break;
+            case TW_OP_JNEI: if (getr(th, a) != (int64_t)(int16_t)b) npc = (uint32_t)imm; break;
             case TW_OP_NOW: setr(th, a, now); break;
             case TW_OP_NODE: setr(th, a, th.w1); break;
-            case TW_OP_NLOAD: setr(th, a, gp(c->nvars)[nix(th.w1, b & 3)]); break;
-            case TW_OP_NSTORE: gp(c->nvars)[nix(th.w1, b & 3)] = getr(th, a); break;
+            case TW_OP_NLOAD: setr(th, a, gp(c.nvars)[nix(th.w1, b & 3)]); break;
+            case TW_OP_NSTORE: gp(c.nvars)[nix(th.w1, b & 3)] = getr(th, a); break;
             case TW_OP_NLOADX:
             case TW_OP_NSTOREX: {
                 uint64_t node = (uint64_t)getr(th, (b >> 8) & 3);
-                if (LP ? node != th.w1 : node >= c->N) { fail(TW_REP_ERR_INSN); act = STOP; break; }
-                int64_t GAS* v = &gp(c->nvars)[nix((uint32_t)node, b & 3)];
-                if (uop == TW_OP_NLOADX) setr(th, a, *v);
+                if (LP ? node != th.w1 : node >= c.N) { fail(TW_REP_ERR_INSN); act = STOP; break; }
+                int64_t GAS* v = &gp(c.nvars)[nix((uint32_t)node, b & 3)];
+                if (op == TW_OP_NLOADX) setr(th, a, *v);
                 else *v = getr(th, a);
                 break;
             }
-            case TW_OP_LINK: setr(th, a, (int64_t)gp(c->out_off)[th.w1] + imm); break;
+            case TW_OP_LINK: setr(th, a, (int64_t)gp(c.out_off)[th.w1] + imm); break;
             case TW_OP_RLINK: {
                 uint64_t l = (uint64_t)getr(th, b & 3);
-                if (l >= c->L) { fail(TW_REP_ERR_INSN); act = STOP; break; }
-                setr(th, a, (int64_t)gp(c->link_rev)[l]);
+                if (l >= c.L) { fail(TW_REP_ERR_INSN); act = STOP; break; }
+                setr(th, a, (int64_t)gp(c.link_rev)[l]);
                 break;
             }
             case TW_OP_SEND: {  // schedule (after d) (deliver ..) unless the link drops it
                 uint64_t link = (uint64_t)getr(th, a);
-                if (link >= c->L) { fail(TW_REP_ERR_INSN); act = STOP; break; }
+                if (link >= c.L) { fail(TW_REP_ERR_INSN); act = STOP; break; }
                 uint32_t kind = b & 0xFFu;
                 int64_t payload = getr(th, (b >> 8) & 3);
-                uint32_t ord = gp(c->link_ord)[lix(link)];
-                gp(c->link_ord)[lix(link)] = ord + 1;
-                uint32_t e = c->link_table ? gp(c->link_table)[tix(link, ord)] : 0u;
+                uint32_t ord = gp(c.link_ord)[lix(link)];
+                gp(c.link_ord)[lix(link)] = ord + 1;
+                uint32_t e = c.link_table ? gp(c.link_table)[tix(link, ord)] : 0u;
                 if (e & TW_LINK_DROP) {
-                    ++dropped;
+                    ++d_dr;
                     hash(th.w1, TW_KIND_DROP | kind, payload);
                     break;
                 }
@@ -773,14 +854,14 @@ struct Lane {
                     // at now, wake pop at now+d, both at this node) and its delivery travels
                     // as a record: the receiver checks its binding at now+d
                     int64_t dly = (int64_t)(e & 0x7FFFFFFFu);
-                    if (dly < c->lookahead) { fail(TW_REP_ERR_INSN); act = STOP; break; }
+                    if (dly < c.lookahead) { fail(TW_REP_ERR_INSN); act = STOP; break; }
                     int64_t ta = now + dly;
-                    hash_t(now, th.w1, TW_KIND_RESUME | TW_PC_DELIVER_STUB, 0);
-                    hash_t(ta, th.w1, TW_KIND_RESUME | (TW_PC_DELIVER_STUB + 1), 0);
-                    events += 2;
-                    ++threads;
+                    hash_add(th.w1, term0(now, TW_KIND_RESUME | TW_PC_DELIVER_STUB) +
+                                        term0(ta, TW_KIND_RESUME | (TW_PC_DELIVER_STUB + 1)));
+                    d_ev += 2;
+                    ++d_th;
                     final_t = ta > final_t ? ta : final_t;
-                    emit(ta, payload, (uint32_t)link, kind, th.w1, gp(c->link_dst)[link]);
+                    emit(ta, payload, (uint32_t)link, kind, th.w1, gp(c.link_dst)[link]);
                     yt = now + 1;
                     act = YIELD;
                     break;
@@ -793,17 +874,17 @@ struct Lane {
             case TW_OP_DELIVER: {  // listener dispatch, ForkStrategy fork_ (MonadDialog.hs:232-256,317)
                 uint64_t link = (uint64_t)th.r1;
                 uint32_t kind = (uint32_t)th.r3;
-                uint32_t dst = gp(c->link_dst)[link];
-                uint32_t set = gp(c->bind)[bix(dst)];
+                uint32_t dst = gp(c.link_dst)[link];
+                uint32_t set = gp(c.bind)[bix(dst)];
                 uint32_t lpc = TW_PC_NONE;
-                if (set && kind < c->n_kinds) lpc = gp(c->lpc)[(size_t)(set - 1) * c->n_kinds + kind];
+                if (set && kind < c.n_kinds) lpc = gp(c.lpc)[(size_t)(set - 1) * c.n_kinds + kind];
                 if (lpc == TW_PC_NONE) {
-                    ++undeliv;
+                    ++d_ud;
                     hash(dst, TW_KIND_UNDELIV | kind, th.r0);
-                    if (LP) { die(th, slot); act = EXIT; }  // the phantom deliverer ends here
+                    if (LP) act = EXIT;  // the phantom deliverer ends here
                     break;
                 }
-                ++delivered;
+                ++d_dl;
                 hash(dst, TW_KIND_RECV | kind, th.r0);
                 cpc = lpc; cnode = dst;
                 q0 = th.r0; q1 = (int64_t)link; q2 = LP ? th.r2 : (int64_t)th.w1; q3 = (int64_t)kind;
@@ -811,19 +892,20 @@ struct Lane {
                 break;
             }
             case TW_OP_LISTEN:
-                if ((uint32_t)imm >= c->n_sets) { fail(TW_REP_ERR_INSN); act = STOP; break; }
-                gp(c->bind)[bix(th.w1)] = (uint32_t)imm + 1;
-                gp(c->bind_own)[bix(th.w1)] = b ? th.w2 : 0xFFFFFFFFu;
+                if ((uint32_t)imm >= c.n_sets) { fail(TW_REP_ERR_INSN); act = STOP; break; }
+                gp(c.bind)[bix(th.w1)] = (uint32_t)imm + 1;
+                gp(c.bind_own)[bix(th.w1)] = b ? th.w2 : 0xFFFFFFFFu;
+                if (b) th_or_flags(th, F_OWNS);
                 break;
             case TW_OP_UNLISTEN:
-                gp(c->bind)[bix(th.w1)] = 0;
-                gp(c->bind_own)[bix(th.w1)] = 0xFFFFFFFFu;
+                gp(c.bind)[bix(th.w1)] = 0;
+                gp(c.bind_own)[bix(th.w1)] = 0xFFFFFFFFu;
                 break;
             case TW_OP_TRACE: hash(th.w1, TW_KIND_TRACE | ((uint32_t)imm & 0xFFFFu), getr(th, a)); break;
             case TW_OP_TMO_BEGIN: {  // schedule (after t) watchdog (TimedT.hs:373-375)
-                if (tmo_ctr >= c->T) { fail(TW_REP_ERR_INSN); act = STOP; break; }
+                if (tmo_ctr >= c.T) { fail(TW_REP_ERR_INSN); act = STOP; break; }
                 uint32_t e = tmo_ctr++;
-                gp(c->tmo_done)[ix(e)] = 0;
+                gp(c.tmo_done)[ix(e)] = 0;
                 setr(th, a, e);
                 cpc = TW_PC_WATCHDOG_STUB; cnode = th.w1;
                 q0 = (int64_t)(((uint64_t)th.w2 << 32) | slot); q1 = (int64_t)e; q2 = K[imm]; q3 = 0;
@@ -842,12 +924,12 @@ struct Lane {
                 if (nf == 0 || (getf(th, nf - 1) >> 16) != 0) { fail(TW_REP_ERR_INSN); act = STOP; break; }
                 uint32_t ep = getf(th, nf - 1) & 0xFFFFu;
                 th_set_nfr(th, nf - 1);
-                if (ep < c->T) gp(c->tmo_done)[ix(ep)] = 1;
+                if (ep < c.T) gp(c.tmo_done)[ix(ep)] = 1;
                 break;
             }
             case TW_OP_TMO_FIRE: {
                 uint64_t e = (uint64_t)th.r1;
-                if (e < c->T && !gp(c->tmo_done)[ix(e)]) {
+                if (e < c.T && !gp(c.tmo_done)[ix(e)]) {
                     tref = th.r0; tcode = TW_EXC_TIMEOUT; tval = 0;
                     act = THROWTO;
                 }
@@ -858,21 +940,30 @@ struct Lane {
                 act = STOP;
                 break;
             }
-#ifdef TW_PROF
-            uint64_t ta0 = __builtin_amdgcn_s_memtime();
+            th_set_pc(th, npc);
+#ifdef TW_PROF_LITE
+            q1t = __builtin_amdgcn_s_memtime();
+            LITE_ACCM(6, q1t - q0t);
+            q0t = q1t;
 #endif
+            if (act == EXIT) {
+                LITE_WRAP(12, die(th, slot));
+                return;
+            }
             if (act == THROWTO) {
-                throw_to(th, slot, tref, tcode, tval);
+                LITE_WRAP(11, throw_to(th, slot, tref, tcode, tval));
                 act = GO;
             }
             if (act == SPAWN) {  // fork (TimedT.hs:326-342): child at now, parent waits 1 µs
                 int64_t ref;
-                if (!spawn(cpc, cnode, q0, q1, q2, q3, ref)) break;
-                if (uop == TW_OP_FORK) setr(th, a, ref);
-                if (LP && uop == TW_OP_DELIVER) {
+                bool ok;
+                LITE_WRAP(9, ok = spawn(cpc, cnode, q0, q1, q2, q3, ref));
+                if (!ok) break;
+                if (op == TW_OP_FORK) setr(th, a, ref);
+                if (LP && op == TW_OP_DELIVER) {
                     // the deliverer's resume pop (at now+1, on the sending node), then it ends
-                    hash_t(now + 1, (uint32_t)th.r2, TW_KIND_RESUME | (TW_PC_DELIVER_STUB + 2), 0);
-                    ++events;
+                    hash_add((uint32_t)th.r2, term0(now + 1, TW_KIND_RESUME | (TW_PC_DELIVER_STUB + 2)));
+                    ++d_ev;
                     final_t = now + 1 > final_t ? now + 1 : final_t;
                     die(th, slot);
                     return;
@@ -881,32 +972,34 @@ struct Lane {
                 act = YIELD;
             }
             if (act == YIELD) {
-                enqueue(th, slot, yt);
-                PROF_INC(P_TAIL, __builtin_amdgcn_s_memtime() - ta0);
+                LITE_WRAP(10, mode = enqueue(th, slot, yt) ? ST_CACHE : ST_THROUGH);
                 break;
             }
-            PROF_INC(P_TAIL, __builtin_amdgcn_s_memtime() - ta0);
-            if (act == EXIT) return;
+#ifdef TW_PROF_LITE
+            q1t = __builtin_amdgcn_s_memtime();
+            LITE_ACCM(7, q1t - q0t);
+            q0t = q1t;
+#endif
             if (act == STOP || status != TW_REP_RUNNING) break;
-            uint32_t npc = th_pc(th);
-            if (npc >= c->n_insns) { fail(TW_REP_ERR_INSN); break; }
+            if (npc >= c.n_insns) { fail(TW_REP_ERR_INSN); break; }
             if (npc == pc + 1) in = nx;
             else in = P[npc];
             pc = npc;
         }
-#ifdef TW_PROF
-        uint64_t ts0 = __builtin_amdgcn_s_memtime();
+#ifdef TW_PROF_LITE
+        q1t = __builtin_amdgcn_s_memtime();
+        LITE_ACCM(7, q1t - q0t);
 #endif
-        store_th(slot, th);
-        PROF_INC(P_STCYC, __builtin_amdgcn_s_memtime() - ts0);
+        store_rec(slot, th, mode);
+        LITE_ACCM(8, __builtin_amdgcn_s_memtime() - q1t);
     }
 };
 
 // ------------------------------------------------------------------ kernels
-__global__ void __launch_bounds__(TW_BLOCK) tw_init_kernel(Dev c, uint32_t main_pc, uint32_t main_node,
-                                                          const int64_t* main_regs, const int64_t* nv_init,
-                                                          const uint32_t* listen_init, int lp_mode) {
-    uint32_t r = blockIdx.x * TW_BLOCK + threadIdx.x;
+__global__ void __launch_bounds__(TW_WG) tw_init_kernel(Dev c, uint32_t main_pc, uint32_t main_node,
+                                                       const int64_t* main_regs, const int64_t* nv_init,
+                                                       const uint32_t* listen_init, int lp_mode) {
+    uint32_t r = blockIdx.x * TW_WG + threadIdx.x;
     if (r >= c.R) return;
     // LP mode: lane r is global node g; only the main node's lane holds the main thread
     const uint32_t g = lp_mode ? c.lp0 + r : 0u;
@@ -916,9 +1009,7 @@ __global__ void __launch_bounds__(TW_BLOCK) tw_init_kernel(Dev c, uint32_t main_
     gp(c.scal)[(size_t)SC_TIDC * c.R + r] = 1;
     gp(c.scal)[(size_t)SC_STATUS * c.R + r] = TW_REP_RUNNING;
     gp(c.scal)[(size_t)SC_PENDING_MAIN * c.R + r] = has_main ? 1 : 0;
-    // free stack: slots S-1 .. 1 (slot 0 = main), pops hand out 1, 2, 3, ...
-    for (uint32_t k = 0; k + 1 < c.S; ++k) gp(c.free_stk)[(size_t)k * c.R + r] = c.S - 1 - k;
-    gp(c.scal)[(size_t)SC_FREE_TOP * c.R + r] = c.S - 1;
+    gp(c.scal)[(size_t)SC_BUMP * c.R + r] = has_main ? 1 : 0;  // slot 0 = main
     uint4 GAS* p = gp(c.slots) + (size_t)r * 4;  // slot 0
     uint32_t w0 = (main_pc & 0xFFFFu) | (F_MAIN << 18);
     p[0] = make_uint4(w0, main_node, has_main ? 0u : 0xFFFFFFFFu, 0u);
@@ -934,10 +1025,6 @@ __global__ void __launch_bounds__(TW_BLOCK) tw_init_kernel(Dev c, uint32_t main_
         gp(c.bind_own)[r] = 0xFFFFFFFFu;
         if (listen_init) gp(c.bind)[r] = listen_init[g];
         gp(c.inbox_n)[r] = 0;
-        if (!has_main) {  // slot 0 is an ordinary free slot on non-main nodes
-            gp(c.free_stk)[(size_t)(c.S - 1) * c.R + r] = 0;
-            gp(c.scal)[(size_t)SC_FREE_TOP * c.R + r] = c.S;
-        }
         return;
     }
     if (nv_init)
@@ -947,81 +1034,90 @@ __global__ void __launch_bounds__(TW_BLOCK) tw_init_kernel(Dev c, uint32_t main_
         for (uint32_t n = 0; n < c.N; ++n) gp(c.bind)[(size_t)n * c.R + r] = listen_init[n];
 }
 
-// LDS per workgroup: near heap keys [NEAR_CAP][64] x 2 words, then (when it
-// fits) the program image and constant pool, so instruction fetch and time
-// constants never leave the CU.
-__host__ __device__ constexpr size_t near_lds_bytes() {
-    return (size_t)TW_NEAR_CAP * TW_BLOCK * 16 + (size_t)TW_RCACHE * 4 * TW_BLOCK * 16;
+// LDS per workgroup: near heap keys + slots, the record cache, then the program
+// image and constant pool, so instruction fetch and time constants never
+// leave the CU.
+__host__ __device__ constexpr size_t fixed_lds_bytes() {
+    return (size_t)TW_NEAR_CAP * TW_WG * 12 + (size_t)TW_RC * 4 * TW_WG * 16;
 }
 
 template <bool LP>
-__global__ void __launch_bounds__(TW_BLOCK) __attribute__((amdgpu_waves_per_eu(1, 2)))
+__global__ void __launch_bounds__(TW_WG) __attribute__((amdgpu_waves_per_eu(1, 2)))
 tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
     extern __shared__ __attribute__((aligned(16))) uint64_t lds_raw[];
-    uint64_t LAS* lds = (uint64_t LAS*)lds_raw;
-    int64_t LAS* s_t = (int64_t LAS*)lds;
-    uint64_t LAS* s_k = lds + TW_NEAR_CAP * TW_BLOCK;
-    uint4 LAS* s_rc = (uint4 LAS*)(lds + 2 * TW_NEAR_CAP * TW_BLOCK);
-    uint2 LAS* s_p = (uint2 LAS*)(s_rc + TW_RCACHE * 4 * TW_BLOCK);
+    uint4 LAS* s_rc = (uint4 LAS*)lds_raw;
+    uint64_t LAS* s_k = (uint64_t LAS*)(s_rc + TW_RC * 4 * TW_WG);
+    uint32_t LAS* s_s = (uint32_t LAS*)(s_k + TW_NEAR_CAP * TW_WG);
+    uint2 LAS* s_p = (uint2 LAS*)(s_s + TW_NEAR_CAP * TW_WG);
     int64_t LAS* s_c = (int64_t LAS*)(s_p + c.n_insns + 1);
     {
-        for (uint32_t i = threadIdx.x; i <= c.n_insns; i += TW_BLOCK) s_p[i] = gp(c.insns)[i];
-        for (uint32_t i = threadIdx.x; i < c.n_consts; i += TW_BLOCK) s_c[i] = gp(c.consts)[i];
+        for (uint32_t i = threadIdx.x; i <= c.n_insns; i += TW_WG) s_p[i] = gp(c.insns)[i];
+        for (uint32_t i = threadIdx.x; i < c.n_consts; i += TW_WG) s_c[i] = gp(c.consts)[i];
         __syncthreads();
     }
-    uint32_t r = blockIdx.x * TW_BLOCK + threadIdx.x;
+    uint32_t r = blockIdx.x * TW_WG + threadIdx.x;
     if (r >= c.R) return;
     uint64_t* sc = gp(c.scal) + r;
     const size_t R = c.R;
     if (sc[SC_STATUS * R] != TW_REP_RUNNING) return;
 
     Lane<LP> L;
-    L.c = &c;
+    L.c = c;
     L.r = r;
-    L.nt = s_t + threadIdx.x;
     L.nk = s_k + threadIdx.x;
+    L.ns = s_s + threadIdx.x;
+    L.rcd = s_rc + threadIdx.x;
     L.P = s_p;
-    L.rcache = s_rc + threadIdx.x;
-    L.cptr = 0;
-#pragma unroll
-    for (int e = 0; e < TW_RCACHE; ++e) L.ctag[e] = 0xFFFFFFFFu;
     L.K = s_c;
+    L.ctag.fill(0xFFFFFFFFu);
+    L.cst.fill(0);
+    L.cdirty = 0;
+    L.clk = 0;
     L.now = (int64_t)sc[SC_NOW * R]; L.final_t = (int64_t)sc[SC_FINAL_T * R];
     L.seq = (uint32_t)sc[SC_SEQ * R]; L.tidc = (uint32_t)sc[SC_TIDC * R]; L.live = (uint32_t)sc[SC_LIVE * R];
-    L.near_n = (uint32_t)sc[SC_NEAR_N * R]; L.far_n = (uint32_t)sc[SC_FAR_N * R];
+    const uint32_t near_n0 = (uint32_t)sc[SC_NEAR_N * R];
+    L.far_n = (uint32_t)sc[SC_FAR_N * R];
     L.status = (uint32_t)sc[SC_STATUS * R]; L.main_exc = (uint32_t)sc[SC_MAIN_EXC * R];
-    L.free_top = (uint32_t)sc[SC_FREE_TOP * R]; L.tmo_ctr = (uint32_t)sc[SC_TMO_CTR * R];
-    L.events = sc[SC_EVENTS * R]; L.delivered = sc[SC_DELIVERED * R]; L.dropped = sc[SC_DROPPED * R];
-    L.undeliv = sc[SC_UNDELIV * R]; L.threads = sc[SC_THREADS * R];
-    L.next_free = L.free_top ? gp(c.free_stk)[(size_t)(L.free_top - 1) * R + r] : 0u;
-    for (uint32_t j = 0; j < L.near_n; ++j) {
-        uint4 e = gp(c.near_spill)[(size_t)j * R + r];
-        L.nt[j * TW_BLOCK] = (int64_t)(((uint64_t)e.y << 32) | e.x);
-        L.nk[j * TW_BLOCK] = ((uint64_t)e.w << 32) | e.z;
-    }
-    L.far_t = 0;
-    L.far_k = 0;
+    L.free_n = (uint32_t)sc[SC_FREE_N * R]; L.ftop = (uint32_t)sc[SC_FTOP * R]; L.bump = (uint32_t)sc[SC_BUMP * R];
+    L.tmo_ctr = (uint32_t)sc[SC_TMO_CTR * R];
+    const uint64_t events0 = sc[SC_EVENTS * R];
+    const uint64_t ev_room64 = max_events > events0 ? max_events - events0 : 0;
+    const uint32_t ev_room = ev_room64 > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)ev_room64;
+    L.d_ev = L.d_dl = L.d_dr = L.d_ud = L.d_th = 0;
+    L.ft = 0; L.fs = 0; L.fsl = 0;
     if (L.far_n) {
         uint4 e = L.far_ld(0);
-        L.far_t = (int64_t)(((uint64_t)e.y << 32) | e.x);
-        L.far_k = ((uint64_t)e.w << 32) | e.z;
+        L.ft = ent_t(e); L.fs = e.w; L.fsl = e.z;
     }
 #pragma unroll
     for (int j = 0; j < TW_RUNS; ++j) {
         L.rh[j] = (uint32_t)sc[(SC_RH0 + j) * R];
-        L.rc[j] = (uint32_t)sc[(SC_RC0 + j) * R];
+        L.rn[j] = (uint32_t)sc[(SC_RC0 + j) * R];
         L.rt[j] = L.ut[j] = 0;
-        L.rk[j] = L.uk[j] = 0;
-        if (L.rc[j]) {
+        L.rs[j] = L.us[j] = L.rsl[j] = 0;
+        if (L.rn[j]) {
             uint4 h = *L.run_at(j, L.rh[j]);
-            uint32_t tp = L.rh[j] + L.rc[j] - 1;
+            uint32_t tp = L.rh[j] + L.rn[j] - 1;
             if (tp >= c.Cr) tp -= c.Cr;
             uint4 u = *L.run_at(j, tp);
-            L.rt[j] = (int64_t)(((uint64_t)h.y << 32) | h.x);
-            L.rk[j] = ((uint64_t)h.w << 32) | h.z;
-            L.ut[j] = (int64_t)(((uint64_t)u.y << 32) | u.x);
-            L.uk[j] = ((uint64_t)u.w << 32) | u.z;
+            L.rt[j] = ent_t(h); L.rs[j] = h.w; L.rsl[j] = h.z;
+            L.ut[j] = ent_t(u); L.us[j] = u.w;
         }
+    }
+    L.far_min();
+    // near heap: re-inserted from the spill area (keys are relative to this launch's base)
+    L.near_n = 0;
+    L.nbase = L.now;
+    L.nrk = 0; L.nrs = 0;
+    for (uint32_t j = 0; j < near_n0; ++j) {
+        uint4 e = gp(c.near_spill)[(size_t)j * R + r];
+        if (L.near_fits(ent_t(e)) || ent_t(e) - L.now < c.horizon) {
+            if (L.near_n < TW_NEAR_CAP && (uint64_t)(ent_t(e) - L.nbase) < 0xFFFFFFFFull) {
+                L.near_push(ent_t(e), e.w, e.z);
+                continue;
+            }
+        }
+        L.push_far(ent_t(e), e.w, e.z);  // the thread's F_NEARQ hint only speeds up throwTo
     }
 
     if (LP) {
@@ -1043,14 +1139,14 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
                 uint4 ea = q[0], eb = q[1];
                 bool less = best < 0;
                 if (!less) {
-                    int64_t t1 = (int64_t)(((uint64_t)ea.y << 32) | ea.x), t2 = (int64_t)(((uint64_t)ba.y << 32) | ba.x);
+                    int64_t t1 = ent_t(ea), t2 = ent_t(ba);
                     uint64_t p1 = ((uint64_t)ea.w << 32) | ea.z, p2 = ((uint64_t)ba.w << 32) | ba.z;
                     less = t1 < t2 || (t1 == t2 && (eb.x < bb.x || (eb.x == bb.x && (p1 < p2 || (p1 == p2 && eb.z < bb.z)))));
                 }
                 if (less) { best = (int)j; ba = ea; bb = eb; }
             }
             used |= 1u << best;
-            int64_t ta = (int64_t)(((uint64_t)ba.y << 32) | ba.x);
+            int64_t ta = ent_t(ba);
             uint32_t s = L.alloc_slot();
             if (s == 0xFFFFFFFFu) break;
             Th ph;
@@ -1063,106 +1159,92 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
             ph.r1 = bb.x;                                     // link
             ph.r2 = bb.z;                                     // sending node
             ph.r3 = bb.y;                                     // kind
-            L.enqueue(ph, s, ta);
-            L.store_th(s, ph);
+            bool on_chip = L.enqueue(ph, s, ta);
+            L.store_rec(s, ph, on_chip ? ST_CACHE : ST_THROUGH);
         }
         gp(c.inbox_n)[r] = 0;
     }
 
-#ifdef TW_PROF
-    for (int i = 0; i < P_COUNT; ++i) L.L_prof[i] = 0;
-    PROF_T(tk0);
-#endif
 #ifdef TW_PROF_LITE
-    uint32_t lite[6] = {0, 0, 0, 0, 0, 0};  // sel, pre, step, loop, iters, pops
+#pragma unroll
+    for (int i = 0; i < 16; ++i) L.lite[i] = 0;
     LITE_T(lk0);
 #endif
     uint32_t pending_main = (uint32_t)sc[SC_PENDING_MAIN * R];
     for (uint32_t it = 0; it < budget; ++it) {
         if (L.status != TW_REP_RUNNING) break;
-        PROF_T(t0);
         LITE_T(l0);
 #ifdef TW_PROF_LITE
         uint64_t l1 = l0;
         LITE_ACC(4, 1);
 #endif
-#ifdef TW_PROF
-        uint64_t t2 = t0;
-#endif
-        KPROF_INC(P_ITERS, 1);
         Th th;
         uint32_t slot;
         bool run = false;
         if (pending_main) {  // runInSandbox main (TimedT.hs:237): runs at t=0, not a pop
             pending_main = 0;
             slot = 0;
-            L.load_th(0, th);
+            L.load_rec(0, th);
             run = true;
         } else {
             if (L.live == 0) {  // whileM_ notDone
                 if (!LP) L.status = TW_REP_DONE;  // an LP may still receive records
                 break;
             }
-            if (L.events >= max_events) break;
+            if (L.d_ev >= ev_room) break;
+            // PQ.minView: the min of the near root and the far sources
+            if (L.far_dirty) L.far_min();
+            bool use_near = L.near_n != 0;
             int64_t t = 0;
-            uint64_t k = 0;
-            int src = L.min_source(t, k);
-            if (src < 0 || t > t_end) break;
-            slot = (uint32_t)k;
-            L.load_th(slot, th);  // issued first: its latency overlaps the queue maintenance
-            if (src == TW_RUNS) L.near_pop();
-            else if (src == TW_RUNS + 1) L.far_pop();
-            else L.run_pop(src);
-#ifdef TW_PROF
-            PROF_T(t1);
-#ifndef TW_PROF_NOWAIT
-            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+            uint32_t sq = 0;
+            if (use_near) { t = L.nbase + (int64_t)(L.nrk >> 32); sq = (uint32_t)L.nrk; slot = L.nrs; }
+            if (L.fsrc >= 0 && (!use_near || tless(L.fmt, L.fms, t, sq))) {
+                use_near = false;
+                t = L.fmt; sq = L.fms; slot = L.fmsl;
+            } else if (!use_near) {
+                break;  // nothing queued (cannot happen while live > 0)
+            }
+            if (t > t_end) break;
+#ifdef TW_PROF_LITE
+            LITE_ACC(13, __builtin_amdgcn_s_memtime() - l0);
 #endif
-            t2 = __builtin_amdgcn_s_memtime();
-            KPROF_INC(P_SEL, t1 - t0);
-            KPROF_INC(P_WAIT, t2 - t1);
-            KPROF_INC(src == TW_RUNS ? P_SRC_NEAR : src == TW_RUNS + 1 ? P_SRC_FAR : P_SRC_RUN, 1);
-            if (th.w3 != (uint32_t)(k >> 32)) KPROF_INC(P_SUPER, 1);
-#endif
+            KLITE_WRAP(14, L.load_rec(slot, th));  // issued first: its latency overlaps the queue maintenance
+            KLITE_WRAP(15, if (use_near) L.near_pop(); else if (L.fsrc == TW_RUNS) L.far_pop(); else L.run_pop(L.fsrc));
 #ifdef TW_PROF_LITE
             l1 = __builtin_amdgcn_s_memtime();
             LITE_ACC(0, l1 - l0);
 #endif
-            if (th.w3 != (uint32_t)(k >> 32)) continue;  // superseded by a throwTo re-stamp
-            KPROF_INC(P_POPS, 1);
+            if (th.w3 != sq) continue;  // superseded by a throwTo re-stamp
             LITE_ACC(5, 1);
-            // PQ.minView; curTime .= timestamp (TimedT.hs:241-247)
+            // curTime .= timestamp (TimedT.hs:241-247)
             th.w3 = 0;
             --L.live;
             L.now = t;
+            if (t - L.nbase > (int64_t)0x7FFFFFFF) L.near_rebase(t);
             // LP phantom = the deliverer's wake, already counted and hashed by the sender
             const bool phantom = LP && (th_flags(th) & F_PHANTOM);
             if (!phantom) {
                 L.final_t = LP ? (t > L.final_t ? t : L.final_t) : t;
-                ++L.events;
+                ++L.d_ev;
             }
             uint32_t exc = th_exc(th);  // asyncExceptions . at tid <<.= Nothing (:252)
             if (exc) {
                 int64_t val = (int64_t)(int32_t)th.w7;
                 th_set_exc(th, 0);
                 th.w7 = 0;
-                L.hash(th.w1, TW_KIND_EXC | exc, 0);
+                L.hash_add(th.w1, term0(t, TW_KIND_EXC | exc));
                 if (!(th_flags(th) & (F_STARTED | F_MAIN))) {  // escapes launchTimedT (:252-263)
                     L.status = TW_REP_ABORTED;
                     L.main_exc = exc;
-                    L.store_th(slot, th);
+                    L.store_rec(slot, th, ST_THROUGH);
                     break;
                 }
                 run = L.unwind(th, slot, exc, val);
             } else {
-                if (!phantom) L.hash(th.w1, TW_KIND_RESUME | th_pc(th), 0);
+                if (!phantom) L.hash_add(th.w1, term0(t, TW_KIND_RESUME | th_pc(th)));
                 run = true;
             }
         }
-#ifdef TW_PROF
-        PROF_T(t3);
-        if (!pending_main) KPROF_INC(P_PRE, t3 - t2);
-#endif
 #ifdef TW_PROF_LITE
         LITE_T(l2);
         LITE_ACC(1, l2 - l1);
@@ -1171,28 +1253,15 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
 #ifdef TW_PROF_LITE
         LITE_ACC(2, __builtin_amdgcn_s_memtime() - l2);
 #endif
-#ifdef TW_PROF
-        PROF_T(t4);
-        KPROF_INC(P_STEP, t4 - t3);
-#endif
     }
 #ifdef TW_PROF_LITE
     LITE_ACC(3, __builtin_amdgcn_s_memtime() - lk0);
     if (c.prof)
-        for (int i = 0; i < 6; ++i)
-            __hip_atomic_fetch_add(gp(c.prof) + i, (unsigned long long)lite[i], __ATOMIC_RELAXED,
+        for (int i = 0; i < 16; ++i)
+            __hip_atomic_fetch_add(gp(c.prof) + i, (unsigned long long)L.lite[i], __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_AGENT);
 #endif
-#ifdef TW_PROF
-    {
-        PROF_T(tk1);
-        KPROF_INC(P_LOOP, tk1 - tk0);
-        if (c.prof)
-            for (int i = 0; i < P_COUNT; ++i)
-                __hip_atomic_fetch_add(gp(c.prof) + i, (unsigned long long)L.L_prof[i], __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_AGENT);
-    }
-#endif
+    L.flush_cache();
     sc[SC_PENDING_MAIN * R] = pending_main;
     if (!LP && L.status == TW_REP_RUNNING && L.live == 0) L.status = TW_REP_DONE;
 
@@ -1200,26 +1269,25 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
     sc[SC_SEQ * R] = L.seq; sc[SC_TIDC * R] = L.tidc; sc[SC_LIVE * R] = L.live;
     sc[SC_NEAR_N * R] = L.near_n; sc[SC_FAR_N * R] = L.far_n;
     sc[SC_STATUS * R] = L.status; sc[SC_MAIN_EXC * R] = L.main_exc;
-    sc[SC_FREE_TOP * R] = L.free_top; sc[SC_TMO_CTR * R] = L.tmo_ctr;
-    sc[SC_EVENTS * R] = L.events; sc[SC_DELIVERED * R] = L.delivered; sc[SC_DROPPED * R] = L.dropped;
-    sc[SC_UNDELIV * R] = L.undeliv; sc[SC_THREADS * R] = L.threads;
+    sc[SC_FREE_N * R] = L.free_n; sc[SC_FTOP * R] = L.ftop; sc[SC_BUMP * R] = L.bump;
+    sc[SC_TMO_CTR * R] = L.tmo_ctr;
+    sc[SC_EVENTS * R] = events0 + L.d_ev;
+    sc[SC_DELIVERED * R] += L.d_dl; sc[SC_DROPPED * R] += L.d_dr;
+    sc[SC_UNDELIV * R] += L.d_ud; sc[SC_THREADS * R] += L.d_th;
 #pragma unroll
     for (int j = 0; j < TW_RUNS; ++j) {
         sc[(SC_RH0 + j) * R] = L.rh[j];
-        sc[(SC_RC0 + j) * R] = L.rc[j];
+        sc[(SC_RC0 + j) * R] = L.rn[j];
     }
     for (uint32_t j = 0; j < L.near_n; ++j) {
-        int64_t t = L.nt[j * TW_BLOCK];
-        uint64_t k = L.nk[j * TW_BLOCK];
-        gp(c.near_spill)[(size_t)j * R + r] =
-            make_uint4((uint32_t)t, (uint32_t)((uint64_t)t >> 32), (uint32_t)k, (uint32_t)(k >> 32));
+        uint64_t k = L.nk[j * TW_WG];
+        gp(c.near_spill)[(size_t)j * R + r] = ent(L.nbase + (int64_t)(k >> 32), L.ns[j * TW_WG], (uint32_t)k);
     }
-    bool active = L.status == TW_REP_RUNNING && L.events < max_events;
+    bool active = L.status == TW_REP_RUNNING && L.d_ev < ev_room;
     int64_t tn = INT64_MAX;
-    {
-        uint64_t k = 0;
-        if (L.min_source(tn, k) < 0) tn = INT64_MAX;
-    }
+    if (L.far_dirty) L.far_min();
+    if (L.near_n) tn = L.nbase + (int64_t)(L.nrk >> 32);
+    if (L.fsrc >= 0 && L.fmt < tn) tn = L.fmt;
     if (active && (tn == INT64_MAX || tn > t_end) && !pending_main) active = false;  // parked beyond t_end
     if (LP && L.status == TW_REP_RUNNING && tn != INT64_MAX)
         __hip_atomic_fetch_min(gp(c.next_t), (uint64_t)tn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1246,7 +1314,7 @@ __global__ void __launch_bounds__(256) tw_lp_scatter(Dev c, const uint4* recs, u
         uint4 GAS* q = gp(c.inbox) + ((size_t)k * c.R + lp) * 2;
         q[0] = a;
         q[1] = b;
-        int64_t ta = (int64_t)(((uint64_t)a.y << 32) | a.x);
+        int64_t ta = ent_t(a);
         __hip_atomic_fetch_min(gp(c.next_t), (uint64_t)ta, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     } else if (foreign) {
         uint32_t k = __hip_atomic_fetch_add(gp(n_foreign), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1321,7 +1389,7 @@ void free_all(tw_ctx* c) {
 
 extern "C" {
 
-const char* tw_version(void) { return "timewarp-mi355x 0.1 (gfx950, lane-per-replica, near-cap " "16)"; }
+const char* tw_version(void) { return "timewarp-mi355x 0.2 (gfx950, lane-per-replica, near-cap 16, LDS write-back record cache)"; }
 
 const char* tw_strerror(int code) {
     switch (code) {
@@ -1412,8 +1480,12 @@ static int load_common(tw_ctx* c, const tw_scenario_desc* s, bool lp, uint32_t l
     d.Cr = s->run_capacity;
     const size_t R = d.R;
     const size_t Rt = s->n_replicas;  // replica dimension of the host tables
-    c->lds_bytes = near_lds_bytes() + 8ull * (d.n_insns + 1) + 8ull * d.n_consts;
-    if (c->lds_bytes > 64 * 1024) { free_all(c); return TW_ERR_INVALID; }  // program + constants must fit in LDS
+    c->lds_bytes = fixed_lds_bytes() + 8ull * (d.n_insns + 1) + 8ull * d.n_consts;
+    if (c->lds_bytes > 160 * 1024) { free_all(c); return TW_ERR_INVALID; }  // program + constants must fit in LDS
+    HIPCHK(hipFuncSetAttribute((const void*)tw_run_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)c->lds_bytes));
+    HIPCHK(hipFuncSetAttribute((const void*)tw_run_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)c->lds_bytes));
     int e;
 #define ALLOC(p, n) if ((e = dalloc(c, &p, (n))) != TW_OK) { free_all(c); return e; }
     uint2* insns; int64_t* consts; uint32_t *lpc, *out_off, *ldst, *lrev, *ltab = nullptr;
@@ -1437,7 +1509,7 @@ static int load_common(tw_ctx* c, const tw_scenario_desc* s, bool lp, uint32_t l
     ALLOC(d.link_ord, (size_t)(d.L ? d.L : 1) * (lp ? 1 : R));
     ALLOC(d.tmo_done, (size_t)(d.T ? d.T : 1) * R);
     ALLOC(d.n_active, 1);
-#if defined(TW_PROF) || defined(TW_PROF_LITE)
+#ifdef TW_PROF_LITE
     ALLOC(d.prof, P_COUNT);
     HIPCHK(hipMemsetAsync(d.prof, 0, 8 * P_COUNT, c->stream));
 #endif
@@ -1512,8 +1584,8 @@ int tw_reset(tw_ctx* c) {
         HIPCHK(hipMemsetAsync(d.lp_err, 0, 4, st));
         HIPCHK(hipMemsetAsync(c->n_foreign, 0, 4, st));
     }
-    uint32_t blocks = (uint32_t)((R + TW_BLOCK - 1) / TW_BLOCK);
-    hipLaunchKernelGGL(tw_init_kernel, dim3(blocks), dim3(TW_BLOCK), 0, st, d, c->main_pc, c->main_node,
+    uint32_t blocks = (uint32_t)((R + TW_WG - 1) / TW_WG);
+    hipLaunchKernelGGL(tw_init_kernel, dim3(blocks), dim3(TW_WG), 0, st, d, c->main_pc, c->main_node,
                        (const int64_t*)c->main_regs, (const int64_t*)c->nv_init, (const uint32_t*)c->listen_init,
                        c->lp ? 1 : 0);
     HIPCHK(hipGetLastError());
@@ -1528,7 +1600,7 @@ int tw_run(tw_ctx* c, int64_t t_end_us, uint64_t max_events, tw_stats* out) {
     HIPCHK(hipSetDevice(c->device));
     hipStream_t st = c->stream;
     const Dev& d = c->d;
-    uint32_t blocks = (d.R + TW_BLOCK - 1) / TW_BLOCK;
+    uint32_t blocks = (d.R + TW_WG - 1) / TW_WG;
     // events before this call (to report per-call deltas)
     std::vector<uint64_t> ev0(d.R);
     HIPCHK(hipMemcpyAsync(ev0.data(), d.scal + (size_t)SC_EVENTS * d.R, 8ull * d.R, hipMemcpyDeviceToHost, st));
@@ -1551,10 +1623,10 @@ int tw_run(tw_ctx* c, int64_t t_end_us, uint64_t max_events, tw_stats* out) {
             if (c->lp) HIPCHK(hipMemsetAsync(d.next_t, 0xFF, 8, st));
             HIPCHK(hipEventRecord(c->ev_pool[2 * i], st));
             if (c->lp)
-                hipLaunchKernelGGL(tw_run_kernel<true>, dim3(blocks), dim3(TW_BLOCK), c->lds_bytes, st, d, t_end_us,
+                hipLaunchKernelGGL(tw_run_kernel<true>, dim3(blocks), dim3(TW_WG), c->lds_bytes, st, d, t_end_us,
                                    limit, budget);
             else
-                hipLaunchKernelGGL(tw_run_kernel<false>, dim3(blocks), dim3(TW_BLOCK), c->lds_bytes, st, d, t_end_us,
+                hipLaunchKernelGGL(tw_run_kernel<false>, dim3(blocks), dim3(TW_WG), c->lds_bytes, st, d, t_end_us,
                                    limit, budget);
             HIPCHK(hipGetLastError());
             HIPCHK(hipEventRecord(c->ev_pool[2 * i + 1], st));
@@ -1742,7 +1814,7 @@ int tw_lp_results(tw_ctx* c, tw_replica_result* agg, uint64_t* node_hashes, size
     return TW_OK;
 }
 
-#if defined(TW_PROF) || defined(TW_PROF_LITE)
+#ifdef TW_PROF_LITE
 // Diagnostic build only: copy the P_COUNT counters out, optionally zeroing them.
 int tw_prof_read(tw_ctx* c, unsigned long long* out, size_t cap, int reset) {
     if (!c || !out || !c->loaded || !c->d.prof) return TW_ERR_STATE;

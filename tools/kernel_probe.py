@@ -26,7 +26,7 @@ NAMES = ["sel_cyc", "wait_cyc", "pre_cyc", "step_cyc", "iters", "pops", "superse
 
 
 
-LITE = ["sel_cyc", "pre_cyc", "step_cyc", "loop_cyc", "iters", "pops"]
+LITE = ["sel_cyc", "pre_cyc", "step_cyc", "loop_cyc", "iters", "pops", "dispatch_cyc", "tail_cyc", "store_cyc", "spawn_cyc", "yenq_cyc", "throw_cyc", "die_cyc", "selmin_cyc", "load_cyc", "pop_cyc"]
 
 
 def read(eng):
@@ -45,7 +45,10 @@ def derived_lite(d):
     pops, it = max(d["pops"], 1), max(d["iters"], 1)
     return {"loop_per_pop": d["loop_cyc"] / pops, "sel_per_iter": d["sel_cyc"] / it,
             "pre_per_pop": d["pre_cyc"] / pops, "step_per_pop": d["step_cyc"] / pops,
-            "iters_per_pop": it / pops}
+            "iters_per_pop": it / pops, "dispatch_per_pop": d["dispatch_cyc"] / pops,
+            "tail_per_pop": d["tail_cyc"] / pops, "store_per_pop": d["store_cyc"] / pops,
+            **{k[:-4] + "_per_pop": d[k] / pops for k in ("spawn_cyc", "yenq_cyc", "throw_cyc", "die_cyc", "selmin_cyc",
+                                                        "load_cyc", "pop_cyc")}}
 
 
 def derived(d):
