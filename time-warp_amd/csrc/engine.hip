@@ -40,8 +40,9 @@
 
 #define TW_NEAR_CAP 16          // on-chip queue entries per replica (LDS)
 #define TW_WG 256               // lanes per workgroup (4 waves share one program image)
+#ifndef TW_RUNS
 #define TW_RUNS 4               // monotone far-queue runs per replica
-#define TW_RC 6                 // write-back thread-record cache entries per lane (LDS)
+#endif
 #define TW_STEP_CAP (1u << 22)  // instructions per thread step (== oracle kStepCap)
 
 // Explicit address spaces: generic (flat) pointers would make every HBM and
@@ -54,23 +55,19 @@
 #define LAS
 #endif
 
-// Diagnostic build (-DTW_PROF_LITE, lib/libtimewarp_lite.so): s_memtime cycle
-// splits summed into Dev::prof at kernel end (tools/kernel_probe.py).  The
-// product build compiles every LITE_* to nothing.
-#ifdef TW_PROF_LITE
-#define LITE_T(v) uint64_t v = __builtin_amdgcn_s_memtime()
-#define LITE_ACC(i, v) (L.lite[(i)] += (uint32_t)(v))
-#define LITE_ACCM(i, v) (lite[(i)] += (uint32_t)(v))
-#define LITE_WRAP(i, stmt) do { uint64_t _w0 = __builtin_amdgcn_s_memtime(); stmt; LITE_ACCM(i, __builtin_amdgcn_s_memtime() - _w0); } while (0)
-#define KLITE_WRAP(i, stmt) do { uint64_t _w0 = __builtin_amdgcn_s_memtime(); stmt; LITE_ACC(i, __builtin_amdgcn_s_memtime() - _w0); } while (0)
-#else
-#define LITE_T(v) ((void)0)
-#define LITE_ACC(i, v) ((void)0)
-#define LITE_ACCM(i, v) ((void)0)
-#define LITE_WRAP(i, stmt) do { stmt; } while (0)
-#define KLITE_WRAP(i, stmt) do { stmt; } while (0)
-#endif
 #define P_COUNT 16
+// Diagnostic build (-DTW_STATS, lib/libtimewarp_stats.so): per-lane event-path
+// counters summed into Dev::prof at kernel end (tools/stats_probe.py).  The
+// product build compiles every STAT to nothing.
+#ifdef TW_STATS
+#define STAT(i) (++st[(i)])
+#define STATL(i) (++L.st[(i)])
+#else
+#define STAT(i) ((void)0)
+#define STATL(i) ((void)0)
+#endif
+enum { K_POP, K_SUPERSEDED, K_PEEK_POOL, K_PEEK_PF, K_PEEK_HBM, K_PUT_POOL, K_PUT_EVICT, K_PUT_HBM, K_PUT_DEAD,
+       K_PF_ISSUE, K_HASH_IMM, K_HASH_FLUSH, K_NEAR_PUSH, K_RUN_PUSH, K_FAR_PUSH, K_INSN };
 
 namespace {
 
@@ -109,30 +106,9 @@ __device__ __forceinline__ void th_clr_flags(Th& t, uint32_t f) { t.w0 &= ~((f &
 __device__ __forceinline__ uint32_t th_exc(const Th& t) { return t.w0 >> 24; }
 __device__ __forceinline__ void th_set_exc(Th& t, uint32_t c) { t.w0 = (t.w0 & 0x00FFFFFFu) | (c << 24); }
 
-// Registers and frames are selected with mask arithmetic, never indexing: a
-// select chain over the fields gets folded into an indexed load, which pins
-// the whole record in scratch memory.  Register operands are wave-uniform
-// (the dispatch is on the whole instruction word), so the masks are scalar.
-__device__ __forceinline__ int64_t getr(const Th& t, uint32_t a) {
-    const int64_t m0 = -(int64_t)(a == 0), m1 = -(int64_t)(a == 1), m2 = -(int64_t)(a == 2), m3 = -(int64_t)(a == 3);
-    return (t.r0 & m0) | (t.r1 & m1) | (t.r2 & m2) | (t.r3 & m3);
-}
-__device__ __forceinline__ void setr(Th& t, uint32_t a, int64_t v) {
-    const int64_t m0 = -(int64_t)(a == 0), m1 = -(int64_t)(a == 1), m2 = -(int64_t)(a == 2), m3 = -(int64_t)(a == 3);
-    t.r0 = (v & m0) | (t.r0 & ~m0);
-    t.r1 = (v & m1) | (t.r1 & ~m1);
-    t.r2 = (v & m2) | (t.r2 & ~m2);
-    t.r3 = (v & m3) | (t.r3 & ~m3);
-}
 __device__ __forceinline__ uint32_t getf(const Th& t, uint32_t i) {
     const uint32_t m0 = 0u - (i == 0), m1 = 0u - (i == 1), m2 = 0u - (i == 2);
     return (t.f0 & m0) | (t.f1 & m1) | (t.f2 & m2);
-}
-__device__ __forceinline__ void setf(Th& t, uint32_t i, uint32_t v) {
-    const uint32_t m0 = 0u - (i == 0), m1 = 0u - (i == 1), m2 = 0u - (i == 2);
-    t.f0 = (v & m0) | (t.f0 & ~m0);
-    t.f1 = (v & m1) | (t.f1 & ~m1);
-    t.f2 = (v & m2) | (t.f2 & ~m2);
 }
 
 enum {
@@ -184,6 +160,9 @@ struct Dev {
 
 // ------------------------------------------------------------------ hashing
 __device__ __forceinline__ uint64_t mix64(uint64_t z) {
+#ifdef TW_X_NOMIX
+        return z;
+#endif
     z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
     z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
     return z ^ (z >> 31);
@@ -203,49 +182,33 @@ __device__ __forceinline__ uint4 ent(int64_t t, uint32_t slot, uint32_t seq) {
 }
 __device__ __forceinline__ int64_t ent_t(uint4 e) { return (int64_t)(((uint64_t)e.y << 32) | e.x); }
 
-enum { ST_CACHE, ST_THROUGH, ST_DEAD };  // store_rec modes
 
-// Six per-lane words with no array behind them: an array written at a per-lane
-// index (the LRU victim) is re-rolled by the compiler into scratch stores.
-static_assert(TW_RC == 6, "RegVec6 holds the record-cache metadata");
-struct RegVec6 {
-    uint32_t v0, v1, v2, v3, v4, v5;
-    __device__ __forceinline__ void fill(uint32_t x) { v0 = v1 = v2 = v3 = v4 = v5 = x; }
-    // per-lane h: mask arithmetic (a select chain would be folded into an
-    // indexed load and pin the whole lane state in scratch)
-    __device__ __forceinline__ uint32_t at(int h) const {
-        return (v0 & (0u - (h == 0))) | (v1 & (0u - (h == 1))) | (v2 & (0u - (h == 2))) |
-               (v3 & (0u - (h == 3))) | (v4 & (0u - (h == 4))) | (v5 & (0u - (h == 5)));
-    }
-    __device__ __forceinline__ void put(int h, uint32_t x) {
-        uint32_t m;
-        m = 0u - (h == 0); v0 = (x & m) | (v0 & ~m);
-        m = 0u - (h == 1); v1 = (x & m) | (v1 & ~m);
-        m = 0u - (h == 2); v2 = (x & m) | (v2 & ~m);
-        m = 0u - (h == 3); v3 = (x & m) | (v3 & ~m);
-        m = 0u - (h == 4); v4 = (x & m) | (v4 & ~m);
-        m = 0u - (h == 5); v5 = (x & m) | (v5 & ~m);
-    }
-    __device__ __forceinline__ int find(uint32_t x) const {
-        int h = -1;
-        h = v0 == x ? 0 : h;
-        h = v1 == x ? 1 : h;
-        h = v2 == x ? 2 : h;
-        h = v3 == x ? 3 : h;
-        h = v4 == x ? 4 : h;
-        h = v5 == x ? 5 : h;
-        return h;
-    }
-    __device__ __forceinline__ int argmin() const {
-        int h = 0;
-        uint32_t b = v0;
-        if (v1 < b) { b = v1; h = 1; }
-        if (v2 < b) { b = v2; h = 2; }
-        if (v3 < b) { b = v3; h = 3; }
-        if (v4 < b) { b = v4; h = 4; }
-        if (v5 < b) { b = v5; h = 5; }
-        return h;
-    }
+// Cold per-lane words in LDS, [CW_*][TW_WG] u32: the far runs' bookkeeping,
+// the far-heap top, rarely-touched counters and the step's spawn/yield
+// staging.  Keeping them out of registers leaves the event loop a small
+// register footprint (one wave per SIMD issues every instruction itself; a
+// large live set turns into register shuffles on every path).
+enum {
+    CW_RH = 0,                      // run head index       [TW_RUNS]
+    CW_RN = CW_RH + TW_RUNS,        // run length
+    CW_RTL = CW_RN + TW_RUNS,       // head time lo
+    CW_RTH = CW_RTL + TW_RUNS,      // head time hi
+    CW_RS = CW_RTH + TW_RUNS,       // head seq
+    CW_RSL = CW_RS + TW_RUNS,       // head slot
+    CW_R2TL = CW_RSL + TW_RUNS,     // second entry (valid while rn >= 2)
+    CW_R2TH = CW_R2TL + TW_RUNS,
+    CW_R2S = CW_R2TH + TW_RUNS,
+    CW_R2SL = CW_R2S + TW_RUNS,
+    CW_UTL = CW_R2SL + TW_RUNS,     // tail time lo / hi / seq
+    CW_UTH = CW_UTL + TW_RUNS,
+    CW_US = CW_UTH + TW_RUNS,
+    CW_FTL = CW_US + TW_RUNS,       // far heap top (t, seq, slot)
+    CW_FTH, CW_FS, CW_FSL,
+    CW_DL, CW_DR, CW_UD, CW_TH, CW_MAINEXC, CW_TMO,   // counters
+    CW_YTL, CW_YTH, CW_CPC, CW_CNODE, CW_CRA, CW_CDEL, // step staging: wake time, child
+    CW_Q0, CW_Q7 = CW_Q0 + 7,                          // child registers (4 x int64)
+    CW_DUMMY,                                          // target of idle lanes' predicated stores
+    CW_COUNT
 };
 
 template <bool LP>
@@ -255,7 +218,8 @@ struct Lane {
     // LDS (lane-offset pointers; element j at [j * TW_WG])
     uint64_t LAS* nk;     // near heap keys: (t - nbase) << 32 | seq
     uint32_t LAS* ns;     // near heap slots
-    uint4 LAS* rcd;       // record cache: entry e quad q at [(e*4+q) * TW_WG]
+    int64_t LAS* rf;      // the running thread's registers r0..r3 during its step
+    uint32_t LAS* cw;     // cold words [CW_*]
     const uint2 LAS* P;   // program image
     const int64_t LAS* K; // constant pool
     // near heap
@@ -263,30 +227,29 @@ struct Lane {
     int64_t nbase;
     uint64_t nrk;  // cached root key
     uint32_t nrs;  // cached root slot
-    // far runs: head index, count, head (t, seq, slot), tail (t, seq)
-    uint32_t rh[TW_RUNS], rn[TW_RUNS];
-    int64_t rt[TW_RUNS], ut[TW_RUNS];
-    uint32_t rs[TW_RUNS], rsl[TW_RUNS], us[TW_RUNS];
-    // far heap top
+    // far sources: heap size, and the cached min over the runs and the heap top
     uint32_t far_n;
-    int64_t ft;
-    uint32_t fs, fsl;
-    // min over far sources (lazily recomputed: a run head reload overlaps the step)
     bool far_dirty;
     int fsrc;  // -1 none, 0..TW_RUNS-1 run, TW_RUNS heap
     int64_t fmt;
     uint32_t fms, fmsl;
-    // write-back record cache: tags, LRU stamps, dirty bits
-    RegVec6 ctag, cst;
-    uint32_t cdirty, clk;
+    // a run's second entry in flight from HBM (committed to LDS at the next run access)
+    int prun;
+    uint4 pent;
+    // prefetched HBM copy of the next pop's record (pf_slot NONE = invalid)
+    Th pf;
+    uint32_t pf_slot;
+    // this iteration's hash terms for the popped thread's node, one atomic at the end
+    uint64_t hacc;
+    uint32_t hnode;
     // free slots: bump pointer + stack with its top in a register
     uint32_t free_n, ftop, bump;
     // replica scalars
     int64_t now, final_t;
-    uint32_t seq, tidc, live, status, main_exc, tmo_ctr;
-    uint32_t d_ev, d_dl, d_dr, d_ud, d_th;  // this launch's counter increments
-#ifdef TW_PROF_LITE
-    uint32_t lite[16];  // sel, pre, step, loop, iters, pops, dispatch, tail, store, spawn, yield-enq, throw, die, selmin, load, pop
+    uint32_t seq, tidc, live, status;
+    uint32_t d_ev;  // this launch's event count
+#ifdef TW_STATS
+    uint32_t st[P_COUNT];
 #endif
 
     __device__ __forceinline__ size_t ix(size_t i) const { return i * c.R + r; }
@@ -300,6 +263,17 @@ struct Lane {
         size_t i = (size_t)link * c.D + ord % c.D;
         return LP ? i : ix(i);
     }
+    // cold words
+    __device__ __forceinline__ uint32_t cg(int w) const { return cw[w * TW_WG]; }
+    __device__ __forceinline__ void cs(int w, uint32_t v) const { cw[w * TW_WG] = v; }
+    __device__ __forceinline__ int64_t cg64(int wl, int wh) const {
+        return (int64_t)(((uint64_t)cw[wh * TW_WG] << 32) | cw[wl * TW_WG]);
+    }
+    __device__ __forceinline__ void cs64(int wl, int wh, int64_t v) const {
+        cw[wl * TW_WG] = (uint32_t)v;
+        cw[wh * TW_WG] = (uint32_t)((uint64_t)v >> 32);
+    }
+    __device__ __forceinline__ void cinc(int w) const { cw[w * TW_WG] += 1; }
 
     __device__ __forceinline__ void fail(uint32_t st) {
         if (status == TW_REP_RUNNING) status = st;
@@ -354,6 +328,7 @@ struct Lane {
         if (i == 0) { nrk = k; nrs = s; }
     }
     __device__ __forceinline__ void near_push(int64_t t, uint32_t sq, uint32_t slot) {
+        STAT(K_NEAR_PUSH);
         near_sift_up(near_n++, nkey(t, sq), slot);
     }
     __device__ __forceinline__ void near_pop() {
@@ -385,8 +360,12 @@ struct Lane {
     // ------------------------------------------------------ far heap (HBM, 4-ary)
     __device__ __forceinline__ uint4 far_ld(uint32_t i) const { return gp(c.far)[ix(i)]; }
     __device__ __forceinline__ void far_st(uint32_t i, uint4 e) const { gp(c.far)[ix(i)] = e; }
+    __device__ __forceinline__ void set_ftop(uint4 e) const {
+        cs(CW_FTL, e.x); cs(CW_FTH, e.y); cs(CW_FS, e.w); cs(CW_FSL, e.z);
+    }
     __device__ __forceinline__ void far_push(int64_t t, uint32_t sq, uint32_t slot) {
         if (far_n >= c.Q) { fail(TW_REP_ERR_QUEUE); return; }
+        STAT(K_FAR_PUSH);
         uint32_t i = far_n++;
         while (i > 0) {
             uint32_t p = (i - 1) >> 2;
@@ -396,7 +375,7 @@ struct Lane {
             i = p;
         }
         far_st(i, ent(t, slot, sq));
-        if (i == 0) { ft = t; fs = sq; fsl = slot; far_dirty = true; }
+        if (i == 0) { set_ftop(ent(t, slot, sq)); far_dirty = true; }
     }
     __device__ __forceinline__ void far_pop() {
         uint32_t n = --far_n;
@@ -420,70 +399,102 @@ struct Lane {
             if (cn > 3 && tless(ent_t(e3), e3.w, ent_t(b), b.w)) { b = e3; best = 3; }
             if (!tless(ent_t(b), b.w, t, le.w)) break;
             far_st(i, b);
-            if (i == 0) { ft = ent_t(b); fs = b.w; fsl = b.z; }
+            if (i == 0) set_ftop(b);
             i = c0 + best;
         }
         far_st(i, le);
-        if (i == 0) { ft = t; fs = le.w; fsl = le.z; }
+        if (i == 0) set_ftop(le);
     }
 
     // ---------------------------------------------------- far runs (HBM FIFOs)
     // Patience-sorting piles: a far event is appended to the run whose tail is
-    // the largest key <= it, so runs stay sorted and pops are O(1) with the next
-    // head prefetched.  TimedT scenarios park threads in monotone streams
-    // (killers at one absolute time, sleepForever timers, re-stamped victims of
-    // a killer sweep), so the heap sees only stragglers.
+    // the largest key <= it, so runs stay sorted and pops are O(1).  TimedT
+    // scenarios park threads in monotone streams (killers at one absolute time,
+    // sleepForever timers, re-stamped victims of a killer sweep), so the heap
+    // sees only stragglers.  Bookkeeping lives in the cold LDS words; the run
+    // indexed by a per-lane number is a per-lane LDS address, not a select chain.
     __device__ __forceinline__ uint4 GAS* run_at(uint32_t j, uint32_t pos) const {
         return gp(c.runs) + ((size_t)j * c.Cr + pos) * c.R + r;
     }
+    // the second entry loaded by the last run_pop lands in LDS
+    __device__ __forceinline__ void run_commit() {
+        if (prun >= 0) {
+            cs(CW_R2TL + prun, pent.x); cs(CW_R2TH + prun, pent.y);
+            cs(CW_R2S + prun, pent.w); cs(CW_R2SL + prun, pent.z);
+            prun = -1;
+        }
+    }
     __device__ __forceinline__ bool run_push(int64_t t, uint32_t sq, uint32_t slot) {
         if (c.Cr == 0) return false;
+        run_commit();
         int best = -1, empty = -1;
         int64_t bt = 0;
         uint32_t bs = 0;
 #pragma unroll
         for (int j = 0; j < TW_RUNS; ++j) {
-            if (rn[j] == 0) {
-                if (empty < 0) empty = j;
-            } else if (rn[j] < c.Cr && !tless(t, sq, ut[j], us[j])) {
-                if (best < 0 || tless(bt, bs, ut[j], us[j])) { best = j; bt = ut[j]; bs = us[j]; }
-            }
+            const uint32_t n = cg(CW_RN + j);
+            const int64_t ut = cg64(CW_UTL + j, CW_UTH + j);
+            const uint32_t us = cg(CW_US + j);
+            const bool e = n == 0 && empty < 0;
+            empty = e ? j : empty;
+            const bool ok = n != 0 && n < c.Cr && !tless(t, sq, ut, us) && (best < 0 || tless(bt, bs, ut, us));
+            best = ok ? j : best;
+            bt = ok ? ut : bt;
+            bs = ok ? us : bs;
         }
-        int sel = best >= 0 ? best : empty;
+        const int sel = best >= 0 ? best : empty;
         if (sel < 0) return false;
-#pragma unroll
-        for (int j = 0; j < TW_RUNS; ++j) {
-            if (j == sel) {
-                uint32_t pos = rh[j] + rn[j];
-                if (pos >= c.Cr) pos -= c.Cr;
-                *run_at(j, pos) = ent(t, slot, sq);
-                if (rn[j] == 0) { rt[j] = t; rs[j] = sq; rsl[j] = slot; far_dirty = true; }
-                ut[j] = t; us[j] = sq;
-                ++rn[j];
-            }
+        STAT(K_RUN_PUSH);
+        const uint32_t n = cg(CW_RN + sel);
+        uint32_t pos = cg(CW_RH + sel) + n;
+        if (pos >= c.Cr) pos -= c.Cr;
+        const uint4 e = ent(t, slot, sq);
+        *run_at(sel, pos) = e;
+        if (n == 0) {
+            cs(CW_RTL + sel, e.x); cs(CW_RTH + sel, e.y); cs(CW_RS + sel, sq); cs(CW_RSL + sel, slot);
+            far_dirty = true;
+        } else if (n == 1) {
+            cs(CW_R2TL + sel, e.x); cs(CW_R2TH + sel, e.y); cs(CW_R2S + sel, sq); cs(CW_R2SL + sel, slot);
         }
+        cs(CW_UTL + sel, e.x); cs(CW_UTH + sel, e.y); cs(CW_US + sel, sq);
+        cs(CW_RN + sel, n + 1);
         return true;
     }
+    // The head moves to the second entry; the entry after it is loaded now and
+    // committed at the next run access, a whole event before it can be the head.
     __device__ __forceinline__ void run_pop(int sel) {
+        run_commit();
         far_dirty = true;
-#pragma unroll
-        for (int j = 0; j < TW_RUNS; ++j) {
-            if (j == sel) {
-                rh[j] = rh[j] + 1 == c.Cr ? 0 : rh[j] + 1;
-                if (--rn[j]) {  // next head: its latency overlaps this event's step
-                    uint4 e = *run_at(j, rh[j]);
-                    rt[j] = ent_t(e); rs[j] = e.w; rsl[j] = e.z;
-                }
-            }
+        uint32_t h = cg(CW_RH + sel) + 1;
+        h = h == c.Cr ? 0 : h;
+        cs(CW_RH + sel, h);
+        cs(CW_RTL + sel, cg(CW_R2TL + sel)); cs(CW_RTH + sel, cg(CW_R2TH + sel));
+        cs(CW_RS + sel, cg(CW_R2S + sel)); cs(CW_RSL + sel, cg(CW_R2SL + sel));
+        const uint32_t n = cg(CW_RN + sel) - 1;
+        cs(CW_RN + sel, n);
+        if (n >= 2) {
+            const uint32_t p2 = h + 1 == c.Cr ? 0 : h + 1;
+            pent = *run_at(sel, p2);
+            prun = sel;
         }
     }
     __device__ __forceinline__ void far_min() {
+        run_commit();
         far_dirty = false;
         fsrc = -1;
-        if (far_n) { fsrc = TW_RUNS; fmt = ft; fms = fs; fmsl = fsl; }
+        fmt = 0; fms = 0; fmsl = 0;
+        if (far_n) { fsrc = TW_RUNS; fmt = cg64(CW_FTL, CW_FTH); fms = cg(CW_FS); fmsl = cg(CW_FSL); }
 #pragma unroll
-        for (int j = 0; j < TW_RUNS; ++j)
-            if (rn[j] && (fsrc < 0 || tless(rt[j], rs[j], fmt, fms))) { fsrc = j; fmt = rt[j]; fms = rs[j]; fmsl = rsl[j]; }
+        for (int j = 0; j < TW_RUNS; ++j) {
+            const uint32_t n = cg(CW_RN + j);
+            const int64_t t = cg64(CW_RTL + j, CW_RTH + j);
+            const uint32_t s = cg(CW_RS + j);
+            const bool b = n != 0 && (fsrc < 0 || tless(t, s, fmt, fms));
+            fsrc = b ? j : fsrc;
+            fmt = b ? t : fmt;
+            fms = b ? s : fms;
+            fmsl = b ? cg(CW_RSL + j) : fmsl;
+        }
     }
     __device__ __forceinline__ void push_far(int64_t t, uint32_t sq, uint32_t slot) {
         if (!run_push(t, sq, slot)) far_push(t, sq, slot);
@@ -505,7 +516,11 @@ struct Lane {
         return false;
     }
 
-    // ------------------------------------------------- thread records (cache)
+    // ------------------------------------------------- thread records
+    // A record lives in HBM while its thread is queued and in registers (the
+    // header) + the LDS register file (r0..r3) while it runs.  `pf` holds a
+    // prefetched copy of the next pop's record, loaded right after the previous
+    // pop so its latency hides behind a whole step.
     __device__ __forceinline__ static void unpack(Th& th, uint4 a, uint4 b, uint4 d, uint4 e) {
         th.w0 = a.x; th.w1 = a.y; th.w2 = a.z; th.w3 = a.w;
         th.f0 = b.x; th.f1 = b.y; th.f2 = b.z; th.w7 = b.w;
@@ -514,70 +529,54 @@ struct Lane {
         th.r2 = (int64_t)(((uint64_t)e.y << 32) | e.x);
         th.r3 = (int64_t)(((uint64_t)e.w << 32) | e.z);
     }
-    __device__ __forceinline__ static void pack(const Th& th, uint4& a, uint4& b, uint4& d, uint4& e) {
-        a = make_uint4(th.w0, th.w1, th.w2, th.w3);
-        b = make_uint4(th.f0, th.f1, th.f2, th.w7);
-        d = make_uint4((uint32_t)th.r0, (uint32_t)((uint64_t)th.r0 >> 32), (uint32_t)th.r1,
-                       (uint32_t)((uint64_t)th.r1 >> 32));
-        e = make_uint4((uint32_t)th.r2, (uint32_t)((uint64_t)th.r2 >> 32), (uint32_t)th.r3,
-                       (uint32_t)((uint64_t)th.r3 >> 32));
-    }
-    __device__ __forceinline__ int cfind(uint32_t slot) const { return ctag.find(slot); }
-    __device__ __forceinline__ void ctouch(int h) { cst.put(h, ++clk); }
     __device__ __forceinline__ uint4 GAS* hrec(uint32_t slot) const { return gp(c.slots) + ix(slot) * 4; }
-    __device__ __forceinline__ uint4 LAS* crec(int e) const { return rcd + (size_t)e * 4 * TW_WG; }
-    // HBM holds a record unless the cache has a (newer) copy.
-    __device__ __forceinline__ void load_rec(uint32_t slot, Th& th) {
-        int h = cfind(slot);
-        if (h >= 0) {
-            const uint4 LAS* q = crec(h);
-            unpack(th, q[0], q[TW_WG], q[2 * TW_WG], q[3 * TW_WG]);
-            ctouch(h);
-            return;
-        }
+    __device__ __forceinline__ void hbm_load(uint32_t slot, Th& th) const {
         const uint4 GAS* p = hrec(slot);
         unpack(th, p[0], p[1], p[2], p[3]);
     }
-    __device__ __forceinline__ void writeback(int e) {
-        const uint4 LAS* q = crec(e);
-        uint4 a = q[0], b = q[TW_WG], d = q[2 * TW_WG], f = q[3 * TW_WG];
-        uint4 GAS* p = hrec(ctag.at(e));
-        p[0] = a; p[1] = b; p[2] = d; p[3] = f;
+    __device__ __forceinline__ void peek_rec(uint32_t slot, Th& th) {
+        if (slot == pf_slot) {
+            STAT(K_PEEK_PF);
+            th = pf;
+        } else {
+            STAT(K_PEEK_HBM);
+            hbm_load(slot, th);
+        }
     }
-    // ST_CACHE: the thread is queued on chip (it runs again soon) -> keep the
-    // record in the cache, dirty; ST_THROUGH: queued far -> write it to HBM and
-    // drop any cached copy; ST_DEAD: only the header quad (the tid that
-    // invalidates stale refs) is written.
-    __device__ __forceinline__ void store_rec(uint32_t slot, const Th& th, int mode) {
-        uint4 a, b, d, f;
-        pack(th, a, b, d, f);
-        int h = cfind(slot);
-        if (mode == ST_CACHE) {
-            if (h < 0) {  // LRU victim (invalid entries carry stamp 0)
-                h = cst.argmin();
-                if (cdirty & (1u << h)) writeback(h);
-                ctag.put(h, slot);
-            }
-            uint4 LAS* q = crec(h);
-            q[0] = a; q[TW_WG] = b; q[2 * TW_WG] = d; q[3 * TW_WG] = f;
-            cdirty |= 1u << h;
-            ctouch(h);
-            return;
-        }
-        if (h >= 0) {
-            ctag.put(h, 0xFFFFFFFFu);
-            cst.put(h, 0);
-            cdirty &= ~(1u << h);
-        }
+    // mode ST_THROUGH: the full record; ST_DEAD: only the header quad (the tid
+    // that invalidates stale refs)
+    __device__ __forceinline__ void put_hdr(uint32_t slot, const Th& th) {
+        if (slot == pf_slot) pf_slot = 0xFFFFFFFFu;
+        STAT(K_PUT_DEAD);
+        hrec(slot)[0] = make_uint4(th.w0, th.w1, th.w2, th.w3);
+    }
+    __device__ __forceinline__ void put_rec(uint32_t slot, const Th& th) {
+        if (slot == pf_slot) pf_slot = 0xFFFFFFFFu;
+        STAT(K_PUT_HBM);
         uint4 GAS* p = hrec(slot);
-        p[0] = a;
-        if (mode == ST_THROUGH) { p[1] = b; p[2] = d; p[3] = f; }
+        p[0] = make_uint4(th.w0, th.w1, th.w2, th.w3);
+        p[1] = make_uint4(th.f0, th.f1, th.f2, th.w7);
+        p[2] = make_uint4((uint32_t)th.r0, (uint32_t)((uint64_t)th.r0 >> 32), (uint32_t)th.r1,
+                          (uint32_t)((uint64_t)th.r1 >> 32));
+        p[3] = make_uint4((uint32_t)th.r2, (uint32_t)((uint64_t)th.r2 >> 32), (uint32_t)th.r3,
+                          (uint32_t)((uint64_t)th.r3 >> 32));
     }
-    __device__ __forceinline__ void flush_cache() {
-#pragma unroll
-        for (int e = 0; e < TW_RC; ++e)
-            if (cdirty & (1u << e)) writeback(e);
-        cdirty = 0;
+    // the running thread: header from registers, r0..r3 from the LDS register file
+    __device__ __forceinline__ void put_running(uint32_t slot, Th& th) {
+        th.r0 = rf[0]; th.r1 = rf[TW_WG]; th.r2 = rf[2 * TW_WG]; th.r3 = rf[3 * TW_WG];
+        put_rec(slot, th);
+    }
+    // Issue the HBM load of the record the next pop will most likely need.
+    __device__ __forceinline__ void prefetch_next(uint32_t cur) {
+        if (far_dirty) far_min();
+        uint32_t s = 0xFFFFFFFFu;
+        if (near_n) s = nrs;
+        if (fsrc >= 0 && (!near_n || tless(fmt, fms, nbase + (int64_t)(nrk >> 32), (uint32_t)nrk))) s = fmsl;
+        if (s != 0xFFFFFFFFu && s != cur && s != pf_slot) {
+            STAT(K_PF_ISSUE);
+            hbm_load(s, pf);
+            pf_slot = s;
+        }
     }
 
     // Free slots: never-used slots come from a bump pointer (no memory read);
@@ -598,12 +597,22 @@ struct Lane {
         ++free_n;
     }
 
-    // Commutative per-node trace hash: a no-return 64-bit atomic add, so the
-    // event's critical path never waits on the node's hash line.
-    __device__ __forceinline__ void hash_add(uint32_t node, uint64_t v) {
+    // Commutative per-node trace hash: no-return 64-bit atomic adds.  Terms for
+    // the popped thread's node (nearly all of them) are summed in a register and
+    // added once at the end of the iteration, after the step's loads were issued
+    // (a load waits for every older store/atomic of the wave: vmcnt is in order).
+    __device__ __forceinline__ void hash_atomic(uint32_t node, uint64_t v) {
         unsigned long long GAS* h = LP ? (unsigned long long GAS*)(gp(c.hash_g) + node)
                                        : (unsigned long long GAS*)(gp(c.hash) + ix(node));
         __hip_atomic_fetch_add(h, (unsigned long long)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __device__ __forceinline__ void hash_add(uint32_t node, uint64_t v) {
+        if (node == hnode) hacc += v;
+        else { STAT(K_HASH_IMM); hash_atomic(node, v); }
+    }
+    __device__ __forceinline__ void hash_flush() {
+        if (hacc) { STAT(K_HASH_FLUSH); hash_atomic(hnode, hacc); }  // adding 0 is a no-op
+        hacc = 0;
     }
     __device__ __forceinline__ void hash(uint32_t node, uint32_t kind, int64_t val) {
         hash_add(node, term(now, kind, val));
@@ -629,15 +638,15 @@ struct Lane {
         if (s == 0xFFFFFFFFu) return false;
         Th ch;
         uint32_t tid = tidc++;
-        ++d_th;
+        cinc(CW_TH);
         ch.w0 = pc & 0xFFFFu;
         ch.w1 = node;
         ch.w2 = tid;
         ch.w3 = 0;
         ch.f0 = ch.f1 = ch.f2 = ch.w7 = 0;
         ch.r0 = q0; ch.r1 = q1; ch.r2 = q2; ch.r3 = q3;
-        bool on_chip = enqueue(ch, s, now);
-        store_rec(s, ch, on_chip ? ST_CACHE : ST_THROUGH);
+        enqueue(ch, s, now);
+        put_rec(s, ch);
         ref = (int64_t)(((uint64_t)tid << 32) | s);
         return true;
     }
@@ -653,10 +662,10 @@ struct Lane {
             return;
         }
         Th t;
-        load_rec(ts, t);
+        peek_rec(ts, t);
         if (t.w2 != tid) return;  // dead (slot free or reused): the map entry is unobservable
-        bool on_chip = (th_flags(t) & F_NEARQ) != 0;
         if (t.w3 != 0) {          // queued: wake to now with a fresh seq
+            bool on_chip = (th_flags(t) & F_NEARQ) != 0;
             uint32_t s = ++seq;
             if (!(on_chip && near_rekey(t.w3, now, s, ts))) {
                 on_chip = near_fits(now);
@@ -671,7 +680,7 @@ struct Lane {
             th_set_exc(t, code);
             t.w7 = (uint32_t)val;
         }
-        store_rec(ts, t, on_chip ? ST_CACHE : ST_THROUGH);
+        put_rec(ts, t);
     }
 
     // Thread ends (END or uncaught exception).
@@ -685,11 +694,12 @@ struct Lane {
         }
         th.w2 = 0xFFFFFFFFu;  // invalidate refs to this slot
         th.w3 = 0;
-        store_rec(slot, th, ST_DEAD);
+        put_hdr(slot, th);
         free_slot(slot);
     }
 
-    // Raise `code` in th; true if a catch frame took it (pc set to handler).
+    // Raise `code` in the running thread; true if a catch frame took it (pc set
+    // to the handler, r0 = value, r3 = code in the register file).
     __device__ __forceinline__ bool unwind(Th& th, uint32_t slot, uint32_t code, int64_t val) {
         const uint32_t n = th_nfr(th);
 #pragma unroll
@@ -703,295 +713,365 @@ struct Lane {
                 } else if (mask & (1u << code)) {
                     th_set_nfr(th, (uint32_t)i);
                     th_set_pc(th, f & 0xFFFFu);
-                    th.r0 = val;
-                    th.r3 = code;
+                    rf[0] = val;
+                    rf[3 * TW_WG] = (int64_t)code;
                     return true;
                 }
             }
         }
         th_set_nfr(th, 0);
-        if (th_flags(th) & F_MAIN) main_exc = code;
+        if (th_flags(th) & F_MAIN) cs(CW_MAINEXC, code);
         die(th, slot);
         return false;
     }
 
-    // Run the thread's continuation until it yields or ends (the ContT
-    // continuation of TimedT.hs:343-355).  Dispatch is a waterfall over the
-    // instruction words present in the wave: readfirstlane picks one, the lanes
-    // holding it execute it with op and register operands wave-uniform (scalar
-    // branches), the others wait for their turn — lanes in lock-step take one
-    // pass per instruction.  Every yielding op funnels into one shared
-    // spawn + enqueue tail.
-    __device__ __forceinline__ void step(Th& th, uint32_t slot) {
-        enum { GO, YIELD, SPAWN, THROWTO, EXIT, STOP };
-        th_or_flags(th, F_STARTED);
-        uint32_t n = 0;
+    // ------------------------------------------------------------- interpreter
+    __device__ __forceinline__ void pfail(bool cond, uint32_t st) {
+        status = (cond && status == TW_REP_RUNNING) ? st : status;
+    }
+    // predicated cold-word store: idle lanes write a dummy word (no branch)
+    __device__ __forceinline__ void csp(bool p, int w, uint32_t v) const { cw[(p ? w : CW_DUMMY) * TW_WG] = v; }
+
+    enum { T_NONE, T_YIELD, T_SPAWN, T_EXIT, T_STOP, T_DIED };
+
+    // Run the popped threads' continuations until each yields or ends (the
+    // ContT continuation of TimedT.hs:343-355).  Called by every lane of the
+    // wave (`run` = this lane popped a runnable thread), so the loop is
+    // wave-uniform: each pass takes the pc of the first running lane, the
+    // lanes at that pc ("me") execute its instruction with the opcode,
+    // operands and immediate in scalar registers; register reads and writes
+    // go to the lane's LDS register file, every other per-lane effect is a
+    // select predicated on `me` (only the rare memory-effect ops open a
+    // divergent region).  Lanes in lock-step take one pass per instruction.
+    // Yield / fork / exit are recorded per lane and carried out after the
+    // loop for all lanes at once.
+    __device__ __forceinline__ void step(Th& th, uint32_t slot, bool run) {
         uint32_t pc = th_pc(th);
-        if (pc >= c.n_insns) { fail(TW_REP_ERR_INSN); store_rec(slot, th, ST_THROUGH); return; }
-        uint2 in = P[pc];
-        int mode = ST_THROUGH;
-        LITE_T(q0t);
-#ifdef TW_PROF_LITE
-        uint64_t q1t = q0t;
-#endif
+        th.w0 = run ? th.w0 | (F_STARTED << 18) : th.w0;
+        bool running = run && pc < c.n_insns;
+        pfail(run && !running, TW_REP_ERR_INSN);
+        uint32_t fin = (run && !running) ? (uint32_t)T_STOP : (uint32_t)T_NONE;
+        uint32_t n = 0;
+        int64_t yt = 0;
         for (;;) {
-            const uint32_t w = in.x;
-            if (w != __builtin_amdgcn_readfirstlane(w)) continue;
-            uint32_t uw;  // opaque scalar copy: keeps every decode below on the SALU
-            asm volatile("v_readfirstlane_b32 %0, %1" : "=s"(uw) : "v"(w));
-            if (++n > TW_STEP_CAP) { fail(TW_REP_ERR_INSN); break; }
-            uint2 nx = P[pc + 1];  // prefetch the fall-through instruction (image padded by one)
+            const uint64_t mask = __builtin_amdgcn_ballot_w64(running);
+            if (mask == 0) break;
+            const uint32_t upc = __builtin_amdgcn_readlane(pc, (uint32_t)__builtin_ctzll(mask));
+            const bool at = running && pc == upc;
+            n += at ? 1u : 0u;
+            const bool capped = at && n > TW_STEP_CAP;  // TW_REP_ERR_INSN before executing it
+            const bool me = at && !capped;
+            const uint2 in = P[upc];
+            const uint32_t uw = __builtin_amdgcn_readfirstlane(in.x);
+            const int32_t imm = (int32_t)__builtin_amdgcn_readfirstlane(in.y);
             const uint32_t op = uw & 0xFFu, a = (uw >> 8) & 3u, b = uw >> 16;
-            const int32_t imm = (int32_t)in.y;
-            uint32_t npc = pc + 1;
-            int act = GO;
-            int64_t yt = 0;                               // YIELD: wake time
-            uint32_t cpc = 0, cnode = 0;                  // SPAWN: child entry + node
-            int64_t q0 = 0, q1 = 0, q2 = 0, q3 = 0;       //        child registers
-            int64_t tref = 0, tval = 0;                   // THROWTO target + payload
+            STAT(K_INSN);
+            const int64_t ra = rf[a * TW_WG];
+            const int64_t rb = rf[(b & 3u) * TW_WG];
+            uint32_t tc = T_NONE;     // per lane: terminal action of this op
+            uint32_t tgt = upc + 1;   // per lane: next pc
+            bool wr = false;          // uniform: the op writes r[a]
+            bool wm = me;             // per lane: ... in this lane
+            int64_t wv = 0;
+            bool thr_any = false, thr = false;  // throwTo after the op (THROW_TO, TMO_FIRE)
+            int64_t tref = 0, tval = 0;
             uint32_t tcode = 0;
             switch (op) {
             case TW_OP_NOP: break;
-            case TW_OP_END: act = EXIT; break;
-            case TW_OP_WAIT_REL: yt = now + K[imm]; act = YIELD; break;
+            case TW_OP_END: tc = T_EXIT; break;
+            case TW_OP_WAIT_REL: yt = me ? now + K[imm] : yt; tc = T_YIELD; break;
             case TW_OP_WAIT_ABS: {
-                int64_t t = K[imm];
-                yt = t > now ? t : now;
-                act = YIELD;
+                const int64_t t = K[imm];
+                yt = me ? (t > now ? t : now) : yt;
+                tc = T_YIELD;
                 break;
             }
-            case TW_OP_WAIT_REG: {
-                int64_t d = getr(th, a);
-                yt = now + (d > 0 ? d : 0);
-                act = YIELD;
-                break;
-            }
+            case TW_OP_WAIT_REG: yt = me ? now + (ra > 0 ? ra : 0) : yt; tc = T_YIELD; break;
             case TW_OP_FORK: {
-                uint32_t node = b == 0xFFFFu ? th.w1 : (uint32_t)getr(th, b & 3);
-                if (LP ? node != th.w1 : node >= c.N) { fail(TW_REP_ERR_INSN); act = STOP; break; }
-                cpc = (uint32_t)imm; cnode = node;
-                q0 = th.r0; q1 = th.r1; q2 = th.r2; q3 = th.r3;
-                act = SPAWN;
+                const uint32_t node = b == 0xFFFFu ? th.w1 : (uint32_t)rb;
+                const bool bad = LP ? node != th.w1 : node >= c.N;
+                pfail(me && bad, TW_REP_ERR_INSN);
+                tc = bad ? T_STOP : T_SPAWN;
+                const bool p = me && !bad;
+                csp(p, CW_CPC, (uint32_t)imm);
+                csp(p, CW_CNODE, node);
+                csp(p, CW_CRA, a);
+                csp(p, CW_CDEL, 2u);  // the child's registers are the parent's
                 break;
             }
-            case TW_OP_MYTID: setr(th, a, (int64_t)(((uint64_t)th.w2 << 32) | slot)); break;
+            case TW_OP_MYTID: wr = true; wv = (int64_t)(((uint64_t)th.w2 << 32) | slot); break;
             case TW_OP_THROW_TO:
-                tref = getr(th, a); tcode = b & 0xFFu; tval = getr(th, (b >> 8) & 3);
-                act = THROWTO;
+                thr_any = true; thr = me;
+                tref = ra; tcode = b & 0xFFu; tval = rf[((b >> 8) & 3u) * TW_WG];
                 break;
             case TW_OP_THROW:
-                th_set_pc(th, npc);
-                if (!unwind(th, slot, b & 0xFFu, getr(th, (b >> 8) & 3))) return;  // died (record stored)
-                npc = th_pc(th);
+                if (me) {
+                    th_set_pc(th, upc + 1);
+                    if (unwind(th, slot, b & 0xFFu, rf[((b >> 8) & 3u) * TW_WG])) tgt = th_pc(th);
+                    else tc = T_DIED;  // died: record stored
+                }
                 break;
-            case TW_OP_CATCH: {
-                uint32_t nf = th_nfr(th);
-                if (nf >= TW_MAX_FRAMES) { fail(TW_REP_ERR_FRAMES); act = STOP; break; }
-                setf(th, nf, (b << 16) | ((uint32_t)imm & 0xFFFFu));
-                th_set_nfr(th, nf + 1);
+            case TW_OP_CATCH:
+            case TW_OP_TMO_PUSH: {
+                const uint32_t nf = th_nfr(th);
+                const bool bad = nf >= TW_MAX_FRAMES;
+                pfail(me && bad, TW_REP_ERR_FRAMES);
+                tc = bad ? T_STOP : T_NONE;
+                const uint32_t fv = op == TW_OP_CATCH ? (b << 16) | ((uint32_t)imm & 0xFFFFu) : (uint32_t)ra & 0xFFFFu;
+                const bool ok = me && !bad;
+                th.f0 = (ok && nf == 0) ? fv : th.f0;
+                th.f1 = (ok && nf == 1) ? fv : th.f1;
+                th.f2 = (ok && nf == 2) ? fv : th.f2;
+                th.w0 = ok ? (th.w0 & ~(3u << 16)) | ((nf + 1) << 16) : th.w0;
                 break;
             }
             case TW_OP_UNCATCH: {
-                uint32_t nf = th_nfr(th);
-                if (nf == 0 || (getf(th, nf - 1) >> 16) == 0) { fail(TW_REP_ERR_INSN); act = STOP; break; }
-                th_set_nfr(th, nf - 1);
+                const uint32_t nf = th_nfr(th);
+                const bool bad = nf == 0 || (getf(th, nf - 1) >> 16) == 0;
+                pfail(me && bad, TW_REP_ERR_INSN);
+                tc = bad ? T_STOP : T_NONE;
+                th.w0 = (me && !bad) ? (th.w0 & ~(3u << 16)) | ((nf - 1) << 16) : th.w0;
                 break;
             }
-            case TW_OP_SETI: setr(th, a, imm); break;
-            case TW_OP_SETK: setr(th, a, K[imm]); break;
-            case TW_OP_ADDI: setr(th, a, getr(th, a) + imm); break;
-            case TW_OP_MULI: setr(th, a, getr(th, a) * imm); break;
-            case TW_OP_MOV: setr(th, a, getr(th, b & 3)); break;
-            case TW_OP_ADD: setr(th, a, getr(th, a) + getr(th, b & 3)); break;
-            case TW_OP_SUB: setr(th, a, getr(th, a) - getr(th, b & 3)); break;
+            case TW_OP_SETI: wr = true; wv = imm; break;
+            case TW_OP_SETK: wr = true; wv = K[imm]; break;
+            case TW_OP_ADDI: wr = true; wv = ra + imm; break;
+            case TW_OP_MULI: wr = true; wv = ra * imm; break;
+            case TW_OP_MOV: wr = true; wv = rb; break;
+            case TW_OP_ADD: wr = true; wv = ra + rb; break;
+            case TW_OP_SUB: wr = true; wv = ra - rb; break;
             case TW_OP_MODI: {
-                int64_t m = getr(th, a) % imm;
-                setr(th, a, m < 0 ? m + imm : m);
+                const int64_t m = ra % (int64_t)imm;
+                wr = true;
+                wv = m < 0 ? m + imm : m;
                 break;
             }
-            case TW_OP_JMP: npc = (uint32_t)imm; break;
-            case TW_OP_JEQ: if (getr(th, a) == getr(th, b & 3)) npc = (uint32_t)imm; break;
-            case TW_OP_JNE: if (getr(th, a) != getr(th, b & 3)) npc = (uint32_t)imm; break;
-            case TW_OP_JLT: if (getr(th, a) < getr(th, b & 3)) npc = (uint32_t)imm; break;
-            case TW_OP_JLE: if (getr(th, a) <= getr(th, b & 3)) npc = (uint32_t)imm; break;
-            case TW_OP_JEQI: if (getr(th, a) == (int64_t)(int16_t)b) npc = (uint32_t)imm; break;
-            case TW_OP_JNEI: if (getr(th, a) != (int64_t)(int16_t)b) npc = (uint32_t)imm; break;
-            case TW_OP_NOW: setr(th, a, now); break;
-            case TW_OP_NODE: setr(th, a, th.w1); break;
-            case TW_OP_NLOAD: setr(th, a, gp(c.nvars)[nix(th.w1, b & 3)]); break;
-            case TW_OP_NSTORE: gp(c.nvars)[nix(th.w1, b & 3)] = getr(th, a); break;
+            case TW_OP_JMP: tgt = (uint32_t)imm; break;
+            case TW_OP_JEQ: tgt = ra == rb ? (uint32_t)imm : tgt; break;
+            case TW_OP_JNE: tgt = ra != rb ? (uint32_t)imm : tgt; break;
+            case TW_OP_JLT: tgt = ra < rb ? (uint32_t)imm : tgt; break;
+            case TW_OP_JLE: tgt = ra <= rb ? (uint32_t)imm : tgt; break;
+            case TW_OP_JEQI: tgt = ra == (int64_t)(int16_t)b ? (uint32_t)imm : tgt; break;
+            case TW_OP_JNEI: tgt = ra != (int64_t)(int16_t)b ? (uint32_t)imm : tgt; break;
+            case TW_OP_NOW: wr = true; wv = now; break;
+            case TW_OP_NODE: wr = true; wv = th.w1; break;
+            case TW_OP_NLOAD: {
+                const uint32_t node = me ? th.w1 : 0u;  // sanitised address for idle lanes
+                wr = true;
+                wv = gp(c.nvars)[nix(node, b & 3)];
+                break;
+            }
+            case TW_OP_NSTORE:
+                if (me) gp(c.nvars)[nix(th.w1, b & 3)] = ra;
+                break;
             case TW_OP_NLOADX:
             case TW_OP_NSTOREX: {
-                uint64_t node = (uint64_t)getr(th, (b >> 8) & 3);
-                if (LP ? node != th.w1 : node >= c.N) { fail(TW_REP_ERR_INSN); act = STOP; break; }
-                int64_t GAS* v = &gp(c.nvars)[nix((uint32_t)node, b & 3)];
-                if (op == TW_OP_NLOADX) setr(th, a, *v);
-                else *v = getr(th, a);
+                const uint64_t node = (uint64_t)rf[((b >> 8) & 3u) * TW_WG];
+                const bool bad = LP ? node != th.w1 : node >= c.N;
+                pfail(me && bad, TW_REP_ERR_INSN);
+                tc = bad ? T_STOP : T_NONE;
+                const bool ok = me && !bad;
+                int64_t GAS* v = &gp(c.nvars)[nix(ok ? (uint32_t)node : 0u, b & 3)];
+                if (op == TW_OP_NLOADX) {
+                    wr = true; wm = ok; wv = *v;
+                } else if (ok) {
+                    *v = ra;
+                }
                 break;
             }
-            case TW_OP_LINK: setr(th, a, (int64_t)gp(c.out_off)[th.w1] + imm); break;
+            case TW_OP_LINK: {
+                const uint32_t node = me ? th.w1 : 0u;
+                wr = true;
+                wv = (int64_t)gp(c.out_off)[node] + imm;
+                break;
+            }
             case TW_OP_RLINK: {
-                uint64_t l = (uint64_t)getr(th, b & 3);
-                if (l >= c.L) { fail(TW_REP_ERR_INSN); act = STOP; break; }
-                setr(th, a, (int64_t)gp(c.link_rev)[l]);
+                const uint64_t l = (uint64_t)rb;
+                const bool bad = l >= c.L;
+                pfail(me && bad, TW_REP_ERR_INSN);
+                tc = bad ? T_STOP : T_NONE;
+                wr = true; wm = me && !bad;
+                wv = (int64_t)gp(c.link_rev)[wm ? l : 0];
                 break;
             }
-            case TW_OP_SEND: {  // schedule (after d) (deliver ..) unless the link drops it
-                uint64_t link = (uint64_t)getr(th, a);
-                if (link >= c.L) { fail(TW_REP_ERR_INSN); act = STOP; break; }
-                uint32_t kind = b & 0xFFu;
-                int64_t payload = getr(th, (b >> 8) & 3);
-                uint32_t ord = gp(c.link_ord)[lix(link)];
-                gp(c.link_ord)[lix(link)] = ord + 1;
-                uint32_t e = c.link_table ? gp(c.link_table)[tix(link, ord)] : 0u;
-                if (e & TW_LINK_DROP) {
-                    ++d_dr;
-                    hash(th.w1, TW_KIND_DROP | kind, payload);
-                    break;
+            case TW_OP_SEND:  // schedule (after d) (deliver ..) unless the link drops it
+                if (me) {
+                    const uint64_t link = (uint64_t)ra;
+                    if (link >= c.L) {
+                        fail(TW_REP_ERR_INSN);
+                        tc = T_STOP;
+                    } else {
+                        const uint32_t kind = b & 0xFFu;
+                        const int64_t payload = rf[((b >> 8) & 3u) * TW_WG];
+                        const uint32_t ord = gp(c.link_ord)[lix(link)];
+                        gp(c.link_ord)[lix(link)] = ord + 1;
+                        const uint32_t e = c.link_table ? gp(c.link_table)[tix(link, ord)] : 0u;
+                        if (e & TW_LINK_DROP) {
+                            cinc(CW_DR);
+                            hash(th.w1, TW_KIND_DROP | kind, payload);
+                        } else if (LP) {
+                            // the deliverer `schedule (after d) deliver` is accounted here (start pop
+                            // at now, wake pop at now+d, both at this node) and its delivery travels
+                            // as a record: the receiver checks its binding at now+d
+                            const int64_t dly = (int64_t)(e & 0x7FFFFFFFu);
+                            if (dly < c.lookahead) {
+                                fail(TW_REP_ERR_INSN);
+                                tc = T_STOP;
+                            } else {
+                                const int64_t ta = now + dly;
+                                hash_add(th.w1, term0(now, TW_KIND_RESUME | TW_PC_DELIVER_STUB) +
+                                                    term0(ta, TW_KIND_RESUME | (TW_PC_DELIVER_STUB + 1)));
+                                d_ev += 2;
+                                cinc(CW_TH);
+                                final_t = ta > final_t ? ta : final_t;
+                                emit(ta, payload, (uint32_t)link, kind, th.w1, gp(c.link_dst)[link]);
+                                yt = now + 1;
+                                tc = T_YIELD;
+                            }
+                        } else {
+                            cs(CW_CPC, TW_PC_DELIVER_STUB); cs(CW_CNODE, th.w1); cs(CW_CRA, 4); cs(CW_CDEL, 0);
+                            cs64(CW_Q0, CW_Q0 + 1, payload); cs64(CW_Q0 + 2, CW_Q0 + 3, (int64_t)link);
+                            cs64(CW_Q0 + 4, CW_Q0 + 5, (int64_t)(e & 0x7FFFFFFFu)); cs64(CW_Q0 + 6, CW_Q7, (int64_t)kind);
+                            tc = T_SPAWN;
+                        }
+                    }
                 }
-                if (LP) {
-                    // the deliverer `schedule (after d) deliver` is accounted here (start pop
-                    // at now, wake pop at now+d, both at this node) and its delivery travels
-                    // as a record: the receiver checks its binding at now+d
-                    int64_t dly = (int64_t)(e & 0x7FFFFFFFu);
-                    if (dly < c.lookahead) { fail(TW_REP_ERR_INSN); act = STOP; break; }
-                    int64_t ta = now + dly;
-                    hash_add(th.w1, term0(now, TW_KIND_RESUME | TW_PC_DELIVER_STUB) +
-                                        term0(ta, TW_KIND_RESUME | (TW_PC_DELIVER_STUB + 1)));
-                    d_ev += 2;
-                    ++d_th;
-                    final_t = ta > final_t ? ta : final_t;
-                    emit(ta, payload, (uint32_t)link, kind, th.w1, gp(c.link_dst)[link]);
-                    yt = now + 1;
-                    act = YIELD;
-                    break;
+                break;
+            case TW_OP_DELIVER:  // listener dispatch, ForkStrategy fork_ (MonadDialog.hs:232-256,317)
+                if (me) {
+                    const int64_t r0 = rf[0], r1 = rf[TW_WG], r2 = rf[2 * TW_WG], r3 = rf[3 * TW_WG];
+                    const uint64_t link = (uint64_t)r1;
+                    const uint32_t kind = (uint32_t)r3;
+                    const uint32_t dst = gp(c.link_dst)[link];
+                    const uint32_t set = gp(c.bind)[bix(dst)];
+                    uint32_t lpc = TW_PC_NONE;
+                    if (set && kind < c.n_kinds) lpc = gp(c.lpc)[(size_t)(set - 1) * c.n_kinds + kind];
+                    if (lpc == TW_PC_NONE) {
+                        cinc(CW_UD);
+                        hash(dst, TW_KIND_UNDELIV | kind, r0);
+                        if (LP) tc = T_EXIT;  // the phantom deliverer ends here
+                    } else {
+                        cinc(CW_DL);
+                        hash(dst, TW_KIND_RECV | kind, r0);
+                        cs(CW_CPC, lpc); cs(CW_CNODE, dst); cs(CW_CRA, 4); cs(CW_CDEL, LP ? 1u : 0u);
+                        cs64(CW_Q0, CW_Q0 + 1, r0); cs64(CW_Q0 + 2, CW_Q0 + 3, (int64_t)link);
+                        cs64(CW_Q0 + 4, CW_Q0 + 5, LP ? r2 : (int64_t)th.w1); cs64(CW_Q0 + 6, CW_Q7, (int64_t)kind);
+                        tc = T_SPAWN;
+                    }
                 }
-                cpc = TW_PC_DELIVER_STUB; cnode = th.w1;
-                q0 = payload; q1 = (int64_t)link; q2 = (int64_t)(e & 0x7FFFFFFFu); q3 = (int64_t)kind;
-                act = SPAWN;
+                break;
+            case TW_OP_LISTEN: {
+                const bool bad = (uint32_t)imm >= c.n_sets;
+                pfail(me && bad, TW_REP_ERR_INSN);
+                tc = bad ? T_STOP : T_NONE;
+                if (me && !bad) {
+                    gp(c.bind)[bix(th.w1)] = (uint32_t)imm + 1;
+                    gp(c.bind_own)[bix(th.w1)] = b ? th.w2 : 0xFFFFFFFFu;
+                }
+                th.w0 = (me && !bad && b) ? th.w0 | (F_OWNS << 18) : th.w0;
                 break;
             }
-            case TW_OP_DELIVER: {  // listener dispatch, ForkStrategy fork_ (MonadDialog.hs:232-256,317)
-                uint64_t link = (uint64_t)th.r1;
-                uint32_t kind = (uint32_t)th.r3;
-                uint32_t dst = gp(c.link_dst)[link];
-                uint32_t set = gp(c.bind)[bix(dst)];
-                uint32_t lpc = TW_PC_NONE;
-                if (set && kind < c.n_kinds) lpc = gp(c.lpc)[(size_t)(set - 1) * c.n_kinds + kind];
-                if (lpc == TW_PC_NONE) {
-                    ++d_ud;
-                    hash(dst, TW_KIND_UNDELIV | kind, th.r0);
-                    if (LP) act = EXIT;  // the phantom deliverer ends here
-                    break;
-                }
-                ++d_dl;
-                hash(dst, TW_KIND_RECV | kind, th.r0);
-                cpc = lpc; cnode = dst;
-                q0 = th.r0; q1 = (int64_t)link; q2 = LP ? th.r2 : (int64_t)th.w1; q3 = (int64_t)kind;
-                act = SPAWN;
-                break;
-            }
-            case TW_OP_LISTEN:
-                if ((uint32_t)imm >= c.n_sets) { fail(TW_REP_ERR_INSN); act = STOP; break; }
-                gp(c.bind)[bix(th.w1)] = (uint32_t)imm + 1;
-                gp(c.bind_own)[bix(th.w1)] = b ? th.w2 : 0xFFFFFFFFu;
-                if (b) th_or_flags(th, F_OWNS);
-                break;
             case TW_OP_UNLISTEN:
-                gp(c.bind)[bix(th.w1)] = 0;
-                gp(c.bind_own)[bix(th.w1)] = 0xFFFFFFFFu;
-                break;
-            case TW_OP_TRACE: hash(th.w1, TW_KIND_TRACE | ((uint32_t)imm & 0xFFFFu), getr(th, a)); break;
-            case TW_OP_TMO_BEGIN: {  // schedule (after t) watchdog (TimedT.hs:373-375)
-                if (tmo_ctr >= c.T) { fail(TW_REP_ERR_INSN); act = STOP; break; }
-                uint32_t e = tmo_ctr++;
-                gp(c.tmo_done)[ix(e)] = 0;
-                setr(th, a, e);
-                cpc = TW_PC_WATCHDOG_STUB; cnode = th.w1;
-                q0 = (int64_t)(((uint64_t)th.w2 << 32) | slot); q1 = (int64_t)e; q2 = K[imm]; q3 = 0;
-                act = SPAWN;
-                break;
-            }
-            case TW_OP_TMO_PUSH: {
-                uint32_t nf = th_nfr(th);
-                if (nf >= TW_MAX_FRAMES) { fail(TW_REP_ERR_FRAMES); act = STOP; break; }
-                setf(th, nf, (uint32_t)getr(th, a) & 0xFFFFu);
-                th_set_nfr(th, nf + 1);
-                break;
-            }
-            case TW_OP_TMO_END: {
-                uint32_t nf = th_nfr(th);
-                if (nf == 0 || (getf(th, nf - 1) >> 16) != 0) { fail(TW_REP_ERR_INSN); act = STOP; break; }
-                uint32_t ep = getf(th, nf - 1) & 0xFFFFu;
-                th_set_nfr(th, nf - 1);
-                if (ep < c.T) gp(c.tmo_done)[ix(ep)] = 1;
-                break;
-            }
-            case TW_OP_TMO_FIRE: {
-                uint64_t e = (uint64_t)th.r1;
-                if (e < c.T && !gp(c.tmo_done)[ix(e)]) {
-                    tref = th.r0; tcode = TW_EXC_TIMEOUT; tval = 0;
-                    act = THROWTO;
+                if (me) {
+                    gp(c.bind)[bix(th.w1)] = 0;
+                    gp(c.bind_own)[bix(th.w1)] = 0xFFFFFFFFu;
                 }
+                break;
+            case TW_OP_TRACE:  // th.w1 is the popped thread's node: the term joins hacc
+                hacc += me ? term(now, TW_KIND_TRACE | ((uint32_t)imm & 0xFFFFu), ra) : 0ull;
+                break;
+            case TW_OP_TMO_BEGIN:  // schedule (after t) watchdog (TimedT.hs:373-375)
+                if (me) {
+                    const uint32_t tmo = cg(CW_TMO);
+                    if (tmo >= c.T) {
+                        fail(TW_REP_ERR_INSN);
+                        tc = T_STOP;
+                    } else {
+                        cs(CW_TMO, tmo + 1);
+                        gp(c.tmo_done)[ix(tmo)] = 0;
+                        rf[a * TW_WG] = tmo;
+                        cs(CW_CPC, TW_PC_WATCHDOG_STUB); cs(CW_CNODE, th.w1); cs(CW_CRA, 4); cs(CW_CDEL, 0);
+                        cs64(CW_Q0, CW_Q0 + 1, (int64_t)(((uint64_t)th.w2 << 32) | slot));
+                        cs64(CW_Q0 + 2, CW_Q0 + 3, (int64_t)tmo);
+                        cs64(CW_Q0 + 4, CW_Q0 + 5, K[imm]); cs64(CW_Q0 + 6, CW_Q7, 0);
+                        tc = T_SPAWN;
+                    }
+                }
+                break;
+            case TW_OP_TMO_END:
+                if (me) {
+                    const uint32_t nf = th_nfr(th);
+                    if (nf == 0 || (getf(th, nf - 1) >> 16) != 0) {
+                        fail(TW_REP_ERR_INSN);
+                        tc = T_STOP;
+                    } else {
+                        const uint32_t ep = getf(th, nf - 1) & 0xFFFFu;
+                        th_set_nfr(th, nf - 1);
+                        if (ep < c.T) gp(c.tmo_done)[ix(ep)] = 1;
+                    }
+                }
+                break;
+            case TW_OP_TMO_FIRE: {
+                const uint64_t e = (uint64_t)rf[TW_WG];
+                const bool ok = me && e < c.T;
+                thr_any = true;
+                thr = ok && !gp(c.tmo_done)[ix(ok ? e : 0)];
+                tref = rf[0]; tcode = TW_EXC_TIMEOUT; tval = 0;
                 break;
             }
             default:
-                fail(TW_REP_ERR_INSN);
-                act = STOP;
+                pfail(me, TW_REP_ERR_INSN);
+                tc = T_STOP;
                 break;
             }
-            th_set_pc(th, npc);
-#ifdef TW_PROF_LITE
-            q1t = __builtin_amdgcn_s_memtime();
-            LITE_ACCM(6, q1t - q0t);
-            q0t = q1t;
-#endif
-            if (act == EXIT) {
-                LITE_WRAP(12, die(th, slot));
-                return;
+            if (wr) rf[a * TW_WG] = wm ? wv : ra;
+            if (thr_any) {
+                if (thr) throw_to(th, slot, tref, tcode, tval);
             }
-            if (act == THROWTO) {
-                LITE_WRAP(11, throw_to(th, slot, tref, tcode, tval));
-                act = GO;
-            }
-            if (act == SPAWN) {  // fork (TimedT.hs:326-342): child at now, parent waits 1 µs
-                int64_t ref;
-                bool ok;
-                LITE_WRAP(9, ok = spawn(cpc, cnode, q0, q1, q2, q3, ref));
-                if (!ok) break;
-                if (op == TW_OP_FORK) setr(th, a, ref);
-                if (LP && op == TW_OP_DELIVER) {
+            // per-lane epilogue of the pass
+            pc = me ? tgt : pc;
+            pfail(capped, TW_REP_ERR_INSN);
+            const bool oob = tc == T_NONE && pc >= c.n_insns;
+            pfail(me && oob, TW_REP_ERR_INSN);
+            tc = capped ? (uint32_t)T_STOP : tc;
+            tc = (tc == T_NONE && (status != TW_REP_RUNNING || oob)) ? (uint32_t)T_STOP : tc;
+            fin = at ? tc : fin;
+            running = running && !(at && tc != T_NONE);
+        }
+        if (!run) return;
+        th_set_pc(th, pc);
+        // fork (TimedT.hs:326-342): the child is queued at now, then the parent waits 1 µs
+        if (fin == T_SPAWN) {
+            const uint32_t cdel = cg(CW_CDEL), cra = cg(CW_CRA);
+            int64_t ref;
+            bool ok;
+            if (cdel & 2u) ok = spawn(cg(CW_CPC), cg(CW_CNODE), rf[0], rf[TW_WG], rf[2 * TW_WG], rf[3 * TW_WG], ref);
+            else ok = spawn(cg(CW_CPC), cg(CW_CNODE), cg64(CW_Q0, CW_Q0 + 1), cg64(CW_Q0 + 2, CW_Q0 + 3),
+                            cg64(CW_Q0 + 4, CW_Q0 + 5), cg64(CW_Q0 + 6, CW_Q7), ref);
+            if (!ok) {
+                fin = T_STOP;
+            } else {
+                if (cra < 4) rf[cra * TW_WG] = ref;
+                if (LP && (cdel & 1u)) {
                     // the deliverer's resume pop (at now+1, on the sending node), then it ends
-                    hash_add((uint32_t)th.r2, term0(now + 1, TW_KIND_RESUME | (TW_PC_DELIVER_STUB + 2)));
+                    hash_add((uint32_t)rf[2 * TW_WG], term0(now + 1, TW_KIND_RESUME | (TW_PC_DELIVER_STUB + 2)));
                     ++d_ev;
                     final_t = now + 1 > final_t ? now + 1 : final_t;
-                    die(th, slot);
-                    return;
+                    fin = T_EXIT;
+                } else {
+                    yt = now + 1;
+                    fin = T_YIELD;
                 }
-                yt = now + 1;
-                act = YIELD;
             }
-            if (act == YIELD) {
-                LITE_WRAP(10, mode = enqueue(th, slot, yt) ? ST_CACHE : ST_THROUGH);
-                break;
-            }
-#ifdef TW_PROF_LITE
-            q1t = __builtin_amdgcn_s_memtime();
-            LITE_ACCM(7, q1t - q0t);
-            q0t = q1t;
-#endif
-            if (act == STOP || status != TW_REP_RUNNING) break;
-            if (npc >= c.n_insns) { fail(TW_REP_ERR_INSN); break; }
-            if (npc == pc + 1) in = nx;
-            else in = P[npc];
-            pc = npc;
         }
-#ifdef TW_PROF_LITE
-        q1t = __builtin_amdgcn_s_memtime();
-        LITE_ACCM(7, q1t - q0t);
-#endif
-        store_rec(slot, th, mode);
-        LITE_ACCM(8, __builtin_amdgcn_s_memtime() - q1t);
+        if (fin == T_YIELD) {
+            enqueue(th, slot, yt);
+            put_running(slot, th);
+        } else if (fin == T_EXIT) {
+            die(th, slot);
+        } else if (fin == T_STOP) {
+            put_running(slot, th);
+        }
     }
 };
 
@@ -1034,21 +1114,22 @@ __global__ void __launch_bounds__(TW_WG) tw_init_kernel(Dev c, uint32_t main_pc,
         for (uint32_t n = 0; n < c.N; ++n) gp(c.bind)[(size_t)n * c.R + r] = listen_init[n];
 }
 
-// LDS per workgroup: near heap keys + slots, the record cache, then the program
-// image and constant pool, so instruction fetch and time constants never
-// leave the CU.
+// LDS per workgroup: near heap keys + slots, the running threads' register
+// files, the cold words, then the program image and constant pool, so
+// instruction fetch and time constants never leave the CU.
 __host__ __device__ constexpr size_t fixed_lds_bytes() {
-    return (size_t)TW_NEAR_CAP * TW_WG * 12 + (size_t)TW_RC * 4 * TW_WG * 16;
+    return (size_t)TW_NEAR_CAP * TW_WG * 12 + (size_t)4 * TW_WG * 8 + (size_t)CW_COUNT * TW_WG * 4;
 }
 
 template <bool LP>
 __global__ void __launch_bounds__(TW_WG) __attribute__((amdgpu_waves_per_eu(1, 2)))
 tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
     extern __shared__ __attribute__((aligned(16))) uint64_t lds_raw[];
-    uint4 LAS* s_rc = (uint4 LAS*)lds_raw;
-    uint64_t LAS* s_k = (uint64_t LAS*)(s_rc + TW_RC * 4 * TW_WG);
-    uint32_t LAS* s_s = (uint32_t LAS*)(s_k + TW_NEAR_CAP * TW_WG);
-    uint2 LAS* s_p = (uint2 LAS*)(s_s + TW_NEAR_CAP * TW_WG);
+    uint64_t LAS* s_k = (uint64_t LAS*)lds_raw;
+    int64_t LAS* s_rf = (int64_t LAS*)(s_k + TW_NEAR_CAP * TW_WG);
+    uint32_t LAS* s_s = (uint32_t LAS*)(s_rf + 4 * TW_WG);
+    uint32_t LAS* s_cw = s_s + TW_NEAR_CAP * TW_WG;
+    uint2 LAS* s_p = (uint2 LAS*)(s_cw + CW_COUNT * TW_WG);
     int64_t LAS* s_c = (int64_t LAS*)(s_p + c.n_insns + 1);
     {
         for (uint32_t i = threadIdx.x; i <= c.n_insns; i += TW_WG) s_p[i] = gp(c.insns)[i];
@@ -1066,42 +1147,45 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
     L.r = r;
     L.nk = s_k + threadIdx.x;
     L.ns = s_s + threadIdx.x;
-    L.rcd = s_rc + threadIdx.x;
+    L.rf = s_rf + threadIdx.x;
+    L.cw = s_cw + threadIdx.x;
     L.P = s_p;
     L.K = s_c;
-    L.ctag.fill(0xFFFFFFFFu);
-    L.cst.fill(0);
-    L.cdirty = 0;
-    L.clk = 0;
+    L.pf_slot = 0xFFFFFFFFu;
+    L.prun = -1;
+    L.hacc = 0;
+    L.hnode = 0xFFFFFFFFu;
     L.now = (int64_t)sc[SC_NOW * R]; L.final_t = (int64_t)sc[SC_FINAL_T * R];
     L.seq = (uint32_t)sc[SC_SEQ * R]; L.tidc = (uint32_t)sc[SC_TIDC * R]; L.live = (uint32_t)sc[SC_LIVE * R];
     const uint32_t near_n0 = (uint32_t)sc[SC_NEAR_N * R];
     L.far_n = (uint32_t)sc[SC_FAR_N * R];
-    L.status = (uint32_t)sc[SC_STATUS * R]; L.main_exc = (uint32_t)sc[SC_MAIN_EXC * R];
+    L.status = (uint32_t)sc[SC_STATUS * R];
     L.free_n = (uint32_t)sc[SC_FREE_N * R]; L.ftop = (uint32_t)sc[SC_FTOP * R]; L.bump = (uint32_t)sc[SC_BUMP * R];
-    L.tmo_ctr = (uint32_t)sc[SC_TMO_CTR * R];
+    for (int w = 0; w < CW_COUNT; ++w) L.cs(w, 0);
+    L.cs(CW_MAINEXC, (uint32_t)sc[SC_MAIN_EXC * R]);
+    L.cs(CW_TMO, (uint32_t)sc[SC_TMO_CTR * R]);
     const uint64_t events0 = sc[SC_EVENTS * R];
     const uint64_t ev_room64 = max_events > events0 ? max_events - events0 : 0;
     const uint32_t ev_room = ev_room64 > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)ev_room64;
-    L.d_ev = L.d_dl = L.d_dr = L.d_ud = L.d_th = 0;
-    L.ft = 0; L.fs = 0; L.fsl = 0;
-    if (L.far_n) {
-        uint4 e = L.far_ld(0);
-        L.ft = ent_t(e); L.fs = e.w; L.fsl = e.z;
-    }
+    L.d_ev = 0;
+    if (L.far_n) L.set_ftop(L.far_ld(0));
 #pragma unroll
     for (int j = 0; j < TW_RUNS; ++j) {
-        L.rh[j] = (uint32_t)sc[(SC_RH0 + j) * R];
-        L.rn[j] = (uint32_t)sc[(SC_RC0 + j) * R];
-        L.rt[j] = L.ut[j] = 0;
-        L.rs[j] = L.us[j] = L.rsl[j] = 0;
-        if (L.rn[j]) {
-            uint4 h = *L.run_at(j, L.rh[j]);
-            uint32_t tp = L.rh[j] + L.rn[j] - 1;
+        const uint32_t rh = (uint32_t)sc[(SC_RH0 + j) * R], rn = (uint32_t)sc[(SC_RC0 + j) * R];
+        L.cs(CW_RH + j, rh);
+        L.cs(CW_RN + j, rn);
+        if (rn) {
+            uint4 h = *L.run_at(j, rh);
+            uint32_t tp = rh + rn - 1;
             if (tp >= c.Cr) tp -= c.Cr;
             uint4 u = *L.run_at(j, tp);
-            L.rt[j] = ent_t(h); L.rs[j] = h.w; L.rsl[j] = h.z;
-            L.ut[j] = ent_t(u); L.us[j] = u.w;
+            L.cs(CW_RTL + j, h.x); L.cs(CW_RTH + j, h.y); L.cs(CW_RS + j, h.w); L.cs(CW_RSL + j, h.z);
+            L.cs(CW_UTL + j, u.x); L.cs(CW_UTH + j, u.y); L.cs(CW_US + j, u.w);
+            if (rn >= 2) {
+                uint32_t p2 = rh + 1 == c.Cr ? 0 : rh + 1;
+                uint4 s2 = *L.run_at(j, p2);
+                L.cs(CW_R2TL + j, s2.x); L.cs(CW_R2TH + j, s2.y); L.cs(CW_R2S + j, s2.w); L.cs(CW_R2SL + j, s2.z);
+            }
         }
     }
     L.far_min();
@@ -1159,125 +1243,121 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
             ph.r1 = bb.x;                                     // link
             ph.r2 = bb.z;                                     // sending node
             ph.r3 = bb.y;                                     // kind
-            bool on_chip = L.enqueue(ph, s, ta);
-            L.store_rec(s, ph, on_chip ? ST_CACHE : ST_THROUGH);
+            L.enqueue(ph, s, ta);
+            L.put_rec(s, ph);
         }
         gp(c.inbox_n)[r] = 0;
     }
 
-#ifdef TW_PROF_LITE
-#pragma unroll
-    for (int i = 0; i < 16; ++i) L.lite[i] = 0;
-    LITE_T(lk0);
+#ifdef TW_STATS
+    for (int i = 0; i < P_COUNT; ++i) L.st[i] = 0;
 #endif
     uint32_t pending_main = (uint32_t)sc[SC_PENDING_MAIN * R];
+    // The loop is wave-uniform: a lane that stops (quiescence, t_end, event
+    // cap, error) just idles through the remaining iterations, so no per-lane
+    // break/continue splits the wave's control flow.
+    bool alive = L.status == TW_REP_RUNNING;
     for (uint32_t it = 0; it < budget; ++it) {
-        if (L.status != TW_REP_RUNNING) break;
-        LITE_T(l0);
-#ifdef TW_PROF_LITE
-        uint64_t l1 = l0;
-        LITE_ACC(4, 1);
-#endif
+        if (!__builtin_amdgcn_ballot_w64(alive)) break;
         Th th;
-        uint32_t slot;
+        uint32_t slot = 0;
         bool run = false;
-        if (pending_main) {  // runInSandbox main (TimedT.hs:237): runs at t=0, not a pop
-            pending_main = 0;
-            slot = 0;
-            L.load_rec(0, th);
-            run = true;
-        } else {
-            if (L.live == 0) {  // whileM_ notDone
-                if (!LP) L.status = TW_REP_DONE;  // an LP may still receive records
-                break;
-            }
-            if (L.d_ev >= ev_room) break;
-            // PQ.minView: the min of the near root and the far sources
-            if (L.far_dirty) L.far_min();
-            bool use_near = L.near_n != 0;
-            int64_t t = 0;
-            uint32_t sq = 0;
-            if (use_near) { t = L.nbase + (int64_t)(L.nrk >> 32); sq = (uint32_t)L.nrk; slot = L.nrs; }
-            if (L.fsrc >= 0 && (!use_near || tless(L.fmt, L.fms, t, sq))) {
-                use_near = false;
-                t = L.fmt; sq = L.fms; slot = L.fmsl;
-            } else if (!use_near) {
-                break;  // nothing queued (cannot happen while live > 0)
-            }
-            if (t > t_end) break;
-#ifdef TW_PROF_LITE
-            LITE_ACC(13, __builtin_amdgcn_s_memtime() - l0);
-#endif
-            KLITE_WRAP(14, L.load_rec(slot, th));  // issued first: its latency overlaps the queue maintenance
-            KLITE_WRAP(15, if (use_near) L.near_pop(); else if (L.fsrc == TW_RUNS) L.far_pop(); else L.run_pop(L.fsrc));
-#ifdef TW_PROF_LITE
-            l1 = __builtin_amdgcn_s_memtime();
-            LITE_ACC(0, l1 - l0);
-#endif
-            if (th.w3 != sq) continue;  // superseded by a throwTo re-stamp
-            LITE_ACC(5, 1);
-            // curTime .= timestamp (TimedT.hs:241-247)
-            th.w3 = 0;
-            --L.live;
-            L.now = t;
-            if (t - L.nbase > (int64_t)0x7FFFFFFF) L.near_rebase(t);
-            // LP phantom = the deliverer's wake, already counted and hashed by the sender
-            const bool phantom = LP && (th_flags(th) & F_PHANTOM);
-            if (!phantom) {
-                L.final_t = LP ? (t > L.final_t ? t : L.final_t) : t;
-                ++L.d_ev;
-            }
-            uint32_t exc = th_exc(th);  // asyncExceptions . at tid <<.= Nothing (:252)
-            if (exc) {
-                int64_t val = (int64_t)(int32_t)th.w7;
-                th_set_exc(th, 0);
-                th.w7 = 0;
-                L.hash_add(th.w1, term0(t, TW_KIND_EXC | exc));
-                if (!(th_flags(th) & (F_STARTED | F_MAIN))) {  // escapes launchTimedT (:252-263)
-                    L.status = TW_REP_ABORTED;
-                    L.main_exc = exc;
-                    L.store_rec(slot, th, ST_THROUGH);
-                    break;
-                }
-                run = L.unwind(th, slot, exc, val);
-            } else {
-                if (!phantom) L.hash_add(th.w1, term0(t, TW_KIND_RESUME | th_pc(th)));
+        if (alive) {
+            if (pending_main) {  // runInSandbox main (TimedT.hs:237): runs at t=0, not a pop
+                pending_main = 0;
+                L.peek_rec(0, th);
+                L.rf[0] = th.r0; L.rf[TW_WG] = th.r1; L.rf[2 * TW_WG] = th.r2; L.rf[3 * TW_WG] = th.r3;
+                L.hnode = th.w1;
                 run = true;
+            } else if (L.live == 0) {  // whileM_ notDone
+                if (!LP) L.status = TW_REP_DONE;  // an LP may still receive records
+                alive = false;
+            } else if (L.d_ev >= ev_room) {
+                alive = false;
+            } else {
+                // PQ.minView: the min of the near root and the far sources
+                if (L.far_dirty) L.far_min();
+                bool use_near = L.near_n != 0;
+                int64_t t = 0;
+                uint32_t sq = 0;
+                if (use_near) { t = L.nbase + (int64_t)(L.nrk >> 32); sq = (uint32_t)L.nrk; slot = L.nrs; }
+                const bool use_far = L.fsrc >= 0 && (!use_near || tless(L.fmt, L.fms, t, sq));
+                if (use_far) { t = L.fmt; sq = L.fms; slot = L.fmsl; }
+                if ((!use_near && !use_far) || t > t_end) {
+                    alive = false;  // parked beyond t_end (an empty queue cannot happen while live > 0)
+                } else {
+                    L.peek_rec(slot, th);  // prefetched copy or HBM
+                    if (!use_far) L.near_pop();
+                    else if (L.fsrc == TW_RUNS) L.far_pop();
+                    else L.run_pop(L.fsrc);
+                    if (slot == L.pf_slot) L.pf_slot = 0xFFFFFFFFu;
+                    if (th.w3 != sq) {
+                        STATL(K_SUPERSEDED);  // superseded by a throwTo re-stamp
+                    } else {
+                        STATL(K_POP);
+                        // curTime .= timestamp (TimedT.hs:241-247)
+                        th.w3 = 0;
+                        --L.live;
+                        L.now = t;
+                        if (t - L.nbase > (int64_t)0x7FFFFFFF) L.near_rebase(t);
+                        L.prefetch_next(slot);
+                        L.hnode = th.w1;
+                        L.rf[0] = th.r0; L.rf[TW_WG] = th.r1; L.rf[2 * TW_WG] = th.r2; L.rf[3 * TW_WG] = th.r3;
+                        // LP phantom = the deliverer's wake, already counted and hashed by the sender
+                        const bool phantom = LP && (th_flags(th) & F_PHANTOM);
+                        if (!phantom) {
+                            L.final_t = LP ? (t > L.final_t ? t : L.final_t) : t;
+                            ++L.d_ev;
+                        }
+                        const uint32_t exc = th_exc(th);  // asyncExceptions . at tid <<.= Nothing (:252)
+                        if (exc) {
+                            const int64_t val = (int64_t)(int32_t)th.w7;
+                            th_set_exc(th, 0);
+                            th.w7 = 0;
+                            L.hacc += term0(t, TW_KIND_EXC | exc);
+                            if (!(th_flags(th) & (F_STARTED | F_MAIN))) {  // escapes launchTimedT (:252-263)
+                                L.status = TW_REP_ABORTED;
+                                L.cs(CW_MAINEXC, exc);
+                                L.put_rec(slot, th);
+                            } else {
+                                run = L.unwind(th, slot, exc, val);
+                            }
+                        } else {
+                            if (!phantom) L.hacc += term0(t, TW_KIND_RESUME | th_pc(th));
+                            run = true;
+                        }
+                    }
+                }
             }
         }
-#ifdef TW_PROF_LITE
-        LITE_T(l2);
-        LITE_ACC(1, l2 - l1);
-#endif
-        if (run) L.step(th, slot);
-#ifdef TW_PROF_LITE
-        LITE_ACC(2, __builtin_amdgcn_s_memtime() - l2);
-#endif
+        L.step(th, slot, run);
+        L.hash_flush();
+        alive = alive && L.status == TW_REP_RUNNING;
     }
-#ifdef TW_PROF_LITE
-    LITE_ACC(3, __builtin_amdgcn_s_memtime() - lk0);
+    L.hash_flush();
+    L.run_commit();
+#ifdef TW_STATS
     if (c.prof)
-        for (int i = 0; i < 16; ++i)
-            __hip_atomic_fetch_add(gp(c.prof) + i, (unsigned long long)L.lite[i], __ATOMIC_RELAXED,
+        for (int i = 0; i < P_COUNT; ++i)
+            __hip_atomic_fetch_add(gp(c.prof) + i, (unsigned long long)L.st[i], __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_AGENT);
 #endif
-    L.flush_cache();
     sc[SC_PENDING_MAIN * R] = pending_main;
     if (!LP && L.status == TW_REP_RUNNING && L.live == 0) L.status = TW_REP_DONE;
 
     sc[SC_NOW * R] = (uint64_t)L.now; sc[SC_FINAL_T * R] = (uint64_t)L.final_t;
     sc[SC_SEQ * R] = L.seq; sc[SC_TIDC * R] = L.tidc; sc[SC_LIVE * R] = L.live;
     sc[SC_NEAR_N * R] = L.near_n; sc[SC_FAR_N * R] = L.far_n;
-    sc[SC_STATUS * R] = L.status; sc[SC_MAIN_EXC * R] = L.main_exc;
+    sc[SC_STATUS * R] = L.status; sc[SC_MAIN_EXC * R] = L.cg(CW_MAINEXC);
     sc[SC_FREE_N * R] = L.free_n; sc[SC_FTOP * R] = L.ftop; sc[SC_BUMP * R] = L.bump;
-    sc[SC_TMO_CTR * R] = L.tmo_ctr;
+    sc[SC_TMO_CTR * R] = L.cg(CW_TMO);
     sc[SC_EVENTS * R] = events0 + L.d_ev;
-    sc[SC_DELIVERED * R] += L.d_dl; sc[SC_DROPPED * R] += L.d_dr;
-    sc[SC_UNDELIV * R] += L.d_ud; sc[SC_THREADS * R] += L.d_th;
+    sc[SC_DELIVERED * R] += L.cg(CW_DL); sc[SC_DROPPED * R] += L.cg(CW_DR);
+    sc[SC_UNDELIV * R] += L.cg(CW_UD); sc[SC_THREADS * R] += L.cg(CW_TH);
 #pragma unroll
     for (int j = 0; j < TW_RUNS; ++j) {
-        sc[(SC_RH0 + j) * R] = L.rh[j];
-        sc[(SC_RC0 + j) * R] = L.rn[j];
+        sc[(SC_RH0 + j) * R] = L.cg(CW_RH + j);
+        sc[(SC_RC0 + j) * R] = L.cg(CW_RN + j);
     }
     for (uint32_t j = 0; j < L.near_n; ++j) {
         uint64_t k = L.nk[j * TW_WG];
@@ -1509,7 +1589,7 @@ static int load_common(tw_ctx* c, const tw_scenario_desc* s, bool lp, uint32_t l
     ALLOC(d.link_ord, (size_t)(d.L ? d.L : 1) * (lp ? 1 : R));
     ALLOC(d.tmo_done, (size_t)(d.T ? d.T : 1) * R);
     ALLOC(d.n_active, 1);
-#ifdef TW_PROF_LITE
+#ifdef TW_STATS
     ALLOC(d.prof, P_COUNT);
     HIPCHK(hipMemsetAsync(d.prof, 0, 8 * P_COUNT, c->stream));
 #endif
@@ -1814,7 +1894,7 @@ int tw_lp_results(tw_ctx* c, tw_replica_result* agg, uint64_t* node_hashes, size
     return TW_OK;
 }
 
-#ifdef TW_PROF_LITE
+#ifdef TW_STATS
 // Diagnostic build only: copy the P_COUNT counters out, optionally zeroing them.
 int tw_prof_read(tw_ctx* c, unsigned long long* out, size_t cap, int reset) {
     if (!c || !out || !c->loaded || !c->d.prof) return TW_ERR_STATE;

@@ -17,8 +17,9 @@ for s in "$@"; do
     pytest) step pytest_gpu 600 python -u -m pytest tests/ -q -m gpu -x --timeout 120 --timeout-method thread ;;
     smoke)  step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     phase)  step phase 300 python tools/phase_probe.py 65536 4096 ;;
+    micro)  step micro 300 python tools/micro_probe.py 65536 8 ;;
     probe)  step probe 300 env TW_LIB=$PWD/time-warp_amd/lib/libtimewarp_prof.so python tools/kernel_probe.py 65536 4096 ;;
-    lite) step lite 300 env TW_PROBE_LITE=1 TW_LIB=$PWD/time-warp_amd/lib/libtimewarp_lite.so python tools/kernel_probe.py 65536 4096 ;;
+    stats) step stats 300 env TW_LIB=$PWD/time-warp_amd/lib/libtimewarp_stats.so python tools/stats_probe.py 65536 4096 ;;
     probe2) step probe2 300 env TW_LIB=$PWD/time-warp_amd/lib/libtimewarp_prof2.so python tools/kernel_probe.py 65536 4096 ;;
     bench)  step bench 500 python bench.py ;;
     benchq) step benchq 300 python bench.py --steps 2 --no-cpu-baseline ;;

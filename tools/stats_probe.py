@@ -1,0 +1,58 @@
+"""Per-phase event-path counters from the diagnostic build (lib/libtimewarp_stats.so, -DTW_STATS=1).
+
+Runs the config-3 token ring in three phases (start-up t < 1 s, token phase t <
+launchDuration, teardown) and prints, per committed pop, how often each path of
+the event loop ran: record source (LDS pool / prefetched copy / HBM), record
+placement (pool / eviction / HBM / dead header), prefetches issued, hash atomics,
+queue pushes by tier, interpreted instructions.  Also times each phase.
+
+usage: TW_LIB=.../libtimewarp_stats.so python tools/stats_probe.py [replicas] [nodes]
+"""
+import ctypes as C
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+os.environ.setdefault("TW_LIB", os.path.join(ROOT, "time-warp_amd", "lib", "libtimewarp_stats.so"))
+sys.path.insert(0, os.path.join(ROOT, "time-warp_amd"))
+from timewarp import scenarios  # noqa: E402
+from timewarp.engine import Engine  # noqa: E402
+
+NAMES = ["pop", "superseded", "peek_pool", "peek_pf", "peek_hbm", "put_pool", "put_evict", "put_hbm", "put_dead",
+         "pf_issue", "hash_imm", "hash_flush", "near_push", "run_push", "far_push", "insn"]
+
+
+def read(eng):
+    buf = (C.c_ulonglong * 16)()
+    fn = eng.lib.tw_prof_read
+    fn.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]
+    n = fn(eng.ctx, buf, 16, 1)
+    if n < 0:
+        raise RuntimeError(f"tw_prof_read: {n}")
+    return {k: buf[i] for i, k in enumerate(NAMES)}
+
+
+def main():
+    R = int(sys.argv[1]) if len(sys.argv) > 1 else 65536
+    N = int(sys.argv[2]) if len(sys.argv) > 2 else 4096
+    Ld = 120_000_000
+    scn = scenarios.token_ring(n_nodes=N, n_replicas=R, launch_duration=Ld, drop_log2=10)
+    eng = Engine(0).load(scn)
+    if not hasattr(eng.lib, "tw_prof_read"):
+        raise SystemExit("TW_LIB is not the diagnostic build (tw_prof_read missing)")
+    read(eng)
+    eng.reset()
+    for name, t_end in [("startup<1s", 999_999), ("token<L", Ld - 1), ("teardown", (1 << 63) - 1)]:
+        st = eng.run(t_end=t_end)
+        d = read(eng)
+        ms = float(eng.launch_ms().sum())
+        pops = max(d["pop"], 1)
+        rec = {"phase": name, "events": st.events, "kernel_ms": round(ms, 3),
+               "ev_per_s": st.events / max(ms, 1e-9) * 1e3,
+               "per_pop": {k: round(v / pops, 4) for k, v in d.items() if k != "pop"}, "counters": d}
+        print(json.dumps(rec), flush=True)
+
+
+if __name__ == "__main__":
+    main()
