@@ -44,6 +44,7 @@
 #define TW_RUNS 4               // monotone far-queue runs per replica
 #endif
 #define TW_STEP_CAP (1u << 22)  // instructions per thread step (== oracle kStepCap)
+#define TW_TAIL_VMEM 9          // vector-memory ops of every iteration after the record prefetch
 
 // Explicit address spaces: generic (flat) pointers would make every HBM and
 // LDS access a flat_* instruction that waits on both memory counters.
@@ -55,7 +56,7 @@
 #define LAS
 #endif
 
-#define P_COUNT 16
+#define P_COUNT 24
 // Diagnostic build (-DTW_STATS, lib/libtimewarp_stats.so): per-lane event-path
 // counters summed into Dev::prof at kernel end (tools/stats_probe.py).  The
 // product build compiles every STAT to nothing.
@@ -66,8 +67,22 @@
 #define STAT(i) ((void)0)
 #define STATL(i) ((void)0)
 #endif
-enum { K_POP, K_SUPERSEDED, K_PEEK_POOL, K_PEEK_PF, K_PEEK_HBM, K_PUT_POOL, K_PUT_EVICT, K_PUT_HBM, K_PUT_DEAD,
-       K_PF_ISSUE, K_HASH_IMM, K_HASH_FLUSH, K_NEAR_PUSH, K_RUN_PUSH, K_FAR_PUSH, K_INSN };
+enum { K_POP, K_SUPERSEDED, K_PEEK_PF, K_PEEK_HBM, K_PUT_HBM, K_PUT_DEAD, K_PF_ISSUE, K_HASH_IMM, K_HASH_FLUSH,
+       K_NEAR_PUSH, K_RUN_PUSH, K_FAR_PUSH, K_INSN, K_CYC_POP, K_CYC_INTERP, K_CYC_TAIL,
+       K_CYC_SEL, K_CYC_FETCH, K_CYC_QPOP, K_CYC_COMMIT, K_CYC_PF, K_CYC_TERM, K_CYC_STORE, K_CYC_HASH };
+#ifdef TW_STATS
+#define STIME(v) const uint64_t v = __builtin_amdgcn_s_memtime()
+#define STADD(i, v) (st[(i)] += (uint32_t)(v))
+#define STADDL(i, v) (L.st[(i)] += (uint32_t)(v))
+#else
+#define STIME(v) ((void)0)
+#define STADD(i, v) ((void)0)
+#define STADDL(i, v) ((void)0)
+#endif
+
+// m0 is set by the LDS-DMA (global_load_lds) inline asm only; no other code of
+// these kernels uses it.
+#pragma clang diagnostic ignored "-Winline-asm"
 
 namespace {
 
@@ -138,6 +153,7 @@ struct Dev {
     uint4* far;          // [Q][R]  {t_lo, t_hi, slot, seq}
     uint4* runs;         // [TW_RUNS][Cr][R] monotone FIFO runs (ring buffers)
     uint4* near_spill;   // [NEAR_CAP][R]  near heap between launches
+    uint4* dummy;        // [5][R] per-lane sink of the fixed-shape store tail's unused stores
     int64_t* nvars;      // [N*4][R]
     uint64_t* hash;      // [N][R]
     uint32_t* bind;      // [N][R] 0 or set+1
@@ -216,28 +232,28 @@ struct Lane {
     Dev c;  // by value: kernel arguments stay in SGPRs
     uint32_t r;       // replica
     // LDS (lane-offset pointers; element j at [j * TW_WG])
-    uint64_t LAS* nk;     // near heap keys: (t - nbase) << 32 | seq
+    uint64_t LAS* nk;     // near heap keys: (t - nbase) << 32 | seq; a free position holds ~0
     uint32_t LAS* ns;     // near heap slots
     int64_t LAS* rf;      // the running thread's registers r0..r3 during its step
+    uint4 LAS* pfs;       // prefetch staging: quad q of the next pop's record at [q * TW_WG]
+    uint32_t pfs_wave;    // LDS byte address of this wave's staging (quad 0), wave-uniform
     uint32_t LAS* cw;     // cold words [CW_*]
     const uint2 LAS* P;   // program image
     const int64_t LAS* K; // constant pool
-    // near heap
+    // near heap: count, time base, cached root
     uint32_t near_n;
     int64_t nbase;
-    uint64_t nrk;  // cached root key
-    uint32_t nrs;  // cached root slot
+    uint64_t nrk;  // root key (~0 when empty)
+    uint32_t nrs;  // root slot
     // far sources: heap size, and the cached min over the runs and the heap top
     uint32_t far_n;
     bool far_dirty;
     int fsrc;  // -1 none, 0..TW_RUNS-1 run, TW_RUNS heap
     int64_t fmt;
     uint32_t fms, fmsl;
-    // a run's second entry in flight from HBM (committed to LDS at the next run access)
+    // run whose next second entry is in flight into LDS staging quad 4 (-1 none)
     int prun;
-    uint4 pent;
-    // prefetched HBM copy of the next pop's record (pf_slot NONE = invalid)
-    Th pf;
+    // slot whose record the staging holds or is loading (NONE = invalid)
     uint32_t pf_slot;
     // this iteration's hash terms for the popped thread's node, one atomic at the end
     uint64_t hacc;
@@ -280,80 +296,133 @@ struct Lane {
     }
 
     // ---------------------------------------------------------- near heap (LDS)
-    // 4-ary heap of unique 64-bit keys: 16 entries are two levels, the four
-    // children of a node are read together (one LDS round trip per level).
+    // 4-ary min-heap of unique 64-bit keys, TW_NEAR_CAP = 16 positions = root
+    // + two levels; a free position holds ~0, so no read is guarded by the
+    // heap size.  Sift-up and sift-down are straight-line code over both
+    // levels: the reads of a level are issued together, every move is an
+    // unconditional store of a selected value (a "move" onto itself when the
+    // entry stays), and no data-dependent branch is taken -- at one wave per
+    // SIMD each branch and each dependent LDS round trip costs in full.
+    static_assert(TW_NEAR_CAP == 16, "the near heap is root + two 4-ary levels");
     __device__ __forceinline__ uint64_t nkey(int64_t t, uint32_t s) const {
         return ((uint64_t)(t - nbase) << 32) | s;
     }
     __device__ __forceinline__ bool near_fits(int64_t t) const {
         return near_n < TW_NEAR_CAP && t - now < c.horizon && (uint64_t)(t - nbase) < 0xFFFFFFFFull;
     }
-    __device__ __forceinline__ void near_sift_up(uint32_t i, uint64_t k, uint32_t s) {
-        while (i > 0) {
-            uint32_t p = (i - 1) >> 2;
-            uint64_t pk = nk[p * TW_WG];
-            uint32_t ps = ns[p * TW_WG];
-            if (k > pk) break;
-            nk[i * TW_WG] = pk;
-            ns[i * TW_WG] = ps;
-            i = p;
-        }
-        nk[i * TW_WG] = k;
-        ns[i * TW_WG] = s;
-        if (i == 0) { nrk = k; nrs = s; }
+    __device__ __forceinline__ void near_init() {
+#pragma unroll
+        for (int i = 0; i < TW_NEAR_CAP; ++i) nk[i * TW_WG] = ~0ull;
+        near_n = 0;
+        nrk = ~0ull; nrs = 0;
     }
-    __device__ __forceinline__ void near_sift_down(uint32_t i, uint64_t k, uint32_t s) {
-        const uint32_t n = near_n;
-        for (;;) {
-            uint32_t c0 = 4 * i + 1;
-            if (c0 >= n) break;
-            uint64_t k0 = nk[c0 * TW_WG], k1 = ~0ull, k2 = ~0ull, k3 = ~0ull;
-            uint32_t s0 = ns[c0 * TW_WG], s1 = 0, s2 = 0, s3 = 0;
-            if (c0 + 1 < n) { k1 = nk[(c0 + 1) * TW_WG]; s1 = ns[(c0 + 1) * TW_WG]; }
-            if (c0 + 2 < n) { k2 = nk[(c0 + 2) * TW_WG]; s2 = ns[(c0 + 2) * TW_WG]; }
-            if (c0 + 3 < n) { k3 = nk[(c0 + 3) * TW_WG]; s3 = ns[(c0 + 3) * TW_WG]; }
-            uint64_t bk = k0;
-            uint32_t bs = s0, bi = c0;
-            if (k1 < bk) { bk = k1; bs = s1; bi = c0 + 1; }
-            if (k2 < bk) { bk = k2; bs = s2; bi = c0 + 2; }
-            if (k3 < bk) { bk = k3; bs = s3; bi = c0 + 3; }
-            if (k < bk) break;
-            nk[i * TW_WG] = bk;
-            ns[i * TW_WG] = bs;
-            if (i == 0) { nrk = bk; nrs = bs; }
-            i = bi;
-        }
-        nk[i * TW_WG] = k;
-        ns[i * TW_WG] = s;
-        if (i == 0) { nrk = k; nrs = s; }
+    // min of the four children 4p+1..4p+4 of p (positions >= 16 read as ~0)
+    __device__ __forceinline__ void near_kids(uint32_t p, uint64_t& kb, uint32_t& sb, uint32_t& ib) const {
+        const uint32_t c0 = 4 * p + 1;
+        const bool v1 = c0 + 1 < TW_NEAR_CAP, v2 = c0 + 2 < TW_NEAR_CAP, v3 = c0 + 3 < TW_NEAR_CAP;
+        const uint32_t a0 = c0 < TW_NEAR_CAP ? c0 : 0, a1 = v1 ? c0 + 1 : 0, a2 = v2 ? c0 + 2 : 0, a3 = v3 ? c0 + 3 : 0;
+        uint64_t k0 = nk[a0 * TW_WG], k1 = nk[a1 * TW_WG], k2 = nk[a2 * TW_WG], k3 = nk[a3 * TW_WG];
+        const uint32_t s0 = ns[a0 * TW_WG], s1 = ns[a1 * TW_WG], s2 = ns[a2 * TW_WG], s3 = ns[a3 * TW_WG];
+        k0 = c0 < TW_NEAR_CAP ? k0 : ~0ull;
+        k1 = v1 ? k1 : ~0ull; k2 = v2 ? k2 : ~0ull; k3 = v3 ? k3 : ~0ull;
+        const bool m01 = k1 < k0, m23 = k3 < k2;
+        const uint64_t ka = m01 ? k1 : k0, kc = m23 ? k3 : k2;
+        const uint32_t sa = m01 ? s1 : s0, sc = m23 ? s3 : s2;
+        const uint32_t ia = m01 ? c0 + 1 : c0, ic = m23 ? c0 + 3 : c0 + 2;
+        const bool m = kc < ka;
+        kb = m ? kc : ka; sb = m ? sc : sa; ib = m ? ic : ia;
+    }
+    // Place (k, s) at the root hole and sift it down.
+    __device__ __forceinline__ void near_down(uint64_t k, uint32_t s) {
+        uint64_t k1; uint32_t s1, c1;
+        near_kids(0, k1, s1, c1);                // c1 in 1..4
+        const bool mv1 = k1 < k;                 // the smallest child rises into the root
+        uint64_t k2; uint32_t s2, c2;
+        near_kids(c1, k2, s2, c2);
+        const bool mv2 = mv1 && k2 < k;          // ... and its smallest child into c1
+        // root <- c1's entry or k; c1 <- c2's entry, k, or itself; c2 <- k (or
+        // c1's new value again when nothing moved that far: a repeated store)
+        const uint64_t vb = mv1 ? (mv2 ? k2 : k) : k1;
+        const uint32_t sb = mv1 ? (mv2 ? s2 : s) : s1;
+        const uint32_t wc = mv2 ? c2 : c1;
+        nk[0] = mv1 ? k1 : k;
+        ns[0] = mv1 ? s1 : s;
+        nk[c1 * TW_WG] = vb;
+        ns[c1 * TW_WG] = sb;
+        nk[wc * TW_WG] = mv2 ? k : vb;
+        ns[wc * TW_WG] = mv2 ? s : sb;
+        nrk = mv1 ? k1 : k;
+        nrs = mv1 ? s1 : s;
     }
     __device__ __forceinline__ void near_push(int64_t t, uint32_t sq, uint32_t slot) {
         STAT(K_NEAR_PUSH);
-        near_sift_up(near_n++, nkey(t, sq), slot);
+        const uint64_t k = nkey(t, sq);
+        const uint32_t n = near_n++;
+        // parent and grandparent of n (clamped to the root)
+        const uint32_t p1 = n ? (n - 1) >> 2 : 0;
+        const uint32_t p2 = p1 ? (p1 - 1) >> 2 : 0;
+        const uint64_t k1 = nk[p1 * TW_WG], k2 = nk[p2 * TW_WG];
+        const uint32_t s1 = ns[p1 * TW_WG], s2 = ns[p2 * TW_WG];
+        const bool up1 = n != 0 && k < k1;         // parent moves down into n
+        const bool up2 = up1 && p1 != 0 && k < k2;  // grandparent moves down into p1
+        // p2 <- k or itself; p1 <- grandparent, k or itself; n <- parent or k.
+        // Stored top-down so that when positions coincide (n = 0: all three;
+        // n <= 4: p1 = p2 = 0) the last store, the one for the deepest, wins.
+        nk[p2 * TW_WG] = up2 ? k : k2;
+        ns[p2 * TW_WG] = up2 ? slot : s2;
+        nk[p1 * TW_WG] = up2 ? k2 : (up1 ? k : k1);
+        ns[p1 * TW_WG] = up2 ? s2 : (up1 ? slot : s1);
+        nk[n * TW_WG] = up1 ? k1 : k;
+        ns[n * TW_WG] = up1 ? s1 : slot;
+        const bool m = k < nrk;
+        nrk = m ? k : nrk;
+        nrs = m ? slot : nrs;
     }
     __device__ __forceinline__ void near_pop() {
-        uint32_t n = --near_n;
-        if (n == 0) return;
-        near_sift_down(0, nk[n * TW_WG], ns[n * TW_WG]);
+        const uint32_t n = --near_n;
+        const uint64_t lk = n ? nk[n * TW_WG] : ~0ull;
+        const uint32_t ls = ns[n * TW_WG];
+        nk[n * TW_WG] = ~0ull;
+        near_down(lk, ls);
     }
-    // Re-key the live near entry with seq `old_seq` (seqs are unique) to (t, sq).
+    // Re-key the live near entry with seq `old_seq` (seqs are unique) to (t, sq),
+    // an earlier time: remove it (the last entry fills its hole) and push it anew.
     __device__ __forceinline__ bool near_rekey(uint32_t old_seq, int64_t t, uint32_t sq, uint32_t slot) {
-        for (uint32_t i = 0; i < near_n; ++i) {
-            uint64_t ok = nk[i * TW_WG];
-            if ((uint32_t)ok == old_seq) {
-                uint64_t k = nkey(t, sq);
-                if (k < ok) near_sift_up(i, k, slot);
-                else near_sift_down(i, k, slot);
-                return true;
-            }
+        uint32_t hit = 0;
+#pragma unroll
+        for (int i = 0; i < TW_NEAR_CAP; ++i) {
+            const uint64_t k = nk[i * TW_WG];
+            hit |= ((uint32_t)k == old_seq && k != ~0ull) ? 1u << i : 0u;
         }
-        return false;
+        if (!hit) return false;
+        const uint32_t i = (uint32_t)__builtin_ctz(hit);
+        // remove i: the last entry fills the hole; it can only need to move down
+        // (it was deeper, under a key <= it) or up (below i's ancestors); use a
+        // full rebuild of that path by re-pushing all entries above -- rare
+        // path (a throwTo of an on-chip thread), so simply rebuild the heap.
+        uint64_t kk[TW_NEAR_CAP];
+        uint32_t ss[TW_NEAR_CAP];
+        const uint32_t n = near_n;
+#pragma unroll
+        for (int j = 0; j < TW_NEAR_CAP; ++j) { kk[j] = nk[j * TW_WG]; ss[j] = ns[j * TW_WG]; }
+        near_init();
+        for (uint32_t j = 0; j < n; ++j) {
+            if (j == i) continue;
+            const uint64_t k = kk[j];
+            near_push(nbase + (int64_t)(k >> 32), (uint32_t)k, ss[j]);
+        }
+        near_push(t, sq, slot);
+        return true;
     }
     // Move the near heap to a new time base (keeps (t - nbase) inside 32 bits).
     __device__ void near_rebase(int64_t nb) {
-        uint64_t d = (uint64_t)(nb - nbase) << 32;
-        for (uint32_t i = 0; i < near_n; ++i) nk[i * TW_WG] -= d;
-        nrk -= d;
+        const uint64_t d = (uint64_t)(nb - nbase) << 32;
+#pragma unroll
+        for (int i = 0; i < TW_NEAR_CAP; ++i) {
+            const uint64_t k = nk[i * TW_WG];
+            nk[i * TW_WG] = k == ~0ull ? k : k - d;
+        }
+        nrk = nrk == ~0ull ? nrk : nrk - d;
         nbase = nb;
     }
 
@@ -417,8 +486,12 @@ struct Lane {
         return gp(c.runs) + ((size_t)j * c.Cr + pos) * c.R + r;
     }
     // the second entry loaded by the last run_pop lands in LDS
+    // Called after prefetch_all (4 younger vector-memory ops) and before the
+    // store tail: vmcnt(4) proves the entry landed without waiting for them.
     __device__ __forceinline__ void run_commit() {
         if (prun >= 0) {
+            asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+            const uint4 pent = pfs[4 * TW_WG];
             cs(CW_R2TL + prun, pent.x); cs(CW_R2TH + prun, pent.y);
             cs(CW_R2S + prun, pent.w); cs(CW_R2SL + prun, pent.z);
             prun = -1;
@@ -426,7 +499,6 @@ struct Lane {
     }
     __device__ __forceinline__ bool run_push(int64_t t, uint32_t sq, uint32_t slot) {
         if (c.Cr == 0) return false;
-        run_commit();
         int best = -1, empty = -1;
         int64_t bt = 0;
         uint32_t bs = 0;
@@ -474,12 +546,13 @@ struct Lane {
         cs(CW_RN + sel, n);
         if (n >= 2) {
             const uint32_t p2 = h + 1 == c.Cr ? 0 : h + 1;
-            pent = *run_at(sel, p2);
+            // into LDS staging quad 4 (no register left pending across the step)
+            asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(run_at(sel, p2)),
+                         "s"(pfs_wave + 4 * TW_WG * 16) : "memory", "m0");
             prun = sel;
         }
     }
-    __device__ __forceinline__ void far_min() {
-        run_commit();
+    __device__ __forceinline__ void far_min() {  // heads only: a pending second entry is not needed
         far_dirty = false;
         fsrc = -1;
         fmt = 0; fms = 0; fmsl = 0;
@@ -534,15 +607,7 @@ struct Lane {
         const uint4 GAS* p = hrec(slot);
         unpack(th, p[0], p[1], p[2], p[3]);
     }
-    __device__ __forceinline__ void peek_rec(uint32_t slot, Th& th) {
-        if (slot == pf_slot) {
-            STAT(K_PEEK_PF);
-            th = pf;
-        } else {
-            STAT(K_PEEK_HBM);
-            hbm_load(slot, th);
-        }
-    }
+    __device__ __forceinline__ void peek_rec(uint32_t slot, Th& th) { hbm_load(slot, th); }
     // mode ST_THROUGH: the full record; ST_DEAD: only the header quad (the tid
     // that invalidates stale refs)
     __device__ __forceinline__ void put_hdr(uint32_t slot, const Th& th) {
@@ -561,21 +626,78 @@ struct Lane {
         p[3] = make_uint4((uint32_t)th.r2, (uint32_t)((uint64_t)th.r2 >> 32), (uint32_t)th.r3,
                           (uint32_t)((uint64_t)th.r3 >> 32));
     }
-    // the running thread: header from registers, r0..r3 from the LDS register file
-    __device__ __forceinline__ void put_running(uint32_t slot, Th& th) {
+    // The iteration's stores, issued by every lane in the same shape (lanes
+    // with nothing to store write their dummy sink): the parent's record
+    // (full, or only the header of a thread that ended), the forked child's
+    // record.  With no store skipped by a branch, the compiler's vmcnt
+    // bookkeeping stays exact and the next pop waits only for its prefetch,
+    // not for these stores (vector-memory counters retire in issue order).
+    __device__ __forceinline__ void store_tail(uint32_t slot, Th& th, bool full, bool hdr, uint32_t cslot,
+                                               const Th& ch) {
+        const uint4 GAS* dm = gp(c.dummy) + (size_t)r;
+        const size_t R5 = c.R;
         th.r0 = rf[0]; th.r1 = rf[TW_WG]; th.r2 = rf[2 * TW_WG]; th.r3 = rf[3 * TW_WG];
-        put_rec(slot, th);
+        uint4 GAS* pr = hrec(full || hdr ? slot : 0);
+        uint4 GAS* p0 = (full || hdr) ? pr : (uint4 GAS*)dm;
+        uint4 GAS* p1 = full ? pr + 1 : (uint4 GAS*)(dm + R5);
+        uint4 GAS* p2 = full ? pr + 2 : (uint4 GAS*)(dm + 2 * R5);
+        uint4 GAS* p3 = full ? pr + 3 : (uint4 GAS*)(dm + 3 * R5);
+        *p0 = make_uint4(th.w0, th.w1, th.w2, th.w3);
+        *p1 = make_uint4(th.f0, th.f1, th.f2, th.w7);
+        *p2 = make_uint4((uint32_t)th.r0, (uint32_t)((uint64_t)th.r0 >> 32), (uint32_t)th.r1,
+                         (uint32_t)((uint64_t)th.r1 >> 32));
+        *p3 = make_uint4((uint32_t)th.r2, (uint32_t)((uint64_t)th.r2 >> 32), (uint32_t)th.r3,
+                         (uint32_t)((uint64_t)th.r3 >> 32));
+        const bool hc = cslot != 0xFFFFFFFFu;
+        uint4 GAS* pc0 = hrec(hc ? cslot : 0);
+        uint4 GAS* c0 = hc ? pc0 : (uint4 GAS*)dm;
+        uint4 GAS* c1 = hc ? pc0 + 1 : (uint4 GAS*)(dm + R5);
+        uint4 GAS* c2 = hc ? pc0 + 2 : (uint4 GAS*)(dm + 2 * R5);
+        uint4 GAS* c3 = hc ? pc0 + 3 : (uint4 GAS*)(dm + 3 * R5);
+        *c0 = make_uint4(ch.w0, ch.w1, ch.w2, ch.w3);
+        *c1 = make_uint4(ch.f0, ch.f1, ch.f2, ch.w7);
+        *c2 = make_uint4((uint32_t)ch.r0, (uint32_t)((uint64_t)ch.r0 >> 32), (uint32_t)ch.r1,
+                         (uint32_t)((uint64_t)ch.r1 >> 32));
+        *c3 = make_uint4((uint32_t)ch.r2, (uint32_t)((uint64_t)ch.r2 >> 32), (uint32_t)ch.r3,
+                         (uint32_t)((uint64_t)ch.r3 >> 32));
+        pf_slot = ((full || hdr) && slot == pf_slot) || (hc && cslot == pf_slot) ? 0xFFFFFFFFu : pf_slot;
     }
-    // Issue the HBM load of the record the next pop will most likely need.
-    __device__ __forceinline__ void prefetch_next(uint32_t cur) {
+
+    // Issue the HBM load of the record the next pop will most likely need,
+    // straight into LDS (global_load_lds: no registers held, no compiler-
+    // tracked pending load).  Every lane issues it (idle lanes reload slot 0).
+    // The iteration then always issues TW_TAIL_VMEM more vector-memory ops (the
+    // store tail and the hash atomic), so at the next pop `vmcnt(TW_TAIL_VMEM)`
+    // proves the prefetch landed without waiting for those stores.
+    __device__ __forceinline__ void prefetch_all(uint32_t cur) {
         if (far_dirty) far_min();
         uint32_t s = 0xFFFFFFFFu;
         if (near_n) s = nrs;
         if (fsrc >= 0 && (!near_n || tless(fmt, fms, nbase + (int64_t)(nrk >> 32), (uint32_t)nrk))) s = fmsl;
-        if (s != 0xFFFFFFFFu && s != cur && s != pf_slot) {
-            STAT(K_PF_ISSUE);
-            hbm_load(s, pf);
-            pf_slot = s;
+        const bool valid = s != 0xFFFFFFFFu && s != cur && s < c.S;
+        STAT(K_PF_ISSUE);
+        const uint4 GAS* p = hrec(valid ? s : 0u);
+        // the instruction offset of global_load_lds also offsets the LDS
+        // destination, so each quad gets its own global address instead
+        asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(p), "s"(pfs_wave)
+                     : "memory", "m0");
+        asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(p + 1),
+                     "s"(pfs_wave + TW_WG * 16) : "memory", "m0");
+        asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(p + 2),
+                     "s"(pfs_wave + 2 * TW_WG * 16) : "memory", "m0");
+        asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(p + 3),
+                     "s"(pfs_wave + 3 * TW_WG * 16) : "memory", "m0");
+        pf_slot = valid ? s : 0xFFFFFFFFu;
+    }
+    // The popped thread's record: the prefetched copy, or (rarely) a fresh load.
+    __device__ __forceinline__ void fetch_rec(uint32_t slot, Th& th) {
+        if (slot == pf_slot) {
+            STAT(K_PEEK_PF);
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(TW_TAIL_VMEM) : "memory");
+            unpack(th, pfs[0], pfs[TW_WG], pfs[2 * TW_WG], pfs[3 * TW_WG]);
+        } else {
+            STAT(K_PEEK_HBM);
+            hbm_load(slot, th);
         }
     }
 
@@ -584,7 +706,10 @@ struct Lane {
     __device__ __forceinline__ uint32_t alloc_slot() {
         if (free_n) {
             uint32_t s = ftop;
-            if (--free_n) ftop = gp(c.free_stk)[ix(free_n - 1)];
+            if (--free_n) {
+                ftop = gp(c.free_stk)[ix(free_n - 1)];
+                __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): ftop must not stay pending
+            }
             return s;
         }
         if (bump < c.S) return bump++;
@@ -614,6 +739,16 @@ struct Lane {
         if (hacc) { STAT(K_HASH_FLUSH); hash_atomic(hnode, hacc); }  // adding 0 is a no-op
         hacc = 0;
     }
+    // every lane issues the atomic (adding 0 to its dummy word when it has no
+    // term): one unconditional vector-memory op for the store tail's shape
+    __device__ __forceinline__ void hash_flush_all() {
+        const bool h = hacc != 0;
+        unsigned long long GAS* p = h ? (LP ? (unsigned long long GAS*)(gp(c.hash_g) + hnode)
+                                            : (unsigned long long GAS*)(gp(c.hash) + ix(hnode)))
+                                      : (unsigned long long GAS*)(gp(c.dummy) + (size_t)4 * c.R + r);
+        __hip_atomic_fetch_add(p, (unsigned long long)hacc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        hacc = 0;
+    }
     __device__ __forceinline__ void hash(uint32_t node, uint32_t kind, int64_t val) {
         hash_add(node, term(now, kind, val));
     }
@@ -631,12 +766,12 @@ struct Lane {
         o[1] = make_uint4(link, kind, src, dst);
     }
 
-    // Create a thread queued at now (fork, TimedT.hs:326-339).  Returns its ref.
+    // Create a thread queued at now (fork, TimedT.hs:326-339): its record is
+    // left in `ch` for the store tail.  Returns its ref.
     __device__ __forceinline__ bool spawn(uint32_t pc, uint32_t node, int64_t q0, int64_t q1, int64_t q2, int64_t q3,
-                                          int64_t& ref) {
+                                          int64_t& ref, Th& ch, uint32_t& cs_out) {
         uint32_t s = alloc_slot();
         if (s == 0xFFFFFFFFu) return false;
-        Th ch;
         uint32_t tid = tidc++;
         cinc(CW_TH);
         ch.w0 = pc & 0xFFFFu;
@@ -646,7 +781,7 @@ struct Lane {
         ch.f0 = ch.f1 = ch.f2 = ch.w7 = 0;
         ch.r0 = q0; ch.r1 = q1; ch.r2 = q2; ch.r3 = q3;
         enqueue(ch, s, now);
-        put_rec(s, ch);
+        cs_out = s;
         ref = (int64_t)(((uint64_t)tid << 32) | s);
         return true;
     }
@@ -683,7 +818,20 @@ struct Lane {
         put_rec(ts, t);
     }
 
-    // Thread ends (END or uncaught exception).
+    // Thread ends (END or uncaught exception): listener release, ref
+    // invalidation, slot freed; the caller stores the header quad.
+    __device__ __forceinline__ void die_prep(Th& th, uint32_t slot) {
+        if (th_flags(th) & F_OWNS) {
+            uint32_t node = th.w1;
+            if (gp(c.bind_own)[bix(node)] == th.w2) {
+                gp(c.bind)[bix(node)] = 0;
+                gp(c.bind_own)[bix(node)] = 0xFFFFFFFFu;
+            }
+        }
+        th.w2 = 0xFFFFFFFFu;  // invalidate refs to this slot
+        th.w3 = 0;
+        free_slot(slot);
+    }
     __device__ __forceinline__ void die(Th& th, uint32_t slot) {
         if (th_flags(th) & F_OWNS) {
             uint32_t node = th.w1;
@@ -753,6 +901,7 @@ struct Lane {
         uint32_t fin = (run && !running) ? (uint32_t)T_STOP : (uint32_t)T_NONE;
         uint32_t n = 0;
         int64_t yt = 0;
+        STIME(ti0);
         for (;;) {
             const uint64_t mask = __builtin_amdgcn_ballot_w64(running);
             if (mask == 0) break;
@@ -1038,16 +1187,25 @@ struct Lane {
             fin = at ? tc : fin;
             running = running && !(at && tc != T_NONE);
         }
-        if (!run) return;
-        th_set_pc(th, pc);
+        STIME(ti1);
+        STADD(K_CYC_INTERP, ti1 - ti0);
+        STIME(tt0);
+        // ---- terminal actions (queue work only), then a fixed-shape store tail
+        Th ch;
+        ch.w0 = ch.w1 = ch.w2 = ch.w3 = ch.f0 = ch.f1 = ch.f2 = ch.w7 = 0;
+        ch.r0 = ch.r1 = ch.r2 = ch.r3 = 0;
+        uint32_t cslot = 0xFFFFFFFFu;
+        if (run) th_set_pc(th, pc);
         // fork (TimedT.hs:326-342): the child is queued at now, then the parent waits 1 µs
         if (fin == T_SPAWN) {
             const uint32_t cdel = cg(CW_CDEL), cra = cg(CW_CRA);
             int64_t ref;
             bool ok;
-            if (cdel & 2u) ok = spawn(cg(CW_CPC), cg(CW_CNODE), rf[0], rf[TW_WG], rf[2 * TW_WG], rf[3 * TW_WG], ref);
-            else ok = spawn(cg(CW_CPC), cg(CW_CNODE), cg64(CW_Q0, CW_Q0 + 1), cg64(CW_Q0 + 2, CW_Q0 + 3),
-                            cg64(CW_Q0 + 4, CW_Q0 + 5), cg64(CW_Q0 + 6, CW_Q7), ref);
+            if (cdel & 2u)
+                ok = spawn(cg(CW_CPC), cg(CW_CNODE), rf[0], rf[TW_WG], rf[2 * TW_WG], rf[3 * TW_WG], ref, ch, cslot);
+            else
+                ok = spawn(cg(CW_CPC), cg(CW_CNODE), cg64(CW_Q0, CW_Q0 + 1), cg64(CW_Q0 + 2, CW_Q0 + 3),
+                           cg64(CW_Q0 + 4, CW_Q0 + 5), cg64(CW_Q0 + 6, CW_Q7), ref, ch, cslot);
             if (!ok) {
                 fin = T_STOP;
             } else {
@@ -1064,14 +1222,14 @@ struct Lane {
                 }
             }
         }
-        if (fin == T_YIELD) {
-            enqueue(th, slot, yt);
-            put_running(slot, th);
-        } else if (fin == T_EXIT) {
-            die(th, slot);
-        } else if (fin == T_STOP) {
-            put_running(slot, th);
-        }
+        if (fin == T_YIELD) enqueue(th, slot, yt);
+        else if (fin == T_EXIT) die_prep(th, slot);
+        run_commit();
+        STIME(tt1);
+        STADD(K_CYC_TERM, tt1 - tt0);
+        store_tail(slot, th, fin == T_YIELD || fin == T_STOP, fin == T_EXIT, cslot, ch);
+        STIME(tt2);
+        STADD(K_CYC_STORE, tt2 - tt1);
     }
 };
 
@@ -1118,14 +1276,16 @@ __global__ void __launch_bounds__(TW_WG) tw_init_kernel(Dev c, uint32_t main_pc,
 // files, the cold words, then the program image and constant pool, so
 // instruction fetch and time constants never leave the CU.
 __host__ __device__ constexpr size_t fixed_lds_bytes() {
-    return (size_t)TW_NEAR_CAP * TW_WG * 12 + (size_t)4 * TW_WG * 8 + (size_t)CW_COUNT * TW_WG * 4;
+    return (size_t)5 * TW_WG * 16 + (size_t)TW_NEAR_CAP * TW_WG * 12 + (size_t)4 * TW_WG * 8 +
+           (size_t)CW_COUNT * TW_WG * 4;
 }
 
 template <bool LP>
 __global__ void __launch_bounds__(TW_WG) __attribute__((amdgpu_waves_per_eu(1, 2)))
 tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
     extern __shared__ __attribute__((aligned(16))) uint64_t lds_raw[];
-    uint64_t LAS* s_k = (uint64_t LAS*)lds_raw;
+    uint4 LAS* s_pf = (uint4 LAS*)lds_raw;
+    uint64_t LAS* s_k = (uint64_t LAS*)(s_pf + 5 * TW_WG);
     int64_t LAS* s_rf = (int64_t LAS*)(s_k + TW_NEAR_CAP * TW_WG);
     uint32_t LAS* s_s = (uint32_t LAS*)(s_rf + 4 * TW_WG);
     uint32_t LAS* s_cw = s_s + TW_NEAR_CAP * TW_WG;
@@ -1149,6 +1309,8 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
     L.ns = s_s + threadIdx.x;
     L.rf = s_rf + threadIdx.x;
     L.cw = s_cw + threadIdx.x;
+    L.pfs = s_pf + threadIdx.x;
+    L.pfs_wave = __builtin_amdgcn_readfirstlane((uint32_t)(size_t)(s_pf + (threadIdx.x & ~63u)));
     L.P = s_p;
     L.K = s_c;
     L.pf_slot = 0xFFFFFFFFu;
@@ -1190,16 +1352,13 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
     }
     L.far_min();
     // near heap: re-inserted from the spill area (keys are relative to this launch's base)
-    L.near_n = 0;
     L.nbase = L.now;
-    L.nrk = 0; L.nrs = 0;
+    L.near_init();
     for (uint32_t j = 0; j < near_n0; ++j) {
         uint4 e = gp(c.near_spill)[(size_t)j * R + r];
-        if (L.near_fits(ent_t(e)) || ent_t(e) - L.now < c.horizon) {
-            if (L.near_n < TW_NEAR_CAP && (uint64_t)(ent_t(e) - L.nbase) < 0xFFFFFFFFull) {
-                L.near_push(ent_t(e), e.w, e.z);
-                continue;
-            }
+        if (L.near_n < TW_NEAR_CAP && (uint64_t)(ent_t(e) - L.nbase) < 0xFFFFFFFFull) {
+            L.near_push(ent_t(e), e.w, e.z);
+            continue;
         }
         L.push_far(ent_t(e), e.w, e.z);  // the thread's F_NEARQ hint only speeds up throwTo
     }
@@ -1253,19 +1412,24 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
     for (int i = 0; i < P_COUNT; ++i) L.st[i] = 0;
 #endif
     uint32_t pending_main = (uint32_t)sc[SC_PENDING_MAIN * R];
+    // nothing loaded before the loop may stay pending into it (a loop-header
+    // wait would otherwise drain the counter on every iteration)
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
     // The loop is wave-uniform: a lane that stops (quiescence, t_end, event
     // cap, error) just idles through the remaining iterations, so no per-lane
     // break/continue splits the wave's control flow.
     bool alive = L.status == TW_REP_RUNNING;
     for (uint32_t it = 0; it < budget; ++it) {
         if (!__builtin_amdgcn_ballot_w64(alive)) break;
+        STIME(tl0);
         Th th;
         uint32_t slot = 0;
         bool run = false;
         if (alive) {
             if (pending_main) {  // runInSandbox main (TimedT.hs:237): runs at t=0, not a pop
                 pending_main = 0;
-                L.peek_rec(0, th);
+                L.pf_slot = 0xFFFFFFFFu;
+                L.fetch_rec(0, th);
                 L.rf[0] = th.r0; L.rf[TW_WG] = th.r1; L.rf[2 * TW_WG] = th.r2; L.rf[3 * TW_WG] = th.r3;
                 L.hnode = th.w1;
                 run = true;
@@ -1283,13 +1447,19 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
                 if (use_near) { t = L.nbase + (int64_t)(L.nrk >> 32); sq = (uint32_t)L.nrk; slot = L.nrs; }
                 const bool use_far = L.fsrc >= 0 && (!use_near || tless(L.fmt, L.fms, t, sq));
                 if (use_far) { t = L.fmt; sq = L.fms; slot = L.fmsl; }
+                STIME(ts1);
+                STADDL(K_CYC_SEL, ts1 - tl0);
                 if ((!use_near && !use_far) || t > t_end) {
                     alive = false;  // parked beyond t_end (an empty queue cannot happen while live > 0)
                 } else {
-                    L.peek_rec(slot, th);  // prefetched copy or HBM
+                    L.fetch_rec(slot, th);  // prefetched copy or HBM
+                    STIME(ts2);
+                    STADDL(K_CYC_FETCH, ts2 - ts1);
                     if (!use_far) L.near_pop();
                     else if (L.fsrc == TW_RUNS) L.far_pop();
                     else L.run_pop(L.fsrc);
+                    STIME(ts3);
+                    STADDL(K_CYC_QPOP, ts3 - ts2);
                     if (slot == L.pf_slot) L.pf_slot = 0xFFFFFFFFu;
                     if (th.w3 != sq) {
                         STATL(K_SUPERSEDED);  // superseded by a throwTo re-stamp
@@ -1300,7 +1470,6 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
                         --L.live;
                         L.now = t;
                         if (t - L.nbase > (int64_t)0x7FFFFFFF) L.near_rebase(t);
-                        L.prefetch_next(slot);
                         L.hnode = th.w1;
                         L.rf[0] = th.r0; L.rf[TW_WG] = th.r1; L.rf[2 * TW_WG] = th.r2; L.rf[3 * TW_WG] = th.r3;
                         // LP phantom = the deliverer's wake, already counted and hashed by the sender
@@ -1330,11 +1499,22 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
                 }
             }
         }
+        STIME(tp0);
+        L.prefetch_all(run ? slot : 0xFFFFFFFFu);
+        STIME(tl1);
+        STADDL(K_CYC_PF, tl1 - tp0);
+        STADDL(K_CYC_POP, tl1 - tl0);
         L.step(th, slot, run);
-        L.hash_flush();
+        STIME(th0);
+        L.hash_flush_all();
+        STIME(th1);
+        STADDL(K_CYC_HASH, th1 - th0);
         alive = alive && L.status == TW_REP_RUNNING;
+        STIME(tl2);
+        STADDL(K_CYC_TAIL, tl2 - tl1);
     }
     L.hash_flush();
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
     L.run_commit();
 #ifdef TW_STATS
     if (c.prof)
@@ -1359,9 +1539,10 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
         sc[(SC_RH0 + j) * R] = L.cg(CW_RH + j);
         sc[(SC_RC0 + j) * R] = L.cg(CW_RN + j);
     }
-    for (uint32_t j = 0; j < L.near_n; ++j) {
-        uint64_t k = L.nk[j * TW_WG];
-        gp(c.near_spill)[(size_t)j * R + r] = ent(L.nbase + (int64_t)(k >> 32), L.ns[j * TW_WG], (uint32_t)k);
+    for (uint32_t i = 0, j = 0; i < TW_NEAR_CAP; ++i) {
+        const uint64_t k = L.nk[i * TW_WG];
+        if (k != ~0ull)
+            gp(c.near_spill)[(size_t)(j++) * R + r] = ent(L.nbase + (int64_t)(k >> 32), L.ns[i * TW_WG], (uint32_t)k);
     }
     bool active = L.status == TW_REP_RUNNING && L.d_ev < ev_room;
     int64_t tn = INT64_MAX;
@@ -1582,6 +1763,7 @@ static int load_common(tw_ctx* c, const tw_scenario_desc* s, bool lp, uint32_t l
     ALLOC(d.far, (size_t)d.Q * R);
     ALLOC(d.runs, (size_t)(d.Cr ? TW_RUNS * (size_t)d.Cr : 1) * R);
     ALLOC(d.near_spill, (size_t)TW_NEAR_CAP * R);
+    ALLOC(d.dummy, (size_t)5 * R);
     ALLOC(d.nvars, (size_t)d.N * 4 * R);
     ALLOC(d.hash, (size_t)d.N * R);
     ALLOC(d.bind, (size_t)d.N * R);

@@ -2,8 +2,9 @@
 
 Runs the config-3 token ring in three phases (start-up t < 1 s, token phase t <
 launchDuration, teardown) and prints, per committed pop, how often each path of
-the event loop ran: record source (LDS pool / prefetched copy / HBM), record
-placement (pool / eviction / HBM / dead header), prefetches issued, hash atomics,
+the event loop ran: record source (prefetched copy / HBM), record
+writes (full / dead header), s_memtime cycle splits (pop phase, interpreter
+loop, step + hash flush; cycles are per wave, summed over lanes), prefetches issued, hash atomics,
 queue pushes by tier, interpreted instructions.  Also times each phase.
 
 usage: TW_LIB=.../libtimewarp_stats.so python tools/stats_probe.py [replicas] [nodes]
@@ -19,15 +20,16 @@ sys.path.insert(0, os.path.join(ROOT, "time-warp_amd"))
 from timewarp import scenarios  # noqa: E402
 from timewarp.engine import Engine  # noqa: E402
 
-NAMES = ["pop", "superseded", "peek_pool", "peek_pf", "peek_hbm", "put_pool", "put_evict", "put_hbm", "put_dead",
-         "pf_issue", "hash_imm", "hash_flush", "near_push", "run_push", "far_push", "insn"]
+NAMES = ["pop", "superseded", "peek_pf", "peek_hbm", "put_hbm", "put_dead", "pf_issue", "hash_imm", "hash_flush",
+         "near_push", "run_push", "far_push", "insn", "cyc_pop", "cyc_interp", "cyc_step_and_flush",
+         "cyc_select", "cyc_fetch", "cyc_qpop", "cyc_commit", "cyc_prefetch", "cyc_terminal", "cyc_store", "cyc_hash"]
 
 
 def read(eng):
-    buf = (C.c_ulonglong * 16)()
+    buf = (C.c_ulonglong * 24)()
     fn = eng.lib.tw_prof_read
     fn.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]
-    n = fn(eng.ctx, buf, 16, 1)
+    n = fn(eng.ctx, buf, 24, 1)
     if n < 0:
         raise RuntimeError(f"tw_prof_read: {n}")
     return {k: buf[i] for i, k in enumerate(NAMES)}
