@@ -152,7 +152,8 @@ def main():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", default="token_ring", choices=["token_ring", "ping_pong", "hotspot", "gossip"])
-    ap.add_argument("--replicas", type=int, default=65536, help="replicas per GPU")
+    ap.add_argument("--replicas", type=int, default=None,
+                    help="replicas per GPU: 65536 (token_ring, C3), 1048576 (ping_pong, C2), 4096 (hotspot, C5)")
     ap.add_argument("--nodes", type=int, default=None, help="4096 (token_ring), 256 senders (hotspot), 1M (gossip)")
     ap.add_argument("--duration-s", type=int, default=120)
     ap.add_argument("--drop-log2", type=int, default=10)
@@ -163,6 +164,8 @@ def main():
     args = ap.parse_args()
     if args.nodes is None:
         args.nodes = {"token_ring": 4096, "hotspot": 256, "gossip": 1 << 20}.get(args.config, 2)
+    if args.replicas is None:
+        args.replicas = {"token_ring": 65536, "ping_pong": 1 << 20, "hotspot": 4096}.get(args.config, 1)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -207,6 +210,8 @@ def main():
         elapsed += time.perf_counter() - t0
         events += st.events
         sends += st.sends
+        print(f"[bench] rank {rank} step: {st.events} events in {(time.perf_counter() - t0) * 1e3:.1f} ms",
+              file=sys.stderr, flush=True)
         kernel_ms += float(eng.launch_ms().sum())
         launches += st.launches
         if st.replicas_error:
@@ -257,13 +262,17 @@ def main():
         }
         prof = os.path.join(ROOT, "profiles", "pmc_summary.json")
         if os.path.exists(prof) and args.config == "token_ring" and args.replicas == 65536 and args.nodes == 4096:
+            # measured HBM bytes of the same workload (tools/pmc.sh: separate --pmc passes over a 1-step run
+            # of this bench), per launch like `achieved`: one step's traffic / one step's launches
             pm = json.load(open(prof))
             if pm.get("bench_args", "").strip() == "" and "hbm_bytes_total" in pm:
                 per_step = float(pm["hbm_bytes_total"])
-                out["roofline"]["traffic"] = per_step
-                out["roofline"]["traffic_unit"] = ("HBM bytes per step, rocprofv3 (2*FETCH_SIZE + WRITE_SIZE)*1024 "
-                                                   "over the step's tw_run_kernel dispatches (profiles/pmc_summary.json)")
+                out["roofline"]["traffic"] = per_step / max(1, launches / args.steps)
+                out["roofline"]["traffic_unit"] = ("HBM bytes per launch: rocprofv3 (2*FETCH_SIZE + WRITE_SIZE)*1024 "
+                                                   "over one step's tw_run_kernel dispatches / its launches "
+                                                   "(profiles/pmc_summary.json, MI355X_MICROARCH.md HBM section)")
                 out["roofline"]["traffic_per_event"] = per_step / max(1, events / args.steps)
+                out["roofline"]["algorithmic_per_event"] = alg_bytes / max(1, events)
         if not args.no_cpu_baseline:
             cb, parity, n = cpu_baseline(scn, res, hashes, args.cpu_seconds)
             out["cpu_baseline"] = cb
