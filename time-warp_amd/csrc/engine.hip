@@ -227,6 +227,49 @@ enum {
     CW_COUNT
 };
 
+// Pre-decoded instruction class ("uop" flags, built once per launch in the
+// kernel prologue from the program image): the interpreter's hot pass computes
+// register results, jumps and yields with a few wave-uniform selects and
+// enters the per-opcode switch only for the rare ops (U_FX).
+enum : uint32_t {
+    A_NONE, A_IMM, A_K, A_ADDI, A_MULI, A_MOV, A_ADD, A_SUB, A_NOW, A_NODE, A_TID,  // r[a] <- ...
+};
+enum : uint32_t { J_NONE, J_ALWAYS, J_EQ, J_NE, J_LT, J_LE, J_EQI, J_NEI };      // pc <- imm if ...
+enum : uint32_t { TK_NONE, TK_WREL, TK_WABS, TK_WREG, TK_EXIT, TK_FORK };          // the step ends with ...
+#define U_ALU(f) ((f) & 0xFu)
+#define U_J(f) (((f) >> 4) & 7u)
+#define U_TK(f) (((f) >> 8) & 7u)
+#define U_FX (1u << 12)
+__device__ __forceinline__ uint32_t uop_of(uint32_t op) {
+    auto u = [](uint32_t alu, uint32_t j, uint32_t tk) { return alu | (j << 4) | (tk << 8); };
+    switch (op) {
+    case TW_OP_NOP: return 0;
+    case TW_OP_END: return u(A_NONE, J_NONE, TK_EXIT);
+    case TW_OP_WAIT_REL: return u(A_NONE, J_NONE, TK_WREL);
+    case TW_OP_WAIT_ABS: return u(A_NONE, J_NONE, TK_WABS);
+    case TW_OP_WAIT_REG: return u(A_NONE, J_NONE, TK_WREG);
+    case TW_OP_FORK: return u(A_NONE, J_NONE, TK_FORK);
+    case TW_OP_MYTID: return u(A_TID, J_NONE, TK_NONE);
+    case TW_OP_SETI: return u(A_IMM, J_NONE, TK_NONE);
+    case TW_OP_SETK: return u(A_K, J_NONE, TK_NONE);
+    case TW_OP_ADDI: return u(A_ADDI, J_NONE, TK_NONE);
+    case TW_OP_MULI: return u(A_MULI, J_NONE, TK_NONE);
+    case TW_OP_MOV: return u(A_MOV, J_NONE, TK_NONE);
+    case TW_OP_ADD: return u(A_ADD, J_NONE, TK_NONE);
+    case TW_OP_SUB: return u(A_SUB, J_NONE, TK_NONE);
+    case TW_OP_JMP: return u(A_NONE, J_ALWAYS, TK_NONE);
+    case TW_OP_JEQ: return u(A_NONE, J_EQ, TK_NONE);
+    case TW_OP_JNE: return u(A_NONE, J_NE, TK_NONE);
+    case TW_OP_JLT: return u(A_NONE, J_LT, TK_NONE);
+    case TW_OP_JLE: return u(A_NONE, J_LE, TK_NONE);
+    case TW_OP_JEQI: return u(A_NONE, J_EQI, TK_NONE);
+    case TW_OP_JNEI: return u(A_NONE, J_NEI, TK_NONE);
+    case TW_OP_NOW: return u(A_NOW, J_NONE, TK_NONE);
+    case TW_OP_NODE: return u(A_NODE, J_NONE, TK_NONE);
+    default: return U_FX;  // every other opcode (and invalid ones) takes the switch
+    }
+}
+
 template <bool LP>
 struct Lane {
     Dev c;  // by value: kernel arguments stay in SGPRs
@@ -239,6 +282,7 @@ struct Lane {
     uint32_t pfs_wave;    // LDS byte address of this wave's staging (quad 0), wave-uniform
     uint32_t LAS* cw;     // cold words [CW_*]
     const uint2 LAS* P;   // program image
+    const uint32_t LAS* PU;  // its uop flags
     const int64_t LAS* K; // constant pool
     // near heap: count, time base, cached root
     uint32_t near_n;
@@ -907,10 +951,15 @@ struct Lane {
             if (mask == 0) break;
             const uint32_t upc = __builtin_amdgcn_readlane(pc, (uint32_t)__builtin_ctzll(mask));
             const bool at = running && pc == upc;
+#ifndef TW_X_NOCAP
             n += at ? 1u : 0u;
             const bool capped = at && n > TW_STEP_CAP;  // TW_REP_ERR_INSN before executing it
+#else
+            const bool capped = false;
+#endif
             const bool me = at && !capped;
             const uint2 in = P[upc];
+            const uint32_t fl = __builtin_amdgcn_readfirstlane(PU[upc]);
             const uint32_t uw = __builtin_amdgcn_readfirstlane(in.x);
             const int32_t imm = (int32_t)__builtin_amdgcn_readfirstlane(in.y);
             const uint32_t op = uw & 0xFFu, a = (uw >> 8) & 3u, b = uw >> 16;
@@ -925,30 +974,55 @@ struct Lane {
             bool thr_any = false, thr = false;  // throwTo after the op (THROW_TO, TMO_FIRE)
             int64_t tref = 0, tval = 0;
             uint32_t tcode = 0;
+            // ---- hot classes: register result, jump, yield/exit/fork (uniform selects)
+            const uint32_t ak = U_ALU(fl), jk = U_J(fl), tk = U_TK(fl);
+            if (ak != A_NONE) {
+                const int64_t i64 = imm;
+                const int64_t kv = K[ak == A_K ? imm : 0];
+                int64_t v = i64;
+                v = ak == A_K ? kv : v;
+                v = ak == A_ADDI ? ra + i64 : v;
+                v = ak == A_MULI ? ra * i64 : v;
+                v = ak == A_MOV ? rb : v;
+                v = ak == A_ADD ? ra + rb : v;
+                v = ak == A_SUB ? ra - rb : v;
+                v = ak == A_NOW ? now : v;
+                v = ak == A_NODE ? (int64_t)th.w1 : v;
+                v = ak == A_TID ? (int64_t)(((uint64_t)th.w2 << 32) | slot) : v;
+                wr = true;
+                wv = v;
+            }
+            if (jk != J_NONE) {
+                const int64_t b16 = (int64_t)(int16_t)b;
+                const bool cj = jk == J_ALWAYS || (jk == J_EQ && ra == rb) || (jk == J_NE && ra != rb) ||
+                                (jk == J_LT && ra < rb) || (jk == J_LE && ra <= rb) || (jk == J_EQI && ra == b16) ||
+                                (jk == J_NEI && ra != b16);
+                tgt = cj ? (uint32_t)imm : tgt;
+            }
+            if (tk != TK_NONE) {
+                if (tk == TK_EXIT) {
+                    tc = T_EXIT;
+                } else if (tk == TK_FORK) {
+                    const uint32_t node = b == 0xFFFFu ? th.w1 : (uint32_t)rb;
+                    const bool bad = LP ? node != th.w1 : node >= c.N;
+                    pfail(me && bad, TW_REP_ERR_INSN);
+                    tc = bad ? T_STOP : T_SPAWN;
+                    const bool p = me && !bad;
+                    csp(p, CW_CPC, (uint32_t)imm);
+                    csp(p, CW_CNODE, node);
+                    csp(p, CW_CRA, a);
+                    csp(p, CW_CDEL, 2u);  // the child's registers are the parent's
+                } else {
+                    const int64_t kt = K[tk == TK_WREG ? 0 : imm];
+                    int64_t w = now + (ra > 0 ? ra : 0);               // wait (for r[a])
+                    w = tk == TK_WREL ? now + kt : w;                    // wait (for K)
+                    w = tk == TK_WABS ? (kt > now ? kt : now) : w;       // wait (till K)
+                    yt = me ? w : yt;
+                    tc = T_YIELD;
+                }
+            }
+            if (fl & U_FX) {
             switch (op) {
-            case TW_OP_NOP: break;
-            case TW_OP_END: tc = T_EXIT; break;
-            case TW_OP_WAIT_REL: yt = me ? now + K[imm] : yt; tc = T_YIELD; break;
-            case TW_OP_WAIT_ABS: {
-                const int64_t t = K[imm];
-                yt = me ? (t > now ? t : now) : yt;
-                tc = T_YIELD;
-                break;
-            }
-            case TW_OP_WAIT_REG: yt = me ? now + (ra > 0 ? ra : 0) : yt; tc = T_YIELD; break;
-            case TW_OP_FORK: {
-                const uint32_t node = b == 0xFFFFu ? th.w1 : (uint32_t)rb;
-                const bool bad = LP ? node != th.w1 : node >= c.N;
-                pfail(me && bad, TW_REP_ERR_INSN);
-                tc = bad ? T_STOP : T_SPAWN;
-                const bool p = me && !bad;
-                csp(p, CW_CPC, (uint32_t)imm);
-                csp(p, CW_CNODE, node);
-                csp(p, CW_CRA, a);
-                csp(p, CW_CDEL, 2u);  // the child's registers are the parent's
-                break;
-            }
-            case TW_OP_MYTID: wr = true; wv = (int64_t)(((uint64_t)th.w2 << 32) | slot); break;
             case TW_OP_THROW_TO:
                 thr_any = true; thr = me;
                 tref = ra; tcode = b & 0xFFu; tval = rf[((b >> 8) & 3u) * TW_WG];
@@ -982,28 +1056,12 @@ struct Lane {
                 th.w0 = (me && !bad) ? (th.w0 & ~(3u << 16)) | ((nf - 1) << 16) : th.w0;
                 break;
             }
-            case TW_OP_SETI: wr = true; wv = imm; break;
-            case TW_OP_SETK: wr = true; wv = K[imm]; break;
-            case TW_OP_ADDI: wr = true; wv = ra + imm; break;
-            case TW_OP_MULI: wr = true; wv = ra * imm; break;
-            case TW_OP_MOV: wr = true; wv = rb; break;
-            case TW_OP_ADD: wr = true; wv = ra + rb; break;
-            case TW_OP_SUB: wr = true; wv = ra - rb; break;
             case TW_OP_MODI: {
                 const int64_t m = ra % (int64_t)imm;
                 wr = true;
                 wv = m < 0 ? m + imm : m;
                 break;
             }
-            case TW_OP_JMP: tgt = (uint32_t)imm; break;
-            case TW_OP_JEQ: tgt = ra == rb ? (uint32_t)imm : tgt; break;
-            case TW_OP_JNE: tgt = ra != rb ? (uint32_t)imm : tgt; break;
-            case TW_OP_JLT: tgt = ra < rb ? (uint32_t)imm : tgt; break;
-            case TW_OP_JLE: tgt = ra <= rb ? (uint32_t)imm : tgt; break;
-            case TW_OP_JEQI: tgt = ra == (int64_t)(int16_t)b ? (uint32_t)imm : tgt; break;
-            case TW_OP_JNEI: tgt = ra != (int64_t)(int16_t)b ? (uint32_t)imm : tgt; break;
-            case TW_OP_NOW: wr = true; wv = now; break;
-            case TW_OP_NODE: wr = true; wv = th.w1; break;
             case TW_OP_NLOAD: {
                 const uint32_t node = me ? th.w1 : 0u;  // sanitised address for idle lanes
                 wr = true;
@@ -1173,17 +1231,20 @@ struct Lane {
                 tc = T_STOP;
                 break;
             }
+            }  // U_FX
             if (wr) rf[a * TW_WG] = wm ? wv : ra;
             if (thr_any) {
                 if (thr) throw_to(th, slot, tref, tcode, tval);
             }
             // per-lane epilogue of the pass
             pc = me ? tgt : pc;
+#ifndef TW_X_NOEPI
             pfail(capped, TW_REP_ERR_INSN);
             const bool oob = tc == T_NONE && pc >= c.n_insns;
             pfail(me && oob, TW_REP_ERR_INSN);
             tc = capped ? (uint32_t)T_STOP : tc;
             tc = (tc == T_NONE && (status != TW_REP_RUNNING || oob)) ? (uint32_t)T_STOP : tc;
+#endif
             fin = at ? tc : fin;
             running = running && !(at && tc != T_NONE);
         }
@@ -1291,8 +1352,13 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
     uint32_t LAS* s_cw = s_s + TW_NEAR_CAP * TW_WG;
     uint2 LAS* s_p = (uint2 LAS*)(s_cw + CW_COUNT * TW_WG);
     int64_t LAS* s_c = (int64_t LAS*)(s_p + c.n_insns + 1);
+    uint32_t LAS* s_u = (uint32_t LAS*)(s_c + c.n_consts);
     {
-        for (uint32_t i = threadIdx.x; i <= c.n_insns; i += TW_WG) s_p[i] = gp(c.insns)[i];
+        for (uint32_t i = threadIdx.x; i <= c.n_insns; i += TW_WG) {
+            const uint2 in = gp(c.insns)[i];
+            s_p[i] = in;
+            s_u[i] = uop_of(in.x & 0xFFu);
+        }
         for (uint32_t i = threadIdx.x; i < c.n_consts; i += TW_WG) s_c[i] = gp(c.consts)[i];
         __syncthreads();
     }
@@ -1312,6 +1378,7 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
     L.pfs = s_pf + threadIdx.x;
     L.pfs_wave = __builtin_amdgcn_readfirstlane((uint32_t)(size_t)(s_pf + (threadIdx.x & ~63u)));
     L.P = s_p;
+    L.PU = s_u;
     L.K = s_c;
     L.pf_slot = 0xFFFFFFFFu;
     L.prun = -1;
@@ -1741,7 +1808,7 @@ static int load_common(tw_ctx* c, const tw_scenario_desc* s, bool lp, uint32_t l
     d.Cr = s->run_capacity;
     const size_t R = d.R;
     const size_t Rt = s->n_replicas;  // replica dimension of the host tables
-    c->lds_bytes = fixed_lds_bytes() + 8ull * (d.n_insns + 1) + 8ull * d.n_consts;
+    c->lds_bytes = fixed_lds_bytes() + 12ull * (d.n_insns + 1) + 8ull * d.n_consts;
     if (c->lds_bytes > 160 * 1024) { free_all(c); return TW_ERR_INVALID; }  // program + constants must fit in LDS
     HIPCHK(hipFuncSetAttribute((const void*)tw_run_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                (int)c->lds_bytes));
