@@ -204,23 +204,16 @@ __device__ __forceinline__ int64_t ent_t(uint4 e) { return (int64_t)(((uint64_t)
 // staging.  Keeping them out of registers leaves the event loop a small
 // register footprint (one wave per SIMD issues every instruction itself; a
 // large live set turns into register shuffles on every path).
+// The far runs' bookkeeping, as quads in LDS [RQ_*][TW_WG]: head and second
+// entry of each run in the queue-entry format {t lo, t hi, slot, seq}, the
+// tail {t lo, t hi, seq, length}, and the four head indices in one quad.
+static_assert(TW_RUNS == 4, "run head indices share one quad");
+enum { RQ_HEAD = 0, RQ_SEC = TW_RUNS, RQ_TAIL = 2 * TW_RUNS, RQ_IDX = 3 * TW_RUNS, RQ_COUNT };
+
 enum {
-    CW_RH = 0,                      // run head index       [TW_RUNS]
-    CW_RN = CW_RH + TW_RUNS,        // run length
-    CW_RTL = CW_RN + TW_RUNS,       // head time lo
-    CW_RTH = CW_RTL + TW_RUNS,      // head time hi
-    CW_RS = CW_RTH + TW_RUNS,       // head seq
-    CW_RSL = CW_RS + TW_RUNS,       // head slot
-    CW_R2TL = CW_RSL + TW_RUNS,     // second entry (valid while rn >= 2)
-    CW_R2TH = CW_R2TL + TW_RUNS,
-    CW_R2S = CW_R2TH + TW_RUNS,
-    CW_R2SL = CW_R2S + TW_RUNS,
-    CW_UTL = CW_R2SL + TW_RUNS,     // tail time lo / hi / seq
-    CW_UTH = CW_UTL + TW_RUNS,
-    CW_US = CW_UTH + TW_RUNS,
-    CW_FTL = CW_US + TW_RUNS,       // far heap top (t, seq, slot)
+    CW_FTL = 0,                     // far heap top (t, seq, slot)
     CW_FTH, CW_FS, CW_FSL,
-    CW_DL, CW_DR, CW_UD, CW_TH, CW_MAINEXC, CW_TMO,   // counters
+    CW_DL, CW_DR, CW_UD, CW_MAINEXC, CW_TMO,          // counters
     CW_YTL, CW_YTH, CW_CPC, CW_CNODE, CW_CRA, CW_CDEL, // step staging: wake time, child
     CW_Q0, CW_Q7 = CW_Q0 + 7,                          // child registers (4 x int64)
     CW_DUMMY,                                          // target of idle lanes' predicated stores
@@ -281,6 +274,7 @@ struct Lane {
     uint4 LAS* pfs;       // prefetch staging: quad q of the next pop's record at [q * TW_WG]
     uint32_t pfs_wave;    // LDS byte address of this wave's staging (quad 0), wave-uniform
     uint32_t LAS* cw;     // cold words [CW_*]
+    uint4 LAS* rq;        // far runs' bookkeeping quads [RQ_*]
     const uint2 LAS* P;   // program image
     const uint32_t LAS* PU;  // its uop flags
     const int64_t LAS* K; // constant pool
@@ -307,7 +301,7 @@ struct Lane {
     // replica scalars
     int64_t now, final_t;
     uint32_t seq, tidc, live, status;
-    uint32_t d_ev;  // this launch's event count
+    uint32_t d_ev, d_th;  // this launch's event and thread counts
 #ifdef TW_STATS
     uint32_t st[P_COUNT];
 #endif
@@ -530,64 +524,70 @@ struct Lane {
         return gp(c.runs) + ((size_t)j * c.Cr + pos) * c.R + r;
     }
     // the second entry loaded by the last run_pop lands in LDS
+    __device__ __forceinline__ uint4 LAS* rqp(int w) const { return rq + w * TW_WG; }
+    __device__ __forceinline__ static uint32_t q_at(uint4 q, int j) {
+        return j == 0 ? q.x : j == 1 ? q.y : j == 2 ? q.z : q.w;
+    }
     // Called after prefetch_all (4 younger vector-memory ops) and before the
     // store tail: vmcnt(4) proves the entry landed without waiting for them.
     __device__ __forceinline__ void run_commit() {
         if (prun >= 0) {
             asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-            const uint4 pent = pfs[4 * TW_WG];
-            cs(CW_R2TL + prun, pent.x); cs(CW_R2TH + prun, pent.y);
-            cs(CW_R2S + prun, pent.w); cs(CW_R2SL + prun, pent.z);
+            *rqp(RQ_SEC + prun) = pfs[4 * TW_WG];
             prun = -1;
         }
     }
     __device__ __forceinline__ bool run_push(int64_t t, uint32_t sq, uint32_t slot) {
         if (c.Cr == 0) return false;
+        uint4 tl[TW_RUNS];
+#pragma unroll
+        for (int j = 0; j < TW_RUNS; ++j) tl[j] = *rqp(RQ_TAIL + j);
+        const uint4 ix4 = *rqp(RQ_IDX);
         int best = -1, empty = -1;
         int64_t bt = 0;
-        uint32_t bs = 0;
+        uint32_t bs = 0, bn = 0, brh = 0;
 #pragma unroll
         for (int j = 0; j < TW_RUNS; ++j) {
-            const uint32_t n = cg(CW_RN + j);
-            const int64_t ut = cg64(CW_UTL + j, CW_UTH + j);
-            const uint32_t us = cg(CW_US + j);
+            const uint32_t n = tl[j].w;
+            const int64_t ut = (int64_t)(((uint64_t)tl[j].y << 32) | tl[j].x);
+            const uint32_t us = tl[j].z;
             const bool e = n == 0 && empty < 0;
             empty = e ? j : empty;
             const bool ok = n != 0 && n < c.Cr && !tless(t, sq, ut, us) && (best < 0 || tless(bt, bs, ut, us));
             best = ok ? j : best;
             bt = ok ? ut : bt;
             bs = ok ? us : bs;
+            bn = ok ? n : bn;
+            brh = ok ? q_at(ix4, j) : brh;
         }
+        if (best < 0 && empty >= 0) { bn = 0; brh = q_at(ix4, empty); }
         const int sel = best >= 0 ? best : empty;
         if (sel < 0) return false;
         STAT(K_RUN_PUSH);
-        const uint32_t n = cg(CW_RN + sel);
-        uint32_t pos = cg(CW_RH + sel) + n;
+        uint32_t pos = brh + bn;
         if (pos >= c.Cr) pos -= c.Cr;
         const uint4 e = ent(t, slot, sq);
         *run_at(sel, pos) = e;
-        if (n == 0) {
-            cs(CW_RTL + sel, e.x); cs(CW_RTH + sel, e.y); cs(CW_RS + sel, sq); cs(CW_RSL + sel, slot);
-            far_dirty = true;
-        } else if (n == 1) {
-            cs(CW_R2TL + sel, e.x); cs(CW_R2TH + sel, e.y); cs(CW_R2S + sel, sq); cs(CW_R2SL + sel, slot);
-        }
-        cs(CW_UTL + sel, e.x); cs(CW_UTH + sel, e.y); cs(CW_US + sel, sq);
-        cs(CW_RN + sel, n + 1);
+        if (bn == 0) { *rqp(RQ_HEAD + sel) = e; far_dirty = true; }
+        else if (bn == 1) *rqp(RQ_SEC + sel) = e;
+        *rqp(RQ_TAIL + sel) = make_uint4(e.x, e.y, sq, bn + 1);
         return true;
     }
-    // The head moves to the second entry; the entry after it is loaded now and
-    // committed at the next run access, a whole event before it can be the head.
+    // The head moves to the second entry; the entry after it is loaded now, by
+    // LDS-DMA into staging quad 4, and committed before the store tail.
     __device__ __forceinline__ void run_pop(int sel) {
         run_commit();
         far_dirty = true;
-        uint32_t h = cg(CW_RH + sel) + 1;
+        uint4 ix4 = *rqp(RQ_IDX);
+        uint32_t h = q_at(ix4, sel) + 1;
         h = h == c.Cr ? 0 : h;
-        cs(CW_RH + sel, h);
-        cs(CW_RTL + sel, cg(CW_R2TL + sel)); cs(CW_RTH + sel, cg(CW_R2TH + sel));
-        cs(CW_RS + sel, cg(CW_R2S + sel)); cs(CW_RSL + sel, cg(CW_R2SL + sel));
-        const uint32_t n = cg(CW_RN + sel) - 1;
-        cs(CW_RN + sel, n);
+        ix4.x = sel == 0 ? h : ix4.x; ix4.y = sel == 1 ? h : ix4.y;
+        ix4.z = sel == 2 ? h : ix4.z; ix4.w = sel == 3 ? h : ix4.w;
+        *rqp(RQ_IDX) = ix4;
+        *rqp(RQ_HEAD + sel) = *rqp(RQ_SEC + sel);
+        uint4 tl = *rqp(RQ_TAIL + sel);
+        const uint32_t n = --tl.w;
+        *rqp(RQ_TAIL + sel) = tl;
         if (n >= 2) {
             const uint32_t p2 = h + 1 == c.Cr ? 0 : h + 1;
             // into LDS staging quad 4 (no register left pending across the step)
@@ -598,19 +598,20 @@ struct Lane {
     }
     __device__ __forceinline__ void far_min() {  // heads only: a pending second entry is not needed
         far_dirty = false;
+        uint4 hd[TW_RUNS], tl[TW_RUNS];
+#pragma unroll
+        for (int j = 0; j < TW_RUNS; ++j) { hd[j] = *rqp(RQ_HEAD + j); tl[j] = *rqp(RQ_TAIL + j); }
         fsrc = -1;
         fmt = 0; fms = 0; fmsl = 0;
         if (far_n) { fsrc = TW_RUNS; fmt = cg64(CW_FTL, CW_FTH); fms = cg(CW_FS); fmsl = cg(CW_FSL); }
 #pragma unroll
         for (int j = 0; j < TW_RUNS; ++j) {
-            const uint32_t n = cg(CW_RN + j);
-            const int64_t t = cg64(CW_RTL + j, CW_RTH + j);
-            const uint32_t s = cg(CW_RS + j);
-            const bool b = n != 0 && (fsrc < 0 || tless(t, s, fmt, fms));
+            const int64_t t = ent_t(hd[j]);
+            const bool b = tl[j].w != 0 && (fsrc < 0 || tless(t, hd[j].w, fmt, fms));
             fsrc = b ? j : fsrc;
             fmt = b ? t : fmt;
-            fms = b ? s : fms;
-            fmsl = b ? cg(CW_RSL + j) : fmsl;
+            fms = b ? hd[j].w : fms;
+            fmsl = b ? hd[j].z : fmsl;
         }
     }
     __device__ __forceinline__ void push_far(int64_t t, uint32_t sq, uint32_t slot) {
@@ -817,7 +818,7 @@ struct Lane {
         uint32_t s = alloc_slot();
         if (s == 0xFFFFFFFFu) return false;
         uint32_t tid = tidc++;
-        cinc(CW_TH);
+        ++d_th;
         ch.w0 = pc & 0xFFFFu;
         ch.w1 = node;
         ch.w2 = tid;
@@ -1129,7 +1130,7 @@ struct Lane {
                                 hash_add(th.w1, term0(now, TW_KIND_RESUME | TW_PC_DELIVER_STUB) +
                                                     term0(ta, TW_KIND_RESUME | (TW_PC_DELIVER_STUB + 1)));
                                 d_ev += 2;
-                                cinc(CW_TH);
+                                ++d_th;
                                 final_t = ta > final_t ? ta : final_t;
                                 emit(ta, payload, (uint32_t)link, kind, th.w1, gp(c.link_dst)[link]);
                                 yt = now + 1;
@@ -1337,8 +1338,8 @@ __global__ void __launch_bounds__(TW_WG) tw_init_kernel(Dev c, uint32_t main_pc,
 // files, the cold words, then the program image and constant pool, so
 // instruction fetch and time constants never leave the CU.
 __host__ __device__ constexpr size_t fixed_lds_bytes() {
-    return (size_t)5 * TW_WG * 16 + (size_t)TW_NEAR_CAP * TW_WG * 12 + (size_t)4 * TW_WG * 8 +
-           (size_t)CW_COUNT * TW_WG * 4;
+    return (size_t)5 * TW_WG * 16 + (size_t)RQ_COUNT * TW_WG * 16 + (size_t)TW_NEAR_CAP * TW_WG * 12 +
+           (size_t)4 * TW_WG * 8 + (size_t)CW_COUNT * TW_WG * 4;
 }
 
 template <bool LP>
@@ -1346,7 +1347,8 @@ __global__ void __launch_bounds__(TW_WG) __attribute__((amdgpu_waves_per_eu(1, 2
 tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
     extern __shared__ __attribute__((aligned(16))) uint64_t lds_raw[];
     uint4 LAS* s_pf = (uint4 LAS*)lds_raw;
-    uint64_t LAS* s_k = (uint64_t LAS*)(s_pf + 5 * TW_WG);
+    uint4 LAS* s_rq = s_pf + 5 * TW_WG;
+    uint64_t LAS* s_k = (uint64_t LAS*)(s_rq + RQ_COUNT * TW_WG);
     int64_t LAS* s_rf = (int64_t LAS*)(s_k + TW_NEAR_CAP * TW_WG);
     uint32_t LAS* s_s = (uint32_t LAS*)(s_rf + 4 * TW_WG);
     uint32_t LAS* s_cw = s_s + TW_NEAR_CAP * TW_WG;
@@ -1376,6 +1378,7 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
     L.rf = s_rf + threadIdx.x;
     L.cw = s_cw + threadIdx.x;
     L.pfs = s_pf + threadIdx.x;
+    L.rq = s_rq + threadIdx.x;
     L.pfs_wave = __builtin_amdgcn_readfirstlane((uint32_t)(size_t)(s_pf + (threadIdx.x & ~63u)));
     L.P = s_p;
     L.PU = s_u;
@@ -1397,25 +1400,27 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
     const uint64_t ev_room64 = max_events > events0 ? max_events - events0 : 0;
     const uint32_t ev_room = ev_room64 > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)ev_room64;
     L.d_ev = 0;
+    L.d_th = 0;
     if (L.far_n) L.set_ftop(L.far_ld(0));
+    {
+        uint32_t rh4[TW_RUNS];
 #pragma unroll
-    for (int j = 0; j < TW_RUNS; ++j) {
-        const uint32_t rh = (uint32_t)sc[(SC_RH0 + j) * R], rn = (uint32_t)sc[(SC_RC0 + j) * R];
-        L.cs(CW_RH + j, rh);
-        L.cs(CW_RN + j, rn);
-        if (rn) {
-            uint4 h = *L.run_at(j, rh);
-            uint32_t tp = rh + rn - 1;
-            if (tp >= c.Cr) tp -= c.Cr;
-            uint4 u = *L.run_at(j, tp);
-            L.cs(CW_RTL + j, h.x); L.cs(CW_RTH + j, h.y); L.cs(CW_RS + j, h.w); L.cs(CW_RSL + j, h.z);
-            L.cs(CW_UTL + j, u.x); L.cs(CW_UTH + j, u.y); L.cs(CW_US + j, u.w);
-            if (rn >= 2) {
-                uint32_t p2 = rh + 1 == c.Cr ? 0 : rh + 1;
-                uint4 s2 = *L.run_at(j, p2);
-                L.cs(CW_R2TL + j, s2.x); L.cs(CW_R2TH + j, s2.y); L.cs(CW_R2S + j, s2.w); L.cs(CW_R2SL + j, s2.z);
+        for (int j = 0; j < TW_RUNS; ++j) {
+            const uint32_t rh = (uint32_t)sc[(SC_RH0 + j) * R], rn = (uint32_t)sc[(SC_RC0 + j) * R];
+            rh4[j] = rh;
+            uint4 h = make_uint4(0, 0, 0, 0), s2 = h, u = h;
+            if (rn) {
+                h = *L.run_at(j, rh);
+                uint32_t tp = rh + rn - 1;
+                if (tp >= c.Cr) tp -= c.Cr;
+                u = *L.run_at(j, tp);
+                if (rn >= 2) s2 = *L.run_at(j, rh + 1 == c.Cr ? 0 : rh + 1);
             }
+            *L.rqp(RQ_HEAD + j) = h;
+            *L.rqp(RQ_SEC + j) = s2;
+            *L.rqp(RQ_TAIL + j) = make_uint4(u.x, u.y, u.w, rn);
         }
+        *L.rqp(RQ_IDX) = make_uint4(rh4[0], rh4[1], rh4[2], rh4[3]);
     }
     L.far_min();
     // near heap: re-inserted from the spill area (keys are relative to this launch's base)
@@ -1600,11 +1605,14 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
     sc[SC_TMO_CTR * R] = L.cg(CW_TMO);
     sc[SC_EVENTS * R] = events0 + L.d_ev;
     sc[SC_DELIVERED * R] += L.cg(CW_DL); sc[SC_DROPPED * R] += L.cg(CW_DR);
-    sc[SC_UNDELIV * R] += L.cg(CW_UD); sc[SC_THREADS * R] += L.cg(CW_TH);
+    sc[SC_UNDELIV * R] += L.cg(CW_UD); sc[SC_THREADS * R] += L.d_th;
+    {
+        const uint4 ix4 = *L.rqp(RQ_IDX);
 #pragma unroll
-    for (int j = 0; j < TW_RUNS; ++j) {
-        sc[(SC_RH0 + j) * R] = L.cg(CW_RH + j);
-        sc[(SC_RC0 + j) * R] = L.cg(CW_RN + j);
+        for (int j = 0; j < TW_RUNS; ++j) {
+            sc[(SC_RH0 + j) * R] = Lane<LP>::q_at(ix4, j);
+            sc[(SC_RC0 + j) * R] = L.rqp(RQ_TAIL + j)->w;
+        }
     }
     for (uint32_t i = 0, j = 0; i < TW_NEAR_CAP; ++i) {
         const uint64_t k = L.nk[i * TW_WG];
