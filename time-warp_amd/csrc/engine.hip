@@ -158,6 +158,8 @@ struct Dev {
     uint64_t* hash;      // [N][R]
     uint32_t* bind;      // [N][R] 0 or set+1
     uint32_t* bind_own;  // [N][R] owner tid or 0xFFFFFFFF
+    uint32_t* bind_rel;  // [N][R] tid of the last owner that died (0xFFFFFFFE: none); the
+                         // binding is live iff bind != 0 && bind_own != bind_rel
     uint32_t* link_ord;  // [L][R]
     uint8_t* tmo_done;   // [T][R]
     uint32_t* n_active;  // [1]
@@ -866,25 +868,17 @@ struct Lane {
     // Thread ends (END or uncaught exception): listener release, ref
     // invalidation, slot freed; the caller stores the header quad.
     __device__ __forceinline__ void die_prep(Th& th, uint32_t slot) {
-        if (th_flags(th) & F_OWNS) {
-            uint32_t node = th.w1;
-            if (gp(c.bind_own)[bix(node)] == th.w2) {
-                gp(c.bind)[bix(node)] = 0;
-                gp(c.bind_own)[bix(node)] = 0xFFFFFFFFu;
-            }
-        }
+        // an owned listener (token-ring `serve`) is released when its thread
+        // dies: recorded with a store, no read (DELIVER compares the owner)
+        if (th_flags(th) & F_OWNS) gp(c.bind_rel)[bix(th.w1)] = th.w2;
         th.w2 = 0xFFFFFFFFu;  // invalidate refs to this slot
         th.w3 = 0;
         free_slot(slot);
     }
     __device__ __forceinline__ void die(Th& th, uint32_t slot) {
-        if (th_flags(th) & F_OWNS) {
-            uint32_t node = th.w1;
-            if (gp(c.bind_own)[bix(node)] == th.w2) {
-                gp(c.bind)[bix(node)] = 0;
-                gp(c.bind_own)[bix(node)] = 0xFFFFFFFFu;
-            }
-        }
+        // an owned listener (token-ring `serve`) is released when its thread
+        // dies: recorded with a store, no read (DELIVER compares the owner)
+        if (th_flags(th) & F_OWNS) gp(c.bind_rel)[bix(th.w1)] = th.w2;
         th.w2 = 0xFFFFFFFFu;  // invalidate refs to this slot
         th.w3 = 0;
         put_hdr(slot, th);
@@ -1151,7 +1145,9 @@ struct Lane {
                     const uint64_t link = (uint64_t)r1;
                     const uint32_t kind = (uint32_t)r3;
                     const uint32_t dst = gp(c.link_dst)[link];
-                    const uint32_t set = gp(c.bind)[bix(dst)];
+                    const uint32_t set0 = gp(c.bind)[bix(dst)];
+                    const uint32_t own = gp(c.bind_own)[bix(dst)], rel = gp(c.bind_rel)[bix(dst)];
+                    const uint32_t set = own == rel ? 0u : set0;  // owner died: released
                     uint32_t lpc = TW_PC_NONE;
                     if (set && kind < c.n_kinds) lpc = gp(c.lpc)[(size_t)(set - 1) * c.n_kinds + kind];
                     if (lpc == TW_PC_NONE) {
@@ -1323,13 +1319,17 @@ __global__ void __launch_bounds__(TW_WG) tw_init_kernel(Dev c, uint32_t main_pc,
         if (nv_init)
             for (uint32_t i = 0; i < 4; ++i) gp(c.nvars)[(size_t)i * c.R + r] = nv_init[(size_t)g * 4 + i];
         gp(c.bind_own)[r] = 0xFFFFFFFFu;
+        gp(c.bind_rel)[r] = 0xFFFFFFFEu;
         if (listen_init) gp(c.bind)[r] = listen_init[g];
         gp(c.inbox_n)[r] = 0;
         return;
     }
     if (nv_init)
         for (uint32_t i = 0; i < c.N * 4; ++i) gp(c.nvars)[(size_t)i * c.R + r] = nv_init[i];
-    for (uint32_t n = 0; n < c.N; ++n) gp(c.bind_own)[(size_t)n * c.R + r] = 0xFFFFFFFFu;
+    for (uint32_t n = 0; n < c.N; ++n) {
+        gp(c.bind_own)[(size_t)n * c.R + r] = 0xFFFFFFFFu;
+        gp(c.bind_rel)[(size_t)n * c.R + r] = 0xFFFFFFFEu;
+    }
     if (listen_init)
         for (uint32_t n = 0; n < c.N; ++n) gp(c.bind)[(size_t)n * c.R + r] = listen_init[n];
 }
@@ -1843,6 +1843,7 @@ static int load_common(tw_ctx* c, const tw_scenario_desc* s, bool lp, uint32_t l
     ALLOC(d.hash, (size_t)d.N * R);
     ALLOC(d.bind, (size_t)d.N * R);
     ALLOC(d.bind_own, (size_t)d.N * R);
+    ALLOC(d.bind_rel, (size_t)d.N * R);
     ALLOC(d.link_ord, (size_t)(d.L ? d.L : 1) * (lp ? 1 : R));
     ALLOC(d.tmo_done, (size_t)(d.T ? d.T : 1) * R);
     ALLOC(d.n_active, 1);
