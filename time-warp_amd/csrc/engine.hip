@@ -472,19 +472,55 @@ struct Lane {
     __device__ __forceinline__ void set_ftop(uint4 e) const {
         cs(CW_FTL, e.x); cs(CW_FTH, e.y); cs(CW_FS, e.w); cs(CW_FSL, e.z);
     }
+    // Heaps of up to TW_FAR_FAST entries are at most TW_FAR_D levels deep below
+    // the root; their sift code reads before it writes: a push reads every
+    // ancestor in one batch of independent loads, a pop walks down with loads
+    // only, and the moves are stored at the end.  (A load waits for every older
+    // store of the wave -- interleaving them would add a store round trip to
+    // every level.)  Larger heaps take the plain loops.
+#define TW_FAR_D 8
+#define TW_FAR_FAST 87380u  // indices below (4^9 - 1) / 3 have at most 8 ancestors
     __device__ __forceinline__ void far_push(int64_t t, uint32_t sq, uint32_t slot) {
         if (far_n >= c.Q) { fail(TW_REP_ERR_QUEUE); return; }
         STAT(K_FAR_PUSH);
-        uint32_t i = far_n++;
-        while (i > 0) {
-            uint32_t p = (i - 1) >> 2;
-            uint4 e = far_ld(p);
-            if (!tless(t, sq, ent_t(e), e.w)) break;
+        const uint32_t i0 = far_n++;
+        const uint4 e = ent(t, slot, sq);
+        if (c.Q > TW_FAR_FAST) {
+            uint32_t i = i0;
+            while (i > 0) {
+                uint32_t p = (i - 1) >> 2;
+                uint4 q = far_ld(p);
+                if (!tless(t, sq, ent_t(q), q.w)) break;
+                far_st(i, q);
+                i = p;
+            }
             far_st(i, e);
-            i = p;
+            if (i == 0) { set_ftop(e); far_dirty = true; }
+            return;
         }
-        far_st(i, ent(t, slot, sq));
-        if (i == 0) { set_ftop(ent(t, slot, sq)); far_dirty = true; }
+        uint32_t a[TW_FAR_D];
+        bool v[TW_FAR_D];
+        uint4 q[TW_FAR_D];
+        uint32_t cur = i0;
+#pragma unroll
+        for (int k = 0; k < TW_FAR_D; ++k) {
+            v[k] = cur > 0;
+            a[k] = v[k] ? (cur - 1) >> 2 : 0u;
+            cur = a[k];
+        }
+#pragma unroll
+        for (int k = 0; k < TW_FAR_D; ++k) q[k] = far_ld(a[k]);
+        uint32_t hole = i0;
+        bool go = true;
+#pragma unroll
+        for (int k = 0; k < TW_FAR_D; ++k) {
+            const bool mv = go && v[k] && tless(t, sq, ent_t(q[k]), q[k].w);
+            if (mv) far_st(hole, q[k]);
+            hole = mv ? a[k] : hole;
+            go = mv;
+        }
+        far_st(hole, e);
+        if (hole == 0) { set_ftop(e); far_dirty = true; }
     }
     __device__ __forceinline__ void far_pop() {
         uint32_t n = --far_n;
@@ -492,27 +528,63 @@ struct Lane {
         if (n == 0) return;
         uint4 le = far_ld(n);
         int64_t t = ent_t(le);
-        uint32_t i = 0;
-        for (;;) {
-            uint32_t c0 = 4 * i + 1;
-            if (c0 >= n) break;
-            uint32_t cn = n - c0 < 4 ? n - c0 : 4;
-            uint4 e0 = far_ld(c0);
-            uint4 e1 = cn > 1 ? far_ld(c0 + 1) : e0;
-            uint4 e2 = cn > 2 ? far_ld(c0 + 2) : e0;
-            uint4 e3 = cn > 3 ? far_ld(c0 + 3) : e0;
+        if (c.Q > TW_FAR_FAST) {
+            uint32_t i = 0;
+            for (;;) {
+                uint32_t c0 = 4 * i + 1;
+                if (c0 >= n) break;
+                uint32_t cn = n - c0 < 4 ? n - c0 : 4;
+                uint4 e0 = far_ld(c0);
+                uint4 e1 = cn > 1 ? far_ld(c0 + 1) : e0;
+                uint4 e2 = cn > 2 ? far_ld(c0 + 2) : e0;
+                uint4 e3 = cn > 3 ? far_ld(c0 + 3) : e0;
+                uint4 b = e0;
+                uint32_t best = 0;
+                if (cn > 1 && tless(ent_t(e1), e1.w, ent_t(b), b.w)) { b = e1; best = 1; }
+                if (cn > 2 && tless(ent_t(e2), e2.w, ent_t(b), b.w)) { b = e2; best = 2; }
+                if (cn > 3 && tless(ent_t(e3), e3.w, ent_t(b), b.w)) { b = e3; best = 3; }
+                if (!tless(ent_t(b), b.w, t, le.w)) break;
+                far_st(i, b);
+                if (i == 0) set_ftop(b);
+                i = c0 + best;
+            }
+            far_st(i, le);
+            if (i == 0) set_ftop(le);
+            return;
+        }
+        // walk down with loads only; the moves (entry mk[k] into position pk[k]) are stored after
+        uint32_t pk[TW_FAR_D];
+        uint4 mk[TW_FAR_D];
+        bool mvk[TW_FAR_D];
+        uint32_t hole = 0;
+        bool go = true;
+#pragma unroll
+        for (int k = 0; k < TW_FAR_D; ++k) {
+            const uint32_t c0 = 4 * hole + 1;
+            const bool ok = go && c0 < n;
+            const uint32_t b0 = ok ? c0 : 0u;
+            const uint32_t cn = !ok ? 0u : (n - c0 < 4 ? n - c0 : 4u);
+            const uint4 e0 = far_ld(b0);
+            const uint4 e1 = far_ld(cn > 1 ? b0 + 1 : b0);
+            const uint4 e2 = far_ld(cn > 2 ? b0 + 2 : b0);
+            const uint4 e3 = far_ld(cn > 3 ? b0 + 3 : b0);
             uint4 b = e0;
             uint32_t best = 0;
             if (cn > 1 && tless(ent_t(e1), e1.w, ent_t(b), b.w)) { b = e1; best = 1; }
             if (cn > 2 && tless(ent_t(e2), e2.w, ent_t(b), b.w)) { b = e2; best = 2; }
             if (cn > 3 && tless(ent_t(e3), e3.w, ent_t(b), b.w)) { b = e3; best = 3; }
-            if (!tless(ent_t(b), b.w, t, le.w)) break;
-            far_st(i, b);
-            if (i == 0) set_ftop(b);
-            i = c0 + best;
+            const bool mv = ok && tless(ent_t(b), b.w, t, le.w);
+            pk[k] = hole;
+            mk[k] = b;
+            mvk[k] = mv;
+            hole = mv ? c0 + best : hole;
+            go = mv;
         }
-        far_st(i, le);
-        if (i == 0) set_ftop(le);
+#pragma unroll
+        for (int k = 0; k < TW_FAR_D; ++k)
+            if (mvk[k]) far_st(pk[k], mk[k]);
+        far_st(hole, le);
+        set_ftop(mvk[0] ? mk[0] : le);
     }
 
     // ---------------------------------------------------- far runs (HBM FIFOs)

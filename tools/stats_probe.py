@@ -36,16 +36,23 @@ def read(eng):
 
 
 def main():
-    R = int(sys.argv[1]) if len(sys.argv) > 1 else 65536
-    N = int(sys.argv[2]) if len(sys.argv) > 2 else 4096
-    Ld = 120_000_000
-    scn = scenarios.token_ring(n_nodes=N, n_replicas=R, launch_duration=Ld, drop_log2=10)
+    if len(sys.argv) > 1 and sys.argv[1] == "hotspot":  # config 5: one phase per 0.25 s of virtual time
+        R = int(sys.argv[2]) if len(sys.argv) > 2 else 4096
+        S = int(sys.argv[3]) if len(sys.argv) > 3 else 256
+        scn = scenarios.hotspot(n_senders=S, n_replicas=R, msg_num=1000)
+        phases = [("t<0.25s", 249_999), ("t<0.5s", 499_999), ("t<1s", 999_999), ("rest", (1 << 63) - 1)]
+    else:
+        R = int(sys.argv[1]) if len(sys.argv) > 1 else 65536
+        N = int(sys.argv[2]) if len(sys.argv) > 2 else 4096
+        Ld = 120_000_000
+        scn = scenarios.token_ring(n_nodes=N, n_replicas=R, launch_duration=Ld, drop_log2=10)
+        phases = [("startup<1s", 999_999), ("token<L", Ld - 1), ("teardown", (1 << 63) - 1)]
     eng = Engine(0).load(scn)
     if not hasattr(eng.lib, "tw_prof_read"):
         raise SystemExit("TW_LIB is not the diagnostic build (tw_prof_read missing)")
     read(eng)
     eng.reset()
-    for name, t_end in [("startup<1s", 999_999), ("token<L", Ld - 1), ("teardown", (1 << 63) - 1)]:
+    for name, t_end in phases:
         st = eng.run(t_end=t_end)
         d = read(eng)
         ms = float(eng.launch_ms().sum())
