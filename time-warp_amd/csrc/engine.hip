@@ -1016,8 +1016,17 @@ struct Lane {
         for (;;) {
             const uint64_t mask = __builtin_amdgcn_ballot_w64(running);
             if (mask == 0) break;
-            const uint32_t upc = __builtin_amdgcn_readlane(pc, (uint32_t)__builtin_ctzll(mask));
-            const bool at = running && pc == upc;
+            // every lane fetches its own instruction; the pass runs the first running
+            // lane's opcode in all lanes holding that opcode (their operands and
+            // immediates stay per lane), so divergent lanes at different pcs still
+            // share a pass when they execute the same kind of instruction
+            const uint32_t lpc = pc < c.n_insns ? pc : c.n_insns;  // image padded by one NOP
+            const uint2 in = P[lpc];
+            const uint32_t lfl = PU[lpc];
+            const uint32_t first = (uint32_t)__builtin_ctzll(mask);
+            const uint32_t op = __builtin_amdgcn_readlane(in.x, first) & 0xFFu;
+            const uint32_t fl = __builtin_amdgcn_readlane(lfl, first);
+            const bool at = running && (in.x & 0xFFu) == op;
 #ifndef TW_X_NOCAP
             n += at ? 1u : 0u;
             const bool capped = at && n > TW_STEP_CAP;  // TW_REP_ERR_INSN before executing it
@@ -1025,16 +1034,14 @@ struct Lane {
             const bool capped = false;
 #endif
             const bool me = at && !capped;
-            const uint2 in = P[upc];
-            const uint32_t fl = __builtin_amdgcn_readfirstlane(PU[upc]);
-            const uint32_t uw = __builtin_amdgcn_readfirstlane(in.x);
-            const int32_t imm = (int32_t)__builtin_amdgcn_readfirstlane(in.y);
-            const uint32_t op = uw & 0xFFu, a = (uw >> 8) & 3u, b = uw >> 16;
+            const uint32_t uw = in.x;
+            const int32_t imm = (int32_t)in.y;
+            const uint32_t a = (uw >> 8) & 3u, b = uw >> 16;
             STAT(K_INSN);
             const int64_t ra = rf[a * TW_WG];
             const int64_t rb = rf[(b & 3u) * TW_WG];
             uint32_t tc = T_NONE;     // per lane: terminal action of this op
-            uint32_t tgt = upc + 1;   // per lane: next pc
+            uint32_t tgt = pc + 1;    // per lane: next pc
             bool wr = false;          // uniform: the op writes r[a]
             bool wm = me;             // per lane: ... in this lane
             int64_t wv = 0;
@@ -1096,7 +1103,7 @@ struct Lane {
                 break;
             case TW_OP_THROW:
                 if (me) {
-                    th_set_pc(th, upc + 1);
+                    th_set_pc(th, pc + 1);
                     if (unwind(th, slot, b & 0xFFu, rf[((b >> 8) & 3u) * TW_WG])) tgt = th_pc(th);
                     else tc = T_DIED;  // died: record stored
                 }
@@ -1302,6 +1309,7 @@ struct Lane {
             }
             }  // U_FX
             if (wr) rf[a * TW_WG] = wm ? wv : ra;
+            (void)lfl;
             if (thr_any) {
                 if (thr) throw_to(th, slot, tref, tcode, tval);
             }
