@@ -808,16 +808,22 @@ struct Lane {
                      "s"(pfs_wave + 3 * TW_WG * 16) : "memory", "m0");
         pf_slot = valid ? s : 0xFFFFFFFFu;
     }
-    // The popped thread's record: the prefetched copy, or (rarely) a fresh load.
+    // The popped thread's record: the prefetched copy, or (rarely) a fresh load
+    // that the missing lane copies into its own staging quads first.  Every
+    // lane then reads the staging quads, so no register stays pending on a
+    // load across the merge (which made the compiler wait vmcnt(0) -- for the
+    // previous iteration's store tail too -- on the common path).
     __device__ __forceinline__ void fetch_rec(uint32_t slot, Th& th) {
-        if (slot == pf_slot) {
-            STAT(K_PEEK_PF);
-            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(TW_TAIL_VMEM) : "memory");
-            unpack(th, pfs[0], pfs[TW_WG], pfs[2 * TW_WG], pfs[3 * TW_WG]);
-        } else {
+        if (slot != pf_slot) {
             STAT(K_PEEK_HBM);
-            hbm_load(slot, th);
+            const uint4 GAS* p = hrec(slot);
+            const uint4 a = p[0], b = p[1], d = p[2], e = p[3];
+            pfs[0] = a; pfs[TW_WG] = b; pfs[2 * TW_WG] = d; pfs[3 * TW_WG] = e;
+        } else {
+            STAT(K_PEEK_PF);
         }
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(TW_TAIL_VMEM) : "memory");
+        unpack(th, pfs[0], pfs[TW_WG], pfs[2 * TW_WG], pfs[3 * TW_WG]);
     }
 
     // Free slots: never-used slots come from a bump pointer (no memory read);
