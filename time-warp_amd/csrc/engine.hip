@@ -56,7 +56,7 @@
 #define LAS
 #endif
 
-#define P_COUNT 24
+#define P_COUNT 28
 // Diagnostic build (-DTW_STATS, lib/libtimewarp_stats.so): per-lane event-path
 // counters summed into Dev::prof at kernel end (tools/stats_probe.py).  The
 // product build compiles every STAT to nothing.
@@ -69,7 +69,8 @@
 #endif
 enum { K_POP, K_SUPERSEDED, K_PEEK_PF, K_PEEK_HBM, K_PUT_HBM, K_PUT_DEAD, K_PF_ISSUE, K_HASH_IMM, K_HASH_FLUSH,
        K_NEAR_PUSH, K_RUN_PUSH, K_FAR_PUSH, K_INSN, K_CYC_POP, K_CYC_INTERP, K_CYC_TAIL,
-       K_CYC_SEL, K_CYC_FETCH, K_CYC_QPOP, K_CYC_COMMIT, K_CYC_PF, K_CYC_TERM, K_CYC_STORE, K_CYC_HASH };
+       K_CYC_SEL, K_CYC_FETCH, K_CYC_QPOP, K_CYC_COMMIT, K_CYC_PF, K_CYC_TERM, K_CYC_STORE, K_CYC_HASH,
+       K_CYC_SPAWN, K_CYC_ENQ, K_SPAWN, K_ALLOC_LD };
 #ifdef TW_STATS
 #define STIME(v) const uint64_t v = __builtin_amdgcn_s_memtime()
 #define STADD(i, v) (st[(i)] += (uint32_t)(v))
@@ -229,38 +230,42 @@ enum {
 enum : uint32_t {
     A_NONE, A_IMM, A_K, A_ADDI, A_MULI, A_MOV, A_ADD, A_SUB, A_NOW, A_NODE, A_TID,  // r[a] <- ...
 };
-enum : uint32_t { J_NONE, J_ALWAYS, J_EQ, J_NE, J_LT, J_LE, J_EQI, J_NEI };      // pc <- imm if ...
 enum : uint32_t { TK_NONE, TK_WREL, TK_WABS, TK_WREG, TK_EXIT, TK_FORK };          // the step ends with ...
+// Jumps are an 8-entry truth table over (r[a]==r[b], r[a]<r[b], r[a]==simm16),
+// indexed by those three bits: `pc <- imm` is a shift and a select, no branch.
+enum : uint32_t {
+    JM_NONE = 0x00, JM_ALWAYS = 0xFF, JM_EQ = 0xAA, JM_NE = 0x55, JM_LT = 0xCC, JM_LE = 0xEE, JM_EQI = 0xF0, JM_NEI = 0x0F
+};
 #define U_ALU(f) ((f) & 0xFu)
-#define U_J(f) (((f) >> 4) & 7u)
 #define U_TK(f) (((f) >> 8) & 7u)
 #define U_FX (1u << 12)
+#define U_JM(f) (((f) >> 16) & 0xFFu)
 __device__ __forceinline__ uint32_t uop_of(uint32_t op) {
-    auto u = [](uint32_t alu, uint32_t j, uint32_t tk) { return alu | (j << 4) | (tk << 8); };
+    auto u = [](uint32_t alu, uint32_t jm, uint32_t tk) { return alu | (tk << 8) | (jm << 16); };
     switch (op) {
     case TW_OP_NOP: return 0;
-    case TW_OP_END: return u(A_NONE, J_NONE, TK_EXIT);
-    case TW_OP_WAIT_REL: return u(A_NONE, J_NONE, TK_WREL);
-    case TW_OP_WAIT_ABS: return u(A_NONE, J_NONE, TK_WABS);
-    case TW_OP_WAIT_REG: return u(A_NONE, J_NONE, TK_WREG);
-    case TW_OP_FORK: return u(A_NONE, J_NONE, TK_FORK);
-    case TW_OP_MYTID: return u(A_TID, J_NONE, TK_NONE);
-    case TW_OP_SETI: return u(A_IMM, J_NONE, TK_NONE);
-    case TW_OP_SETK: return u(A_K, J_NONE, TK_NONE);
-    case TW_OP_ADDI: return u(A_ADDI, J_NONE, TK_NONE);
-    case TW_OP_MULI: return u(A_MULI, J_NONE, TK_NONE);
-    case TW_OP_MOV: return u(A_MOV, J_NONE, TK_NONE);
-    case TW_OP_ADD: return u(A_ADD, J_NONE, TK_NONE);
-    case TW_OP_SUB: return u(A_SUB, J_NONE, TK_NONE);
-    case TW_OP_JMP: return u(A_NONE, J_ALWAYS, TK_NONE);
-    case TW_OP_JEQ: return u(A_NONE, J_EQ, TK_NONE);
-    case TW_OP_JNE: return u(A_NONE, J_NE, TK_NONE);
-    case TW_OP_JLT: return u(A_NONE, J_LT, TK_NONE);
-    case TW_OP_JLE: return u(A_NONE, J_LE, TK_NONE);
-    case TW_OP_JEQI: return u(A_NONE, J_EQI, TK_NONE);
-    case TW_OP_JNEI: return u(A_NONE, J_NEI, TK_NONE);
-    case TW_OP_NOW: return u(A_NOW, J_NONE, TK_NONE);
-    case TW_OP_NODE: return u(A_NODE, J_NONE, TK_NONE);
+    case TW_OP_END: return u(A_NONE, JM_NONE, TK_EXIT);
+    case TW_OP_WAIT_REL: return u(A_NONE, JM_NONE, TK_WREL);
+    case TW_OP_WAIT_ABS: return u(A_NONE, JM_NONE, TK_WABS);
+    case TW_OP_WAIT_REG: return u(A_NONE, JM_NONE, TK_WREG);
+    case TW_OP_FORK: return u(A_NONE, JM_NONE, TK_FORK);
+    case TW_OP_MYTID: return u(A_TID, JM_NONE, TK_NONE);
+    case TW_OP_SETI: return u(A_IMM, JM_NONE, TK_NONE);
+    case TW_OP_SETK: return u(A_K, JM_NONE, TK_NONE);
+    case TW_OP_ADDI: return u(A_ADDI, JM_NONE, TK_NONE);
+    case TW_OP_MULI: return u(A_MULI, JM_NONE, TK_NONE);
+    case TW_OP_MOV: return u(A_MOV, JM_NONE, TK_NONE);
+    case TW_OP_ADD: return u(A_ADD, JM_NONE, TK_NONE);
+    case TW_OP_SUB: return u(A_SUB, JM_NONE, TK_NONE);
+    case TW_OP_JMP: return u(A_NONE, JM_ALWAYS, TK_NONE);
+    case TW_OP_JEQ: return u(A_NONE, JM_EQ, TK_NONE);
+    case TW_OP_JNE: return u(A_NONE, JM_NE, TK_NONE);
+    case TW_OP_JLT: return u(A_NONE, JM_LT, TK_NONE);
+    case TW_OP_JLE: return u(A_NONE, JM_LE, TK_NONE);
+    case TW_OP_JEQI: return u(A_NONE, JM_EQI, TK_NONE);
+    case TW_OP_JNEI: return u(A_NONE, JM_NEI, TK_NONE);
+    case TW_OP_NOW: return u(A_NOW, JM_NONE, TK_NONE);
+    case TW_OP_NODE: return u(A_NODE, JM_NONE, TK_NONE);
     default: return U_FX;  // every other opcode (and invalid ones) takes the switch
     }
 }
@@ -832,6 +837,7 @@ struct Lane {
         if (free_n) {
             uint32_t s = ftop;
             if (--free_n) {
+                STAT(K_ALLOC_LD);
                 ftop = gp(c.free_stk)[ix(free_n - 1)];
                 __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): ftop must not stay pending
             }
@@ -1054,8 +1060,10 @@ struct Lane {
             bool thr_any = false, thr = false;  // throwTo after the op (THROW_TO, TMO_FIRE)
             int64_t tref = 0, tval = 0;
             uint32_t tcode = 0;
-            // ---- hot classes: register result, jump, yield/exit/fork (uniform selects)
-            const uint32_t ak = U_ALU(fl), jk = U_J(fl), tk = U_TK(fl);
+            // ---- hot classes: register result, jump, yield/exit/fork, each behind one
+            // wave-uniform branch on its uop field (skipped blocks cost a scalar
+            // branch; computing every class in every pass costs more VALU issue)
+            const uint32_t ak = U_ALU(fl), tk = U_TK(fl), jm = U_JM(fl);
             if (ak != A_NONE) {
                 const int64_t i64 = imm;
                 const int64_t kv = K[ak == A_K ? imm : 0];
@@ -1072,12 +1080,10 @@ struct Lane {
                 wr = true;
                 wv = v;
             }
-            if (jk != J_NONE) {
+            if (jm) {
                 const int64_t b16 = (int64_t)(int16_t)b;
-                const bool cj = jk == J_ALWAYS || (jk == J_EQ && ra == rb) || (jk == J_NE && ra != rb) ||
-                                (jk == J_LT && ra < rb) || (jk == J_LE && ra <= rb) || (jk == J_EQI && ra == b16) ||
-                                (jk == J_NEI && ra != b16);
-                tgt = cj ? (uint32_t)imm : tgt;
+                const uint32_t ci = (ra == rb ? 1u : 0u) | (ra < rb ? 2u : 0u) | (ra == b16 ? 4u : 0u);
+                tgt = ((jm >> ci) & 1u) ? (uint32_t)imm : tgt;
             }
             if (tk != TK_NONE) {
                 if (tk == TK_EXIT) {
@@ -1342,6 +1348,7 @@ struct Lane {
         if (run) th_set_pc(th, pc);
         // fork (TimedT.hs:326-342): the child is queued at now, then the parent waits 1 µs
         if (fin == T_SPAWN) {
+            STAT(K_SPAWN);
             const uint32_t cdel = cg(CW_CDEL), cra = cg(CW_CRA);
             int64_t ref;
             bool ok;
@@ -1366,8 +1373,12 @@ struct Lane {
                 }
             }
         }
+        STIME(tt0a);
+        STADD(K_CYC_SPAWN, tt0a - tt0);
         if (fin == T_YIELD) enqueue(th, slot, yt);
         else if (fin == T_EXIT) die_prep(th, slot);
+        STIME(tt0b);
+        STADD(K_CYC_ENQ, tt0b - tt0a);
         run_commit();
         STIME(tt1);
         STADD(K_CYC_TERM, tt1 - tt0);

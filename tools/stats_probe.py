@@ -22,14 +22,15 @@ from timewarp.engine import Engine  # noqa: E402
 
 NAMES = ["pop", "superseded", "peek_pf", "peek_hbm", "put_hbm", "put_dead", "pf_issue", "hash_imm", "hash_flush",
          "near_push", "run_push", "far_push", "insn", "cyc_pop", "cyc_interp", "cyc_step_and_flush",
-         "cyc_select", "cyc_fetch", "cyc_qpop", "cyc_commit", "cyc_prefetch", "cyc_terminal", "cyc_store", "cyc_hash"]
+         "cyc_select", "cyc_fetch", "cyc_qpop", "cyc_commit", "cyc_prefetch", "cyc_terminal", "cyc_store", "cyc_hash",
+         "cyc_spawn", "cyc_enqueue", "spawn", "alloc_ld"]
 
 
 def read(eng):
-    buf = (C.c_ulonglong * 24)()
+    buf = (C.c_ulonglong * len(NAMES))()
     fn = eng.lib.tw_prof_read
     fn.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]
-    n = fn(eng.ctx, buf, 24, 1)
+    n = fn(eng.ctx, buf, len(NAMES), 1)
     if n < 0:
         raise RuntimeError(f"tw_prof_read: {n}")
     return {k: buf[i] for i, k in enumerate(NAMES)}
