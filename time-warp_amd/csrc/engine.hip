@@ -239,7 +239,10 @@ enum : uint32_t {
 #define U_ALU(f) ((f) & 0xFu)
 #define U_TK(f) (((f) >> 8) & 7u)
 #define U_FX (1u << 12)
+#define U_TR (1u << 13)                // TRACE: a hash term of r[a]
+#define U_LD(f) (((f) >> 14) & 3u)     // table load into r[a]
 #define U_JM(f) (((f) >> 16) & 0xFFu)
+enum : uint32_t { LD_NONE, LD_NV, LD_OUT, LD_RL };  // node var / out-link base / reverse link
 __device__ __forceinline__ uint32_t uop_of(uint32_t op) {
     auto u = [](uint32_t alu, uint32_t jm, uint32_t tk) { return alu | (tk << 8) | (jm << 16); };
     switch (op) {
@@ -266,9 +269,24 @@ __device__ __forceinline__ uint32_t uop_of(uint32_t op) {
     case TW_OP_JNEI: return u(A_NONE, JM_NEI, TK_NONE);
     case TW_OP_NOW: return u(A_NOW, JM_NONE, TK_NONE);
     case TW_OP_NODE: return u(A_NODE, JM_NONE, TK_NONE);
+    case TW_OP_TRACE: return U_TR;
+    case TW_OP_NLOAD: return LD_NV << 14;
+    case TW_OP_LINK: return LD_OUT << 14;
+    case TW_OP_RLINK: return LD_RL << 14;
     default: return U_FX;  // every other opcode (and invalid ones) takes the switch
     }
 }
+
+// A load's result consumed in a branch of the interpreter must not stay
+// "pending" in the compiler's bookkeeping past that branch: the loop header
+// would otherwise wait vmcnt(0) on every pass, i.e. for the record prefetch
+// and the previous store tail.  Paths that load already waited for it.
+__device__ __forceinline__ void tw_vm_drain() { __builtin_amdgcn_s_waitcnt(0x0F70); }
+
+template <bool B>
+struct BoolC {
+    static constexpr bool value = B;
+};
 
 template <bool LP>
 struct Lane {
@@ -1038,7 +1056,11 @@ struct Lane {
             const uint32_t first = (uint32_t)__builtin_ctzll(mask);
             const uint32_t op = __builtin_amdgcn_readlane(in.x, first) & 0xFFu;
             const uint32_t fl = __builtin_amdgcn_readlane(lfl, first);
-            const bool at = running && (in.x & 0xFFu) == op;
+            // a pass of a hot-class op (no U_FX) serves every running lane at any
+            // hot-class op, each with its own uop fields; a rare op serves the
+            // lanes holding that opcode
+            const bool hot = !(fl & U_FX);
+            const bool at = running & ((hot & !(lfl & U_FX)) | (!hot & ((in.x & 0xFFu) == op)));
 #ifndef TW_X_NOCAP
             n += at ? 1u : 0u;
             const bool capped = at && n > TW_STEP_CAP;  // TW_REP_ERR_INSN before executing it
@@ -1060,52 +1082,98 @@ struct Lane {
             bool thr_any = false, thr = false;  // throwTo after the op (THROW_TO, TMO_FIRE)
             int64_t tref = 0, tval = 0;
             uint32_t tcode = 0;
-            // ---- hot classes: register result, jump, yield/exit/fork, each behind one
-            // wave-uniform branch on its uop field (skipped blocks cost a scalar
-            // branch; computing every class in every pass costs more VALU issue)
-            const uint32_t ak = U_ALU(fl), tk = U_TK(fl), jm = U_JM(fl);
-            if (ak != A_NONE) {
-                const int64_t i64 = imm;
-                const int64_t kv = K[ak == A_K ? imm : 0];
-                int64_t v = i64;
-                v = ak == A_K ? kv : v;
-                v = ak == A_ADDI ? ra + i64 : v;
-                v = ak == A_MULI ? ra * i64 : v;
-                v = ak == A_MOV ? rb : v;
-                v = ak == A_ADD ? ra + rb : v;
-                v = ak == A_SUB ? ra - rb : v;
-                v = ak == A_NOW ? now : v;
-                v = ak == A_NODE ? (int64_t)th.w1 : v;
-                v = ak == A_TID ? (int64_t)(((uint64_t)th.w2 << 32) | slot) : v;
-                wr = true;
-                wv = v;
-            }
-            if (jm) {
-                const int64_t b16 = (int64_t)(int16_t)b;
-                const uint32_t ci = (ra == rb ? 1u : 0u) | (ra < rb ? 2u : 0u) | (ra == b16 ? 4u : 0u);
-                tgt = ((jm >> ci) & 1u) ? (uint32_t)imm : tgt;
-            }
-            if (tk != TK_NONE) {
-                if (tk == TK_EXIT) {
-                    tc = T_EXIT;
-                } else if (tk == TK_FORK) {
-                    const uint32_t node = b == 0xFFFFu ? th.w1 : (uint32_t)rb;
-                    const bool bad = LP ? node != th.w1 : node >= c.N;
-                    pfail(me && bad, TW_REP_ERR_INSN);
-                    tc = bad ? T_STOP : T_SPAWN;
-                    const bool p = me && !bad;
-                    csp(p, CW_CPC, (uint32_t)imm);
-                    csp(p, CW_CNODE, node);
-                    csp(p, CW_CRA, a);
-                    csp(p, CW_CDEL, 2u);  // the child's registers are the parent's
-                } else {
-                    const int64_t kt = K[tk == TK_WREG ? 0 : imm];
-                    int64_t w = now + (ra > 0 ? ra : 0);               // wait (for r[a])
-                    w = tk == TK_WREL ? now + kt : w;                    // wait (for K)
-                    w = tk == TK_WABS ? (kt > now ? kt : now) : w;       // wait (till K)
-                    yt = me ? w : yt;
-                    tc = T_YIELD;
+            // ---- hot classes: register result, table load, trace, jump, yield/exit/
+            // fork.  When every lane of the pass holds the same uop (lock-step
+            // lanes) the classes are wave-uniform scalar branches on the first
+            // lane's uop; otherwise each lane evaluates its own uop and a class
+            // runs when some lane needs it (ballot).
+            auto hot_body = [&](auto uni, uint32_t f) {
+                constexpr bool U = decltype(uni)::value;
+                auto need = [&](bool lane_cond) -> bool {
+                    if constexpr (U) return lane_cond;
+                    else return __builtin_amdgcn_ballot_w64(me && lane_cond) != 0;
+                };
+                const uint32_t ak = U_ALU(f), tk = U_TK(f), jm = U_JM(f), ld = U_LD(f);
+                bool lw = false;
+                if (need(ak != A_NONE)) {
+                    const int64_t i64 = imm;
+                    int64_t kv = K[ak == A_K ? imm : 0];
+                    int64_t v = i64;
+                    v = ak == A_ADDI ? ra + i64 : v;
+                    v = ak == A_MULI ? ra * i64 : v;
+                    v = ak == A_MOV ? rb : v;
+                    v = ak == A_ADD ? ra + rb : v;
+                    v = ak == A_SUB ? ra - rb : v;
+                    v = ak == A_NOW ? now : v;
+                    v = ak == A_NODE ? (int64_t)th.w1 : v;
+                    v = ak == A_TID ? (int64_t)(((uint64_t)th.w2 << 32) | slot) : v;
+                    // per-lane mode: keep the pool read unconditional (the compiler would
+                    // otherwise sink it into a divergent region)
+                    if constexpr (!U) asm volatile("" : "+v"(kv));
+                    v = ak == A_K ? kv : v;
+                    wr = true;
+                    lw = ak != A_NONE;
+                    wv = v;
                 }
+                if (need(ld != LD_NONE)) {
+                    // NLOAD r[a] <- var b of this node; LINK r[a] <- out_off[node] + imm;
+                    // RLINK r[a] <- link_rev[r[b]] (an out-of-range link stops the replica)
+                    const bool nv = me && ld == LD_NV, ol = me && ld == LD_OUT, rl = me && ld == LD_RL;
+                    const bool bad = rl && (uint64_t)rb >= c.L;
+                    pfail(bad, TW_REP_ERR_INSN);
+                    tc = bad ? (uint32_t)T_STOP : tc;
+                    int64_t v = wv;
+                    if (need(ld == LD_NV)) {
+                        const int64_t x = gp(c.nvars)[nix(nv ? th.w1 : 0u, b & 3)];
+                        v = nv ? x : v;
+                    }
+                    if (need(ld == LD_OUT || ld == LD_RL)) {
+                        const uint32_t GAS* tb = ol ? gp(c.out_off) : gp(c.link_rev);
+                        const uint32_t x = tb[ol ? (size_t)th.w1 : (rl && !bad ? (size_t)rb : 0)];
+                        v = ol ? (int64_t)x + imm : (rl ? (int64_t)x : v);
+                    }
+                    tw_vm_drain();
+                    wr = true;
+                    lw = lw || ((nv || ol || rl) && !bad);
+                    wv = v;
+                }
+                wm = me && lw;
+                if (need((f & U_TR) != 0))  // the popped node's term joins hacc
+                    hacc += (me && (f & U_TR)) ? term(now, TW_KIND_TRACE | ((uint32_t)imm & 0xFFFFu), ra) : 0ull;
+                if (need(jm != JM_NONE)) {
+                    const int64_t b16 = (int64_t)(int16_t)b;
+                    const uint32_t ci = (ra == rb ? 1u : 0u) | (ra < rb ? 2u : 0u) | (ra == b16 ? 4u : 0u);
+                    tgt = ((jm >> ci) & 1u) ? (uint32_t)imm : tgt;
+                }
+                if (need(tk != TK_NONE)) {
+                    tc = tk == TK_EXIT ? (uint32_t)T_EXIT : tc;
+                    if (need(tk == TK_FORK)) {
+                        const bool fk = tk == TK_FORK;
+                        const uint32_t node = b == 0xFFFFu ? th.w1 : (uint32_t)rb;
+                        const bool bad = fk && (LP ? node != th.w1 : node >= c.N);
+                        pfail(me && bad, TW_REP_ERR_INSN);
+                        tc = fk ? (bad ? (uint32_t)T_STOP : (uint32_t)T_SPAWN) : tc;
+                        const bool p = me && fk && !bad;
+                        csp(p, CW_CPC, (uint32_t)imm);
+                        csp(p, CW_CNODE, node);
+                        csp(p, CW_CRA, a);
+                        csp(p, CW_CDEL, 2u);  // the child's registers are the parent's
+                    }
+                    const bool wt = tk == TK_WREL || tk == TK_WABS || tk == TK_WREG;
+                    if (need(wt)) {
+                        int64_t kt = K[(wt && tk != TK_WREG) ? imm : 0];
+                        int64_t w = now + (ra > 0 ? ra : 0);               // wait (for r[a])
+                        if constexpr (!U) asm volatile("" : "+v"(kt));
+                        w = tk == TK_WREL ? now + kt : w;                    // wait (for K)
+                        w = tk == TK_WABS ? (kt > now ? kt : now) : w;       // wait (till K)
+                        yt = (me && wt) ? w : yt;
+                        tc = wt ? (uint32_t)T_YIELD : tc;
+                    }
+                }
+            };
+            if (hot) {
+                if (__builtin_amdgcn_ballot_w64(at && lfl != fl) == 0) hot_body(BoolC<true>{}, fl);
+                else hot_body(BoolC<false>{}, lfl);
             }
             if (fl & U_FX) {
             switch (op) {
@@ -1148,12 +1216,6 @@ struct Lane {
                 wv = m < 0 ? m + imm : m;
                 break;
             }
-            case TW_OP_NLOAD: {
-                const uint32_t node = me ? th.w1 : 0u;  // sanitised address for idle lanes
-                wr = true;
-                wv = gp(c.nvars)[nix(node, b & 3)];
-                break;
-            }
             case TW_OP_NSTORE:
                 if (me) gp(c.nvars)[nix(th.w1, b & 3)] = ra;
                 break;
@@ -1170,21 +1232,7 @@ struct Lane {
                 } else if (ok) {
                     *v = ra;
                 }
-                break;
-            }
-            case TW_OP_LINK: {
-                const uint32_t node = me ? th.w1 : 0u;
-                wr = true;
-                wv = (int64_t)gp(c.out_off)[node] + imm;
-                break;
-            }
-            case TW_OP_RLINK: {
-                const uint64_t l = (uint64_t)rb;
-                const bool bad = l >= c.L;
-                pfail(me && bad, TW_REP_ERR_INSN);
-                tc = bad ? T_STOP : T_NONE;
-                wr = true; wm = me && !bad;
-                wv = (int64_t)gp(c.link_rev)[wm ? l : 0];
+                tw_vm_drain();
                 break;
             }
             case TW_OP_SEND:  // schedule (after d) (deliver ..) unless the link drops it
@@ -1229,6 +1277,7 @@ struct Lane {
                         }
                     }
                 }
+                tw_vm_drain();
                 break;
             case TW_OP_DELIVER:  // listener dispatch, ForkStrategy fork_ (MonadDialog.hs:232-256,317)
                 if (me) {
@@ -1254,6 +1303,7 @@ struct Lane {
                         tc = T_SPAWN;
                     }
                 }
+                tw_vm_drain();
                 break;
             case TW_OP_LISTEN: {
                 const bool bad = (uint32_t)imm >= c.n_sets;
@@ -1271,9 +1321,6 @@ struct Lane {
                     gp(c.bind)[bix(th.w1)] = 0;
                     gp(c.bind_own)[bix(th.w1)] = 0xFFFFFFFFu;
                 }
-                break;
-            case TW_OP_TRACE:  // th.w1 is the popped thread's node: the term joins hacc
-                hacc += me ? term(now, TW_KIND_TRACE | ((uint32_t)imm & 0xFFFFu), ra) : 0ull;
                 break;
             case TW_OP_TMO_BEGIN:  // schedule (after t) watchdog (TimedT.hs:373-375)
                 if (me) {
@@ -1312,6 +1359,7 @@ struct Lane {
                 thr_any = true;
                 thr = ok && !gp(c.tmo_done)[ix(ok ? e : 0)];
                 tref = rf[0]; tcode = TW_EXC_TIMEOUT; tval = 0;
+                tw_vm_drain();
                 break;
             }
             default:
@@ -1324,6 +1372,7 @@ struct Lane {
             (void)lfl;
             if (thr_any) {
                 if (thr) throw_to(th, slot, tref, tcode, tval);
+                tw_vm_drain();
             }
             // per-lane epilogue of the pass
             pc = me ? tgt : pc;
