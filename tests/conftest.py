@@ -28,3 +28,18 @@ def engine_mod():
 
     engine.load_library()
     return engine
+
+
+@pytest.fixture(autouse=True)
+def tw_geometry(request, monkeypatch):
+    """GPU tests run under both kernel geometries (dense: 256 replicas per
+    workgroup; sparse: 16 per workgroup with the 768-entry on-chip queue)."""
+    g = getattr(request, "param", None)
+    if g is not None:
+        monkeypatch.setenv("TW_GEOMETRY", g)
+    return g
+
+
+def pytest_generate_tests(metafunc):
+    if "tw_geometry" in metafunc.fixturenames and metafunc.definition.get_closest_marker("gpu"):
+        metafunc.parametrize("tw_geometry", ["dense", "sparse"], indirect=True)

@@ -32,6 +32,7 @@
 
 #include <chrono>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <vector>
@@ -40,6 +41,11 @@
 
 #define TW_NEAR_CAP 16          // on-chip queue entries per replica (LDS)
 #define TW_WG 256               // lanes per workgroup (4 waves share one program image)
+// Sparse geometry (few replicas: at most a few per SIMD): 16 replicas per
+// workgroup, one workgroup per CU, so each replica gets ~10 KB of LDS and a
+// 768-entry near heap (most of a hotspot receiver's backlog stays on chip).
+#define TW_WG_SPARSE 16
+#define TW_NEAR_SPARSE 768
 #ifndef TW_RUNS
 #define TW_RUNS 4               // monotone far-queue runs per replica
 #endif
@@ -288,15 +294,15 @@ struct BoolC {
     static constexpr bool value = B;
 };
 
-template <bool LP>
+template <bool LP, int WG, int NC>
 struct Lane {
     Dev c;  // by value: kernel arguments stay in SGPRs
     uint32_t r;       // replica
-    // LDS (lane-offset pointers; element j at [j * TW_WG])
+    // LDS (lane-offset pointers; element j at [j * WG])
     uint64_t LAS* nk;     // near heap keys: (t - nbase) << 32 | seq; a free position holds ~0
     uint32_t LAS* ns;     // near heap slots
     int64_t LAS* rf;      // the running thread's registers r0..r3 during its step
-    uint4 LAS* pfs;       // prefetch staging: quad q of the next pop's record at [q * TW_WG]
+    uint4 LAS* pfs;       // prefetch staging: quad q of the next pop's record at [q * WG]
     uint32_t pfs_wave;    // LDS byte address of this wave's staging (quad 0), wave-uniform
     uint32_t LAS* cw;     // cold words [CW_*]
     uint4 LAS* rq;        // far runs' bookkeeping quads [RQ_*]
@@ -343,50 +349,60 @@ struct Lane {
         return LP ? i : ix(i);
     }
     // cold words
-    __device__ __forceinline__ uint32_t cg(int w) const { return cw[w * TW_WG]; }
-    __device__ __forceinline__ void cs(int w, uint32_t v) const { cw[w * TW_WG] = v; }
+    __device__ __forceinline__ uint32_t cg(int w) const { return cw[w * WG]; }
+    __device__ __forceinline__ void cs(int w, uint32_t v) const { cw[w * WG] = v; }
     __device__ __forceinline__ int64_t cg64(int wl, int wh) const {
-        return (int64_t)(((uint64_t)cw[wh * TW_WG] << 32) | cw[wl * TW_WG]);
+        return (int64_t)(((uint64_t)cw[wh * WG] << 32) | cw[wl * WG]);
     }
     __device__ __forceinline__ void cs64(int wl, int wh, int64_t v) const {
-        cw[wl * TW_WG] = (uint32_t)v;
-        cw[wh * TW_WG] = (uint32_t)((uint64_t)v >> 32);
+        cw[wl * WG] = (uint32_t)v;
+        cw[wh * WG] = (uint32_t)((uint64_t)v >> 32);
     }
-    __device__ __forceinline__ void cinc(int w) const { cw[w * TW_WG] += 1; }
+    __device__ __forceinline__ void cinc(int w) const { cw[w * WG] += 1; }
 
     __device__ __forceinline__ void fail(uint32_t st) {
         if (status == TW_REP_RUNNING) status = st;
     }
 
     // ---------------------------------------------------------- near heap (LDS)
-    // 4-ary min-heap of unique 64-bit keys, TW_NEAR_CAP = 16 positions = root
-    // + two levels; a free position holds ~0, so no read is guarded by the
-    // heap size.  Sift-up and sift-down are straight-line code over both
+    // 4-ary min-heap of unique 64-bit keys; a free position holds ~0, so no
+    // read is guarded by the heap size.  NC = 16 (the replica-dense geometry):
+    // root + two levels, sift-up and sift-down straight-line code over both
     // levels: the reads of a level are issued together, every move is an
     // unconditional store of a selected value (a "move" onto itself when the
     // entry stays), and no data-dependent branch is taken -- at one wave per
     // SIMD each branch and each dependent LDS round trip costs in full.
-    static_assert(TW_NEAR_CAP == 16, "the near heap is root + two 4-ary levels");
+    // Larger NC (the sparse geometry, few replicas per CU): sift-up reads the
+    // whole ancestor path at once (one round trip), sift-down walks the levels
+    // in a wave-uniform loop.
+    static constexpr int near_depth() {
+        int d = 0;
+        long cap = 1, lvl = 1;
+        while (cap < NC) { lvl *= 4; cap += lvl; ++d; }
+        return d;
+    }
+    static constexpr int ND = near_depth();  // levels below the root
+    static_assert(NC >= 16, "near heap too small");
     __device__ __forceinline__ uint64_t nkey(int64_t t, uint32_t s) const {
         return ((uint64_t)(t - nbase) << 32) | s;
     }
     __device__ __forceinline__ bool near_fits(int64_t t) const {
-        return near_n < TW_NEAR_CAP && t - now < c.horizon && (uint64_t)(t - nbase) < 0xFFFFFFFFull;
+        return near_n < NC && t - now < c.horizon && (uint64_t)(t - nbase) < 0xFFFFFFFFull;
     }
     __device__ __forceinline__ void near_init() {
-#pragma unroll
-        for (int i = 0; i < TW_NEAR_CAP; ++i) nk[i * TW_WG] = ~0ull;
+#pragma unroll 16
+        for (int i = 0; i < NC; ++i) nk[i * WG] = ~0ull;
         near_n = 0;
         nrk = ~0ull; nrs = 0;
     }
     // min of the four children 4p+1..4p+4 of p (positions >= 16 read as ~0)
     __device__ __forceinline__ void near_kids(uint32_t p, uint64_t& kb, uint32_t& sb, uint32_t& ib) const {
         const uint32_t c0 = 4 * p + 1;
-        const bool v1 = c0 + 1 < TW_NEAR_CAP, v2 = c0 + 2 < TW_NEAR_CAP, v3 = c0 + 3 < TW_NEAR_CAP;
-        const uint32_t a0 = c0 < TW_NEAR_CAP ? c0 : 0, a1 = v1 ? c0 + 1 : 0, a2 = v2 ? c0 + 2 : 0, a3 = v3 ? c0 + 3 : 0;
-        uint64_t k0 = nk[a0 * TW_WG], k1 = nk[a1 * TW_WG], k2 = nk[a2 * TW_WG], k3 = nk[a3 * TW_WG];
-        const uint32_t s0 = ns[a0 * TW_WG], s1 = ns[a1 * TW_WG], s2 = ns[a2 * TW_WG], s3 = ns[a3 * TW_WG];
-        k0 = c0 < TW_NEAR_CAP ? k0 : ~0ull;
+        const bool v1 = c0 + 1 < NC, v2 = c0 + 2 < NC, v3 = c0 + 3 < NC;
+        const uint32_t a0 = c0 < NC ? c0 : 0, a1 = v1 ? c0 + 1 : 0, a2 = v2 ? c0 + 2 : 0, a3 = v3 ? c0 + 3 : 0;
+        uint64_t k0 = nk[a0 * WG], k1 = nk[a1 * WG], k2 = nk[a2 * WG], k3 = nk[a3 * WG];
+        const uint32_t s0 = ns[a0 * WG], s1 = ns[a1 * WG], s2 = ns[a2 * WG], s3 = ns[a3 * WG];
+        k0 = c0 < NC ? k0 : ~0ull;
         k1 = v1 ? k1 : ~0ull; k2 = v2 ? k2 : ~0ull; k3 = v3 ? k3 : ~0ull;
         const bool m01 = k1 < k0, m23 = k3 < k2;
         const uint64_t ka = m01 ? k1 : k0, kc = m23 ? k3 : k2;
@@ -410,51 +426,131 @@ struct Lane {
         const uint32_t wc = mv2 ? c2 : c1;
         nk[0] = mv1 ? k1 : k;
         ns[0] = mv1 ? s1 : s;
-        nk[c1 * TW_WG] = vb;
-        ns[c1 * TW_WG] = sb;
-        nk[wc * TW_WG] = mv2 ? k : vb;
-        ns[wc * TW_WG] = mv2 ? s : sb;
+        nk[c1 * WG] = vb;
+        ns[c1 * WG] = sb;
+        nk[wc * WG] = mv2 ? k : vb;
+        ns[wc * WG] = mv2 ? s : sb;
         nrk = mv1 ? k1 : k;
         nrs = mv1 ? s1 : s;
     }
+    // Generic NC: place (k, s) at hole p0 and sift it up through the whole
+    // ancestor path (read in one round trip; stores top-down so that the
+    // clamped repeats of the root are overwritten by the deepest level).
+    __device__ __forceinline__ void near_up_from(uint32_t p0, uint64_t k, uint32_t s) {
+        uint32_t path[ND + 1];
+        uint64_t pk[ND + 2];
+        uint32_t ps[ND + 2];
+        bool up[ND + 2];
+        path[0] = p0;
+#pragma unroll
+        for (int j = 1; j <= ND; ++j) path[j] = path[j - 1] ? (path[j - 1] - 1) >> 2 : 0u;
+#pragma unroll
+        for (int j = 1; j <= ND; ++j) { pk[j] = nk[path[j] * WG]; ps[j] = ns[path[j] * WG]; }
+        pk[ND + 1] = 0; ps[ND + 1] = 0;
+        up[0] = true;
+#pragma unroll
+        for (int j = 1; j <= ND; ++j) up[j] = up[j - 1] && path[j - 1] != 0 && k < pk[j];
+        up[ND + 1] = false;
+#pragma unroll
+        for (int j = ND; j >= 1; --j) {
+            nk[path[j] * WG] = up[j + 1] ? pk[j + 1] : (up[j] ? k : pk[j]);
+            ns[path[j] * WG] = up[j + 1] ? ps[j + 1] : (up[j] ? s : ps[j]);
+        }
+        nk[p0 * WG] = up[1] ? pk[1] : k;
+        ns[p0 * WG] = up[1] ? ps[1] : s;
+    }
+    // Generic NC: place (k, s) at hole p and sift it down (uniform level loop;
+    // a lane that stopped rewrites its entry in place).
+    __device__ __forceinline__ void near_down_from(uint32_t p, uint64_t k, uint32_t s) {
+        bool go = true;
+        for (int l = 0; l < ND; ++l) {
+            if (!__builtin_amdgcn_ballot_w64(go)) break;
+            uint64_t kb; uint32_t sb, ib;
+            near_kids(p, kb, sb, ib);
+            const bool mv = go && kb < k;
+            nk[p * WG] = mv ? kb : k;
+            ns[p * WG] = mv ? sb : s;
+            go = mv;
+            p = mv ? ib : p;
+        }
+        nk[p * WG] = k;
+        ns[p * WG] = s;
+    }
     __device__ __forceinline__ void near_push(int64_t t, uint32_t sq, uint32_t slot) {
+        if constexpr (NC != 16) {
+            STAT(K_NEAR_PUSH);
+            const uint64_t k = nkey(t, sq);
+            near_up_from(near_n++, k, slot);
+            const bool m = k < nrk;
+            nrk = m ? k : nrk;
+            nrs = m ? slot : nrs;
+            return;
+        }
         STAT(K_NEAR_PUSH);
         const uint64_t k = nkey(t, sq);
         const uint32_t n = near_n++;
         // parent and grandparent of n (clamped to the root)
         const uint32_t p1 = n ? (n - 1) >> 2 : 0;
         const uint32_t p2 = p1 ? (p1 - 1) >> 2 : 0;
-        const uint64_t k1 = nk[p1 * TW_WG], k2 = nk[p2 * TW_WG];
-        const uint32_t s1 = ns[p1 * TW_WG], s2 = ns[p2 * TW_WG];
+        const uint64_t k1 = nk[p1 * WG], k2 = nk[p2 * WG];
+        const uint32_t s1 = ns[p1 * WG], s2 = ns[p2 * WG];
         const bool up1 = n != 0 && k < k1;         // parent moves down into n
         const bool up2 = up1 && p1 != 0 && k < k2;  // grandparent moves down into p1
         // p2 <- k or itself; p1 <- grandparent, k or itself; n <- parent or k.
         // Stored top-down so that when positions coincide (n = 0: all three;
         // n <= 4: p1 = p2 = 0) the last store, the one for the deepest, wins.
-        nk[p2 * TW_WG] = up2 ? k : k2;
-        ns[p2 * TW_WG] = up2 ? slot : s2;
-        nk[p1 * TW_WG] = up2 ? k2 : (up1 ? k : k1);
-        ns[p1 * TW_WG] = up2 ? s2 : (up1 ? slot : s1);
-        nk[n * TW_WG] = up1 ? k1 : k;
-        ns[n * TW_WG] = up1 ? s1 : slot;
+        nk[p2 * WG] = up2 ? k : k2;
+        ns[p2 * WG] = up2 ? slot : s2;
+        nk[p1 * WG] = up2 ? k2 : (up1 ? k : k1);
+        ns[p1 * WG] = up2 ? s2 : (up1 ? slot : s1);
+        nk[n * WG] = up1 ? k1 : k;
+        ns[n * WG] = up1 ? s1 : slot;
         const bool m = k < nrk;
         nrk = m ? k : nrk;
         nrs = m ? slot : nrs;
     }
     __device__ __forceinline__ void near_pop() {
         const uint32_t n = --near_n;
-        const uint64_t lk = n ? nk[n * TW_WG] : ~0ull;
-        const uint32_t ls = ns[n * TW_WG];
-        nk[n * TW_WG] = ~0ull;
-        near_down(lk, ls);
+        const uint64_t lk = n ? nk[n * WG] : ~0ull;
+        const uint32_t ls = ns[n * WG];
+        nk[n * WG] = ~0ull;
+        if constexpr (NC != 16) {
+            near_down_from(0, lk, ls);
+            nrk = nk[0];
+            nrs = ns[0];
+        } else {
+            near_down(lk, ls);
+        }
     }
     // Re-key the live near entry with seq `old_seq` (seqs are unique) to (t, sq),
     // an earlier time: remove it (the last entry fills its hole) and push it anew.
     __device__ __forceinline__ bool near_rekey(uint32_t old_seq, int64_t t, uint32_t sq, uint32_t slot) {
+        if constexpr (NC != 16) {
+            // find the entry, fill its hole with the last entry (sifted whichever
+            // way it must go), then push the re-keyed entry
+            uint32_t i = 0xFFFFFFFFu;
+            for (uint32_t j = 0; j < near_n; ++j) {
+                const uint64_t k = nk[j * WG];
+                if ((uint32_t)k == old_seq && k != ~0ull) { i = j; break; }
+            }
+            if (i == 0xFFFFFFFFu) return false;
+            const uint32_t n = --near_n;
+            const uint64_t lk = nk[n * WG];
+            const uint32_t ls = ns[n * WG];
+            nk[n * WG] = ~0ull;
+            if (i != n) {
+                if (i > 0 && lk < nk[((i - 1) >> 2) * WG]) near_up_from(i, lk, ls);
+                else near_down_from(i, lk, ls);
+            }
+            near_up_from(near_n++, nkey(t, sq), slot);
+            nrk = nk[0];
+            nrs = ns[0];
+            return true;
+        } else {
         uint32_t hit = 0;
 #pragma unroll
-        for (int i = 0; i < TW_NEAR_CAP; ++i) {
-            const uint64_t k = nk[i * TW_WG];
+        for (int i = 0; i < NC; ++i) {
+            const uint64_t k = nk[i * WG];
             hit |= ((uint32_t)k == old_seq && k != ~0ull) ? 1u << i : 0u;
         }
         if (!hit) return false;
@@ -463,11 +559,11 @@ struct Lane {
         // (it was deeper, under a key <= it) or up (below i's ancestors); use a
         // full rebuild of that path by re-pushing all entries above -- rare
         // path (a throwTo of an on-chip thread), so simply rebuild the heap.
-        uint64_t kk[TW_NEAR_CAP];
-        uint32_t ss[TW_NEAR_CAP];
+        uint64_t kk[NC];
+        uint32_t ss[NC];
         const uint32_t n = near_n;
 #pragma unroll
-        for (int j = 0; j < TW_NEAR_CAP; ++j) { kk[j] = nk[j * TW_WG]; ss[j] = ns[j * TW_WG]; }
+        for (int j = 0; j < NC; ++j) { kk[j] = nk[j * WG]; ss[j] = ns[j * WG]; }
         near_init();
         for (uint32_t j = 0; j < n; ++j) {
             if (j == i) continue;
@@ -476,14 +572,15 @@ struct Lane {
         }
         near_push(t, sq, slot);
         return true;
+        }
     }
     // Move the near heap to a new time base (keeps (t - nbase) inside 32 bits).
     __device__ void near_rebase(int64_t nb) {
         const uint64_t d = (uint64_t)(nb - nbase) << 32;
-#pragma unroll
-        for (int i = 0; i < TW_NEAR_CAP; ++i) {
-            const uint64_t k = nk[i * TW_WG];
-            nk[i * TW_WG] = k == ~0ull ? k : k - d;
+#pragma unroll 16
+        for (int i = 0; i < NC; ++i) {
+            const uint64_t k = nk[i * WG];
+            nk[i * WG] = k == ~0ull ? k : k - d;
         }
         nrk = nrk == ~0ull ? nrk : nrk - d;
         nbase = nb;
@@ -621,7 +718,7 @@ struct Lane {
         return gp(c.runs) + ((size_t)j * c.Cr + pos) * c.R + r;
     }
     // the second entry loaded by the last run_pop lands in LDS
-    __device__ __forceinline__ uint4 LAS* rqp(int w) const { return rq + w * TW_WG; }
+    __device__ __forceinline__ uint4 LAS* rqp(int w) const { return rq + w * WG; }
     __device__ __forceinline__ static uint32_t q_at(uint4 q, int j) {
         return j == 0 ? q.x : j == 1 ? q.y : j == 2 ? q.z : q.w;
     }
@@ -630,7 +727,7 @@ struct Lane {
     __device__ __forceinline__ void run_commit() {
         if (prun >= 0) {
             asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-            *rqp(RQ_SEC + prun) = pfs[4 * TW_WG];
+            *rqp(RQ_SEC + prun) = pfs[4 * WG];
             prun = -1;
         }
     }
@@ -689,7 +786,7 @@ struct Lane {
             const uint32_t p2 = h + 1 == c.Cr ? 0 : h + 1;
             // into LDS staging quad 4 (no register left pending across the step)
             asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(run_at(sel, p2)),
-                         "s"(pfs_wave + 4 * TW_WG * 16) : "memory", "m0");
+                         "s"(pfs_wave + 4 * WG * 16) : "memory", "m0");
             prun = sel;
         }
     }
@@ -778,7 +875,7 @@ struct Lane {
                                                const Th& ch) {
         const uint4 GAS* dm = gp(c.dummy) + (size_t)r;
         const size_t R5 = c.R;
-        th.r0 = rf[0]; th.r1 = rf[TW_WG]; th.r2 = rf[2 * TW_WG]; th.r3 = rf[3 * TW_WG];
+        th.r0 = rf[0]; th.r1 = rf[WG]; th.r2 = rf[2 * WG]; th.r3 = rf[3 * WG];
         uint4 GAS* pr = hrec(full || hdr ? slot : 0);
         uint4 GAS* p0 = (full || hdr) ? pr : (uint4 GAS*)dm;
         uint4 GAS* p1 = full ? pr + 1 : (uint4 GAS*)(dm + R5);
@@ -824,11 +921,11 @@ struct Lane {
         asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(p), "s"(pfs_wave)
                      : "memory", "m0");
         asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(p + 1),
-                     "s"(pfs_wave + TW_WG * 16) : "memory", "m0");
+                     "s"(pfs_wave + WG * 16) : "memory", "m0");
         asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(p + 2),
-                     "s"(pfs_wave + 2 * TW_WG * 16) : "memory", "m0");
+                     "s"(pfs_wave + 2 * WG * 16) : "memory", "m0");
         asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(p + 3),
-                     "s"(pfs_wave + 3 * TW_WG * 16) : "memory", "m0");
+                     "s"(pfs_wave + 3 * WG * 16) : "memory", "m0");
         pf_slot = valid ? s : 0xFFFFFFFFu;
     }
     // The popped thread's record: the prefetched copy, or (rarely) a fresh load
@@ -841,12 +938,12 @@ struct Lane {
             STAT(K_PEEK_HBM);
             const uint4 GAS* p = hrec(slot);
             const uint4 a = p[0], b = p[1], d = p[2], e = p[3];
-            pfs[0] = a; pfs[TW_WG] = b; pfs[2 * TW_WG] = d; pfs[3 * TW_WG] = e;
+            pfs[0] = a; pfs[WG] = b; pfs[2 * WG] = d; pfs[3 * WG] = e;
         } else {
             STAT(K_PEEK_PF);
         }
         asm volatile("s_waitcnt vmcnt(%0)" ::"n"(TW_TAIL_VMEM) : "memory");
-        unpack(th, pfs[0], pfs[TW_WG], pfs[2 * TW_WG], pfs[3 * TW_WG]);
+        unpack(th, pfs[0], pfs[WG], pfs[2 * WG], pfs[3 * WG]);
     }
 
     // Free slots: never-used slots come from a bump pointer (no memory read);
@@ -1003,7 +1100,7 @@ struct Lane {
                     th_set_nfr(th, (uint32_t)i);
                     th_set_pc(th, f & 0xFFFFu);
                     rf[0] = val;
-                    rf[3 * TW_WG] = (int64_t)code;
+                    rf[3 * WG] = (int64_t)code;
                     return true;
                 }
             }
@@ -1019,7 +1116,7 @@ struct Lane {
         status = (cond && status == TW_REP_RUNNING) ? st : status;
     }
     // predicated cold-word store: idle lanes write a dummy word (no branch)
-    __device__ __forceinline__ void csp(bool p, int w, uint32_t v) const { cw[(p ? w : CW_DUMMY) * TW_WG] = v; }
+    __device__ __forceinline__ void csp(bool p, int w, uint32_t v) const { cw[(p ? w : CW_DUMMY) * WG] = v; }
 
     enum { T_NONE, T_YIELD, T_SPAWN, T_EXIT, T_STOP, T_DIED };
 
@@ -1072,8 +1169,8 @@ struct Lane {
             const int32_t imm = (int32_t)in.y;
             const uint32_t a = (uw >> 8) & 3u, b = uw >> 16;
             STAT(K_INSN);
-            const int64_t ra = rf[a * TW_WG];
-            const int64_t rb = rf[(b & 3u) * TW_WG];
+            const int64_t ra = rf[a * WG];
+            const int64_t rb = rf[(b & 3u) * WG];
             uint32_t tc = T_NONE;     // per lane: terminal action of this op
             uint32_t tgt = pc + 1;    // per lane: next pc
             bool wr = false;          // uniform: the op writes r[a]
@@ -1179,12 +1276,12 @@ struct Lane {
             switch (op) {
             case TW_OP_THROW_TO:
                 thr_any = true; thr = me;
-                tref = ra; tcode = b & 0xFFu; tval = rf[((b >> 8) & 3u) * TW_WG];
+                tref = ra; tcode = b & 0xFFu; tval = rf[((b >> 8) & 3u) * WG];
                 break;
             case TW_OP_THROW:
                 if (me) {
                     th_set_pc(th, pc + 1);
-                    if (unwind(th, slot, b & 0xFFu, rf[((b >> 8) & 3u) * TW_WG])) tgt = th_pc(th);
+                    if (unwind(th, slot, b & 0xFFu, rf[((b >> 8) & 3u) * WG])) tgt = th_pc(th);
                     else tc = T_DIED;  // died: record stored
                 }
                 break;
@@ -1221,7 +1318,7 @@ struct Lane {
                 break;
             case TW_OP_NLOADX:
             case TW_OP_NSTOREX: {
-                const uint64_t node = (uint64_t)rf[((b >> 8) & 3u) * TW_WG];
+                const uint64_t node = (uint64_t)rf[((b >> 8) & 3u) * WG];
                 const bool bad = LP ? node != th.w1 : node >= c.N;
                 pfail(me && bad, TW_REP_ERR_INSN);
                 tc = bad ? T_STOP : T_NONE;
@@ -1243,7 +1340,7 @@ struct Lane {
                         tc = T_STOP;
                     } else {
                         const uint32_t kind = b & 0xFFu;
-                        const int64_t payload = rf[((b >> 8) & 3u) * TW_WG];
+                        const int64_t payload = rf[((b >> 8) & 3u) * WG];
                         const uint32_t ord = gp(c.link_ord)[lix(link)];
                         gp(c.link_ord)[lix(link)] = ord + 1;
                         const uint32_t e = c.link_table ? gp(c.link_table)[tix(link, ord)] : 0u;
@@ -1281,7 +1378,7 @@ struct Lane {
                 break;
             case TW_OP_DELIVER:  // listener dispatch, ForkStrategy fork_ (MonadDialog.hs:232-256,317)
                 if (me) {
-                    const int64_t r0 = rf[0], r1 = rf[TW_WG], r2 = rf[2 * TW_WG], r3 = rf[3 * TW_WG];
+                    const int64_t r0 = rf[0], r1 = rf[WG], r2 = rf[2 * WG], r3 = rf[3 * WG];
                     const uint64_t link = (uint64_t)r1;
                     const uint32_t kind = (uint32_t)r3;
                     const uint32_t dst = gp(c.link_dst)[link];
@@ -1331,7 +1428,7 @@ struct Lane {
                     } else {
                         cs(CW_TMO, tmo + 1);
                         gp(c.tmo_done)[ix(tmo)] = 0;
-                        rf[a * TW_WG] = tmo;
+                        rf[a * WG] = tmo;
                         cs(CW_CPC, TW_PC_WATCHDOG_STUB); cs(CW_CNODE, th.w1); cs(CW_CRA, 4); cs(CW_CDEL, 0);
                         cs64(CW_Q0, CW_Q0 + 1, (int64_t)(((uint64_t)th.w2 << 32) | slot));
                         cs64(CW_Q0 + 2, CW_Q0 + 3, (int64_t)tmo);
@@ -1354,7 +1451,7 @@ struct Lane {
                 }
                 break;
             case TW_OP_TMO_FIRE: {
-                const uint64_t e = (uint64_t)rf[TW_WG];
+                const uint64_t e = (uint64_t)rf[WG];
                 const bool ok = me && e < c.T;
                 thr_any = true;
                 thr = ok && !gp(c.tmo_done)[ix(ok ? e : 0)];
@@ -1368,7 +1465,7 @@ struct Lane {
                 break;
             }
             }  // U_FX
-            if (wr) rf[a * TW_WG] = wm ? wv : ra;
+            if (wr) rf[a * WG] = wm ? wv : ra;
             (void)lfl;
             if (thr_any) {
                 if (thr) throw_to(th, slot, tref, tcode, tval);
@@ -1402,17 +1499,17 @@ struct Lane {
             int64_t ref;
             bool ok;
             if (cdel & 2u)
-                ok = spawn(cg(CW_CPC), cg(CW_CNODE), rf[0], rf[TW_WG], rf[2 * TW_WG], rf[3 * TW_WG], ref, ch, cslot);
+                ok = spawn(cg(CW_CPC), cg(CW_CNODE), rf[0], rf[WG], rf[2 * WG], rf[3 * WG], ref, ch, cslot);
             else
                 ok = spawn(cg(CW_CPC), cg(CW_CNODE), cg64(CW_Q0, CW_Q0 + 1), cg64(CW_Q0 + 2, CW_Q0 + 3),
                            cg64(CW_Q0 + 4, CW_Q0 + 5), cg64(CW_Q0 + 6, CW_Q7), ref, ch, cslot);
             if (!ok) {
                 fin = T_STOP;
             } else {
-                if (cra < 4) rf[cra * TW_WG] = ref;
+                if (cra < 4) rf[cra * WG] = ref;
                 if (LP && (cdel & 1u)) {
                     // the deliverer's resume pop (at now+1, on the sending node), then it ends
-                    hash_add((uint32_t)rf[2 * TW_WG], term0(now + 1, TW_KIND_RESUME | (TW_PC_DELIVER_STUB + 2)));
+                    hash_add((uint32_t)rf[2 * WG], term0(now + 1, TW_KIND_RESUME | (TW_PC_DELIVER_STUB + 2)));
                     ++d_ev;
                     final_t = now + 1 > final_t ? now + 1 : final_t;
                     fin = T_EXIT;
@@ -1483,40 +1580,41 @@ __global__ void __launch_bounds__(TW_WG) tw_init_kernel(Dev c, uint32_t main_pc,
 // LDS per workgroup: near heap keys + slots, the running threads' register
 // files, the cold words, then the program image and constant pool, so
 // instruction fetch and time constants never leave the CU.
+template <int WG, int NC>
 __host__ __device__ constexpr size_t fixed_lds_bytes() {
-    return (size_t)5 * TW_WG * 16 + (size_t)RQ_COUNT * TW_WG * 16 + (size_t)TW_NEAR_CAP * TW_WG * 12 +
-           (size_t)4 * TW_WG * 8 + (size_t)CW_COUNT * TW_WG * 4;
+    return (size_t)5 * WG * 16 + (size_t)RQ_COUNT * WG * 16 + (size_t)NC * WG * 12 +
+           (size_t)4 * WG * 8 + (size_t)CW_COUNT * WG * 4;
 }
 
-template <bool LP>
-__global__ void __launch_bounds__(TW_WG) __attribute__((amdgpu_waves_per_eu(1, 2)))
+template <bool LP, int WG, int NC>
+__global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(1, 2)))
 tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
     extern __shared__ __attribute__((aligned(16))) uint64_t lds_raw[];
     uint4 LAS* s_pf = (uint4 LAS*)lds_raw;
-    uint4 LAS* s_rq = s_pf + 5 * TW_WG;
-    uint64_t LAS* s_k = (uint64_t LAS*)(s_rq + RQ_COUNT * TW_WG);
-    int64_t LAS* s_rf = (int64_t LAS*)(s_k + TW_NEAR_CAP * TW_WG);
-    uint32_t LAS* s_s = (uint32_t LAS*)(s_rf + 4 * TW_WG);
-    uint32_t LAS* s_cw = s_s + TW_NEAR_CAP * TW_WG;
-    uint2 LAS* s_p = (uint2 LAS*)(s_cw + CW_COUNT * TW_WG);
+    uint4 LAS* s_rq = s_pf + 5 * WG;
+    uint64_t LAS* s_k = (uint64_t LAS*)(s_rq + RQ_COUNT * WG);
+    int64_t LAS* s_rf = (int64_t LAS*)(s_k + NC * WG);
+    uint32_t LAS* s_s = (uint32_t LAS*)(s_rf + 4 * WG);
+    uint32_t LAS* s_cw = s_s + NC * WG;
+    uint2 LAS* s_p = (uint2 LAS*)(s_cw + CW_COUNT * WG);
     int64_t LAS* s_c = (int64_t LAS*)(s_p + c.n_insns + 1);
     uint32_t LAS* s_u = (uint32_t LAS*)(s_c + c.n_consts);
     {
-        for (uint32_t i = threadIdx.x; i <= c.n_insns; i += TW_WG) {
+        for (uint32_t i = threadIdx.x; i <= c.n_insns; i += WG) {
             const uint2 in = gp(c.insns)[i];
             s_p[i] = in;
             s_u[i] = uop_of(in.x & 0xFFu);
         }
-        for (uint32_t i = threadIdx.x; i < c.n_consts; i += TW_WG) s_c[i] = gp(c.consts)[i];
+        for (uint32_t i = threadIdx.x; i < c.n_consts; i += WG) s_c[i] = gp(c.consts)[i];
         __syncthreads();
     }
-    uint32_t r = blockIdx.x * TW_WG + threadIdx.x;
+    uint32_t r = blockIdx.x * WG + threadIdx.x;
     if (r >= c.R) return;
     uint64_t* sc = gp(c.scal) + r;
     const size_t R = c.R;
     if (sc[SC_STATUS * R] != TW_REP_RUNNING) return;
 
-    Lane<LP> L;
+    Lane<LP, WG, NC> L;
     L.c = c;
     L.r = r;
     L.nk = s_k + threadIdx.x;
@@ -1574,7 +1672,7 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
     L.near_init();
     for (uint32_t j = 0; j < near_n0; ++j) {
         uint4 e = gp(c.near_spill)[(size_t)j * R + r];
-        if (L.near_n < TW_NEAR_CAP && (uint64_t)(ent_t(e) - L.nbase) < 0xFFFFFFFFull) {
+        if (L.near_n < NC && (uint64_t)(ent_t(e) - L.nbase) < 0xFFFFFFFFull) {
             L.near_push(ent_t(e), e.w, e.z);
             continue;
         }
@@ -1648,7 +1746,7 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
                 pending_main = 0;
                 L.pf_slot = 0xFFFFFFFFu;
                 L.fetch_rec(0, th);
-                L.rf[0] = th.r0; L.rf[TW_WG] = th.r1; L.rf[2 * TW_WG] = th.r2; L.rf[3 * TW_WG] = th.r3;
+                L.rf[0] = th.r0; L.rf[WG] = th.r1; L.rf[2 * WG] = th.r2; L.rf[3 * WG] = th.r3;
                 L.hnode = th.w1;
                 run = true;
             } else if (L.live == 0) {  // whileM_ notDone
@@ -1689,7 +1787,7 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
                         L.now = t;
                         if (t - L.nbase > (int64_t)0x7FFFFFFF) L.near_rebase(t);
                         L.hnode = th.w1;
-                        L.rf[0] = th.r0; L.rf[TW_WG] = th.r1; L.rf[2 * TW_WG] = th.r2; L.rf[3 * TW_WG] = th.r3;
+                        L.rf[0] = th.r0; L.rf[WG] = th.r1; L.rf[2 * WG] = th.r2; L.rf[3 * WG] = th.r3;
                         // LP phantom = the deliverer's wake, already counted and hashed by the sender
                         const bool phantom = LP && (th_flags(th) & F_PHANTOM);
                         if (!phantom) {
@@ -1756,14 +1854,14 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
         const uint4 ix4 = *L.rqp(RQ_IDX);
 #pragma unroll
         for (int j = 0; j < TW_RUNS; ++j) {
-            sc[(SC_RH0 + j) * R] = Lane<LP>::q_at(ix4, j);
+            sc[(SC_RH0 + j) * R] = Lane<LP, WG, NC>::q_at(ix4, j);
             sc[(SC_RC0 + j) * R] = L.rqp(RQ_TAIL + j)->w;
         }
     }
-    for (uint32_t i = 0, j = 0; i < TW_NEAR_CAP; ++i) {
-        const uint64_t k = L.nk[i * TW_WG];
+    for (uint32_t i = 0, j = 0; i < NC; ++i) {
+        const uint64_t k = L.nk[i * WG];
         if (k != ~0ull)
-            gp(c.near_spill)[(size_t)(j++) * R + r] = ent(L.nbase + (int64_t)(k >> 32), L.ns[i * TW_WG], (uint32_t)k);
+            gp(c.near_spill)[(size_t)(j++) * R + r] = ent(L.nbase + (int64_t)(k >> 32), L.ns[i * WG], (uint32_t)k);
     }
     bool active = L.status == TW_REP_RUNNING && L.d_ev < ev_room;
     int64_t tn = INT64_MAX;
@@ -1826,6 +1924,7 @@ struct tw_ctx {
     int64_t* nv_init = nullptr;
     uint32_t* listen_init = nullptr;
     size_t lds_bytes = 0;
+    int geo = 0;  // 0: dense (TW_WG, TW_NEAR_CAP); 1: sparse (TW_WG_SPARSE, TW_NEAR_SPARSE)
     // LP mode
     bool lp = false;
     uint4* foreign = nullptr;      // [out_cap][2]
@@ -1868,6 +1967,13 @@ void free_all(tw_ctx* c) {
 }
 
 }  // namespace
+
+template <bool LP, int WG, int NC>
+static void launch_run(tw_ctx* c, hipStream_t st, int64_t t_end, uint64_t limit, uint32_t budget) {
+    const uint32_t blocks = (uint32_t)((c->d.R + WG - 1) / WG);
+    hipLaunchKernelGGL((tw_run_kernel<LP, WG, NC>), dim3(blocks), dim3(WG), c->lds_bytes, st, c->d, t_end, limit,
+                       budget);
+}
 
 extern "C" {
 
@@ -1962,12 +2068,29 @@ static int load_common(tw_ctx* c, const tw_scenario_desc* s, bool lp, uint32_t l
     d.Cr = s->run_capacity;
     const size_t R = d.R;
     const size_t Rt = s->n_replicas;  // replica dimension of the host tables
-    c->lds_bytes = fixed_lds_bytes() + 12ull * (d.n_insns + 1) + 8ull * d.n_consts;
+    const size_t prog_lds = 12ull * (d.n_insns + 1) + 8ull * d.n_consts;
+    // geometry: sparse when the replicas fill at most ~2 workgroups per CU of
+    // the sparse layout (TW_GEOMETRY=dense|sparse overrides; LP mode is dense)
+    {
+        const char* g = getenv("TW_GEOMETRY");
+        int geo = (!lp && R <= 8192) ? 1 : 0;
+        if (g && !strcmp(g, "dense")) geo = 0;
+        if (g && !strcmp(g, "sparse")) geo = 1;
+        if (lp || fixed_lds_bytes<TW_WG_SPARSE, TW_NEAR_SPARSE>() + prog_lds > 160 * 1024) geo = 0;
+        c->geo = geo;
+    }
+    c->lds_bytes = (c->geo ? fixed_lds_bytes<TW_WG_SPARSE, TW_NEAR_SPARSE>() : fixed_lds_bytes<TW_WG, TW_NEAR_CAP>()) +
+                   prog_lds;
     if (c->lds_bytes > 160 * 1024) { free_all(c); return TW_ERR_INVALID; }  // program + constants must fit in LDS
-    HIPCHK(hipFuncSetAttribute((const void*)tw_run_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                               (int)c->lds_bytes));
-    HIPCHK(hipFuncSetAttribute((const void*)tw_run_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                               (int)c->lds_bytes));
+    if (c->geo)
+        HIPCHK(hipFuncSetAttribute((const void*)tw_run_kernel<false, TW_WG_SPARSE, TW_NEAR_SPARSE>,
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)c->lds_bytes));
+    else if (lp)
+        HIPCHK(hipFuncSetAttribute((const void*)tw_run_kernel<true, TW_WG, TW_NEAR_CAP>,
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)c->lds_bytes));
+    else
+        HIPCHK(hipFuncSetAttribute((const void*)tw_run_kernel<false, TW_WG, TW_NEAR_CAP>,
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)c->lds_bytes));
     int e;
 #define ALLOC(p, n) if ((e = dalloc(c, &p, (n))) != TW_OK) { free_all(c); return e; }
     uint2* insns; int64_t* consts; uint32_t *lpc, *out_off, *ldst, *lrev, *ltab = nullptr;
@@ -1983,7 +2106,7 @@ static int load_common(tw_ctx* c, const tw_scenario_desc* s, bool lp, uint32_t l
     ALLOC(d.free_stk, (size_t)d.S * R);
     ALLOC(d.far, (size_t)d.Q * R);
     ALLOC(d.runs, (size_t)(d.Cr ? TW_RUNS * (size_t)d.Cr : 1) * R);
-    ALLOC(d.near_spill, (size_t)TW_NEAR_CAP * R);
+    ALLOC(d.near_spill, (size_t)(c->geo ? TW_NEAR_SPARSE : TW_NEAR_CAP) * R);
     ALLOC(d.dummy, (size_t)5 * R);
     ALLOC(d.nvars, (size_t)d.N * 4 * R);
     ALLOC(d.hash, (size_t)d.N * R);
@@ -2084,7 +2207,6 @@ int tw_run(tw_ctx* c, int64_t t_end_us, uint64_t max_events, tw_stats* out) {
     HIPCHK(hipSetDevice(c->device));
     hipStream_t st = c->stream;
     const Dev& d = c->d;
-    uint32_t blocks = (d.R + TW_WG - 1) / TW_WG;
     // events before this call (to report per-call deltas)
     std::vector<uint64_t> ev0(d.R);
     HIPCHK(hipMemcpyAsync(ev0.data(), d.scal + (size_t)SC_EVENTS * d.R, 8ull * d.R, hipMemcpyDeviceToHost, st));
@@ -2107,11 +2229,11 @@ int tw_run(tw_ctx* c, int64_t t_end_us, uint64_t max_events, tw_stats* out) {
             if (c->lp) HIPCHK(hipMemsetAsync(d.next_t, 0xFF, 8, st));
             HIPCHK(hipEventRecord(c->ev_pool[2 * i], st));
             if (c->lp)
-                hipLaunchKernelGGL(tw_run_kernel<true>, dim3(blocks), dim3(TW_WG), c->lds_bytes, st, d, t_end_us,
-                                   limit, budget);
+                launch_run<true, TW_WG, TW_NEAR_CAP>(c, st, t_end_us, limit, budget);
+            else if (c->geo)
+                launch_run<false, TW_WG_SPARSE, TW_NEAR_SPARSE>(c, st, t_end_us, limit, budget);
             else
-                hipLaunchKernelGGL(tw_run_kernel<false>, dim3(blocks), dim3(TW_WG), c->lds_bytes, st, d, t_end_us,
-                                   limit, budget);
+                launch_run<false, TW_WG, TW_NEAR_CAP>(c, st, t_end_us, limit, budget);
             HIPCHK(hipGetLastError());
             HIPCHK(hipEventRecord(c->ev_pool[2 * i + 1], st));
             ++launches;

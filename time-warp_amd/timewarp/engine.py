@@ -125,9 +125,25 @@ class Engine:
         except Exception:
             pass
 
-    def load(self, scn: Scenario) -> "Engine":
+    def load(self, scn: Scenario, geometry: Optional[str] = None) -> "Engine":
+        """Upload the scenario.  `geometry` picks the kernel layout: "dense"
+        (256 replicas per workgroup, 16-entry on-chip queue), "sparse" (16
+        replicas per workgroup, 768-entry on-chip queue) or None = the
+        library's choice (sparse for <= 8192 replicas; env TW_GEOMETRY)."""
         d = scn.desc()
-        _check(self.lib.tw_load(self.ctx, C.addressof(d)), "tw_load")
+        old = os.environ.get("TW_GEOMETRY")
+        if geometry is not None:
+            if geometry not in ("dense", "sparse"):
+                raise ValueError(f"geometry must be 'dense' or 'sparse', not {geometry!r}")
+            os.environ["TW_GEOMETRY"] = geometry
+        try:
+            _check(self.lib.tw_load(self.ctx, C.addressof(d)), "tw_load")
+        finally:
+            if geometry is not None:
+                if old is None:
+                    os.environ.pop("TW_GEOMETRY", None)
+                else:
+                    os.environ["TW_GEOMETRY"] = old
         self.scn = scn
         return self
 
