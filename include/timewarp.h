@@ -133,6 +133,12 @@ enum tw_op {
 #define TW_PC_WATCHDOG_STUB 3u /* WAIT_REG r2 ; TMO_FIRE ; END                  */
 #define TW_PC_USER 6u          /* first user instruction                        */
 #define TW_PC_NONE 0xFFFFFFFFu
+/* listener_pc flag: the handler runs in place in the delivering thread
+ * (ForkStrategy `const id`, MonadDialog.hs:114-117) instead of in a thread
+ * forked by `fork_` (the default strategy, MonadDialog.hs:317).  The delivering
+ * thread takes the handler's registers {payload, link, sender, kind}, moves to
+ * the destination node and continues at the handler's pc. */
+#define TW_LPC_INLINE 0x80000000u
 
 typedef struct tw_insn {
     uint32_t w0;  /* op | a<<8 | b<<16 */

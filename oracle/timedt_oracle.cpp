@@ -452,6 +452,14 @@ struct Sim {
                 ++res.delivered;
                 hash(dst, TW_KIND_RECV | kind, r[0]);
                 int64_t regs[4] = {r[0], (int64_t)link, (int64_t)th->node, (int64_t)kind};
+                if (lpc & TW_LPC_INLINE) {
+                    // ForkStrategy `const id` (MonadDialog.hs:114-117): the handler runs
+                    // in this thread, on the destination node, with the handler's registers
+                    for (int i = 0; i < 4; ++i) r[i] = regs[i];
+                    th->node = dst;
+                    th->pc = lpc & ~TW_LPC_INLINE;
+                    break;
+                }
                 // ForkStrategy default fork_ (MonadDialog.hs:317)
                 if (!fork(th, lpc, dst, regs)) return;
                 enqueue(th, cur + 1);

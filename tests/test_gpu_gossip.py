@@ -23,6 +23,18 @@ def test_gossip_partitioned_equals_oracle(engine_mod, oracle_mod, n, parts, drop
     assert windows > 1
 
 
+@pytest.mark.parametrize("parts", [1, 4])
+def test_gossip_inline_handlers_partitioned(engine_mod, oracle_mod, parts):
+    """In-place handler dispatch (MonadDialog.hs:114-117) on the LP engine: the
+    phantom deliverer runs the handler itself."""
+    scn = scenarios.gossip(3000, seed=11, fork_strategy="inline")
+    agg, hashes, windows = engine_mod.run_partitioned(scn, parts=parts)
+    o = oracle_mod.run(scn, trace_cap=0)
+    for f in FIELDS:
+        assert int(agg[f]) == int(o.result[f]), (f, int(agg[f]), o.result[f])
+    assert np.array_equal(hashes, o.hashes)
+
+
 def test_gossip_replica_engine(engine_mod, oracle_mod):
     """The same scenario as one replica on the replica engine."""
     scn = scenarios.gossip(2000, seed=5)

@@ -50,3 +50,11 @@ def test_ping_pong(engine_mod, oracle_mod):
 def test_hotspot_small(engine_mod, oracle_mod):
     scn = scenarios.hotspot(n_senders=8, n_replicas=130, msg_num=40)
     _compare(scn, engine_mod, oracle_mod)
+
+
+def test_hotspot_inline_handlers(engine_mod, oracle_mod):
+    """ForkStrategy `const id` (MonadDialog.hs:114-117): Ping and Pong handlers
+    run in place in the delivering thread, on the destination node."""
+    scn = scenarios.hotspot(n_senders=8, n_replicas=130, msg_num=40, fork_strategy="inline")
+    st, ores = _compare(scn, engine_mod, oracle_mod)
+    assert ores["delivered"].sum() > 0

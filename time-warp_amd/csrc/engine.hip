@@ -1391,6 +1391,20 @@ struct Lane {
                         cinc(CW_UD);
                         hash(dst, TW_KIND_UNDELIV | kind, r0);
                         if (LP) tc = T_EXIT;  // the phantom deliverer ends here
+                    } else if (lpc & TW_LPC_INLINE) {
+                        // ForkStrategy `const id` (MonadDialog.hs:114-117): the handler runs
+                        // in this thread on the destination node -- its terms go to dst
+                        cinc(CW_DL);
+                        hash(dst, TW_KIND_RECV | kind, r0);
+                        hash_flush();
+                        rf[0] = r0; rf[WG] = (int64_t)link; rf[2 * WG] = LP ? r2 : (int64_t)th.w1;
+                        rf[3 * WG] = (int64_t)kind;
+                        hnode = dst;
+                        th.w1 = dst;
+                        // LP: the phantom deliverer becomes the handler thread, whose
+                        // later pops are ordinary (counted and hashed) pops
+                        th_clr_flags(th, F_PHANTOM);
+                        tgt = lpc & ~TW_LPC_INLINE;
                     } else {
                         cinc(CW_DL);
                         hash(dst, TW_KIND_RECV | kind, r0);

@@ -34,7 +34,7 @@ opaque register value usable only by throw_to / kill_thread.
 from __future__ import annotations
 
 from dataclasses import dataclass, field
-from typing import Callable, Dict, List, Optional, Union
+from typing import Callable, Dict, List, Optional, Sequence, Union
 
 import numpy as np
 
@@ -71,6 +71,7 @@ class Program:
         self._deferred: List[Callable[[], None]] = []
         self.msg_kinds: Dict[str, int] = {}
         self.listener_sets: List[Dict[int, Label]] = []
+        self.listener_inline: List[set] = []
         self._nfresh = 0
         # fixed stubs (include/timewarp.h TW_PC_*): deliverer and timeout watchdog
         self._emit(isa.OP_WAIT_REG, 2)
@@ -123,10 +124,18 @@ class Program:
             self.msg_kinds[name] = len(self.msg_kinds)
         return self.msg_kinds[name]
 
-    def listener_set(self, listeners: Dict[str, Union[str, Label]]) -> int:
-        """A `listen` binding's listener list: message name -> handler entry."""
+    def listener_set(self, listeners: Dict[str, Union[str, Label]], inline: Sequence[str] = ()) -> int:
+        """A `listen` binding's listener list: message name -> handler entry.
+
+        `inline` names the messages whose handler runs in place in the
+        delivering thread (ForkStrategy `const id`, MonadDialog.hs:114-117);
+        the others are forked with `fork_` (the default, MonadDialog.hs:317)."""
+        unknown = set(inline) - set(listeners)
+        if unknown:
+            raise ValueError(f"inline strategy for messages without a listener: {sorted(unknown)}")
         s = {self.kind(k): (v if isinstance(v, Label) else self.label(v)) for k, v in listeners.items()}
         self.listener_sets.append(s)
+        self.listener_inline.append({self.kind(k) for k in inline})
         return len(self.listener_sets) - 1
 
     def defer(self, fn: Callable[[], None]) -> None:
@@ -152,7 +161,7 @@ class Program:
             for k, lab in s.items():
                 if lab.pc is None:
                     raise ValueError(f"unbound listener {lab.name}")
-                ls[si, k] = lab.pc
+                ls[si, k] = lab.pc | (isa.LPC_INLINE if k in self.listener_inline[si] else 0)
         consts = np.array(self.consts if self.consts else [0], dtype=np.int64)
         return Image(insns=insns, consts=consts, listener_pc=ls, n_msg_kinds=nk,
                      n_listener_sets=len(self.listener_sets), labels=dict(self._labels))

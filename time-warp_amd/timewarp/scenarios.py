@@ -234,7 +234,7 @@ def ping_pong(n_replicas: int = 1, round_trips: int = 1, network_delay=(ms(1), m
 # ------------------------------------------------------------------ hotspot
 def hotspot(n_senders: int = 256, n_replicas: int = 1, msg_num: int = 1000, msg_rate: int = 1000,
             duration_s: int = 10, network_delay=(ms(1), ms(5)), seed_base: int = 0,
-            near_horizon_us: int = sec(10)) -> Scenario:
+            near_horizon_us: int = sec(10), fork_strategy: str = "fork") -> Scenario:
     """bench/Network many-senders -> one-receiver request/response.
 
     Sender (Sender/Main.hs:34-64): listen for Pong, then per message
@@ -243,14 +243,21 @@ def hotspot(n_senders: int = 256, n_replicas: int = 1, msg_num: int = 1000, msg_
     finally ``wait (for 1 sec)`` and close.  Receiver (Receiver/Main.hs:32-41):
     listen, on Ping reply Pong, stop after ``duration``.  Node i < S = sender i,
     node S = receiver, node S+1 hosts main.  Links: i -> S (id i), S -> i (id S+i).
+
+    ``fork_strategy="inline"`` dispatches Ping and Pong in place in the
+    delivering thread (ForkStrategy `const id`, MonadDialog.hs:114-117) instead
+    of the default `fork_` (MonadDialog.hs:317): two pops fewer per delivery.
     """
+    if fork_strategy not in ("fork", "inline"):
+        raise ValueError(f"fork_strategy must be 'fork' or 'inline', not {fork_strategy!r}")
+    inl = fork_strategy == "inline"
     S = int(n_senders)
     RECV, SYS = S, S + 1
     send_delay = 1_000_000 // msg_rate
     p = Program()
     K_PING, K_PONG = p.kind("Ping"), p.kind("Pong")
-    recv_set = p.listener_set({"Ping": "on_ping"})
-    send_set = p.listener_set({"Pong": "on_pong"})
+    recv_set = p.listener_set({"Ping": "on_ping"}, inline=("Ping",) if inl else ())
+    send_set = p.listener_set({"Pong": "on_pong"}, inline=("Pong",) if inl else ())
 
     c = p.function("main")
     c.seti(0, RECV).fork_("receiver_main", node_reg=0)
@@ -303,7 +310,7 @@ def hotspot(n_senders: int = 256, n_replicas: int = 1, msg_num: int = 1000, msg_
     in_flight = (network_delay[1] // max(1, send_delay) + 2) * 2
     max_slots = S * (in_flight + 2) + 64
     return Scenario(
-        name=f"hotspot_s{S}", image=img, topo=topo, n_replicas=n_replicas,
+        name=f"hotspot_s{S}" + ("_inline" if inl else ""), image=img, topo=topo, n_replicas=n_replicas,
         main_pc=img.pc_of("main"), main_node=SYS, link_table=table,
         max_slots=_capped(max_slots), queue_capacity=_capped(2 * max_slots + 256),
         run_capacity=_capped(2 * S + 64), near_horizon_us=near_horizon_us,
@@ -318,7 +325,7 @@ K_RUMOR_PAYLOAD = 7      # forwarding is payload-independent (tie-insensitive by
 
 def gossip(n_nodes: int = 1024, fanout: int = 4, n_replicas: int = 1, network_delay=(ms(1), ms(5)),
            seed: int = 0, start_us: int = sec(1), origin: int = 0, drop_log2: int = 0,
-           near_horizon_us: int = sec(10)) -> Scenario:
+           near_horizon_us: int = sec(10), fork_strategy: str = "fork") -> Scenario:
     """Config 4: one gossip/broadcast scenario (build-defined; the reference has
     no gossip example — it composes MonadDialog `listen`/`send`, MonadDialog.hs
     :149-271, exactly like examples/ping-pong).
@@ -331,12 +338,15 @@ def gossip(n_nodes: int = 1024, fanout: int = 4, n_replicas: int = 1, network_de
     constant, so the outcome does not depend on the order of equal-time
     deliveries.  Peers (distinct, != self) and per-link delays U[1 ms, 5 ms] are
     drawn from mkStdGen(seed); the minimum link delay (1 ms) is the lookahead
-    of the node-partitioned engine.
+    of the node-partitioned engine.  ``fork_strategy="inline"`` runs the
+    handler in place in the delivering thread (MonadDialog.hs:114-117).
     """
+    if fork_strategy not in ("fork", "inline"):
+        raise ValueError(f"fork_strategy must be 'fork' or 'inline', not {fork_strategy!r}")
     N, F = int(n_nodes), int(fanout)
     p = Program()
     K = p.kind("rumor")
-    lset = p.listener_set({"rumor": "on_rumor"})
+    lset = p.listener_set({"rumor": "on_rumor"}, inline=("rumor",) if fork_strategy == "inline" else ())
 
     c = p.function("main")
     c.wait(for_(start_us))
@@ -398,7 +408,7 @@ def gossip(n_nodes: int = 1024, fanout: int = 4, n_replicas: int = 1, network_de
     table[:, 0, :] = delays[:, None]
     listen = np.full(N, lset + 1, np.uint32)
     return Scenario(
-        name=f"gossip_n{N}", image=img, topo=topo, n_replicas=n_replicas,
+        name=f"gossip_n{N}" + ("_inline" if fork_strategy == "inline" else ""), image=img, topo=topo, n_replicas=n_replicas,
         main_pc=img.pc_of("main"), main_node=origin, link_table=table, node_listen=listen,
         max_slots=_capped(8 * N + 64), queue_capacity=_capped(8 * N + 256), run_capacity=_capped(4 * N + 64),
         near_horizon_us=near_horizon_us,
