@@ -247,6 +247,27 @@ int tw_read_hashes(tw_ctx* ctx, uint64_t* out, size_t n);
 int tw_read_final(tw_ctx* ctx, int64_t* max_final_t, uint64_t* delivered,
                   uint64_t* dropped, uint64_t* events);
 
+/* Trace records: every executed TRACE instruction (the reference's
+ * `logMeasure` / log lines, bench/Network/Common/Bench/Network/Commons.hs:
+ * 121-171 and Sender/Main.hs:46-61, Receiver/Main.hs:33-38) appended to a
+ * per-replica buffer, in the replica's execution order: the input of the
+ * LogReader's measures.csv (bench/Network/LogReader/Main.hs:85-119). */
+typedef struct tw_trace_rec {
+    int64_t t;      /* virtual time (µs)                    */
+    int64_t val;    /* the traced register                  */
+    uint32_t node;  /* the running thread's node            */
+    uint32_t tag;   /* the TRACE immediate                  */
+} tw_trace_rec;
+
+/* Record up to cap TRACE records per replica from the next tw_reset on
+ * (0 = off, the default; the count beyond cap is still reported).  Call after
+ * tw_load; allocates cap * n_replicas * 32 bytes of HBM. */
+int tw_set_trace(tw_ctx* ctx, uint32_t cap);
+
+/* A replica's trace records: copies min(cap, emitted, trace cap) records and
+ * stores the number emitted (possibly more than were kept) in *n_emitted. */
+int tw_read_trace(tw_ctx* ctx, uint32_t replica, tw_trace_rec* out, size_t cap, uint64_t* n_emitted);
+
 /* Duration (ms) of every event-kernel launch of the last tw_run, measured with
  * HIP events on the library's stream; returns the count written. */
 int tw_last_launch_ms(tw_ctx* ctx, double* out, size_t cap);

@@ -58,3 +58,32 @@ def test_hotspot_inline_handlers(engine_mod, oracle_mod):
     scn = scenarios.hotspot(n_senders=8, n_replicas=130, msg_num=40, fork_strategy="inline")
     st, ores = _compare(scn, engine_mod, oracle_mod)
     assert ores["delivered"].sum() > 0
+
+
+def test_hotspot_trace_records_and_measures(engine_mod, oracle_mod):
+    """TRACE records (tw_set_trace / tw_read_trace) equal the oracle's trace log
+    record for record, so measures.csv (bench/Network/LogReader/Main.hs:85-119)
+    built from the GPU run is the oracle's."""
+    from timewarp.measures import format_measures_csv, measures_from_trace, trace_tuples
+
+    scn = scenarios.hotspot(n_senders=6, n_replicas=70, msg_num=12)
+    with engine_mod.Engine() as e:
+        e.load(scn)
+        e.set_trace(1 << 11)
+        e.reset()
+        e.run()
+        for rep in (0, 33, 69):
+            recs, n = e.trace(rep)
+            o = oracle_mod.run(scn, replica=rep, trace_cap=1 << 11)
+            assert n == len(o.traces) == len(recs) > 0
+            assert trace_tuples(recs) == trace_tuples(o.traces)
+            assert format_measures_csv(measures_from_trace(trace_tuples(recs))) == \
+                format_measures_csv(measures_from_trace(trace_tuples(o.traces)))
+        # a small capacity keeps the first records and still counts the rest
+        e.set_trace(5)
+        e.reset()
+        e.run()
+        recs, n = e.trace(7)
+        o = oracle_mod.run(scn, replica=7, trace_cap=1 << 11)
+        assert len(recs) == 5 and n == len(o.traces)
+        assert trace_tuples(recs) == trace_tuples(o.traces)[:5]

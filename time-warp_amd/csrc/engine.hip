@@ -136,7 +136,7 @@ __device__ __forceinline__ uint32_t getf(const Th& t, uint32_t i) {
 enum {
     SC_NOW, SC_FINAL_T, SC_EVENTS, SC_DELIVERED, SC_DROPPED, SC_UNDELIV, SC_THREADS, SC_SEQ, SC_TIDC,
     SC_LIVE, SC_NEAR_N, SC_FAR_N, SC_STATUS, SC_MAIN_EXC, SC_PENDING_MAIN, SC_FREE_N, SC_FTOP, SC_BUMP,
-    SC_TMO_CTR, SC_RH0, SC_RC0 = SC_RH0 + TW_RUNS, SC_COUNT = SC_RC0 + TW_RUNS
+    SC_TMO_CTR, SC_RH0, SC_RC0 = SC_RH0 + TW_RUNS, SC_TRACE_N = SC_RC0 + TW_RUNS, SC_COUNT
 };
 
 struct Dev {
@@ -181,6 +181,8 @@ struct Dev {
     uint64_t* next_t;    // [1] min next-event time (atomicMin)
     uint32_t* lp_err;    // [1] inbox/outbox overflow
     unsigned long long* prof;  // [P_COUNT] diagnostic build only
+    uint4* trace;        // [trace_cap][R][2] TRACE records (tw_set_trace), replica mode
+    uint32_t trace_cap;
 };
 
 // ------------------------------------------------------------------ hashing
@@ -225,6 +227,7 @@ enum {
     CW_DL, CW_DR, CW_UD, CW_MAINEXC, CW_TMO,          // counters
     CW_YTL, CW_YTH, CW_CPC, CW_CNODE, CW_CRA, CW_CDEL, // step staging: wake time, child
     CW_Q0, CW_Q7 = CW_Q0 + 7,                          // child registers (4 x int64)
+    CW_TRN,                                            // TRACE records emitted (tw_set_trace)
     CW_DUMMY,                                          // target of idle lanes' predicated stores
     CW_COUNT
 };
@@ -1111,6 +1114,17 @@ struct Lane {
         return false;
     }
 
+    // TRACE record (tw_set_trace): appended in this replica's execution order
+    __device__ __forceinline__ void trace_rec(uint32_t node, int32_t tag, int64_t val) {
+        const uint32_t n = cg(CW_TRN);
+        cs(CW_TRN, n + 1);
+        if (n < c.trace_cap) {
+            uint4 GAS* q = gp(c.trace) + ((size_t)n * c.R + r) * 2;
+            q[0] = make_uint4((uint32_t)now, (uint32_t)((uint64_t)now >> 32), node, (uint32_t)tag);
+            q[1] = make_uint4((uint32_t)val, (uint32_t)((uint64_t)val >> 32), 0u, 0u);
+        }
+    }
+
     // ------------------------------------------------------------- interpreter
     __device__ __forceinline__ void pfail(bool cond, uint32_t st) {
         status = (cond && status == TW_REP_RUNNING) ? st : status;
@@ -1235,8 +1249,10 @@ struct Lane {
                     wv = v;
                 }
                 wm = me && lw;
-                if (need((f & U_TR) != 0))  // the popped node's term joins hacc
+                if (need((f & U_TR) != 0)) {  // the popped node's term joins hacc
                     hacc += (me && (f & U_TR)) ? term(now, TW_KIND_TRACE | ((uint32_t)imm & 0xFFFFu), ra) : 0ull;
+                    if (c.trace_cap && me && (f & U_TR)) trace_rec(th.w1, imm, ra);
+                }
                 if (need(jm != JM_NONE)) {
                     const int64_t b16 = (int64_t)(int16_t)b;
                     const uint32_t ci = (ra == rb ? 1u : 0u) | (ra < rb ? 2u : 0u) | (ra == b16 ? 4u : 0u);
@@ -1654,6 +1670,7 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
     for (int w = 0; w < CW_COUNT; ++w) L.cs(w, 0);
     L.cs(CW_MAINEXC, (uint32_t)sc[SC_MAIN_EXC * R]);
     L.cs(CW_TMO, (uint32_t)sc[SC_TMO_CTR * R]);
+    L.cs(CW_TRN, (uint32_t)sc[SC_TRACE_N * R]);
     const uint64_t events0 = sc[SC_EVENTS * R];
     const uint64_t ev_room64 = max_events > events0 ? max_events - events0 : 0;
     const uint32_t ev_room = ev_room64 > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)ev_room64;
@@ -1861,6 +1878,7 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
     sc[SC_STATUS * R] = L.status; sc[SC_MAIN_EXC * R] = L.cg(CW_MAINEXC);
     sc[SC_FREE_N * R] = L.free_n; sc[SC_FTOP * R] = L.ftop; sc[SC_BUMP * R] = L.bump;
     sc[SC_TMO_CTR * R] = L.cg(CW_TMO);
+    sc[SC_TRACE_N * R] = L.cg(CW_TRN);
     sc[SC_EVENTS * R] = events0 + L.d_ev;
     sc[SC_DELIVERED * R] += L.cg(CW_DL); sc[SC_DROPPED * R] += L.cg(CW_DR);
     sc[SC_UNDELIV * R] += L.cg(CW_UD); sc[SC_THREADS * R] += L.d_th;
@@ -1977,6 +1995,9 @@ int dalloc(tw_ctx* c, T** p, size_t n) {
 void free_all(tw_ctx* c) {
     for (void* p : c->allocs) (void)hipFree(p);
     c->allocs.clear();
+    if (c->d.trace) (void)hipFree(c->d.trace);
+    c->d.trace = nullptr;
+    c->d.trace_cap = 0;
     c->loaded = false;
 }
 
@@ -2444,6 +2465,53 @@ int tw_prof_read(tw_ctx* c, unsigned long long* out, size_t cap, int reset) {
     return (int)n;
 }
 #endif
+
+int tw_set_trace(tw_ctx* c, uint32_t cap) {
+    if (!c) return TW_ERR_INVALID;
+    if (!c->loaded) return TW_ERR_STATE;
+    if (c->lp) return TW_ERR_INVALID;  // LP lanes are nodes: no replica execution order to record
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    if (c->d.trace) {
+        HIPCHK(hipFree(c->d.trace));
+        c->d.trace = nullptr;
+    }
+    c->d.trace_cap = 0;
+    if (cap) {
+        HIPCHK(hipMalloc(&c->d.trace, (size_t)cap * c->d.R * 32));
+        c->d.trace_cap = cap;
+    }
+    return TW_OK;
+}
+
+int tw_read_trace(tw_ctx* c, uint32_t replica, tw_trace_rec* out, size_t cap, uint64_t* n_emitted) {
+    if (!c || (cap && !out)) return TW_ERR_INVALID;
+    if (!c->loaded) return TW_ERR_STATE;
+    const Dev& d = c->d;
+    if (replica >= d.R) return TW_ERR_INVALID;
+    HIPCHK(hipSetDevice(c->device));
+    uint64_t n = 0;
+    HIPCHK(hipMemcpyAsync(&n, d.scal + (size_t)SC_TRACE_N * d.R + replica, 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    if (n_emitted) *n_emitted = n;
+    size_t k = n < d.trace_cap ? (size_t)n : (size_t)d.trace_cap;
+    if (k > cap) k = cap;
+    if (k) {
+        // records of one replica are strided by R: one 2D copy
+        std::vector<uint4> buf(2 * k);
+        HIPCHK(hipMemcpy2DAsync(buf.data(), 32, d.trace + (size_t)replica * 2, (size_t)d.R * 32, 32, k,
+                                hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+        for (size_t i = 0; i < k; ++i) {
+            const uint4 a = buf[2 * i], b = buf[2 * i + 1];
+            out[i].t = (int64_t)(((uint64_t)a.y << 32) | a.x);
+            out[i].val = (int64_t)(((uint64_t)b.y << 32) | b.x);
+            out[i].node = a.z;
+            out[i].tag = a.w;
+        }
+    }
+    return TW_OK;
+}
 
 int tw_last_launch_ms(tw_ctx* c, double* out, size_t cap) {
     if (!c || !out) return TW_ERR_INVALID;

@@ -26,7 +26,11 @@ T_INF = (1 << 63) - 1
 
 EXPORTS = ["tw_create", "tw_load", "tw_reset", "tw_run", "tw_read_results", "tw_read_hashes", "tw_read_final",
            "tw_last_launch_ms", "tw_destroy", "tw_strerror", "tw_version",
-           "tw_lp_load", "tw_lp_window", "tw_lp_take_outbox", "tw_lp_inject", "tw_lp_results"]
+           "tw_lp_load", "tw_lp_window", "tw_lp_take_outbox", "tw_lp_inject", "tw_lp_results",
+           "tw_set_trace", "tw_read_trace"]
+
+# tw_trace_rec (include/timewarp.h)
+TRACE_DTYPE = np.dtype([("t", np.int64), ("val", np.int64), ("node", np.uint32), ("tag", np.uint32)])
 
 # tw_lp_record (include/timewarp.h)
 LP_RECORD_DTYPE = np.dtype([("t_arr", np.int64), ("payload", np.int64), ("link", np.uint32),
@@ -68,9 +72,11 @@ def load_library(path: Optional[str] = None):
     lib.tw_lp_take_outbox.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.POINTER(C.c_size_t)]
     lib.tw_lp_inject.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.POINTER(C.c_int64)]
     lib.tw_lp_results.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t]
+    lib.tw_set_trace.argtypes = [C.c_void_p, C.c_uint32]
+    lib.tw_read_trace.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_size_t, C.POINTER(C.c_uint64)]
     for name in ("tw_create", "tw_load", "tw_reset", "tw_run", "tw_read_results", "tw_read_hashes", "tw_read_final",
                  "tw_last_launch_ms", "tw_lp_load", "tw_lp_window", "tw_lp_take_outbox", "tw_lp_inject",
-                 "tw_lp_results"):
+                 "tw_lp_results", "tw_set_trace", "tw_read_trace"):
         getattr(lib, name).restype = C.c_int
     if path is None:
         _lib = lib
@@ -166,6 +172,20 @@ class Engine:
         out = np.zeros((self.scn.n_replicas, self.scn.n_nodes), np.uint64)
         _check(self.lib.tw_read_hashes(self.ctx, out.ctypes.data, out.size), "tw_read_hashes")
         return out
+
+    def set_trace(self, cap: int) -> "Engine":
+        """Record up to `cap` TRACE records per replica from the next reset on."""
+        _check(self.lib.tw_set_trace(self.ctx, int(cap)), "tw_set_trace")
+        self._trace_cap = int(cap)
+        return self
+
+    def trace(self, replica: int, cap: int = 1 << 20):
+        """(records, n_emitted): a replica's TRACE records in execution order
+        (TRACE_DTYPE), truncated at the trace capacity."""
+        buf = np.zeros(cap, TRACE_DTYPE)
+        n = C.c_uint64()
+        _check(self.lib.tw_read_trace(self.ctx, int(replica), buf.ctypes.data, cap, C.byref(n)), "tw_read_trace")
+        return buf[:min(int(n.value), cap, getattr(self, "_trace_cap", 0))].copy(), int(n.value)
 
     def launch_ms(self) -> np.ndarray:
         buf = np.zeros(1 << 16, np.float64)

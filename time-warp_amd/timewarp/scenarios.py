@@ -28,6 +28,7 @@ TAG_NO_PROGRESS = 5      # token-ring/Main.hs:184-187 "Token value hasn't change
 TAG_PING = 6             # ping-pong/Main.hs:73-75  "Get Ping"; bench PingReceived
 TAG_PONG = 7             # ping-pong/Main.hs:64-66  "Get Pong"; bench PongReceived
 TAG_PING_SENT = 8        # bench/Network/Sender/Main.hs:60 logMeasure PingSent
+TAG_PONG_SENT = 9        # bench/Network/Receiver/Main.hs:36 logMeasure PongSent
 
 EXC_VALUE_RECEIVED = isa.EXC_USER0  # data SignalException = ValueReceived Int (token-ring/Main.hs:156)
 
@@ -274,14 +275,15 @@ def hotspot(n_senders: int = 256, n_replicas: int = 1, msg_num: int = 1000, msg_
     c.end()
 
     c = p.function("on_ping")                         # Ping -> logMeasure; reply Pong
-    c.trace(TAG_PING, 0)
+    c.trace(TAG_PING, 0)                              # logMeasure PingReceived mid
+    c.trace(TAG_PONG_SENT, 0)                         # logMeasure PongSent mid
     c.reply_link(2, 1).send(2, K_PONG, 0)
     c.end()
 
     c = p.function("sender_main")
     c.listen(send_set)                                # listen (AtConnTo addr) [Pong -> ...]
     c.now(1).nstore(1, 0)                             # workTimer <- startTimer
-    c.seti(0, 0)
+    c.node(0).addi(0, 1)                              # msgIds [tid, tid+threadNum .. msgNum] (:40)
     top = c.here()
     stop = c.label()
     c.wait(for_(send_delay))                          # wait (for sendDelay)
@@ -289,8 +291,8 @@ def hotspot(n_senders: int = 256, n_replicas: int = 1, msg_num: int = 1000, msg_
     c.jlt(3, 1, stop)                                 # when (working > duration) mzero
     c.trace(TAG_PING_SENT, 0)
     c.link(1, 0).send(1, K_PING, 0)                   # send addr (Ping sMsgId payload)
-    c.addi(0, 1).seti(2, msg_num)
-    c.jlt(0, 2, top)
+    c.addi(0, S).seti(2, S * msg_num)
+    c.jle(0, 2, top)
     c.bind(stop)
     c.wait(for_(sec(1)))                              # wait (for 1 sec)  -- responses
     c.unlisten()                                      # sequence_ closeConns
