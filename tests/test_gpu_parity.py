@@ -87,3 +87,10 @@ def test_hotspot_trace_records_and_measures(engine_mod, oracle_mod):
         o = oracle_mod.run(scn, replica=7, trace_cap=1 << 11)
         assert len(recs) == 5 and n == len(o.traces)
         assert trace_tuples(recs) == trace_tuples(o.traces)[:5]
+
+
+def test_hotspot_bandwidth_aware_delays(engine_mod, oracle_mod):
+    """Link delays carrying the BinaryP transmission time of 1 kB payloads."""
+    scn = scenarios.hotspot(n_senders=8, n_replicas=90, msg_num=30, payload_bytes=1000,
+                            bandwidth_bytes_per_s=2_000_000)
+    _compare(scn, engine_mod, oracle_mod)

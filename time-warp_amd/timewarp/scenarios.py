@@ -235,7 +235,8 @@ def ping_pong(n_replicas: int = 1, round_trips: int = 1, network_delay=(ms(1), m
 # ------------------------------------------------------------------ hotspot
 def hotspot(n_senders: int = 256, n_replicas: int = 1, msg_num: int = 1000, msg_rate: int = 1000,
             duration_s: int = 10, network_delay=(ms(1), ms(5)), seed_base: int = 0,
-            near_horizon_us: int = sec(10), fork_strategy: str = "fork") -> Scenario:
+            near_horizon_us: int = sec(10), fork_strategy: str = "fork", payload_bytes: int = 0,
+            bandwidth_bytes_per_s: float = 0.0) -> Scenario:
     """bench/Network many-senders -> one-receiver request/response.
 
     Sender (Sender/Main.hs:34-64): listen for Pong, then per message
@@ -248,6 +249,11 @@ def hotspot(n_senders: int = 256, n_replicas: int = 1, msg_num: int = 1000, msg_
     ``fork_strategy="inline"`` dispatches Ping and Pong in place in the
     delivering thread (ForkStrategy `const id`, MonadDialog.hs:114-117) instead
     of the default `fork_` (MonadDialog.hs:317): two pops fewer per delivery.
+
+    ``bandwidth_bytes_per_s > 0`` adds each message's transmission time to its
+    link delay: the BinaryP wire size of `Ping/Pong MsgId Payload` with a
+    ``payload_bytes`` payload (timewarp.wire, Message.hs:155-202,
+    Commons.hs:49-70).
     """
     if fork_strategy not in ("fork", "inline"):
         raise ValueError(f"fork_strategy must be 'fork' or 'inline', not {fork_strategy!r}")
@@ -309,14 +315,19 @@ def hotspot(n_senders: int = 256, n_replicas: int = 1, msg_num: int = 1000, msg_
     table = np.zeros((topo.n_links, 1, n_replicas), np.uint32)
     for l in range(topo.n_links):
         table[l, 0, :] = g.range(*network_delay)
-    in_flight = (network_delay[1] // max(1, send_delay) + 2) * 2
+    if bandwidth_bytes_per_s > 0:
+        from .wire import bench_message_size, transmission_us
+        table[:S] += transmission_us(bench_message_size("Ping", payload_bytes), bandwidth_bytes_per_s)
+        table[S:2 * S] += transmission_us(bench_message_size("Pong", payload_bytes), bandwidth_bytes_per_s)
+    max_delay = int(table.max()) if table.size else int(network_delay[1])
+    in_flight = (max_delay // max(1, send_delay) + 2) * 2
     max_slots = S * (in_flight + 2) + 64
     return Scenario(
         name=f"hotspot_s{S}" + ("_inline" if inl else ""), image=img, topo=topo, n_replicas=n_replicas,
         main_pc=img.pc_of("main"), main_node=SYS, link_table=table,
         max_slots=_capped(max_slots), queue_capacity=_capped(2 * max_slots + 256),
         run_capacity=_capped(2 * S + 64), near_horizon_us=near_horizon_us,
-        meta=dict(config="hotspot", n_senders=S, msg_num=msg_num, msg_rate=msg_rate),
+        meta=dict(config="hotspot", n_senders=S, msg_num=msg_num, msg_rate=msg_rate, payload_bytes=payload_bytes),
     )
 
 
