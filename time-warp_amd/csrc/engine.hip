@@ -1772,33 +1772,40 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
         Th th;
         uint32_t slot = 0;
         bool run = false;
-        if (alive) {
-            if (pending_main) {  // runInSandbox main (TimedT.hs:237): runs at t=0, not a pop
+        // the rare cases (main's first run, quiescence, the event cap) behind one
+        // wave-uniform branch; the common path is a single divergent region
+        const bool rare = alive && (pending_main || L.live == 0 || L.d_ev >= ev_room);
+        if (__builtin_amdgcn_ballot_w64(rare)) {
+            if (rare && pending_main) {  // runInSandbox main (TimedT.hs:237): runs at t=0, not a pop
                 pending_main = 0;
                 L.pf_slot = 0xFFFFFFFFu;
                 L.fetch_rec(0, th);
                 L.rf[0] = th.r0; L.rf[WG] = th.r1; L.rf[2 * WG] = th.r2; L.rf[3 * WG] = th.r3;
                 L.hnode = th.w1;
                 run = true;
-            } else if (L.live == 0) {  // whileM_ notDone
-                if (!LP) L.status = TW_REP_DONE;  // an LP may still receive records
+            } else if (rare) {  // whileM_ notDone, or this launch's event cap
+                if (!LP && L.live == 0) L.status = TW_REP_DONE;  // an LP may still receive records
                 alive = false;
-            } else if (L.d_ev >= ev_room) {
-                alive = false;
-            } else {
-                // PQ.minView: the min of the near root and the far sources
-                if (L.far_dirty) L.far_min();
-                bool use_near = L.near_n != 0;
-                int64_t t = 0;
-                uint32_t sq = 0;
-                if (use_near) { t = L.nbase + (int64_t)(L.nrk >> 32); sq = (uint32_t)L.nrk; slot = L.nrs; }
-                const bool use_far = L.fsrc >= 0 && (!use_near || tless(L.fmt, L.fms, t, sq));
-                if (use_far) { t = L.fmt; sq = L.fms; slot = L.fmsl; }
-                STIME(ts1);
-                STADDL(K_CYC_SEL, ts1 - tl0);
-                if ((!use_near && !use_far) || t > t_end) {
-                    alive = false;  // parked beyond t_end (an empty queue cannot happen while live > 0)
-                } else {
+            }
+        }
+        bool popping = alive && !rare;
+        {
+            // PQ.minView: the min of the near root and the far sources
+            if (L.far_dirty) L.far_min();
+            const bool use_near = L.near_n != 0;
+            const int64_t tn = L.nbase + (int64_t)(L.nrk >> 32);
+            const bool use_far = L.fsrc >= 0 && (!use_near || tless(L.fmt, L.fms, tn, (uint32_t)L.nrk));
+            const int64_t t = use_far ? L.fmt : tn;
+            const uint32_t sq = use_far ? L.fms : (uint32_t)L.nrk;
+            slot = use_far ? L.fmsl : (use_near ? L.nrs : 0u);
+            STIME(ts1);
+            STADDL(K_CYC_SEL, ts1 - tl0);
+            // parked beyond t_end (an empty queue cannot happen while live > 0)
+            const bool parked = popping && ((!use_near && !use_far) || t > t_end);
+            alive = parked ? false : alive;
+            popping = popping && !parked;
+            if (popping) {
+                {
                     L.fetch_rec(slot, th);  // prefetched copy or HBM
                     STIME(ts2);
                     STADDL(K_CYC_FETCH, ts2 - ts1);
@@ -1846,6 +1853,7 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
                 }
             }
         }
+        if (!popping) slot = 0u;  // main's first run is slot 0; idle lanes do not use it
         STIME(tp0);
         L.prefetch_all(run ? slot : 0xFFFFFFFFu);
         STIME(tl1);
