@@ -299,6 +299,11 @@ struct BoolC {
 
 template <bool LP, int WG, int NC>
 struct Lane {
+    // per-lane hot passes (lanes at different hot ops share a pass) pay off where
+    // lanes diverge -- logical processes and the few-replica sparse geometry; the
+    // dense replica geometry runs lock-step programs and keeps the cheaper
+    // opcode-uniform pass
+    static constexpr bool PL = LP || WG < 64;
     Dev c;  // by value: kernel arguments stay in SGPRs
     uint32_t r;       // replica
     // LDS (lane-offset pointers; element j at [j * WG])
@@ -1167,11 +1172,12 @@ struct Lane {
             const uint32_t first = (uint32_t)__builtin_ctzll(mask);
             const uint32_t op = __builtin_amdgcn_readlane(in.x, first) & 0xFFu;
             const uint32_t fl = __builtin_amdgcn_readlane(lfl, first);
-            // a pass of a hot-class op (no U_FX) serves every running lane at any
+            // PL: a pass of a hot-class op (no U_FX) serves every running lane at any
             // hot-class op, each with its own uop fields; a rare op serves the
             // lanes holding that opcode
             const bool hot = !(fl & U_FX);
-            const bool at = running & ((hot & !(lfl & U_FX)) | (!hot & ((in.x & 0xFFu) == op)));
+            const bool at = PL ? (running & ((hot & !(lfl & U_FX)) | (!hot & ((in.x & 0xFFu) == op))))
+                               : (running && (in.x & 0xFFu) == op);
 #ifndef TW_X_NOCAP
             n += at ? 1u : 0u;
             const bool capped = at && n > TW_STEP_CAP;  // TW_REP_ERR_INSN before executing it
@@ -1285,8 +1291,14 @@ struct Lane {
                 }
             };
             if (hot) {
-                if (__builtin_amdgcn_ballot_w64(at && lfl != fl) == 0) hot_body(BoolC<true>{}, fl);
-                else hot_body(BoolC<false>{}, lfl);
+                if constexpr (PL) {
+                    if (__builtin_expect(__builtin_amdgcn_ballot_w64(at && lfl != fl) == 0, 1))
+                        hot_body(BoolC<true>{}, fl);
+                    else
+                        hot_body(BoolC<false>{}, lfl);
+                } else {
+                    hot_body(BoolC<true>{}, fl);
+                }
             }
             if (fl & U_FX) {
             switch (op) {
