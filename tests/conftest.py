@@ -42,4 +42,4 @@ def tw_geometry(request, monkeypatch):
 
 def pytest_generate_tests(metafunc):
     if "tw_geometry" in metafunc.fixturenames and metafunc.definition.get_closest_marker("gpu"):
-        metafunc.parametrize("tw_geometry", ["dense", "sparse"], indirect=True)
+        metafunc.parametrize("tw_geometry", ["dense", "sparse", "half"], indirect=True)

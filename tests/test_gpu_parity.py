@@ -52,6 +52,14 @@ def test_hotspot_small(engine_mod, oracle_mod):
     _compare(scn, engine_mod, oracle_mod)
 
 
+def test_gatekeeper_raw_listener(engine_mod, oracle_mod):
+    """listenR (MonadDialog.hs:226-256): the raw listener runs for every
+    message (also `Junk`, which has no typed listener) and gates the typed one."""
+    scn = scenarios.gatekeeper(n_clients=6, n_replicas=200, msg_num=24, junk_every=3)
+    st, ores = _compare(scn, engine_mod, oracle_mod)
+    assert (ores["status"] == 1).all() and ores["undeliverable"].sum() == 0
+
+
 def test_hotspot_inline_handlers(engine_mod, oracle_mod):
     """ForkStrategy `const id` (MonadDialog.hs:114-117): Ping and Pong handlers
     run in place in the delivering thread, on the destination node."""

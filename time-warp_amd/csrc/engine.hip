@@ -46,6 +46,15 @@
 // 768-entry near heap (most of a hotspot receiver's backlog stays on chip).
 #define TW_WG_SPARSE 16
 #define TW_NEAR_SPARSE 768
+// (One 16-lane wave: spreading them as 4 waves of 4 lanes over the CU's four
+// SIMDs measured the same C5 rate, 0.240 vs 0.245 G events/s -- a hotspot
+// replica's events are a chain of dependent HBM round trips, not issue.)
+// Half geometry (replica-dense runs): the dense LDS layout (256 replicas per
+// workgroup) served by 8 waves of 32 active lanes, so 64k replicas fill two
+// waves per SIMD; that instance is built for 256 registers so both fit, and
+// one wave's scalar, LDS and branch issue overlaps the other's VALU and
+// memory waits.
+#define TW_HALF_LANES 32
 #ifndef TW_RUNS
 #define TW_RUNS 4               // monotone far-queue runs per replica
 #endif
@@ -1628,8 +1637,10 @@ __host__ __device__ constexpr size_t fixed_lds_bytes() {
            (size_t)4 * WG * 8 + (size_t)CW_COUNT * WG * 4;
 }
 
-template <bool LP, int WG, int NC>
-__global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(1, 2)))
+// WG replicas per workgroup share its LDS; TPW of each wave's 64 lanes carry a
+// replica (64, or TW_HALF_LANES for the half geometry: twice the waves).
+template <bool LP, int WG, int NC, int TPW = 64>
+__global__ void __launch_bounds__(WG * 64 / TPW) __attribute__((amdgpu_waves_per_eu((WG * 64 / TPW + 255) / 256, 2)))
 tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
     extern __shared__ __attribute__((aligned(16))) uint64_t lds_raw[];
     uint4 LAS* s_pf = (uint4 LAS*)lds_raw;
@@ -1642,15 +1653,18 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
     int64_t LAS* s_c = (int64_t LAS*)(s_p + c.n_insns + 1);
     uint32_t LAS* s_u = (uint32_t LAS*)(s_c + c.n_consts);
     {
-        for (uint32_t i = threadIdx.x; i <= c.n_insns; i += WG) {
+        for (uint32_t i = threadIdx.x; i <= c.n_insns; i += WG * 64 / TPW) {
             const uint2 in = gp(c.insns)[i];
             s_p[i] = in;
             s_u[i] = uop_of(in.x & 0xFFu);
         }
-        for (uint32_t i = threadIdx.x; i < c.n_consts; i += WG) s_c[i] = gp(c.consts)[i];
+        for (uint32_t i = threadIdx.x; i < c.n_consts; i += WG * 64 / TPW) s_c[i] = gp(c.consts)[i];
         __syncthreads();
     }
-    uint32_t r = blockIdx.x * WG + threadIdx.x;
+    if (TPW < 64 && (threadIdx.x & 63u) >= TPW) return;
+    const uint32_t wbase = (threadIdx.x >> 6) * TPW;  // the wave's first lane in the LDS layout
+    const uint32_t li = wbase + (threadIdx.x & 63u);
+    uint32_t r = blockIdx.x * WG + li;
     if (r >= c.R) return;
     uint64_t* sc = gp(c.scal) + r;
     const size_t R = c.R;
@@ -1659,13 +1673,13 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
     Lane<LP, WG, NC> L;
     L.c = c;
     L.r = r;
-    L.nk = s_k + threadIdx.x;
-    L.ns = s_s + threadIdx.x;
-    L.rf = s_rf + threadIdx.x;
-    L.cw = s_cw + threadIdx.x;
-    L.pfs = s_pf + threadIdx.x;
-    L.rq = s_rq + threadIdx.x;
-    L.pfs_wave = __builtin_amdgcn_readfirstlane((uint32_t)(size_t)(s_pf + (threadIdx.x & ~63u)));
+    L.nk = s_k + li;
+    L.ns = s_s + li;
+    L.rf = s_rf + li;
+    L.cw = s_cw + li;
+    L.pfs = s_pf + li;
+    L.rq = s_rq + li;
+    L.pfs_wave = __builtin_amdgcn_readfirstlane((uint32_t)(size_t)(s_pf + wbase));
     L.P = s_p;
     L.PU = s_u;
     L.K = s_c;
@@ -1976,7 +1990,7 @@ struct tw_ctx {
     int64_t* nv_init = nullptr;
     uint32_t* listen_init = nullptr;
     size_t lds_bytes = 0;
-    int geo = 0;  // 0: dense (TW_WG, TW_NEAR_CAP); 1: sparse (TW_WG_SPARSE, TW_NEAR_SPARSE)
+    int geo = 0;  // 0: dense (TW_WG, TW_NEAR_CAP); 1: sparse (TW_WG_SPARSE, TW_NEAR_SPARSE); 2: half (TW_WG, TW_NEAR_CAP, TW_HALF_LANES lanes per wave)
     // LP mode
     bool lp = false;
     uint4* foreign = nullptr;      // [out_cap][2]
@@ -2023,10 +2037,10 @@ void free_all(tw_ctx* c) {
 
 }  // namespace
 
-template <bool LP, int WG, int NC>
+template <bool LP, int WG, int NC, int TPW = 64>
 static void launch_run(tw_ctx* c, hipStream_t st, int64_t t_end, uint64_t limit, uint32_t budget) {
     const uint32_t blocks = (uint32_t)((c->d.R + WG - 1) / WG);
-    hipLaunchKernelGGL((tw_run_kernel<LP, WG, NC>), dim3(blocks), dim3(WG), c->lds_bytes, st, c->d, t_end, limit,
+    hipLaunchKernelGGL((tw_run_kernel<LP, WG, NC, TPW>), dim3(blocks), dim3(WG * 64 / TPW), c->lds_bytes, st, c->d, t_end, limit,
                        budget);
 }
 
@@ -2131,14 +2145,20 @@ static int load_common(tw_ctx* c, const tw_scenario_desc* s, bool lp, uint32_t l
         int geo = (!lp && R <= 8192) ? 1 : 0;
         if (g && !strcmp(g, "dense")) geo = 0;
         if (g && !strcmp(g, "sparse")) geo = 1;
-        if (lp || fixed_lds_bytes<TW_WG_SPARSE, TW_NEAR_SPARSE>() + prog_lds > 160 * 1024) geo = 0;
+        if (g && !strcmp(g, "half")) geo = 2;
+        if (lp) geo = 0;
+        if (geo == 1 && fixed_lds_bytes<TW_WG_SPARSE, TW_NEAR_SPARSE>() + prog_lds > 160 * 1024) geo = 0;
         c->geo = geo;
     }
-    c->lds_bytes = (c->geo ? fixed_lds_bytes<TW_WG_SPARSE, TW_NEAR_SPARSE>() : fixed_lds_bytes<TW_WG, TW_NEAR_CAP>()) +
+    c->lds_bytes = (c->geo == 1 ? fixed_lds_bytes<TW_WG_SPARSE, TW_NEAR_SPARSE>()
+                                  : fixed_lds_bytes<TW_WG, TW_NEAR_CAP>()) +
                    prog_lds;
     if (c->lds_bytes > 160 * 1024) { free_all(c); return TW_ERR_INVALID; }  // program + constants must fit in LDS
-    if (c->geo)
+    if (c->geo == 1)
         HIPCHK(hipFuncSetAttribute((const void*)tw_run_kernel<false, TW_WG_SPARSE, TW_NEAR_SPARSE>,
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)c->lds_bytes));
+    else if (c->geo == 2)
+        HIPCHK(hipFuncSetAttribute((const void*)tw_run_kernel<false, TW_WG, TW_NEAR_CAP, TW_HALF_LANES>,
                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)c->lds_bytes));
     else if (lp)
         HIPCHK(hipFuncSetAttribute((const void*)tw_run_kernel<true, TW_WG, TW_NEAR_CAP>,
@@ -2161,7 +2181,7 @@ static int load_common(tw_ctx* c, const tw_scenario_desc* s, bool lp, uint32_t l
     ALLOC(d.free_stk, (size_t)d.S * R);
     ALLOC(d.far, (size_t)d.Q * R);
     ALLOC(d.runs, (size_t)(d.Cr ? TW_RUNS * (size_t)d.Cr : 1) * R);
-    ALLOC(d.near_spill, (size_t)(c->geo ? TW_NEAR_SPARSE : TW_NEAR_CAP) * R);
+    ALLOC(d.near_spill, (size_t)(c->geo == 1 ? TW_NEAR_SPARSE : TW_NEAR_CAP) * R);
     ALLOC(d.dummy, (size_t)5 * R);
     ALLOC(d.nvars, (size_t)d.N * 4 * R);
     ALLOC(d.hash, (size_t)d.N * R);
@@ -2285,8 +2305,10 @@ int tw_run(tw_ctx* c, int64_t t_end_us, uint64_t max_events, tw_stats* out) {
             HIPCHK(hipEventRecord(c->ev_pool[2 * i], st));
             if (c->lp)
                 launch_run<true, TW_WG, TW_NEAR_CAP>(c, st, t_end_us, limit, budget);
-            else if (c->geo)
+            else if (c->geo == 1)
                 launch_run<false, TW_WG_SPARSE, TW_NEAR_SPARSE>(c, st, t_end_us, limit, budget);
+            else if (c->geo == 2)
+                launch_run<false, TW_WG, TW_NEAR_CAP, TW_HALF_LANES>(c, st, t_end_us, limit, budget);
             else
                 launch_run<false, TW_WG, TW_NEAR_CAP>(c, st, t_end_us, limit, budget);
             HIPCHK(hipGetLastError());

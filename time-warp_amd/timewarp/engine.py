@@ -139,8 +139,8 @@ class Engine:
         d = scn.desc()
         old = os.environ.get("TW_GEOMETRY")
         if geometry is not None:
-            if geometry not in ("dense", "sparse"):
-                raise ValueError(f"geometry must be 'dense' or 'sparse', not {geometry!r}")
+            if geometry not in ("dense", "sparse", "half"):
+                raise ValueError(f"geometry must be 'dense', 'sparse' or 'half', not {geometry!r}")
             os.environ["TW_GEOMETRY"] = geometry
         try:
             _check(self.lib.tw_load(self.ctx, C.addressof(d)), "tw_load")

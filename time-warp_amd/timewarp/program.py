@@ -24,6 +24,8 @@ reference (file:line)            lowering
 ``virtualTime`` / ``myThreadId`` ``Code.now(r)`` / ``Code.my_thread_id(r)``
 ``send addr msg`` (MonadDialog.hs:154-156)  ``Code.send(link, kind, payload)``
 ``listen (AtPort p) [..]`` (:204-211)       ``Code.listen(set)``
+``listenR binding ls raw`` (:226-256)       ``Code.listen(set)`` with
+                                 ``listener_set(..., raw=fn)``
 ``reply`` (:177-180)             ``Code.reply_link(r, r_in)`` + ``send``
 ===============================  ==============================================
 
@@ -72,6 +74,7 @@ class Program:
         self.msg_kinds: Dict[str, int] = {}
         self.listener_sets: List[Dict[int, Label]] = []
         self.listener_inline: List[set] = []
+        self.listener_raw: List[Optional[Callable[["Code", Label], None]]] = []
         self._nfresh = 0
         # fixed stubs (include/timewarp.h TW_PC_*): deliverer and timeout watchdog
         self._emit(isa.OP_WAIT_REG, 2)
@@ -124,19 +127,58 @@ class Program:
             self.msg_kinds[name] = len(self.msg_kinds)
         return self.msg_kinds[name]
 
-    def listener_set(self, listeners: Dict[str, Union[str, Label]], inline: Sequence[str] = ()) -> int:
+    def listener_set(self, listeners: Dict[str, Union[str, Label]], inline: Sequence[str] = (),
+                     raw: Optional[Callable[["Code", Label], None]] = None) -> int:
         """A `listen` binding's listener list: message name -> handler entry.
 
         `inline` names the messages whose handler runs in place in the
         delivering thread (ForkStrategy `const id`, MonadDialog.hs:114-117);
-        the others are forked with `fork_` (the default, MonadDialog.hs:317)."""
+        the others are forked with `fork_` (the default, MonadDialog.hs:317).
+
+        `raw` makes the binding a ``listenR`` (MonadDialog.hs:226-256): the raw
+        listener runs first, in the handler's thread, for every message that
+        reaches the port -- also for names without a typed listener
+        (:240-244).  ``raw(code, accept)`` emits its body: jumping to
+        ``accept`` is ``return True`` (the typed listener, if any, runs next,
+        :246-253), ending the thread is ``return False``; an uncaught exception
+        also ends the thread, which is what ``invokeRawListenerSafe``'s
+        ``return False`` amounts to (:262-264).  The body sees the handler
+        registers (r0 payload, r1 incoming link, r3 kind) and must leave r0
+        and r1 as it found them; r2 and r3 are scratch (r3 is restored before
+        the typed listener).  It is expanded once per message kind at
+        `finalize`, since the ISA has no call/return."""
         unknown = set(inline) - set(listeners)
-        if unknown:
+        if unknown and raw is None:
             raise ValueError(f"inline strategy for messages without a listener: {sorted(unknown)}")
         s = {self.kind(k): (v if isinstance(v, Label) else self.label(v)) for k, v in listeners.items()}
         self.listener_sets.append(s)
         self.listener_inline.append({self.kind(k) for k in inline})
+        self.listener_raw.append(raw)
         return len(self.listener_sets) - 1
+
+    def _expand_raw_listeners(self) -> None:
+        """listenR: per (set, kind), an entry that runs the raw listener and
+        continues to the typed listener (or ends) on `accept`."""
+        kinds = sorted(self.msg_kinds.values())
+        for si, raw in enumerate(self.listener_raw):
+            if raw is None:
+                continue
+            typed = self.listener_sets[si]
+            entries: Dict[int, Label] = {}
+            for k in kinds:
+                entry = self.label()
+                accept = self.label()
+                self.bind(entry)
+                c = Code(self)
+                raw(c, accept)
+                c.end()  # falling off the raw body = return False
+                self.bind(accept)
+                if k in typed:
+                    c.seti(3, k).jmp(typed[k])
+                else:
+                    c.end()
+                entries[k] = entry
+            self.listener_sets[si] = entries
 
     def defer(self, fn: Callable[[], None]) -> None:
         self._deferred.append(fn)
@@ -147,6 +189,7 @@ class Program:
             fns, self._deferred = self._deferred, []
             for fn in fns:
                 fn()
+        self._expand_raw_listeners()
         insns = np.zeros((len(self._insns), 2), dtype=np.uint32)
         for i, (w0, imm) in enumerate(self._insns):
             if isinstance(imm, Label):

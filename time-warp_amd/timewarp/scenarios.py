@@ -331,6 +331,97 @@ def hotspot(n_senders: int = 256, n_replicas: int = 1, msg_num: int = 1000, msg_
     )
 
 
+# --------------------------------------------------------------- gatekeeper
+TAG_RAW = 10             # raw listener saw a message (MonadDialog.hs:226-256)
+TAG_REQ = 11
+TAG_ACK = 12
+
+
+def gatekeeper(n_clients: int = 4, n_replicas: int = 1, msg_num: int = 20, junk_every: int = 4,
+               network_delay=(ms(1), ms(5)), seed_base: int = 0, raw: bool = True,
+               near_horizon_us: int = sec(10)) -> Scenario:
+    """A ``listenR`` server (MonadDialog.hs:226-256): the raw listener logs
+    every message that reaches the port and returns True only for even
+    payloads; the typed listener for `Req` then replies `Ack`.  Clients also
+    send `Junk`, a name the server has no typed listener for: the reference
+    still runs the raw listener for it (:240-244).
+
+    Node i < C = client i, node C = server, node C+1 hosts main.  Client i
+    sends Req with payload i*msg_num + m every 1 ms (m = 0..msg_num-1) and a
+    Junk after every Req whose payload is -1 mod `junk_every`, then waits 1 s
+    for Acks.  Links:
+    i -> C (id i), C -> i (id C+i), per-link delays ~ U[1, 5] ms from
+    mkStdGen(replica).  ``raw=False`` binds the same typed listener with a
+    plain ``listen`` (every Req is answered, Junk is undeliverable)."""
+    C = int(n_clients)
+    SRV, SYS = C, C + 1
+    p = Program()
+    K_REQ, K_ACK, K_JUNK = p.kind("Req"), p.kind("Ack"), p.kind("Junk")
+
+    def raw_listener(c, accept):
+        c.trace(TAG_RAW, 0)                           # raw (header, raw) -> log it
+        c.mov(2, 0).modi(2, 2)
+        c.jeqi(2, 0, accept)                          # return (even payload)
+
+    srv_set = p.listener_set({"Req": "on_req"}, raw=raw_listener if raw else None)
+    cli_set = p.listener_set({"Ack": "on_ack"})
+
+    c = p.function("main")
+    c.seti(0, SRV).fork_("server_main", node_reg=0)
+    c.seti(0, 0).seti(2, C)
+    loop = c.here()
+    c.fork_("client_main", node_reg=0)
+    c.addi(0, 1).jlt(0, 2, loop)
+    c.end()
+
+    c = p.function("server_main")
+    c.listen(srv_set)                                 # listenR (AtPort p) [Req] raw
+    c.wait(for_(sec(10)))
+    c.unlisten()
+    c.end()
+
+    c = p.function("on_req")
+    c.trace(TAG_REQ, 0)
+    c.reply_link(2, 1).send(2, K_ACK, 0)
+    c.end()
+
+    c = p.function("client_main")
+    c.listen(cli_set)
+    c.node(0).muli(0, msg_num)                        # r0 = first payload
+    c.mov(1, 0).addi(1, msg_num)                      # r1 = end
+    top = c.here()
+    skip = c.label()
+    c.wait(for_(ms(1)))
+    c.link(2, 0).send(2, K_REQ, 0)
+    c.mov(3, 0).modi(3, junk_every).jnei(3, junk_every - 1, skip)
+    c.send(2, K_JUNK, 0)
+    c.bind(skip)
+    c.addi(0, 1).jlt(0, 1, top)
+    c.wait(for_(sec(1)))
+    c.unlisten()
+    c.end()
+
+    c = p.function("on_ack")
+    c.trace(TAG_ACK, 0)
+    c.end()
+
+    img = p.finalize()
+    out = [[SRV] for _ in range(C)] + [list(range(C)), []]
+    topo = Topology.from_out_lists(C + 2, out)
+    g = StdGenVec(seed_base + np.arange(n_replicas, dtype=np.int64))
+    table = np.zeros((topo.n_links, 1, n_replicas), np.uint32)
+    for l in range(topo.n_links):
+        table[l, 0, :] = g.range(*network_delay)
+    max_slots = C * 24 + 64
+    return Scenario(
+        name=f"gatekeeper_c{C}" + ("" if raw else "_plain"), image=img, topo=topo, n_replicas=n_replicas,
+        main_pc=img.pc_of("main"), main_node=SYS, link_table=table,
+        max_slots=_capped(max_slots), queue_capacity=_capped(2 * max_slots + 256),
+        run_capacity=_capped(2 * C + 64), near_horizon_us=near_horizon_us,
+        meta=dict(config="gatekeeper", n_clients=C, msg_num=msg_num, junk_every=junk_every, raw=raw),
+    )
+
+
 # ------------------------------------------------------------------- gossip
 TAG_RUMOR_FIRST = 9      # first receipt of the rumor at a node
 K_RUMOR_PAYLOAD = 7      # forwarding is payload-independent (tie-insensitive by design)

@@ -27,6 +27,8 @@ for s in "$@"; do
     bench_c2) step bench_c2 400 python bench.py --config ping_pong ;;
     bench_c4) step bench_c4 500 python bench.py --config gossip ;;
     bench_c5) step bench_c5 400 python bench.py --config hotspot ;;
+    geo=*) export TW_GEOMETRY=${s#geo=}; SFX=_${s#geo=} ;;
+    pytest_geo) step pytest_geo 600 python -u -m pytest tests/ -q -m gpu -x --timeout 120 --timeout-method thread -k "$TW_GEOMETRY" ;;
     lib=*) export TW_LIB=$PWD/time-warp_amd/lib/libtimewarp_${s#lib=}.so; SFX=_${s#lib=} ;;
     pmc) bash tools/pmc.sh gpurun_out/pmc$SFX > gpurun_out/pmc$SFX.log 2>&1; rc=$?; echo "pmc=$rc"; [ $rc -eq 0 ] || exit $rc ;;
     *) echo "unknown step $s"; exit 2 ;;
