@@ -158,10 +158,24 @@ class Program:
 
     def _expand_raw_listeners(self) -> None:
         """listenR: per (set, kind), an entry that runs the raw listener and
-        continues to the typed listener (or ends) on `accept`."""
+        continues to the typed listener (or ends) on `accept`.  Every set gets
+        an entry for every message kind; `undeliverable` then means that no
+        listener is bound at the destination port."""
         kinds = sorted(self.msg_kinds.values())
+        no_listener: Optional[Label] = None
         for si, raw in enumerate(self.listener_raw):
             if raw is None:
+                # plain listen = listenH = listenR with `const $ return True`
+                # (:216-219): a name without a typed listener still reaches a
+                # handler thread, which only logs "No listener with name"
+                # (:240-244) and ends
+                missing = [k for k in kinds if k not in self.listener_sets[si]]
+                if missing and no_listener is None:
+                    no_listener = self.label()
+                    self.bind(no_listener)
+                    self._emit(isa.OP_END)
+                for k in missing:
+                    self.listener_sets[si][k] = no_listener
                 continue
             typed = self.listener_sets[si]
             entries: Dict[int, Label] = {}

@@ -352,7 +352,8 @@ def gatekeeper(n_clients: int = 4, n_replicas: int = 1, msg_num: int = 20, junk_
     for Acks.  Links:
     i -> C (id i), C -> i (id C+i), per-link delays ~ U[1, 5] ms from
     mkStdGen(replica).  ``raw=False`` binds the same typed listener with a
-    plain ``listen`` (every Req is answered, Junk is undeliverable)."""
+    plain ``listen`` (every Req is answered; Junk ends in a handler thread
+    that only logs "No listener", MonadDialog.hs:240-244)."""
     C = int(n_clients)
     SRV, SYS = C, C + 1
     p = Program()
