@@ -60,6 +60,14 @@ def test_gatekeeper_raw_listener(engine_mod, oracle_mod):
     assert (ores["status"] == 1).all() and ores["undeliverable"].sum() == 0
 
 
+def test_socket_state_user_state(engine_mod, oracle_mod):
+    """examples/socket-state: per-connection `userStateR` counters (state cells
+    addressed by the incoming link) and the server's stop at 10 s."""
+    scn = scenarios.socket_state(n_replicas=300, seed_base=7)
+    st, ores = _compare(scn, engine_mod, oracle_mod)
+    assert (ores["status"] == 1).all() and ores["undeliverable"].sum() > 0
+
+
 def test_hotspot_inline_handlers(engine_mod, oracle_mod):
     """ForkStrategy `const id` (MonadDialog.hs:114-117): Ping and Pong handlers
     run in place in the delivering thread, on the destination node."""

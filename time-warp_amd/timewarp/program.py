@@ -27,6 +27,8 @@ reference (file:line)            lowering
 ``listenR binding ls raw`` (:226-256)       ``Code.listen(set)`` with
                                  ``listener_set(..., raw=fn)``
 ``reply`` (:177-180)             ``Code.reply_link(r, r_in)`` + ``send``
+``userStateR`` (socket-state :91-93)  ``Code.user_state_load/_store`` (a state
+                                 cell per incoming link)
 ===============================  ==============================================
 
 Registers r0..r3 are per-thread int64 and are copied into forked children
@@ -412,6 +414,20 @@ class Code:
 
     def nstorex(self, r: int, var: int, node_reg: int):
         return self._e(isa.OP_NSTOREX, r, (var & 0xFF) | ((node_reg & 3) << 8))
+
+    def user_state_load(self, r: int, var: int, link_reg: int, state_base: int, scratch: int = 2):
+        """``userStateR`` (Transfer.hs; examples/socket-state/Main.hs:91-93):
+        the state of the connection the handled message came in on.  A
+        connection is an incoming link; its state lives in the node vars of a
+        state cell node ``state_base + link`` (4 int64, fresh per replica, like
+        `mkState` on each accepted socket).  Handler registers hold the
+        incoming link in r1."""
+        self.mov(scratch, link_reg).addi(scratch, state_base)
+        return self.nloadx(r, var, scratch)
+
+    def user_state_store(self, r: int, var: int, link_reg: int, state_base: int, scratch: int = 2):
+        self.mov(scratch, link_reg).addi(scratch, state_base)
+        return self.nstorex(r, var, scratch)
 
     def trace(self, tag: int, r: int = 0):
         """Checkpoint / logMeasure-style trace record into the node hash."""

@@ -423,6 +423,85 @@ def gatekeeper(n_clients: int = 4, n_replicas: int = 1, msg_num: int = 20, junk_
     )
 
 
+# ------------------------------------------------------------- socket-state
+TAG_GOT_PING_NO = 13     # socket-state/Main.hs:75-76 "Got Ping #reqNo ..."
+TAG_FROM_CLIENT = 14     # "... from client #cid"
+
+
+def socket_state(n_replicas: int = 1, network_delay=(ms(1), ms(5)), seed_base: int = 0,
+                 max_rounds: int = 64, near_horizon_us: int = sec(20)) -> Scenario:
+    """examples/socket-state/Main.hs re-hosted on the emulated transfer: a
+    server counting requests per client connection with ``userStateR``
+    (:65-76, :91-93), and 3 clients that send ``Ping cid`` once a second while
+    ``ruskaRuletka`` (randomRIO (0,2) > 0, :96) holds, then close (:80-86).
+    The server stops listening after 10 s (``invoke (after 10 sec) stop``).
+
+    Node 0 = server, nodes 1..3 = clients, node 4 hosts main, nodes 5..7 =
+    the state cells of the connections client c -> server (link c-1).  Each
+    client's number of rounds is drawn host-side: draws of U[0, 2] from
+    mkStdGen(seed_base + replica), client 1 first, until a 0 (capped at
+    ``max_rounds``); the reference draws from the global IO generator, which is
+    not reproducible.  Main holds the counts in r1..r3 (``main_regs``)."""
+    SRV, SYS, STATE = 0, 4, 5
+    p = Program()
+    K_PING = p.kind("Ping")
+    srv_set = p.listener_set({"Ping": "on_ping"})
+
+    c = p.function("main")
+    c.seti(0, SRV).fork_("server_main", node_reg=0, scratch=0)
+    for cid in (1, 2, 3):
+        c.mov(0, cid).seti(cid, cid)                  # r0 = rounds of client cid; node cid
+        c.fork_("client_main", node_reg=cid, scratch=cid)
+    c.end()
+
+    c = p.function("server_main")
+    c.listen(srv_set)                                 # stop <- listen (AtPort 4444) [...]
+    c.invoke(for_(sec(10)))                           # invoke (after 10 sec) stop
+    c.unlisten()
+    c.end()
+
+    c = p.function("on_ping")                         # \(Ping cid) -> do
+    c.user_state_load(3, 0, 1, STATE)                 #   counter <- userStateR
+    c.addi(3, 1)                                      #   reqNo <- counter <+= 1
+    c.user_state_store(3, 0, 1, STATE)
+    c.trace(TAG_GOT_PING_NO, 3)                       #   logInfo "Got Ping #reqNo from client #cid"
+    c.trace(TAG_FROM_CLIENT, 0)
+    c.end()
+
+    c = p.function("client_main")
+    c.node(2)                                         # cid
+    c.link(1, 0)                                      # (localhost, 4444)
+    top = c.here()
+    done = c.label()
+    c.jeqi(0, 0, done)                                # whileM ruskaRuletka $ do
+    c.wait(for_(sec(1)))                              #   wait (for 1 sec)
+    c.send(1, K_PING, 2)                              #   send (localhost, 4444) $ Ping cid
+    c.addi(0, -1).jmp(top)
+    c.bind(done)
+    c.end()                                           # close (localhost, 4444)
+
+    img = p.finalize()
+    out = [[], [SRV], [SRV], [SRV], [], [], [], []]
+    topo = Topology.from_out_lists(8, out)
+    g = StdGenVec(seed_base + np.arange(n_replicas, dtype=np.int64))
+    table = np.zeros((topo.n_links, 1, n_replicas), np.uint32)
+    for l in range(topo.n_links):
+        table[l, 0, :] = g.range(*network_delay)
+    regs = np.zeros((n_replicas, 4), np.int64)
+    for cid in (1, 2, 3):
+        going = np.ones(n_replicas, bool)
+        for _ in range(max_rounds):
+            coin = g.range(0, 2) > 0
+            going &= coin
+            regs[:, cid] += going
+    return Scenario(
+        name="socket_state", image=img, topo=topo, n_replicas=n_replicas,
+        main_pc=img.pc_of("main"), main_node=SYS, link_table=table, main_regs=regs,
+        max_slots=64, queue_capacity=256, near_horizon_us=near_horizon_us,
+        meta=dict(config="socket_state", seed_base=seed_base, max_rounds=max_rounds),
+    )
+
+
 # ------------------------------------------------------------------- gossip
 TAG_RUMOR_FIRST = 9      # first receipt of the rumor at a node
 K_RUMOR_PAYLOAD = 7      # forwarding is payload-independent (tie-insensitive by design)
