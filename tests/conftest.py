@@ -32,8 +32,9 @@ def engine_mod():
 
 @pytest.fixture(autouse=True)
 def tw_geometry(request, monkeypatch):
-    """GPU tests run under both kernel geometries (dense: 256 replicas per
-    workgroup; sparse: 16 per workgroup with the 768-entry on-chip queue)."""
+    """GPU tests run under every kernel geometry (dense: 256 replicas per
+    workgroup; sparse: 16 per workgroup with the 768-entry on-chip queue;
+    half: the dense layout as 8 waves of 32 lanes)."""
     g = getattr(request, "param", None)
     if g is not None:
         monkeypatch.setenv("TW_GEOMETRY", g)

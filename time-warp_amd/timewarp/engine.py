@@ -134,7 +134,8 @@ class Engine:
     def load(self, scn: Scenario, geometry: Optional[str] = None) -> "Engine":
         """Upload the scenario.  `geometry` picks the kernel layout: "dense"
         (256 replicas per workgroup, 16-entry on-chip queue), "sparse" (16
-        replicas per workgroup, 768-entry on-chip queue) or None = the
+        replicas per workgroup, 768-entry on-chip queue), "half" (the dense
+        layout as two 32-lane waves per SIMD; an experiment) or None = the
         library's choice (sparse for <= 8192 replicas; env TW_GEOMETRY)."""
         d = scn.desc()
         old = os.environ.get("TW_GEOMETRY")
