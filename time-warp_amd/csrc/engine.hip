@@ -1669,6 +1669,10 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
     uint64_t* sc = gp(c.scal) + r;
     const size_t R = c.R;
     if (sc[SC_STATUS * R] != TW_REP_RUNNING) return;
+    // LP: a node with no live thread and an empty inbox has nothing to do in
+    // this window (every live thread holds its one queued event; a superseded
+    // entry left behind pops without effect whenever the node wakes again)
+    if (LP && sc[SC_LIVE * R] == 0 && sc[SC_PENDING_MAIN * R] == 0 && gp(c.inbox_n)[r] == 0) return;
 
     Lane<LP, WG, NC> L;
     L.c = c;
