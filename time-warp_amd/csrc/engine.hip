@@ -2286,14 +2286,20 @@ int tw_run(tw_ctx* c, int64_t t_end_us, uint64_t max_events, tw_stats* out) {
     HIPCHK(hipSetDevice(c->device));
     hipStream_t st = c->stream;
     const Dev& d = c->d;
-    // events before this call (to report per-call deltas)
-    std::vector<uint64_t> ev0(d.R);
-    HIPCHK(hipMemcpyAsync(ev0.data(), d.scal + (size_t)SC_EVENTS * d.R, 8ull * d.R, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipStreamSynchronize(st));
+    // events before this call (to report per-call deltas; only when asked
+    // for: an LP window would otherwise copy 8 B per node every window)
+    std::vector<uint64_t> ev0;
+    if (out) {
+        ev0.resize(d.R);
+        HIPCHK(hipMemcpyAsync(ev0.data(), d.scal + (size_t)SC_EVENTS * d.R, 8ull * d.R, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+    }
     const uint64_t limit = max_events;  // cumulative per-replica cap
     c->launch_ms.clear();
     const uint32_t budget = 1u << 14;  // pops per lane per launch: bounded kernel time
-    const int per_check = 4;           // launches between host checks
+    // launches between host checks: a replica run needs several budgets; an LP
+    // window is almost always done after one launch
+    const int per_check = c->lp ? 1 : 4;
     uint32_t launches = 0;
     double kms = 0.0;
     for (int round = 0; round < (1 << 20); ++round) {
