@@ -189,10 +189,26 @@ struct Dev {
     uint32_t* out_n;     // [1]
     uint64_t* next_t;    // [1] min next-event time (atomicMin)
     uint32_t* lp_err;    // [1] inbox/outbox overflow
+    // LP work lists: a launch serves only the nodes of list act_cur (those with
+    // a live thread or new delivery records); nodes join list act_cur ^ 1 for
+    // the next window at most once (listed[node] == wid)
+    uint32_t* act;       // [2][R]
+    uint32_t* act_n;     // [2]
+    uint32_t* listed;    // [R]
+    uint32_t act_cur, wid;
     unsigned long long* prof;  // [P_COUNT] diagnostic build only
     uint4* trace;        // [trace_cap][R][2] TRACE records (tw_set_trace), replica mode
     uint32_t trace_cap;
 };
+
+// LP: node r joins the next window's work list (once per window)
+__device__ __forceinline__ void lp_list_next(const Dev& c, uint32_t r) {
+    if (__hip_atomic_exchange(gp(c.listed) + r, c.wid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != c.wid) {
+        const uint32_t nx = c.act_cur ^ 1u;
+        const uint32_t k = __hip_atomic_fetch_add(gp(c.act_n) + nx, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        gp(c.act)[(size_t)nx * c.R + k] = r;
+    }
+}
 
 // ------------------------------------------------------------------ hashing
 __device__ __forceinline__ uint64_t mix64(uint64_t z) {
@@ -1616,6 +1632,8 @@ __global__ void __launch_bounds__(TW_WG) tw_init_kernel(Dev c, uint32_t main_pc,
         gp(c.bind_rel)[r] = 0xFFFFFFFEu;
         if (listen_init) gp(c.bind)[r] = listen_init[g];
         gp(c.inbox_n)[r] = 0;
+        gp(c.listed)[r] = 0;
+        gp(c.act)[(size_t)c.R + r] = r;  // list 1 = every node: the first window scans them all
         return;
     }
     if (nv_init)
@@ -1665,6 +1683,10 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
     const uint32_t wbase = (threadIdx.x >> 6) * TPW;  // the wave's first lane in the LDS layout
     const uint32_t li = wbase + (threadIdx.x & 63u);
     uint32_t r = blockIdx.x * WG + li;
+    if (LP) {
+        if (r >= gp(c.act_n)[c.act_cur]) return;
+        r = gp(c.act)[(size_t)c.act_cur * c.R + r];
+    }
     if (r >= c.R) return;
     uint64_t* sc = gp(c.scal) + r;
     const size_t R = c.R;
@@ -1942,6 +1964,7 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
     if (LP && L.status == TW_REP_RUNNING && tn != INT64_MAX)
         __hip_atomic_fetch_min(gp(c.next_t), (uint64_t)tn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (active) __hip_atomic_fetch_add(gp(c.n_active), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (LP && L.status == TW_REP_RUNNING && (L.live || pending_main)) lp_list_next(c, r);
 }
 
 
@@ -1966,6 +1989,7 @@ __global__ void __launch_bounds__(256) tw_lp_scatter(Dev c, const uint4* recs, u
         q[1] = b;
         int64_t ta = ent_t(a);
         __hip_atomic_fetch_min(gp(c.next_t), (uint64_t)ta, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        lp_list_next(c, lp);
     } else if (foreign) {
         uint32_t k = __hip_atomic_fetch_add(gp(n_foreign), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (k >= foreign_cap) {
@@ -2002,6 +2026,7 @@ struct tw_ctx {
     uint4* staging = nullptr;      // inject staging [out_cap][2]
     std::vector<double> launch_ms;
     std::vector<hipEvent_t> ev_pool;
+    uint32_t act_n_init[2] = {0, 0};
 };
 
 namespace {
@@ -2207,6 +2232,9 @@ static int load_common(tw_ctx* c, const tw_scenario_desc* s, bool lp, uint32_t l
         ALLOC(d.out_n, 1);
         ALLOC(d.next_t, 1);
         ALLOC(d.lp_err, 1);
+        ALLOC(d.act, 2 * R);
+        ALLOC(d.act_n, 2);
+        ALLOC(d.listed, R);
         ALLOC(c->foreign, (size_t)d.out_cap * 2);
         ALLOC(c->n_foreign, 1);
         ALLOC(c->staging, (size_t)d.out_cap * 2);
@@ -2269,6 +2297,11 @@ int tw_reset(tw_ctx* c) {
         HIPCHK(hipMemsetAsync(d.out_n, 0, 4, st));
         HIPCHK(hipMemsetAsync(d.lp_err, 0, 4, st));
         HIPCHK(hipMemsetAsync(c->n_foreign, 0, 4, st));
+        c->d.act_cur = 0;
+        c->d.wid = 0;
+        c->act_n_init[0] = 0;
+        c->act_n_init[1] = (uint32_t)R;
+        HIPCHK(hipMemcpyAsync(d.act_n, c->act_n_init, 8, hipMemcpyHostToDevice, st));
     }
     uint32_t blocks = (uint32_t)((R + TW_WG - 1) / TW_WG);
     hipLaunchKernelGGL(tw_init_kernel, dim3(blocks), dim3(TW_WG), 0, st, d, c->main_pc, c->main_node,
@@ -2296,6 +2329,13 @@ int tw_run(tw_ctx* c, int64_t t_end_us, uint64_t max_events, tw_stats* out) {
     }
     const uint64_t limit = max_events;  // cumulative per-replica cap
     c->launch_ms.clear();
+    if (c->lp) {
+        // a new window: serve the list built since the last call (nodes with a
+        // live thread or new records); start an empty one for the next call
+        c->d.act_cur ^= 1u;
+        c->d.wid += 1u;
+        HIPCHK(hipMemsetAsync(d.act_n + (c->d.act_cur ^ 1u), 0, 4, st));
+    }
     const uint32_t budget = 1u << 14;  // pops per lane per launch: bounded kernel time
     // launches between host checks: a replica run needs several budgets; an LP
     // window is almost always done after one launch
