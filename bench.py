@@ -9,15 +9,20 @@ replica on the device-resident tables and run all of them to quiescence
 PQ.minView pop of the TimedT schedule (TimedT.hs:242); the GPU count equals the
 oracle's (parity-checked on a sample each run).
 
-Multi-GPU: one process per GPU (torchrun), replicas sharded in contiguous
-blocks with no data-path collective (weak scaling: replicas per GPU fixed);
-only the statistics are all-reduced over RCCL.
+Multi-GPU: one process per GPU (torchrun).  The replica configs split ONE
+batch of `--replicas` replicas (65,536 for C3) into contiguous blocks
+[g*R/G, (g+1)*R/G), BASELINE config 3 / SURVEY.md 8(e) -- strong scaling, no
+data-path collective; only the statistics are all-reduced over RCCL.
+`--weak` keeps `--replicas` per GPU instead.  C4 (gossip) partitions one
+scenario by node (strong scaling, RCCL all-to-all per window).
 """
 from __future__ import annotations
 
 import argparse
+import hashlib
 import json
 import os
+import subprocess
 import sys
 import time
 
@@ -31,12 +36,21 @@ BYTES_PER_EVENT = 64            # 16 B event read + 16 B event write + 32 B thre
 BYTES_PER_SEND = 8              # link-table entry + ordinal
 
 
-def build_scenario(args, rank: int):
+def replica_block(args, rank: int, world: int):
+    """(seed_base, n_replicas) of this rank: a contiguous block of the global
+    batch (strong scaling, the default) or `--replicas` per rank (`--weak`)."""
+    from timewarp.dist import strong_block, weak_block
+
+    if args.weak:
+        return weak_block(rank, args.replicas)
+    r0, r1 = strong_block(args.replicas, world, rank)
+    return r0, r1 - r0
+
+
+def build_scenario(args, rank: int, world: int):
     from timewarp import scenarios
 
-    from timewarp.dist import weak_block
-
-    base, R = weak_block(rank, args.replicas)
+    base, R = replica_block(args, rank, world)
     if args.config == "token_ring":
         return scenarios.token_ring(n_nodes=args.nodes, n_replicas=R, launch_duration=args.duration_s * 1_000_000,
                                     drop_log2=args.drop_log2, seed_base=base), (
@@ -57,12 +71,32 @@ def build_scenario(args, rank: int):
     raise SystemExit(f"unknown config {args.config}")
 
 
+def host_cpu():
+    """(threads, description): `nproc` (the CPUs this process may use; honours
+    affinity and OMP_NUM_THREADS, 16 on the GPU box) and the CPU model."""
+    try:
+        n = int(subprocess.run(["nproc"], capture_output=True, text=True, check=True).stdout.strip())
+    except Exception:
+        n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    model = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return max(1, n), f"{model}; nproc {n} of {os.cpu_count()} logical CPUs"
+
+
 def cpu_baseline(scn, gpu_res, gpu_hashes, seconds: float):
-    """Oracle (C++ TimedT restatement, canonical mode) on host cores, bounded sample."""
+    """Oracle (C++ TimedT restatement, canonical mode) on host cores, bounded
+    sample; one replica per std::thread worker, a pool of `nproc` workers
+    (SURVEY.md 8(d))."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle  # the parity checker / CPU baseline — never the measured GPU path
 
-    threads = max(1, min(16, os.cpu_count() or 1))
+    threads, cpu_desc = host_cpu()
     t0 = time.perf_counter()
     r1, _ = oracle.run_batch(scn, 0, 1, threads=1)
     one = max(time.perf_counter() - t0, 1e-4)
@@ -74,10 +108,58 @@ def cpu_baseline(scn, gpu_res, gpu_hashes, seconds: float):
     parity = all(np.array_equal(res[f], gpu_res[f][:n]) for f in res.dtype.names) and \
         np.array_equal(hashes, gpu_hashes[:n])
     return {
-        "value": ev / dt, "unit": "events/s", "cores": threads, "kind": "port",
-        "sample": f"replicas [0,{n}) of the same workload, oracle canonical mode, {threads} std::threads, "
-                  f"{ev} events in {dt:.2f} s",
+        "value": ev / dt, "unit": "events/s", "cores": threads, "kind": "port", "cpu": cpu_desc,
+        "sample": f"replicas [0,{n}) of the same workload, oracle canonical mode, {threads} std::threads "
+                  f"(nproc), {ev} events in {dt:.2f} s; the reference TimedT itself cannot run here (no GHC, "
+                  f"so no RTS -N)",
     }, parity, n
+
+
+def engine_sha() -> str:
+    """Digest of the engine sources: a PMC summary is used only for the build it measured."""
+    h = hashlib.sha256()
+    d = os.path.join(ROOT, "time-warp_amd", "csrc")
+    for f in sorted(os.listdir(d)):
+        h.update(f.encode())
+        h.update(open(os.path.join(d, f), "rb").read())
+    return h.hexdigest()[:16]
+
+
+def measured_traffic(args, launches_per_step: float, events_per_step: float):
+    """HBM traffic of this workload from the newest profiles/*/pmc_summary.json
+    taken with tools/pmc.sh on THIS engine build (engine_sha) and the same
+    workload (bench_workload); None otherwise.  rocprofv3 PMC counters cannot
+    be read inside the un-profiled timed run itself."""
+    want = workload_key(args)
+    best = None
+    for root, _, files in os.walk(os.path.join(ROOT, "profiles")):
+        if "pmc_summary.json" not in files:
+            continue
+        f = os.path.join(root, "pmc_summary.json")
+        try:
+            pm = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        if pm.get("engine_sha") != engine_sha() or pm.get("bench_workload") != want or "fetch_size" not in pm:
+            continue
+        if best is None or f > best[0]:
+            best = (f, pm)
+    if best is None:
+        return None
+    f, pm = best
+    per_step = float(pm["hbm_bytes_total"]) / max(1, int(pm.get("steps", 1)))
+    return {
+        "traffic": per_step / max(1.0, launches_per_step),
+        "traffic_per_event": per_step / max(1.0, events_per_step),
+        "fetch_size_kib": pm["fetch_size"], "write_size_kib": pm["write_size"],
+        "traffic_formula": pm.get("formula", "(2*FETCH_SIZE + WRITE_SIZE)*1024"),
+        "traffic_source": os.path.relpath(f, ROOT) + f" (engine {pm['engine_sha']})",
+    }
+
+
+def workload_key(args) -> str:
+    return (f"{args.config}:nodes={args.nodes}:replicas={args.replicas}:weak={int(args.weak)}:"
+            f"dur={args.duration_s}:drop={args.drop_log2}:rt={args.round_trips}:msgs={args.msg_num}")
 
 
 def bench_gossip(args, scn, workload, world, rank, local, dist_on, barrier):
@@ -109,6 +191,8 @@ def bench_gossip(args, scn, workload, world, rank, local, dist_on, barrier):
         kms += k
         windows = w
     agg, h = eng.lp_results()
+    if int(agg["status"]) >= 2:  # TW_REP_ABORTED or an error status on a local node
+        raise SystemExit(f"gossip: local nodes ended in status {int(agg['status'])}")
     if dist_on:
         tot, hashes = twd.reduce_lp(agg, h, dev)
         (max_elapsed,) = [twd.reduce_stats({"elapsed_s": elapsed}, device=dev)["elapsed_s"]]
@@ -153,7 +237,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", default="token_ring", choices=["token_ring", "ping_pong", "hotspot", "gossip"])
     ap.add_argument("--replicas", type=int, default=None,
-                    help="replicas per GPU: 65536 (token_ring, C3), 1048576 (ping_pong, C2), 4096 (hotspot, C5)")
+                    help="replicas in the whole job, split over the GPUs: 65536 (token_ring, C3), "
+                         "1048576 (ping_pong, C2), 4096 (hotspot, C5)")
+    ap.add_argument("--weak", action="store_true", help="--replicas per GPU instead (weak scaling)")
     ap.add_argument("--nodes", type=int, default=None, help="4096 (token_ring), 256 senders (hotspot), 1M (gossip)")
     ap.add_argument("--duration-s", type=int, default=120)
     ap.add_argument("--drop-log2", type=int, default=10)
@@ -161,11 +247,16 @@ def main():
     ap.add_argument("--msg-num", type=int, default=1000)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--workload-key", action="store_true",
+                    help="print the workload key and engine digest (tools/pmc.sh provenance) and exit")
     args = ap.parse_args()
     if args.nodes is None:
         args.nodes = {"token_ring": 4096, "hotspot": 256, "gossip": 1 << 20}.get(args.config, 2)
     if args.replicas is None:
         args.replicas = {"token_ring": 65536, "ping_pong": 1 << 20, "hotspot": 4096}.get(args.config, 1)
+    if args.workload_key:
+        print(json.dumps({"bench_workload": workload_key(args), "engine_sha": engine_sha()}))
+        return
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -186,7 +277,7 @@ def main():
     from timewarp import dist as twd
     from timewarp.engine import Engine
 
-    scn, workload = build_scenario(args, rank)
+    scn, workload = build_scenario(args, rank, world)
     if args.config == "gossip":
         return bench_gossip(args, scn, workload, world, rank, local, dist_on, barrier)
     eng = Engine(local).load(scn)
@@ -237,15 +328,17 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": max_elapsed * 1e3 / args.steps,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "weak" if args.weak else "strong",
             "vs_baseline": None,
             "dtype": "int64",
             "data": "synthetic (scenario tables drawn from random-1.1 StdGen, seed = replica id)",
             "config": {
                 "workload": workload,
-                "replicas_per_gpu": args.replicas,
+                "replicas_total": args.replicas * (world if args.weak else 1),
+                "replicas_rank0": scn.n_replicas,
                 "events_per_step": int(tot_events / args.steps),
-                "parallelism": f"replica-sharded x{world} (no data-path collective)",
+                "parallelism": f"replica-sharded x{world}, contiguous blocks (no data-path collective)",
+                "geometry": eng.geometry(),
             },
             "roofline": {
                 "bound": "hbm",
@@ -260,19 +353,10 @@ def main():
                 "algorithmic_bytes": "64 B/event + 8 B/send (SURVEY.md 8d)",
             },
         }
-        prof = os.path.join(ROOT, "profiles", "pmc_summary.json")
-        if os.path.exists(prof) and args.config == "token_ring" and args.replicas == 65536 and args.nodes == 4096:
-            # measured HBM bytes of the same workload (tools/pmc.sh: separate --pmc passes over a 1-step run
-            # of this bench), per launch like `achieved`: one step's traffic / one step's launches
-            pm = json.load(open(prof))
-            if pm.get("bench_args", "").strip() == "" and "hbm_bytes_total" in pm:
-                per_step = float(pm["hbm_bytes_total"])
-                out["roofline"]["traffic"] = per_step / max(1, launches / args.steps)
-                out["roofline"]["traffic_unit"] = ("HBM bytes per launch: rocprofv3 (2*FETCH_SIZE + WRITE_SIZE)*1024 "
-                                                   "over one step's tw_run_kernel dispatches / its launches "
-                                                   "(profiles/pmc_summary.json, MI355X_MICROARCH.md HBM section)")
-                out["roofline"]["traffic_per_event"] = per_step / max(1, events / args.steps)
-                out["roofline"]["algorithmic_per_event"] = alg_bytes / max(1, events)
+        out["roofline"]["algorithmic_per_event"] = alg_bytes / max(1, events)
+        mt = measured_traffic(args, launches / args.steps, events / args.steps) if world == 1 else None
+        if mt:
+            out["roofline"].update(mt)
         if not args.no_cpu_baseline:
             cb, parity, n = cpu_baseline(scn, res, hashes, args.cpu_seconds)
             out["cpu_baseline"] = cb

@@ -28,8 +28,9 @@
 extern "C" {
 #endif
 
-#define TW_ABI_VERSION 1u
-/* Async exception payloads (throwTo's value) are carried as int32. */
+#define TW_ABI_VERSION 2u
+/* Async exception payloads (throwTo's value, `SomeException` in the
+ * reference's asyncExceptions map, TimedT.hs:113,359) are carried as int64. */
 
 /* ------------------------------------------------------------------ status */
 typedef enum tw_status {
@@ -39,7 +40,9 @@ typedef enum tw_status {
     TW_ERR_HIP = -3,          /* HIP runtime error                          */
     TW_ERR_OOM = -4,          /* device allocation failed                   */
     TW_ERR_STATE = -5,        /* call out of order (run before load, ...)   */
-    TW_ERR_REPLICA = -6       /* one or more replicas ended in error status */
+    TW_ERR_REPLICA = -6,      /* one or more replicas ended in error status */
+    TW_ERR_INCOMPLETE = -7    /* tw_run's relaunch cap was reached before every
+                                 replica stopped (quiescence / t_end / cap)  */
 } tw_status;
 
 /* per-replica status (tw_replica_result.status) */
@@ -52,7 +55,20 @@ enum {
     TW_REP_ERR_SLOTS = 3,     /* thread-slot capacity exceeded              */
     TW_REP_ERR_QUEUE = 4,     /* event-queue capacity exceeded              */
     TW_REP_ERR_FRAMES = 5,    /* catch-frame depth exceeded                 */
-    TW_REP_ERR_INSN = 6       /* bad opcode / pc / link                     */
+    TW_REP_ERR_INSN = 6,      /* bad opcode / pc / link                     */
+    TW_REP_ERR_COUNTER = 7    /* the replica's 32-bit insertion counter (seq) or
+                                 thread counter (TimedT.hs:288-289) would wrap */
+};
+
+/* tie-order probes (tw_tie_audit): events with equal timestamps pop in
+ * insertion order (FIFO, the canonical order), reverse insertion order, or a
+ * scrambled order.  TimedT orders events by timestamp only (TimedT.hs:100-104),
+ * so a replica whose outputs differ between two of these orders depends on
+ * pqueue's equal-timestamp order, which no reference test pins. */
+enum {
+    TW_TIE_FIFO = 0,
+    TW_TIE_LIFO = 1,
+    TW_TIE_SCRAMBLE = 2
 };
 
 /* ------------------------------------------------------------- exceptions */
@@ -185,9 +201,19 @@ typedef struct tw_scenario_desc {
     uint32_t max_timeouts;     /* timeout epochs per replica (done-flag bitmap size) */
     uint32_t run_capacity;     /* entries per monotone far-queue run (4 runs per
                                   replica); 0 = far events use the heap only */
+    uint32_t max_frames;       /* catch/finally frames per thread (the handler
+                                  stack, TimedT.hs:84,198); 0 = 2, at most
+                                  TW_MAX_FRAMES.  Two live in the thread record,
+                                  deeper ones in a per-slot overflow area.     */
+    /* BinaryP wire sizes (Message.hs:155-202): a message of kind k sent over
+     * link l is delayed by its transmission time
+     * ceil(msg_bytes[k] * 10^6 / link_bw[l]) µs on top of the link-table delay
+     * (computed at send time).  NULL / 0 = no transmission time. */
+    const uint32_t* msg_bytes; /* [n_msg_kinds] */
+    const uint64_t* link_bw;   /* [n_links] bytes per second */
 } tw_scenario_desc;
 
-#define TW_MAX_FRAMES 3        /* catch/finally frames per thread (both engines) */
+#define TW_MAX_FRAMES 14       /* catch/finally frames per thread (both engines) */
 
 typedef struct tw_replica_result {
     int64_t final_t;           /* curTime after the last pop                     */
@@ -199,6 +225,12 @@ typedef struct tw_replica_result {
     uint32_t main_exc;         /* uncaught main-thread exception code, rethrown by
                                   runTimedT after quiescence (TimedT.hs:302-304) */
     uint64_t threads;          /* threads ever created (incl. main)              */
+    uint32_t tie_flags;        /* tw_tie_audit: bit 0 = audited; bit p = the
+                                  outputs under tie probe p (TW_TIE_LIFO,
+                                  TW_TIE_SCRAMBLE) differ from the canonical
+                                  FIFO order, i.e. the replica depends on the
+                                  order of equal-timestamp events            */
+    uint32_t reserved;
 } tw_replica_result;
 
 typedef struct tw_stats {
@@ -267,6 +299,31 @@ int tw_set_trace(tw_ctx* ctx, uint32_t cap);
 /* A replica's trace records: copies min(cap, emitted, trace cap) records and
  * stores the number emitted (possibly more than were kept) in *n_emitted. */
 int tw_read_trace(tw_ctx* ctx, uint32_t replica, tw_trace_rec* out, size_t cap, uint64_t* n_emitted);
+
+/* Tie-order audit: run every replica to quiescence under each probe order
+ * p in 1..probes (TW_TIE_LIFO, TW_TIE_SCRAMBLE), then under the canonical
+ * order, and set tie_flags bit p of every replica whose results or node
+ * hashes differ from the canonical run's.  The canonical run's state is left
+ * loaded, so results/hashes read afterwards are the canonical ones.  `out`
+ * gets the canonical run's stats.  Replaces nothing in the reference: it
+ * flags the replicas for which TimedT's pqueue tie order (TimedT.hs:100-104,
+ * 242) could give a different trace than this engine. */
+int tw_tie_audit(tw_ctx* ctx, uint32_t probes, tw_stats* out);
+
+/* Testing hook: from the next tw_reset on, start every replica's insertion
+ * counter at seq0 and its thread counter at tid0 (>= 1; main is tid 0), so the
+ * TW_REP_ERR_COUNTER guard can be reached in a short run. */
+int tw_set_counter_base(tw_ctx* ctx, uint32_t seq0, uint32_t tid0);
+
+/* Kernel geometry of the loaded scenario, chosen by tw_load from the replica
+ * count (environment TW_GEOMETRY=dense|sparse|half|wave overrides):
+ *   DENSE  one lane per replica, 256 replicas per workgroup (many replicas);
+ *   SPARSE one lane per replica, 16 per workgroup, large on-chip queue;
+ *   HALF   the dense layout as two 32-lane waves per SIMD (an experiment);
+ *   WAVE   one wavefront per replica: lane-parallel queue (few replicas);
+ *   LP     node-partitioned mode (tw_lp_load). */
+enum { TW_GEO_DENSE = 0, TW_GEO_SPARSE = 1, TW_GEO_HALF = 2, TW_GEO_WAVE = 3, TW_GEO_LP = 4 };
+int tw_geometry(tw_ctx* ctx);
 
 /* Duration (ms) of every event-kernel launch of the last tw_run, measured with
  * HIP events on the library's stream; returns the count written. */

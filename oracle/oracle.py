@@ -20,13 +20,15 @@ _PKG = os.path.join(os.path.dirname(_HERE), "time-warp_amd")
 if _PKG not in sys.path:
     sys.path.insert(0, _PKG)
 
-from timewarp.abi import RESULT_DTYPE, TwReplicaResult  # noqa: E402
+from timewarp.abi import RESULT_DTYPE, RESULT_FIELDS, TwReplicaResult  # noqa: E402
 from timewarp.scenario import Scenario  # noqa: E402
 
 LIB_PATH = os.path.join(_HERE, "build", "libtw_oracle.so")
 
 MODE_CANONICAL = 0
 MODE_PQUEUE = 1
+MODE_LIFO = 2        # canonical queue, equal timestamps in reverse insertion order (TW_TIE_LIFO)
+MODE_SCRAMBLE = 3    # canonical queue, equal timestamps in scrambled order (TW_TIE_SCRAMBLE)
 
 
 class TwoLiveDelays(C.Structure):
@@ -128,7 +130,7 @@ def run(scn: Scenario, replica: int = 0, mode: int = MODE_CANONICAL, live_seed: 
     tm = []
     if terms is not None:
         tm = [(terms[i].t, terms[i].node, terms[i].kind, terms[i].val) for i in range(min(o.terms_n, term_cap))]
-    result = {f: getattr(res, f) for f, _ in TwReplicaResult._fields_}
+    result = {f: getattr(res, f) for f in RESULT_FIELDS}
     return OracleRun(result, hashes, tr, tm, rec)
 
 

@@ -31,6 +31,9 @@
 //   mode 1 "pqueue":    pqueue-1.3.1.1 MinQueue transcription (pqueue_min.hpp),
 //          ordered by timestamp only, throwTo rebuilds the whole queue exactly
 //          as TimedT.hs:368.  Used for the tie-order audit (parity unpinned).
+//   modes 2, 3: the canonical queue with equal timestamps in reverse insertion
+//          order (TW_TIE_LIFO) or a scrambled order (TW_TIE_SCRAMBLE): the
+//          engine's tie probes (tw_tie_audit), mirrored for the parity tests.
 #include <algorithm>
 #include <atomic>
 #include <cstdint>
@@ -95,7 +98,7 @@ struct Thread {
     uint32_t node = 0;
     uint32_t pc = 0;
     int64_t r[4] = {0, 0, 0, 0};
-    Frame fr[TW_MAX_FRAMES];
+    Frame fr[TW_MAX_FRAMES];  // the handler list (TimedT.hs:84,198), innermost last
     int nfr = 0;
     bool started = false;
     bool is_main = false;
@@ -118,9 +121,20 @@ struct EvLEq {  // Event's Ord: compare timestamps only (TimedT.hs:100-104)
     bool operator()(const Event& a, const Event& b) const { return a.t <= b.t; }
 };
 
+// The key an insertion counter takes under a tie mode (== the engine's seq_key).
+inline uint32_t seq_key32(int tie, uint32_t s) {
+    if (tie == TW_TIE_FIFO) return s;
+    if (tie == TW_TIE_LIFO) return 0u - s;
+    uint32_t x = s;
+    x ^= x >> 16; x *= 0x7feb352du; x ^= x >> 15; x *= 0x846ca68bu; x ^= x >> 16;
+    return x;
+}
+
 // Canonical (t, seq) binary heap with thread back-pointers for re-stamping.
+// Equal timestamps pop in the order of seq_key32(tie, seq).
 class CanonQueue {
   public:
+    int tie = TW_TIE_FIFO;
     bool empty() const { return h_.empty(); }
     size_t size() const { return h_.size(); }
     void insert(const Event& e) {
@@ -149,8 +163,10 @@ class CanonQueue {
     }
 
   private:
-    static bool less(const Event& a, const Event& b) {
-        return a.t < b.t || (a.t == b.t && a.seq < b.seq);
+    bool less(const Event& a, const Event& b) const {
+        if (a.t != b.t) return a.t < b.t;
+        if (tie == TW_TIE_FIFO) return a.seq < b.seq;
+        return seq_key32(tie, (uint32_t)a.seq) < seq_key32(tie, (uint32_t)b.seq);
     }
     void set(size_t i, const Event& e) {
         h_[i] = e;
@@ -209,8 +225,12 @@ struct Sim {
     tw_replica_result res{};
     uint64_t live_slots = 0;  // concurrent threads, checked against max_slots
 
+    uint32_t max_frames;
+
     Sim(const tw_scenario_desc* d_, uint32_t rep, two_opts* o_, uint64_t* hashes_)
-        : d(d_), replica(rep), o(o_), mode(o_->mode), hashes(hashes_) {
+        : d(d_), replica(rep), o(o_), mode(o_->mode == 1 ? 1 : 0), hashes(hashes_) {
+        cq.tie = o_->mode >= 2 ? o_->mode - 1 : TW_TIE_FIFO;
+        max_frames = d->max_frames ? d->max_frames : 2u;
         node_vars.assign((size_t)d->n_nodes * 4, 0);
         if (d->node_vars) std::memcpy(node_vars.data(), d->node_vars, node_vars.size() * 8);
         bind.assign(d->n_nodes, 0);
@@ -237,8 +257,16 @@ struct Sim {
         if (res.status == TW_REP_RUNNING) res.status = status;
     }
 
+    // The engine's counters are 32-bit; reaching the top is a status, never a
+    // silent wrap (the reference's counters are unbounded Integers).
+    uint64_t next_seq() {
+        if (seq >= 0xFFFFFFFFull) fail(TW_REP_ERR_COUNTER);
+        else ++seq;
+        return seq;
+    }
+
     void enqueue(Thread* th, int64_t t) {
-        Event e{t, ++seq, th};
+        Event e{t, next_seq(), th};
         if (mode == 0) cq.insert(e);
         else pq.insert(e);
     }
@@ -246,6 +274,10 @@ struct Sim {
     Thread* new_thread(uint32_t pc, uint32_t node) {
         if (live_slots >= d->max_slots) {
             fail(TW_REP_ERR_SLOTS);
+            return nullptr;
+        }
+        if (threads_counter >= 0xFFFFFFFFull) {
+            fail(TW_REP_ERR_COUNTER);
             return nullptr;
         }
         ++live_slots;
@@ -283,14 +315,14 @@ struct Sim {
     void throw_to(uint64_t tid, uint32_t code, int64_t val) {
         if (mode == 0) {
             Thread* t = tid < by_tid.size() ? by_tid[tid].get() : nullptr;  // dead => freed
-            if (t && t->hpos >= 0) cq.restamp(t, cur, ++seq);
+            if (t && t->hpos >= 0) cq.restamp(t, cur, next_seq());
         } else {
             std::vector<Event> evs = pq.drain_ascending();  // PQ.toList
             for (Event& e : evs)
                 if (e.th->tid == tid) e.t = cur;               // map modifyRequired
             pq.from_list(evs);                                 // PQ.fromList
         }
-        if (async_exc.find(tid) == async_exc.end()) async_exc[tid] = Exc{code, (int64_t)(int32_t)val};  // old <|> new
+        if (async_exc.find(tid) == async_exc.end()) async_exc[tid] = Exc{code, val};  // old <|> new
     }
 
     // Raise `code` at the thread's current point; unwinding through finally
@@ -312,6 +344,14 @@ struct Sim {
         if (th->is_main) res.main_exc = code;  // caught by runTimedT's `try`
         die(th);                               // forked: threadKilledNotifier
         return false;
+    }
+
+    // BinaryP transmission time (tw_scenario_desc.msg_bytes / link_bw)
+    int64_t tx_us(uint64_t link, uint32_t kind) const {
+        if (!d->msg_bytes || !d->link_bw || kind >= d->n_msg_kinds) return 0;
+        uint64_t bw = d->link_bw[link];
+        if (!bw) return 0;
+        return (int64_t)(((uint64_t)d->msg_bytes[kind] * 1000000ull + bw - 1) / bw);
     }
 
     uint32_t link_entry(uint32_t link) {
@@ -374,7 +414,7 @@ struct Sim {
                 if (!unwind(th, b & 0xFF, r[(b >> 8) & 3])) return;
                 break;
             case TW_OP_CATCH:
-                if (th->nfr >= TW_MAX_FRAMES) { fail(TW_REP_ERR_FRAMES); return; }
+                if ((uint32_t)th->nfr >= max_frames) { fail(TW_REP_ERR_FRAMES); return; }
                 th->fr[th->nfr++] = Frame{(uint16_t)b, (uint16_t)imm};
                 break;
             case TW_OP_UNCATCH:
@@ -431,7 +471,9 @@ struct Sim {
                     hash(th->node, TW_KIND_DROP | kind, payload);
                     break;
                 }
-                int64_t regs[4] = {payload, (int64_t)link, (int64_t)(e & 0x7fffffffu), (int64_t)kind};
+                // delay = link-table delay + BinaryP transmission time of the message
+                int64_t regs[4] = {payload, (int64_t)link, (int64_t)(e & 0x7fffffffu) + tx_us(link, kind),
+                                   (int64_t)kind};
                 // schedule (after d) (deliver ..) = fork_ (wait (after d) >> deliver ..)
                 if (!fork(th, TW_PC_DELIVER_STUB, th->node, regs)) return;
                 enqueue(th, cur + 1);
@@ -491,7 +533,7 @@ struct Sim {
                 return;
             }
             case TW_OP_TMO_PUSH:
-                if (th->nfr >= TW_MAX_FRAMES) { fail(TW_REP_ERR_FRAMES); return; }
+                if ((uint32_t)th->nfr >= max_frames) { fail(TW_REP_ERR_FRAMES); return; }
                 th->fr[th->nfr++] = Frame{0, (uint16_t)r[ra]};
                 break;
             case TW_OP_TMO_END: {

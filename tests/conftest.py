@@ -9,9 +9,15 @@ for p in (os.path.join(ROOT, "time-warp_amd"), os.path.join(ROOT, "oracle"), ROO
         sys.path.insert(0, p)
 
 
+# every replica-mode GPU test runs under each kernel geometry (TW_GEOMETRY)
+GEOMETRIES = ["dense", "sparse", "half"]
+
+
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs through libtimewarp.so on cuda:0)")
     config.addinivalue_line("markers", "slow: larger CPU cases")
+    config.addinivalue_line("markers", "one_geometry: a GPU test whose kernel choice is not a replica geometry "
+                                       "(LP mode) or that pins its own: run once")
 
 
 @pytest.fixture(scope="session")
@@ -43,4 +49,7 @@ def tw_geometry(request, monkeypatch):
 
 def pytest_generate_tests(metafunc):
     if "tw_geometry" in metafunc.fixturenames and metafunc.definition.get_closest_marker("gpu"):
-        metafunc.parametrize("tw_geometry", ["dense", "sparse", "half"], indirect=True)
+        if metafunc.definition.get_closest_marker("one_geometry"):
+            metafunc.parametrize("tw_geometry", [None], indirect=True)
+        else:
+            metafunc.parametrize("tw_geometry", GEOMETRIES, indirect=True)

@@ -461,3 +461,60 @@ def random_program(seed: int, n_threads: int = 6, n_replicas: int = 1):
     s.queue_capacity = 4096
     s.run_capacity = 512
     return s
+
+
+# ------------------------------------------- handler stack, payloads (ABI 2)
+def deep_catch_prog(depth: int, max_frames: int = 8, payload: int = 0):
+    """A handler stack `depth` frames deep (TimedT's `_handlers` list grows per
+    `catch`, TimedT.hs:84,198): catch frames alternate Arith / async masks, a
+    `timeout` finally frame sits at every third level.  A forked child is
+    thrown a ThreadKilled carrying `payload` (throwTo, TimedT.hs:357-368) while
+    parked under its whole stack; each handler traces its level and the value,
+    then throws Overflow, which unwinds to the next Arith frame below
+    (ExceptionSpec.hs:219-229 chained).  Checkpoints: the levels caught."""
+    p = Program()
+    c = p.function("main")
+    c.seti(0, payload) if -(1 << 31) <= payload < (1 << 31) else c.seti(0, payload)
+    c.fork("child", ref=1)
+    c.wait(for_(5))
+    c.throw_to(1, TK, 0)
+    c.wait(for_(100))
+    c.end()
+    c = p.function("child")
+    hs = [c.label() for _ in range(depth)]
+    for i in range(depth):
+        if i % 3 == 2:
+            c.timeout_begin(1_000_000, epoch_reg=3)   # finally frame (watchdog far away)
+        else:
+            c.catch_(ARITH if i % 2 == 0 else ASYNC, hs[i])
+    c.wait(for_(1000))                                # parked under the whole stack
+    cp(c, -1)
+    c.end()
+    for i in range(depth):
+        c.bind(hs[i])
+        c.seti(2, i).trace(TAG_CP, 2)                  # level that caught it
+        c.trace(TAG_TS, 0)                             # the exception value (r0)
+        c.throw(OVERFLOW)                              # unwinds to the next Arith frame below
+    s = single(p, f"deep_catch_{depth}", max_slots=32, max_timeouts=64)
+    s.max_frames = max_frames
+    return s
+
+
+def payload_prog(value: int):
+    """`data SignalException = ValueReceived Int` (examples/token-ring/Main.hs:156)
+    thrown with a full-width Int: the handler traces the value it received."""
+    p = Program()
+    c = p.function("main")
+    c.fork("child", ref=1)
+    c.seti(0, value)
+    c.throw_to(1, isa.EXC_USER0, 0)
+    c.end()
+    c = p.function("child")
+    h = c.label()
+    c.catch_(1 << isa.EXC_USER0, h)
+    c.wait(for_(10))
+    c.uncatch().end()
+    c.bind(h)
+    c.trace(TAG_TS, 0)
+    c.end()
+    return single(p, f"payload_{value}")

@@ -1,0 +1,55 @@
+"""Full-shape parity: the BASELINE configs at their real
+per-replica shape, few replicas each, GPU vs oracle field by field and node
+hash by node hash.
+  C3  examples/token-ring/Main.hs:104-154 at 4,096 nodes, delay+drop nastiness
+  C5  bench/Network Sender/Main.hs:34-64 + Receiver/Main.hs:32-41 with all 256
+      senders on one receiver (the skewed hotspot: a deep receiver backlog)
+  C4  one gossip scenario of 2^20 nodes, 8 logical shards (node partitioning)"""
+import numpy as np
+import pytest
+
+from timewarp import scenarios
+from timewarp.abi import RESULT_FIELDS
+
+pytestmark = pytest.mark.gpu
+
+
+def _compare(engine_mod, oracle_mod, scn):
+    st, res, h = engine_mod.run_scenario(scn)
+    ores, oh = oracle_mod.run_batch(scn, threads=16)
+    for f in RESULT_FIELDS:
+        assert np.array_equal(res[f], ores[f]), (scn.name, f, res[f][:4], ores[f][:4])
+    assert np.array_equal(h, oh), scn.name
+    return res
+
+
+def test_c3_token_ring_4096_nodes(engine_mod, oracle_mod):
+    scn = scenarios.token_ring(n_nodes=4096, n_replicas=64, launch_duration=120_000_000, drop_log2=10)
+    res = _compare(engine_mod, oracle_mod, scn)
+    assert int(res["events"].min()) > 40_000
+
+
+def test_c3_token_ring_full_lap_with_drops(engine_mod, oracle_mod):
+    """launchDuration beyond a full lap (the messaging-dominated shape) with
+    frequent drops, so the token dies and the checker logs no-progress."""
+    scn = scenarios.token_ring(n_nodes=512, n_replicas=32, launch_duration=1_700_000_000, drop_log2=6,
+                               link_depth=4)
+    res = _compare(engine_mod, oracle_mod, scn)
+    assert int(res["dropped"].sum()) > 0 and int(res["delivered"].sum()) > 1000
+
+
+def test_c5_hotspot_256_senders(engine_mod, oracle_mod):
+    scn = scenarios.hotspot(n_senders=256, n_replicas=16, msg_num=100)
+    res = _compare(engine_mod, oracle_mod, scn)
+    assert int(res["delivered"].min()) > 256 * 100
+
+
+@pytest.mark.one_geometry
+def test_c4_gossip_1m_nodes_8_shards(engine_mod, oracle_mod):
+    scn = scenarios.gossip(1 << 20, seed=0)
+    agg, hashes, windows = engine_mod.run_partitioned(scn, parts=8)
+    o = oracle_mod.run(scn, trace_cap=0)
+    for f in RESULT_FIELDS:
+        assert int(agg[f]) == int(o.result[f]), (f, int(agg[f]), o.result[f])
+    assert np.array_equal(hashes, o.hashes)
+    assert windows > 10

@@ -6,11 +6,11 @@ import numpy as np
 import pytest
 
 from timewarp import scenarios
-from timewarp.abi import RESULT_DTYPE
+from timewarp.abi import RESULT_DTYPE, RESULT_FIELDS
 
 pytestmark = pytest.mark.gpu
 
-FIELDS = [f for f in RESULT_DTYPE.names]
+FIELDS = list(RESULT_FIELDS)
 
 
 def _compare(scn, engine_mod, oracle_mod, threads=8):

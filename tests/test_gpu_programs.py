@@ -7,11 +7,11 @@ import pytest
 
 import progs
 from test_golden_c1 import GOLD, c1_table_scenario
-from timewarp.abi import RESULT_DTYPE
+from timewarp.abi import RESULT_DTYPE, RESULT_FIELDS
 
 pytestmark = pytest.mark.gpu
 
-FIELDS = list(RESULT_DTYPE.names)
+FIELDS = list(RESULT_FIELDS)
 
 
 def _gpu(engine_mod, scn, t_end=None, max_events=None):

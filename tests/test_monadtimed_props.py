@@ -72,19 +72,16 @@ def test_now(oracle_mod, pre):
 def test_timeout(oracle_mod, tout, wt):
     """timeoutTimedProp (:275-286).  The watchdog fires at t0+tout, the action
     ends at t0+1+wt (the watchdog's schedule is a fork).  On the exact tie
-    tout == wt+1 the outcome depends on equal-timestamp pop order: the pqueue
-    transcription completes the action when wt >= 1 and fires the watchdog
-    when wt == 0 (its wake was queued before the action's zero wait), the
-    canonical (t,seq) order fires the watchdog first -- either is accepted
-    there, as the reference property accepts both outcomes on a tie."""
+    tout == wt+1 the outcome depends on equal-timestamp pop order, which
+    nothing in the reference pins (pqueue-1.3.1.1 is not vendored; the
+    transcription in oracle/pqueue_min.hpp is recalled, "parity unpinned"):
+    either outcome is accepted there in both queue modes."""
     scn = progs.timeout_prog(tout, wt)
     for mode in (0, 1):
         r = oracle_mod.run(scn, mode=mode)
         (_, outcome), = _times(r)
         if tout == wt + 1:
-            assert outcome in (1, 2)
-            if mode == 1:
-                assert outcome == (1 if wt >= 1 else 2)
+            assert outcome in (1, 2)  # tie: order-dependent, parity unpinned
         elif outcome == 1:
             assert wt <= tout and wt + 1 < tout + 1
         else:

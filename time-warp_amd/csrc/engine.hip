@@ -109,17 +109,20 @@ __device__ __forceinline__ T GAS* gp(T* p) {
 
 // ------------------------------------------------------------------ layout
 // Thread slot record: 64 B, [slot][replica].
-//  w0: pc:16 | nfr:2 | flags:6 | exc_code:8
+//  w0: pc:16 | nfr:4 | flags:6 | exc_code:6
 //  w1: node   w2: tid   w3: wake_seq (0 = not queued)
-//  f0..f2: frames (mask:16 << 16 | pc:16; mask 0 = finally frame of epoch pc)
-//  w7: pending exception value
+//  f0, f1: the two outermost frames (mask:16 << 16 | pc:16; mask 0 = finally
+//          frame of timeout epoch pc); frames 2.. live in the per-slot
+//          overflow area fx (TimedT's handler list, TimedT.hs:84,198)
+//  xl, xh: pending async exception value (int64, TimedT.hs:113,359)
 //  r0..r3: int64 registers
 struct Th {
     uint32_t w0, w1, w2, w3;
-    uint32_t f0, f1, f2;
-    uint32_t w7;
+    uint32_t f0, f1, xl, xh;
     int64_t r0, r1, r2, r3;
 };
+#define FL_SHIFT 20u   // flags field of w0
+#define EXC_SHIFT 26u  // exception-code field of w0
 
 #define F_STARTED 1u
 #define F_MAIN 2u
@@ -129,17 +132,19 @@ struct Th {
 
 __device__ __forceinline__ uint32_t th_pc(const Th& t) { return t.w0 & 0xFFFFu; }
 __device__ __forceinline__ void th_set_pc(Th& t, uint32_t pc) { t.w0 = (t.w0 & 0xFFFF0000u) | (pc & 0xFFFFu); }
-__device__ __forceinline__ uint32_t th_nfr(const Th& t) { return (t.w0 >> 16) & 3u; }
-__device__ __forceinline__ void th_set_nfr(Th& t, uint32_t n) { t.w0 = (t.w0 & ~(3u << 16)) | (n << 16); }
-__device__ __forceinline__ uint32_t th_flags(const Th& t) { return (t.w0 >> 18) & 0x3Fu; }
-__device__ __forceinline__ void th_or_flags(Th& t, uint32_t f) { t.w0 |= (f & 0x3Fu) << 18; }
-__device__ __forceinline__ void th_clr_flags(Th& t, uint32_t f) { t.w0 &= ~((f & 0x3Fu) << 18); }
-__device__ __forceinline__ uint32_t th_exc(const Th& t) { return t.w0 >> 24; }
-__device__ __forceinline__ void th_set_exc(Th& t, uint32_t c) { t.w0 = (t.w0 & 0x00FFFFFFu) | (c << 24); }
-
-__device__ __forceinline__ uint32_t getf(const Th& t, uint32_t i) {
-    const uint32_t m0 = 0u - (i == 0), m1 = 0u - (i == 1), m2 = 0u - (i == 2);
-    return (t.f0 & m0) | (t.f1 & m1) | (t.f2 & m2);
+__device__ __forceinline__ uint32_t th_nfr(const Th& t) { return (t.w0 >> 16) & 15u; }
+__device__ __forceinline__ void th_set_nfr(Th& t, uint32_t n) { t.w0 = (t.w0 & ~(15u << 16)) | (n << 16); }
+__device__ __forceinline__ uint32_t th_flags(const Th& t) { return (t.w0 >> FL_SHIFT) & 0x3Fu; }
+__device__ __forceinline__ void th_or_flags(Th& t, uint32_t f) { t.w0 |= (f & 0x3Fu) << FL_SHIFT; }
+__device__ __forceinline__ void th_clr_flags(Th& t, uint32_t f) { t.w0 &= ~((f & 0x3Fu) << FL_SHIFT); }
+__device__ __forceinline__ uint32_t th_exc(const Th& t) { return t.w0 >> EXC_SHIFT; }
+__device__ __forceinline__ void th_set_exc(Th& t, uint32_t c) {
+    t.w0 = (t.w0 & ((1u << EXC_SHIFT) - 1u)) | (c << EXC_SHIFT);
+}
+__device__ __forceinline__ int64_t th_xval(const Th& t) { return (int64_t)(((uint64_t)t.xh << 32) | t.xl); }
+__device__ __forceinline__ void th_set_xval(Th& t, int64_t v) {
+    t.xl = (uint32_t)v;
+    t.xh = (uint32_t)((uint64_t)v >> 32);
 }
 
 enum {
@@ -199,7 +204,32 @@ struct Dev {
     unsigned long long* prof;  // [P_COUNT] diagnostic build only
     uint4* trace;        // [trace_cap][R][2] TRACE records (tw_set_trace), replica mode
     uint32_t trace_cap;
+    // handler stack beyond the record's two frames: [S][R][FXQ] quads (frames 2..)
+    uint4* fx;
+    uint32_t FXQ, max_frames;
+    // BinaryP transmission time (tw_scenario_desc.msg_bytes / link_bw)
+    const uint32_t* msg_bytes;  // [n_kinds] or null
+    const uint64_t* link_bw;    // [L] or null
+    uint32_t tie_mode;          // TW_TIE_*: order of equal-timestamp events
 };
+
+// The key an insertion counter value takes in the queues (equal timestamps pop
+// in key order): FIFO (canonical), reverse (LIFO) or a scrambled bijection.
+// Every mode maps 0 to 0 and nothing else to 0 (wake_seq 0 = not queued).
+__device__ __forceinline__ uint32_t seq_key(uint32_t mode, uint32_t s) {
+    if (mode == TW_TIE_FIFO) return s;
+    if (mode == TW_TIE_LIFO) return 0u - s;
+    uint32_t x = s;  // xorshift-multiply: a bijection of u32 with x(0) = 0
+    x ^= x >> 16; x *= 0x7feb352du; x ^= x >> 15; x *= 0x846ca68bu; x ^= x >> 16;
+    return x;
+}
+// BinaryP transmission time of a message of `kind` over `link` (µs, rounded up)
+__device__ __forceinline__ int64_t tx_us(const Dev& c, uint64_t link, uint32_t kind) {
+    if (!c.msg_bytes || !c.link_bw || kind >= c.n_kinds) return 0;
+    const uint64_t bw = gp(c.link_bw)[link];
+    if (!bw) return 0;
+    return (int64_t)(((uint64_t)gp(c.msg_bytes)[kind] * 1000000ull + bw - 1) / bw);
+}
 
 // LP: node r joins the next window's work list (once per window)
 __device__ __forceinline__ void lp_list_next(const Dev& c, uint32_t r) {
@@ -846,9 +876,17 @@ struct Lane {
     }
 
     // ------------------------------------------------------------- queue
+    // A fresh insertion counter value, as the key the tie mode gives it.  The
+    // counter is 32-bit: reaching its top is a TW_REP_ERR_COUNTER status (the
+    // replica stops after this step), never a silent wrap.
+    __device__ __forceinline__ uint32_t next_seq() {
+        if (seq == 0xFFFFFFFFu) fail(TW_REP_ERR_COUNTER);
+        else ++seq;
+        return c.tie_mode ? seq_key(c.tie_mode, seq) : seq;
+    }
     // Queue the thread at t with a fresh seq; returns true if the entry is on chip.
     __device__ __forceinline__ bool enqueue(Th& th, uint32_t slot, int64_t t) {
-        uint32_t s = ++seq;
+        uint32_t s = next_seq();
         if (th.w3 == 0) ++live;
         th.w3 = s;
         if (near_fits(t)) {
@@ -868,7 +906,7 @@ struct Lane {
     // pop so its latency hides behind a whole step.
     __device__ __forceinline__ static void unpack(Th& th, uint4 a, uint4 b, uint4 d, uint4 e) {
         th.w0 = a.x; th.w1 = a.y; th.w2 = a.z; th.w3 = a.w;
-        th.f0 = b.x; th.f1 = b.y; th.f2 = b.z; th.w7 = b.w;
+        th.f0 = b.x; th.f1 = b.y; th.xl = b.z; th.xh = b.w;
         th.r0 = (int64_t)(((uint64_t)d.y << 32) | d.x);
         th.r1 = (int64_t)(((uint64_t)d.w << 32) | d.z);
         th.r2 = (int64_t)(((uint64_t)e.y << 32) | e.x);
@@ -892,7 +930,7 @@ struct Lane {
         STAT(K_PUT_HBM);
         uint4 GAS* p = hrec(slot);
         p[0] = make_uint4(th.w0, th.w1, th.w2, th.w3);
-        p[1] = make_uint4(th.f0, th.f1, th.f2, th.w7);
+        p[1] = make_uint4(th.f0, th.f1, th.xl, th.xh);
         p[2] = make_uint4((uint32_t)th.r0, (uint32_t)((uint64_t)th.r0 >> 32), (uint32_t)th.r1,
                           (uint32_t)((uint64_t)th.r1 >> 32));
         p[3] = make_uint4((uint32_t)th.r2, (uint32_t)((uint64_t)th.r2 >> 32), (uint32_t)th.r3,
@@ -915,7 +953,7 @@ struct Lane {
         uint4 GAS* p2 = full ? pr + 2 : (uint4 GAS*)(dm + 2 * R5);
         uint4 GAS* p3 = full ? pr + 3 : (uint4 GAS*)(dm + 3 * R5);
         *p0 = make_uint4(th.w0, th.w1, th.w2, th.w3);
-        *p1 = make_uint4(th.f0, th.f1, th.f2, th.w7);
+        *p1 = make_uint4(th.f0, th.f1, th.xl, th.xh);
         *p2 = make_uint4((uint32_t)th.r0, (uint32_t)((uint64_t)th.r0 >> 32), (uint32_t)th.r1,
                          (uint32_t)((uint64_t)th.r1 >> 32));
         *p3 = make_uint4((uint32_t)th.r2, (uint32_t)((uint64_t)th.r2 >> 32), (uint32_t)th.r3,
@@ -927,7 +965,7 @@ struct Lane {
         uint4 GAS* c2 = hc ? pc0 + 2 : (uint4 GAS*)(dm + 2 * R5);
         uint4 GAS* c3 = hc ? pc0 + 3 : (uint4 GAS*)(dm + 3 * R5);
         *c0 = make_uint4(ch.w0, ch.w1, ch.w2, ch.w3);
-        *c1 = make_uint4(ch.f0, ch.f1, ch.f2, ch.w7);
+        *c1 = make_uint4(ch.f0, ch.f1, ch.xl, ch.xh);
         *c2 = make_uint4((uint32_t)ch.r0, (uint32_t)((uint64_t)ch.r0 >> 32), (uint32_t)ch.r1,
                          (uint32_t)((uint64_t)ch.r1 >> 32));
         *c3 = make_uint4((uint32_t)ch.r2, (uint32_t)((uint64_t)ch.r2 >> 32), (uint32_t)ch.r3,
@@ -1051,13 +1089,14 @@ struct Lane {
                                           int64_t& ref, Th& ch, uint32_t& cs_out) {
         uint32_t s = alloc_slot();
         if (s == 0xFFFFFFFFu) return false;
+        if (tidc == 0xFFFFFFFFu) { fail(TW_REP_ERR_COUNTER); return false; }  // getNextThreadId, TimedT.hs:288-289
         uint32_t tid = tidc++;
         ++d_th;
         ch.w0 = pc & 0xFFFFu;
         ch.w1 = node;
         ch.w2 = tid;
         ch.w3 = 0;
-        ch.f0 = ch.f1 = ch.f2 = ch.w7 = 0;
+        ch.f0 = ch.f1 = ch.xl = ch.xh = 0;
         ch.r0 = q0; ch.r1 = q1; ch.r2 = q2; ch.r3 = q3;
         enqueue(ch, s, now);
         cs_out = s;
@@ -1072,7 +1111,7 @@ struct Lane {
         if (ts >= c.S) return;
         if (ts == self_slot) {  // the running thread: its record lives in registers
             if (self.w2 != tid) return;
-            if (th_exc(self) == 0) { th_set_exc(self, code); self.w7 = (uint32_t)val; }
+            if (th_exc(self) == 0) { th_set_exc(self, code); th_set_xval(self, val); }
             return;
         }
         Th t;
@@ -1080,7 +1119,7 @@ struct Lane {
         if (t.w2 != tid) return;  // dead (slot free or reused): the map entry is unobservable
         if (t.w3 != 0) {          // queued: wake to now with a fresh seq
             bool on_chip = (th_flags(t) & F_NEARQ) != 0;
-            uint32_t s = ++seq;
+            uint32_t s = next_seq();
             if (!(on_chip && near_rekey(t.w3, now, s, ts))) {
                 on_chip = near_fits(now);
                 if (on_chip) near_push(now, s, ts);
@@ -1092,7 +1131,7 @@ struct Lane {
         }
         if (th_exc(t) == 0) {
             th_set_exc(t, code);
-            t.w7 = (uint32_t)val;
+            th_set_xval(t, val);
         }
         put_rec(ts, t);
     }
@@ -1117,25 +1156,36 @@ struct Lane {
         free_slot(slot);
     }
 
+    // Frames 2.. of the thread in `slot` (the handler stack beyond the record).
+    __device__ __forceinline__ uint32_t GAS* fxp(uint32_t slot, uint32_t i) const {
+        return (uint32_t GAS*)(gp(c.fx) + ((size_t)slot * c.R + r) * c.FXQ) + (i - 2);
+    }
+    __device__ __forceinline__ uint32_t frame(const Th& t, uint32_t slot, uint32_t i) const {
+        if (i < 2) return i == 0 ? t.f0 : t.f1;
+        const uint32_t f = *fxp(slot, i);
+        tw_vm_drain();
+        return f;
+    }
+
     // Raise `code` in the running thread; true if a catch frame took it (pc set
-    // to the handler, r0 = value, r3 = code in the register file).
+    // to the handler, r0 = value, r3 = code in the register file).  Frames are
+    // left innermost first, the way TimedT's ContException unwinds the
+    // handler list (TimedT.hs:183-204, 263, 284); finally frames set their
+    // timeout's done flag on the way (TimedT.hs:376).
     __device__ __forceinline__ bool unwind(Th& th, uint32_t slot, uint32_t code, int64_t val) {
         const uint32_t n = th_nfr(th);
-#pragma unroll
-        for (int i = TW_MAX_FRAMES - 1; i >= 0; --i) {
-            if ((uint32_t)i < n) {
-                uint32_t f = i == 0 ? th.f0 : i == 1 ? th.f1 : th.f2;
-                uint32_t mask = f >> 16;
-                if (mask == 0) {
-                    uint32_t e = f & 0xFFFFu;
-                    if (e < c.T) gp(c.tmo_done)[ix(e)] = 1;
-                } else if (mask & (1u << code)) {
-                    th_set_nfr(th, (uint32_t)i);
-                    th_set_pc(th, f & 0xFFFFu);
-                    rf[0] = val;
-                    rf[3 * WG] = (int64_t)code;
-                    return true;
-                }
+        for (int i = (int)n - 1; i >= 0; --i) {
+            const uint32_t f = frame(th, slot, (uint32_t)i);
+            const uint32_t mask = f >> 16;
+            if (mask == 0) {
+                const uint32_t e = f & 0xFFFFu;
+                if (e < c.T) gp(c.tmo_done)[ix(e)] = 1;
+            } else if (mask & (1u << code)) {
+                th_set_nfr(th, (uint32_t)i);
+                th_set_pc(th, f & 0xFFFFu);
+                rf[0] = val;
+                rf[3 * WG] = (int64_t)code;
+                return true;
             }
         }
         th_set_nfr(th, 0);
@@ -1177,7 +1227,7 @@ struct Lane {
     // loop for all lanes at once.
     __device__ __forceinline__ void step(Th& th, uint32_t slot, bool run) {
         uint32_t pc = th_pc(th);
-        th.w0 = run ? th.w0 | (F_STARTED << 18) : th.w0;
+        th.w0 = run ? th.w0 | (F_STARTED << FL_SHIFT) : th.w0;
         bool running = run && pc < c.n_insns;
         pfail(run && !running, TW_REP_ERR_INSN);
         uint32_t fin = (run && !running) ? (uint32_t)T_STOP : (uint32_t)T_NONE;
@@ -1341,23 +1391,23 @@ struct Lane {
             case TW_OP_CATCH:
             case TW_OP_TMO_PUSH: {
                 const uint32_t nf = th_nfr(th);
-                const bool bad = nf >= TW_MAX_FRAMES;
+                const bool bad = nf >= c.max_frames;
                 pfail(me && bad, TW_REP_ERR_FRAMES);
                 tc = bad ? T_STOP : T_NONE;
                 const uint32_t fv = op == TW_OP_CATCH ? (b << 16) | ((uint32_t)imm & 0xFFFFu) : (uint32_t)ra & 0xFFFFu;
                 const bool ok = me && !bad;
                 th.f0 = (ok && nf == 0) ? fv : th.f0;
                 th.f1 = (ok && nf == 1) ? fv : th.f1;
-                th.f2 = (ok && nf == 2) ? fv : th.f2;
-                th.w0 = ok ? (th.w0 & ~(3u << 16)) | ((nf + 1) << 16) : th.w0;
+                if (ok && nf >= 2) *fxp(slot, nf) = fv;  // deeper frames: the overflow area
+                th.w0 = ok ? (th.w0 & ~(15u << 16)) | ((nf + 1) << 16) : th.w0;
                 break;
             }
             case TW_OP_UNCATCH: {
                 const uint32_t nf = th_nfr(th);
-                const bool bad = nf == 0 || (getf(th, nf - 1) >> 16) == 0;
+                const bool bad = nf == 0 || (frame(th, slot, nf > 0 && me ? nf - 1 : 0) >> 16) == 0;
                 pfail(me && bad, TW_REP_ERR_INSN);
                 tc = bad ? T_STOP : T_NONE;
-                th.w0 = (me && !bad) ? (th.w0 & ~(3u << 16)) | ((nf - 1) << 16) : th.w0;
+                th.w0 = (me && !bad) ? (th.w0 & ~(15u << 16)) | ((nf - 1) << 16) : th.w0;
                 break;
             }
             case TW_OP_MODI: {
@@ -1404,7 +1454,7 @@ struct Lane {
                             // the deliverer `schedule (after d) deliver` is accounted here (start pop
                             // at now, wake pop at now+d, both at this node) and its delivery travels
                             // as a record: the receiver checks its binding at now+d
-                            const int64_t dly = (int64_t)(e & 0x7FFFFFFFu);
+                            const int64_t dly = (int64_t)(e & 0x7FFFFFFFu) + tx_us(c, link, kind);
                             if (dly < c.lookahead) {
                                 fail(TW_REP_ERR_INSN);
                                 tc = T_STOP;
@@ -1422,7 +1472,8 @@ struct Lane {
                         } else {
                             cs(CW_CPC, TW_PC_DELIVER_STUB); cs(CW_CNODE, th.w1); cs(CW_CRA, 4); cs(CW_CDEL, 0);
                             cs64(CW_Q0, CW_Q0 + 1, payload); cs64(CW_Q0 + 2, CW_Q0 + 3, (int64_t)link);
-                            cs64(CW_Q0 + 4, CW_Q0 + 5, (int64_t)(e & 0x7FFFFFFFu)); cs64(CW_Q0 + 6, CW_Q7, (int64_t)kind);
+                            cs64(CW_Q0 + 4, CW_Q0 + 5, (int64_t)(e & 0x7FFFFFFFu) + tx_us(c, link, kind));
+                            cs64(CW_Q0 + 6, CW_Q7, (int64_t)kind);
                             tc = T_SPAWN;
                         }
                     }
@@ -1477,7 +1528,7 @@ struct Lane {
                     gp(c.bind)[bix(th.w1)] = (uint32_t)imm + 1;
                     gp(c.bind_own)[bix(th.w1)] = b ? th.w2 : 0xFFFFFFFFu;
                 }
-                th.w0 = (me && !bad && b) ? th.w0 | (F_OWNS << 18) : th.w0;
+                th.w0 = (me && !bad && b) ? th.w0 | (F_OWNS << FL_SHIFT) : th.w0;
                 break;
             }
             case TW_OP_UNLISTEN:
@@ -1507,11 +1558,12 @@ struct Lane {
             case TW_OP_TMO_END:
                 if (me) {
                     const uint32_t nf = th_nfr(th);
-                    if (nf == 0 || (getf(th, nf - 1) >> 16) != 0) {
+                    const uint32_t fr = nf ? frame(th, slot, nf - 1) : 0u;
+                    if (nf == 0 || (fr >> 16) != 0) {
                         fail(TW_REP_ERR_INSN);
                         tc = T_STOP;
                     } else {
-                        const uint32_t ep = getf(th, nf - 1) & 0xFFFFu;
+                        const uint32_t ep = fr & 0xFFFFu;
                         th_set_nfr(th, nf - 1);
                         if (ep < c.T) gp(c.tmo_done)[ix(ep)] = 1;
                     }
@@ -1555,7 +1607,7 @@ struct Lane {
         STIME(tt0);
         // ---- terminal actions (queue work only), then a fixed-shape store tail
         Th ch;
-        ch.w0 = ch.w1 = ch.w2 = ch.w3 = ch.f0 = ch.f1 = ch.f2 = ch.w7 = 0;
+        ch.w0 = ch.w1 = ch.w2 = ch.w3 = ch.f0 = ch.f1 = ch.xl = ch.xh = 0;
         ch.r0 = ch.r1 = ch.r2 = ch.r3 = 0;
         uint32_t cslot = 0xFFFFFFFFu;
         if (run) th_set_pc(th, pc);
@@ -1604,7 +1656,8 @@ struct Lane {
 // ------------------------------------------------------------------ kernels
 __global__ void __launch_bounds__(TW_WG) tw_init_kernel(Dev c, uint32_t main_pc, uint32_t main_node,
                                                        const int64_t* main_regs, const int64_t* nv_init,
-                                                       const uint32_t* listen_init, int lp_mode) {
+                                                       const uint32_t* listen_init, int lp_mode, uint32_t seq0,
+                                                       uint32_t tid0) {
     uint32_t r = blockIdx.x * TW_WG + threadIdx.x;
     if (r >= c.R) return;
     // LP mode: lane r is global node g; only the main node's lane holds the main thread
@@ -1612,12 +1665,13 @@ __global__ void __launch_bounds__(TW_WG) tw_init_kernel(Dev c, uint32_t main_pc,
     const bool has_main = !lp_mode || g == main_node;
     for (uint32_t f = 0; f < SC_COUNT; ++f) gp(c.scal)[(size_t)f * c.R + r] = 0;
     gp(c.scal)[(size_t)SC_THREADS * c.R + r] = has_main ? 1 : 0;
-    gp(c.scal)[(size_t)SC_TIDC * c.R + r] = 1;
+    gp(c.scal)[(size_t)SC_TIDC * c.R + r] = tid0;  // main is tid 0 (TimedT.hs:272-280)
+    gp(c.scal)[(size_t)SC_SEQ * c.R + r] = seq0;
     gp(c.scal)[(size_t)SC_STATUS * c.R + r] = TW_REP_RUNNING;
     gp(c.scal)[(size_t)SC_PENDING_MAIN * c.R + r] = has_main ? 1 : 0;
     gp(c.scal)[(size_t)SC_BUMP * c.R + r] = has_main ? 1 : 0;  // slot 0 = main
     uint4 GAS* p = gp(c.slots) + (size_t)r * 4;  // slot 0
-    uint32_t w0 = (main_pc & 0xFFFFu) | (F_MAIN << 18);
+    uint32_t w0 = (main_pc & 0xFFFFu) | (F_MAIN << FL_SHIFT);
     p[0] = make_uint4(w0, main_node, has_main ? 0u : 0xFFFFFFFFu, 0u);
     p[1] = make_uint4(0u, 0u, 0u, 0u);
     int64_t m[4] = {0, 0, 0, 0};
@@ -1792,11 +1846,11 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
             uint32_t s = L.alloc_slot();
             if (s == 0xFFFFFFFFu) break;
             Th ph;
-            ph.w0 = ((TW_PC_DELIVER_STUB + 1) & 0xFFFFu) | ((F_STARTED | F_PHANTOM) << 18);
+            ph.w0 = ((TW_PC_DELIVER_STUB + 1) & 0xFFFFu) | ((F_STARTED | F_PHANTOM) << FL_SHIFT);
             ph.w1 = c.lp0 + r;
             ph.w2 = 0xFFFFFFFEu;  // never a throwTo target
             ph.w3 = 0;
-            ph.f0 = ph.f1 = ph.f2 = ph.w7 = 0;
+            ph.f0 = ph.f1 = ph.xl = ph.xh = 0;
             ph.r0 = (int64_t)(((uint64_t)ba.w << 32) | ba.z);  // payload
             ph.r1 = bb.x;                                     // link
             ph.r2 = bb.z;                                     // sending node
@@ -1886,9 +1940,9 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
                         }
                         const uint32_t exc = th_exc(th);  // asyncExceptions . at tid <<.= Nothing (:252)
                         if (exc) {
-                            const int64_t val = (int64_t)(int32_t)th.w7;
+                            const int64_t val = th_xval(th);
                             th_set_exc(th, 0);
-                            th.w7 = 0;
+                            th.xl = th.xh = 0;
                             L.hacc += term0(t, TW_KIND_EXC | exc);
                             if (!(th_flags(th) & (F_STARTED | F_MAIN))) {  // escapes launchTimedT (:252-263)
                                 L.status = TW_REP_ABORTED;
@@ -2003,6 +2057,19 @@ __global__ void __launch_bounds__(256) tw_lp_scatter(Dev c, const uint4* recs, u
     }
 }
 
+// Per-replica digest of the results and node hashes (tw_tie_audit compares
+// runs under different tie orders without copying every hash to the host).
+__global__ void __launch_bounds__(256) tw_digest_kernel(Dev c, uint64_t* out) {
+    const uint32_t r = blockIdx.x * 256 + threadIdx.x;
+    if (r >= c.R) return;
+    uint64_t d = 0;
+    const int fields[8] = {SC_FINAL_T, SC_EVENTS, SC_DELIVERED, SC_DROPPED, SC_UNDELIV, SC_STATUS, SC_MAIN_EXC,
+                           SC_THREADS};
+    for (int i = 0; i < 8; ++i) d = mix64(d ^ gp(c.scal)[(size_t)fields[i] * c.R + r]) + (uint64_t)i;
+    for (uint32_t n = 0; n < c.N; ++n) d += mix64(gp(c.hash)[(size_t)n * c.R + r] ^ ((uint64_t)n * 0x9e3779b97f4a7c15ull));
+    gp(out)[r] = d;
+}
+
 }  // namespace
 
 // ======================================================================= C ABI
@@ -2027,6 +2094,8 @@ struct tw_ctx {
     std::vector<double> launch_ms;
     std::vector<hipEvent_t> ev_pool;
     uint32_t act_n_init[2] = {0, 0};
+    std::vector<uint32_t> tie_flags;  // tw_tie_audit, per replica
+    uint32_t seq0 = 0, tid0 = 1;      // tw_set_counter_base
 };
 
 namespace {
@@ -2075,7 +2144,9 @@ static void launch_run(tw_ctx* c, hipStream_t st, int64_t t_end, uint64_t limit,
 
 extern "C" {
 
-const char* tw_version(void) { return "timewarp-mi355x 0.2 (gfx950, lane-per-replica, near-cap 16, LDS write-back record cache)"; }
+const char* tw_version(void) {
+    return "timewarp-mi355x 0.3 (gfx950; lane-per-replica dense/sparse kernels, node-partitioned LP kernel; ABI 2)";
+}
 
 const char* tw_strerror(int code) {
     switch (code) {
@@ -2086,6 +2157,7 @@ const char* tw_strerror(int code) {
     case TW_ERR_OOM: return "device out of memory";
     case TW_ERR_STATE: return "call out of order";
     case TW_ERR_REPLICA: return "replica error";
+    case TW_ERR_INCOMPLETE: return "relaunch cap reached before every replica stopped";
     default: return "unknown error";
     }
 }
@@ -2095,6 +2167,12 @@ int tw_create(int device, tw_ctx** out) {
     *out = nullptr;
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess || n <= 0 || device < 0 || device >= n) return TW_ERR_NO_DEVICE;
+    {
+        // the kernels are built for gfx950 (MI355X) only
+        hipDeviceProp_t prop;
+        if (hipGetDeviceProperties(&prop, device) != hipSuccess || strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+            return TW_ERR_NO_DEVICE;
+    }
     tw_ctx* c = new (std::nothrow) tw_ctx;
     if (!c) return TW_ERR_OOM;
     c->device = device;
@@ -2123,6 +2201,7 @@ static int validate(const tw_scenario_desc* s) {
     if (s->n_replicas == 0 || s->n_nodes == 0 || !s->insns || s->n_insns < TW_PC_USER || s->n_insns > 0xFFFF)
         return TW_ERR_INVALID;
     if (s->max_slots < 1 || s->queue_capacity < 1 || s->link_depth < 1 || !s->out_off) return TW_ERR_INVALID;
+    if (s->max_frames > TW_MAX_FRAMES) return TW_ERR_INVALID;
     if (s->main_pc >= s->n_insns || s->main_node >= s->n_nodes || s->max_timeouts > 65536) return TW_ERR_INVALID;
     if (s->n_links && (!s->link_dst || !s->link_rev)) return TW_ERR_INVALID;
     if (s->n_listener_sets && (!s->listener_pc || !s->n_msg_kinds)) return TW_ERR_INVALID;
@@ -2164,6 +2243,10 @@ static int load_common(tw_ctx* c, const tw_scenario_desc* s, bool lp, uint32_t l
     d.n_insns = s->n_insns; d.n_consts = s->n_consts; d.n_sets = s->n_listener_sets; d.n_kinds = s->n_msg_kinds;
     d.horizon = s->near_horizon_us;
     d.Cr = s->run_capacity;
+    d.max_frames = s->max_frames ? s->max_frames : 2u;
+    d.FXQ = d.max_frames > 2 ? (d.max_frames - 2 + 3) / 4 : 0u;
+    d.tie_mode = TW_TIE_FIFO;
+    c->tie_flags.assign(d.R, 0u);
     const size_t R = d.R;
     const size_t Rt = s->n_replicas;  // replica dimension of the host tables
     const size_t prog_lds = 12ull * (d.n_insns + 1) + 8ull * d.n_consts;
@@ -2220,6 +2303,13 @@ static int load_common(tw_ctx* c, const tw_scenario_desc* s, bool lp, uint32_t l
     ALLOC(d.link_ord, (size_t)(d.L ? d.L : 1) * (lp ? 1 : R));
     ALLOC(d.tmo_done, (size_t)(d.T ? d.T : 1) * R);
     ALLOC(d.n_active, 1);
+    if (d.FXQ) ALLOC(d.fx, (size_t)d.S * R * d.FXQ);
+    uint32_t* mbytes = nullptr;
+    uint64_t* lbw = nullptr;
+    if (s->msg_bytes && s->link_bw && d.n_kinds && d.L) {
+        ALLOC(mbytes, d.n_kinds);
+        ALLOC(lbw, d.L);
+    }
 #ifdef TW_STATS
     ALLOC(d.prof, P_COUNT);
     HIPCHK(hipMemsetAsync(d.prof, 0, 8 * P_COUNT, c->stream));
@@ -2259,6 +2349,12 @@ static int load_common(tw_ctx* c, const tw_scenario_desc* s, bool lp, uint32_t l
     if (mregs) HIPCHK(hipMemcpyAsync(mregs, s->main_regs, 32ull * R, hipMemcpyHostToDevice, st));
     if (nvi) HIPCHK(hipMemcpyAsync(nvi, s->node_vars, 32ull * d.Ntot, hipMemcpyHostToDevice, st));
     if (lsi) HIPCHK(hipMemcpyAsync(lsi, s->node_listen, 4ull * d.Ntot, hipMemcpyHostToDevice, st));
+    if (mbytes) {
+        HIPCHK(hipMemcpyAsync(mbytes, s->msg_bytes, 4ull * d.n_kinds, hipMemcpyHostToDevice, st));
+        HIPCHK(hipMemcpyAsync(lbw, s->link_bw, 8ull * d.L, hipMemcpyHostToDevice, st));
+    }
+    d.msg_bytes = mbytes;
+    d.link_bw = lbw;
     d.insns = insns; d.consts = consts; d.lpc = lpc; d.out_off = out_off; d.link_dst = ldst; d.link_rev = lrev;
     d.link_table = ltab;
     c->main_pc = s->main_pc;
@@ -2306,7 +2402,7 @@ int tw_reset(tw_ctx* c) {
     uint32_t blocks = (uint32_t)((R + TW_WG - 1) / TW_WG);
     hipLaunchKernelGGL(tw_init_kernel, dim3(blocks), dim3(TW_WG), 0, st, d, c->main_pc, c->main_node,
                        (const int64_t*)c->main_regs, (const int64_t*)c->nv_init, (const uint32_t*)c->listen_init,
-                       c->lp ? 1 : 0);
+                       c->lp ? 1 : 0, c->seq0, c->tid0);
     HIPCHK(hipGetLastError());
     return TW_OK;
 }
@@ -2342,6 +2438,7 @@ int tw_run(tw_ctx* c, int64_t t_end_us, uint64_t max_events, tw_stats* out) {
     const int per_check = c->lp ? 1 : 4;
     uint32_t launches = 0;
     double kms = 0.0;
+    bool quiet = false;
     for (int round = 0; round < (1 << 20); ++round) {
         size_t need = 2 * per_check;
         while (c->ev_pool.size() < need) {
@@ -2373,7 +2470,7 @@ int tw_run(tw_ctx* c, int64_t t_end_us, uint64_t max_events, tw_stats* out) {
             c->launch_ms.push_back(ms);
             kms += ms;
         }
-        if (*c->h_active == 0) break;
+        if (*c->h_active == 0) { quiet = true; break; }
     }
     if (out) {
         std::memset(out, 0, sizeof(*out));
@@ -2394,7 +2491,7 @@ int tw_run(tw_ctx* c, int64_t t_end_us, uint64_t max_events, tw_stats* out) {
         out->kernel_ms = kms;
         out->wall_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - w0).count();
     }
-    return TW_OK;
+    return quiet ? TW_OK : TW_ERR_INCOMPLETE;
 }
 
 int tw_read_results(tw_ctx* c, tw_replica_result* out, size_t n) {
@@ -2412,7 +2509,58 @@ int tw_read_results(tw_ctx* c, tw_replica_result* out, size_t n) {
         out[i].delivered = F(SC_DELIVERED, i); out[i].dropped = F(SC_DROPPED, i);
         out[i].undeliverable = F(SC_UNDELIV, i); out[i].status = (uint32_t)F(SC_STATUS, i);
         out[i].main_exc = (uint32_t)F(SC_MAIN_EXC, i); out[i].threads = F(SC_THREADS, i);
+        out[i].tie_flags = i < c->tie_flags.size() ? c->tie_flags[i] : 0u;
+        out[i].reserved = 0;
     }
+    return TW_OK;
+}
+
+static int digest(tw_ctx* c, std::vector<uint64_t>& h) {
+    const Dev& d = c->d;
+    uint64_t* dd = nullptr;
+    HIPCHK(hipMallocAsync((void**)&dd, 8ull * d.R, c->stream));
+    hipLaunchKernelGGL(tw_digest_kernel, dim3((d.R + 255) / 256), dim3(256), 0, c->stream, d, dd);
+    HIPCHK(hipGetLastError());
+    h.resize(d.R);
+    HIPCHK(hipMemcpyAsync(h.data(), dd, 8ull * d.R, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipFreeAsync(dd, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return TW_OK;
+}
+
+int tw_tie_audit(tw_ctx* c, uint32_t probes, tw_stats* out) {
+    if (!c) return TW_ERR_INVALID;
+    if (!c->loaded) return TW_ERR_STATE;
+    if (c->lp || probes < 1 || probes > 2) return TW_ERR_INVALID;
+    HIPCHK(hipSetDevice(c->device));
+    std::vector<std::vector<uint64_t>> dg(probes + 1);
+    int rc = TW_OK;
+    for (uint32_t p = probes; p + 1 > 0 && rc == TW_OK; --p) {  // probes first, the canonical run last
+        c->d.tie_mode = p;
+        rc = tw_reset(c);
+        if (rc == TW_OK) rc = tw_run(c, INT64_MAX, UINT64_MAX, p == 0 ? out : nullptr);
+        if (rc == TW_OK) rc = digest(c, dg[p]);
+        if (p == 0) break;
+    }
+    c->d.tie_mode = TW_TIE_FIFO;
+    if (rc != TW_OK) return rc;
+    c->tie_flags.assign(c->d.R, 1u);
+    for (uint32_t p = 1; p <= probes; ++p)
+        for (uint32_t i = 0; i < c->d.R; ++i)
+            if (dg[p][i] != dg[0][i]) c->tie_flags[i] |= 1u << p;
+    return TW_OK;
+}
+
+int tw_geometry(tw_ctx* c) {
+    if (!c) return TW_ERR_INVALID;
+    if (!c->loaded) return TW_ERR_STATE;
+    return c->lp ? TW_GEO_LP : c->geo;
+}
+
+int tw_set_counter_base(tw_ctx* c, uint32_t seq0, uint32_t tid0) {
+    if (!c || tid0 == 0) return TW_ERR_INVALID;
+    c->seq0 = seq0;
+    c->tid0 = tid0;
     return TW_OK;
 }
 

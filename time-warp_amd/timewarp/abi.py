@@ -34,6 +34,9 @@ class TwScenarioDesc(C.Structure):
         ("near_horizon_us", C.c_int64),
         ("max_timeouts", C.c_uint32),
         ("run_capacity", C.c_uint32),
+        ("max_frames", C.c_uint32),
+        ("msg_bytes", C.c_void_p),
+        ("link_bw", C.c_void_p),
     ]
 
 
@@ -47,6 +50,8 @@ class TwReplicaResult(C.Structure):
         ("status", C.c_uint32),
         ("main_exc", C.c_uint32),
         ("threads", C.c_uint64),
+        ("tie_flags", C.c_uint32),
+        ("reserved", C.c_uint32),
     ]
 
 
@@ -67,6 +72,7 @@ class TwStats(C.Structure):
     ]
 
 
+# the fields a run produces (tie_flags is set by tw_tie_audit only)
 RESULT_FIELDS = ["final_t", "events", "delivered", "dropped", "undeliverable", "status", "main_exc", "threads"]
 
 # numpy dtype with the same layout as tw_replica_result (for bulk reads)
@@ -75,7 +81,7 @@ import numpy as _np  # noqa: E402
 RESULT_DTYPE = _np.dtype([
     ("final_t", _np.int64), ("events", _np.uint64), ("delivered", _np.uint64),
     ("dropped", _np.uint64), ("undeliverable", _np.uint64), ("status", _np.uint32),
-    ("main_exc", _np.uint32), ("threads", _np.uint64),
+    ("main_exc", _np.uint32), ("threads", _np.uint64), ("tie_flags", _np.uint32), ("reserved", _np.uint32),
 ])
 assert RESULT_DTYPE.itemsize == C.sizeof(TwReplicaResult)
-assert isa.ABI_VERSION == 1
+assert isa.ABI_VERSION == 2

@@ -27,7 +27,8 @@ T_INF = (1 << 63) - 1
 EXPORTS = ["tw_create", "tw_load", "tw_reset", "tw_run", "tw_read_results", "tw_read_hashes", "tw_read_final",
            "tw_last_launch_ms", "tw_destroy", "tw_strerror", "tw_version",
            "tw_lp_load", "tw_lp_window", "tw_lp_take_outbox", "tw_lp_inject", "tw_lp_results",
-           "tw_set_trace", "tw_read_trace"]
+           "tw_set_trace", "tw_read_trace", "tw_tie_audit", "tw_set_counter_base", "tw_geometry"]
+GEOMETRIES = ("dense", "sparse", "half", "wave", "lp")  # TW_GEO_* order
 
 # tw_trace_rec (include/timewarp.h)
 TRACE_DTYPE = np.dtype([("t", np.int64), ("val", np.int64), ("node", np.uint32), ("tag", np.uint32)])
@@ -74,9 +75,13 @@ def load_library(path: Optional[str] = None):
     lib.tw_lp_results.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t]
     lib.tw_set_trace.argtypes = [C.c_void_p, C.c_uint32]
     lib.tw_read_trace.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_size_t, C.POINTER(C.c_uint64)]
+    lib.tw_tie_audit.argtypes = [C.c_void_p, C.c_uint32, C.POINTER(TwStats)]
+    lib.tw_set_counter_base.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32]
+    lib.tw_geometry.argtypes = [C.c_void_p]
     for name in ("tw_create", "tw_load", "tw_reset", "tw_run", "tw_read_results", "tw_read_hashes", "tw_read_final",
                  "tw_last_launch_ms", "tw_lp_load", "tw_lp_window", "tw_lp_take_outbox", "tw_lp_inject",
-                 "tw_lp_results", "tw_set_trace", "tw_read_trace"):
+                 "tw_lp_results", "tw_set_trace", "tw_read_trace", "tw_tie_audit", "tw_set_counter_base",
+                 "tw_geometry"):
         getattr(lib, name).restype = C.c_int
     if path is None:
         _lib = lib
@@ -140,8 +145,8 @@ class Engine:
         d = scn.desc()
         old = os.environ.get("TW_GEOMETRY")
         if geometry is not None:
-            if geometry not in ("dense", "sparse", "half"):
-                raise ValueError(f"geometry must be 'dense', 'sparse' or 'half', not {geometry!r}")
+            if geometry not in ("dense", "sparse", "half", "wave"):
+                raise ValueError(f"geometry must be 'dense', 'sparse', 'half' or 'wave', not {geometry!r}")
             os.environ["TW_GEOMETRY"] = geometry
         try:
             _check(self.lib.tw_load(self.ctx, C.addressof(d)), "tw_load")
@@ -154,6 +159,12 @@ class Engine:
         self.scn = scn
         return self
 
+    def geometry(self) -> str:
+        """The kernel geometry tw_load chose (GEOMETRIES)."""
+        g = self.lib.tw_geometry(self.ctx)
+        _check(g, "tw_geometry")
+        return GEOMETRIES[g]
+
     def reset(self) -> "Engine":
         """Back to t=0 on the device-resident tables (no host upload)."""
         _check(self.lib.tw_reset(self.ctx), "tw_reset")
@@ -163,6 +174,22 @@ class Engine:
         st = TwStats()
         _check(self.lib.tw_run(self.ctx, t_end, max_events, C.byref(st)), "tw_run")
         return RunStats(**{f: getattr(st, f) for f, _ in TwStats._fields_ if f != "reserved"})
+
+    def tie_audit(self, probes: int = 2) -> RunStats:
+        """Run every replica under `probes` tie-order probes (reverse and
+        scrambled order of equal-timestamp events) and then canonically;
+        results()['tie_flags'] bit p marks replicas whose outputs differ under
+        probe p (they depend on TimedT's pqueue tie order, TimedT.hs:100-104).
+        The canonical run's results stay loaded."""
+        st = TwStats()
+        _check(self.lib.tw_tie_audit(self.ctx, int(probes), C.byref(st)), "tw_tie_audit")
+        return RunStats(**{f: getattr(st, f) for f, _ in TwStats._fields_ if f != "reserved"})
+
+    def set_counter_base(self, seq0: int, tid0: int = 1) -> "Engine":
+        """Testing hook: start the 32-bit insertion / thread counters at these
+        values from the next reset on (TW_REP_ERR_COUNTER guard)."""
+        _check(self.lib.tw_set_counter_base(self.ctx, int(seq0), int(tid0)), "tw_set_counter_base")
+        return self
 
     def results(self) -> np.ndarray:
         out = np.zeros(self.scn.n_replicas, RESULT_DTYPE)

@@ -29,6 +29,8 @@ reference (file:line)            lowering
 ``reply`` (:177-180)             ``Code.reply_link(r, r_in)`` + ``send``
 ``userStateR`` (socket-state :91-93)  ``Code.user_state_load/_store`` (a state
                                  cell per incoming link)
+``close`` / ``closeR``           ``Code.close_conn`` (the link's state cell is
+  (MonadTransfer.hs:139-142,162)  reset: the next connection starts fresh)
 ===============================  ==============================================
 
 Registers r0..r3 are per-thread int64 and are copied into forked children
@@ -428,6 +430,16 @@ class Code:
     def user_state_store(self, r: int, var: int, link_reg: int, state_base: int, scratch: int = 2):
         self.mov(scratch, link_reg).addi(scratch, state_base)
         return self.nstorex(r, var, scratch)
+
+    def close_conn(self, link_reg: int, state_base: int, scratch: int = 2, zero: int = 3):
+        """``close addr`` / ``closeR`` (MonadTransfer.hs:139-142, 162-163): the
+        connection's socket goes away, so the next one starts from a fresh
+        ``mkState`` -- the state cell of the link is reset to zeros (clobbers
+        `scratch` and `zero`)."""
+        self.mov(scratch, link_reg).addi(scratch, state_base).seti(zero, 0)
+        for var in range(4):
+            self.nstorex(zero, var, scratch)
+        return self
 
     def trace(self, tag: int, r: int = 0):
         """Checkpoint / logMeasure-style trace record into the node hash."""

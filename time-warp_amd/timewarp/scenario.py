@@ -69,6 +69,9 @@ class Scenario:
     near_horizon_us: int = 10_000_000
     max_timeouts: int = 0
     run_capacity: int = 0
+    max_frames: int = 0                       # catch/finally frames per thread (0 = 2)
+    msg_bytes: Optional[np.ndarray] = None    # uint32 [n_msg_kinds]: BinaryP wire size per kind
+    link_bw: Optional[np.ndarray] = None      # uint64 [n_links]: bytes/s (0 = no transmission time)
     meta: dict = field(default_factory=dict)
     # oracle-only: the reference's live Delays function (kind/lo/hi per link)
     live_kind: Optional[np.ndarray] = None
@@ -131,5 +134,13 @@ class Scenario:
         d.near_horizon_us = self.near_horizon_us
         d.max_timeouts = self.max_timeouts
         d.run_capacity = self.run_capacity
+        d.max_frames = self.max_frames
+        if (self.msg_bytes is None) != (self.link_bw is None):
+            raise ValueError("msg_bytes and link_bw go together")
+        if self.msg_bytes is not None:
+            assert self.msg_bytes.shape == (self.image.n_msg_kinds,)
+            assert self.link_bw.shape == (self.topo.n_links,)
+        d.msg_bytes = ptr(self.msg_bytes, np.uint32)
+        d.link_bw = ptr(self.link_bw, np.uint64)
         d._keep = keep  # type: ignore[attr-defined]
         return d

@@ -429,7 +429,7 @@ TAG_FROM_CLIENT = 14     # "... from client #cid"
 
 
 def socket_state(n_replicas: int = 1, network_delay=(ms(1), ms(5)), seed_base: int = 0,
-                 max_rounds: int = 64, near_horizon_us: int = sec(20)) -> Scenario:
+                 max_rounds: int = 64, near_horizon_us: int = sec(20), close_every: int = 0) -> Scenario:
     """examples/socket-state/Main.hs re-hosted on the emulated transfer: a
     server counting requests per client connection with ``userStateR``
     (:65-76, :91-93), and 3 clients that send ``Ping cid`` once a second while
@@ -441,7 +441,11 @@ def socket_state(n_replicas: int = 1, network_delay=(ms(1), ms(5)), seed_base: i
     client's number of rounds is drawn host-side: draws of U[0, 2] from
     mkStdGen(seed_base + replica), client 1 first, until a 0 (capped at
     ``max_rounds``); the reference draws from the global IO generator, which is
-    not reproducible.  Main holds the counts in r1..r3 (``main_regs``)."""
+    not reproducible.  Main holds the counts in r1..r3 (``main_regs``).
+
+    ``close_every`` > 0: a client ``close``s its connection after every that
+    many pings and reconnects on the next send (MonadTransfer.hs:139-142), so
+    the server's per-connection counter restarts from a fresh state."""
     SRV, SYS, STATE = 0, 4, 5
     p = Program()
     K_PING = p.kind("Ping")
@@ -476,9 +480,17 @@ def socket_state(n_replicas: int = 1, network_delay=(ms(1), ms(5)), seed_base: i
     c.jeqi(0, 0, done)                                # whileM ruskaRuletka $ do
     c.wait(for_(sec(1)))                              #   wait (for 1 sec)
     c.send(1, K_PING, 2)                              #   send (localhost, 4444) $ Ping cid
-    c.addi(0, -1).jmp(top)
+    c.addi(0, -1)
+    if close_every:
+        keep = c.label()
+        c.mov(3, 0).modi(3, close_every).jnei(3, 0, keep)
+        c.close_conn(1, STATE, scratch=2, zero=3)     #   close (localhost, 4444): fresh socket next time
+        c.node(2)
+        c.bind(keep)
+    c.jmp(top)
     c.bind(done)
-    c.end()                                           # close (localhost, 4444)
+    c.close_conn(1, STATE, scratch=2, zero=3)         # close (localhost, 4444)
+    c.end()
 
     img = p.finalize()
     out = [[], [SRV], [SRV], [SRV], [], [], [], []]
@@ -498,7 +510,7 @@ def socket_state(n_replicas: int = 1, network_delay=(ms(1), ms(5)), seed_base: i
         name="socket_state", image=img, topo=topo, n_replicas=n_replicas,
         main_pc=img.pc_of("main"), main_node=SYS, link_table=table, main_regs=regs,
         max_slots=64, queue_capacity=256, near_horizon_us=near_horizon_us,
-        meta=dict(config="socket_state", seed_base=seed_base, max_rounds=max_rounds),
+        meta=dict(config="socket_state", seed_base=seed_base, max_rounds=max_rounds, close_every=close_every),
     )
 
 

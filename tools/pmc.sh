@@ -17,7 +17,12 @@ done
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/stats -o run -- python3 bench.py $ARGS > $OUT/stats.log 2>&1
 echo "stats rc=$?"
 python3 tools/pmc_summary.py $OUT/summary.json $OUT/stats $OUT/pass1 $OUT/pass2 $OUT/pass3 $OUT/pass4 $OUT/pass5 > $OUT/summary.log 2>&1
-python3 - "$OUT/summary.json" "$*" <<'PY'
+# provenance: the engine build and workload these counters belong to (bench.py
+# uses the summary for roofline.traffic only when both match)
+python3 bench.py --workload-key $* > $OUT/workload.json
+python3 - "$OUT/summary.json" "$*" "$OUT/workload.json" <<'PY'
 import json, sys
-s = json.load(open(sys.argv[1])); s["bench_args"] = sys.argv[2]; json.dump(s, open(sys.argv[1], "w"), indent=1)
+s = json.load(open(sys.argv[1])); s["bench_args"] = sys.argv[2]; s["steps"] = 1
+s.update(json.load(open(sys.argv[3])))
+json.dump(s, open(sys.argv[1], "w"), indent=1)
 PY
