@@ -300,15 +300,16 @@ int tw_set_trace(tw_ctx* ctx, uint32_t cap);
  * stores the number emitted (possibly more than were kept) in *n_emitted. */
 int tw_read_trace(tw_ctx* ctx, uint32_t replica, tw_trace_rec* out, size_t cap, uint64_t* n_emitted);
 
-/* Tie-order audit: run every replica to quiescence under each probe order
- * p in 1..probes (TW_TIE_LIFO, TW_TIE_SCRAMBLE), then under the canonical
- * order, and set tie_flags bit p of every replica whose results or node
+/* Tie-order audit: run every replica (as tw_run with t_end_us / max_events)
+ * under each probe order p in 1..probes (TW_TIE_LIFO, TW_TIE_SCRAMBLE), then
+ * under the canonical order, and set tie_flags bit p of every replica whose
+ * results or node
  * hashes differ from the canonical run's.  The canonical run's state is left
  * loaded, so results/hashes read afterwards are the canonical ones.  `out`
  * gets the canonical run's stats.  Replaces nothing in the reference: it
  * flags the replicas for which TimedT's pqueue tie order (TimedT.hs:100-104,
  * 242) could give a different trace than this engine. */
-int tw_tie_audit(tw_ctx* ctx, uint32_t probes, tw_stats* out);
+int tw_tie_audit(tw_ctx* ctx, int64_t t_end_us, uint64_t max_events, uint32_t probes, tw_stats* out);
 
 /* Testing hook: from the next tw_reset on, start every replica's insertion
  * counter at seq0 and its thread counter at tid0 (>= 1; main is tid 0), so the

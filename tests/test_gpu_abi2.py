@@ -77,9 +77,9 @@ def test_tie_audit_flags_tie_sensitive_replicas(engine_mod, oracle_mod):
     for seed in range(16):
         scn = progs.random_program(seed)
         with Engine(0) as e:
-            e.load(scn).tie_audit(probes=2)
+            e.load(scn).tie_audit(probes=2, t_end=3000)
             res, h = e.results(), e.hashes()
-        r = [oracle_mod.run(scn, mode=m) for m in (0, 2, 3)]
+        r = [oracle_mod.run(scn, mode=m, t_end=3000) for m in (0, 2, 3)]
         for f in RESULT_FIELDS:
             assert res[f][0] == r[0].result[f], (seed, f)
         assert np.array_equal(h[0], r[0].hashes), seed

@@ -38,6 +38,7 @@
 #include <vector>
 
 #include "../../include/timewarp.h"
+#include "tw_dev.hpp"
 
 #define TW_NEAR_CAP 16          // on-chip queue entries per replica (LDS)
 #define TW_WG 256               // lanes per workgroup (4 waves share one program image)
@@ -55,21 +56,8 @@
 // one wave's scalar, LDS and branch issue overlaps the other's VALU and
 // memory waits.
 #define TW_HALF_LANES 32
-#ifndef TW_RUNS
-#define TW_RUNS 4               // monotone far-queue runs per replica
-#endif
 #define TW_STEP_CAP (1u << 22)  // instructions per thread step (== oracle kStepCap)
 #define TW_TAIL_VMEM 9          // vector-memory ops of every iteration after the record prefetch
-
-// Explicit address spaces: generic (flat) pointers would make every HBM and
-// LDS access a flat_* instruction that waits on both memory counters.
-#if defined(__HIP_DEVICE_COMPILE__)
-#define GAS __attribute__((address_space(1)))
-#define LAS __attribute__((address_space(3)))
-#else
-#define GAS
-#define LAS
-#endif
 
 #define P_COUNT 28
 // Diagnostic build (-DTW_STATS, lib/libtimewarp_stats.so): per-lane event-path
@@ -102,168 +90,7 @@ enum { K_POP, K_SUPERSEDED, K_PEEK_PF, K_PEEK_HBM, K_PUT_HBM, K_PUT_DEAD, K_PF_I
 
 namespace {
 
-template <class T>
-__device__ __forceinline__ T GAS* gp(T* p) {
-    return (T GAS*)p;
-}
-
-// ------------------------------------------------------------------ layout
-// Thread slot record: 64 B, [slot][replica].
-//  w0: pc:16 | nfr:4 | flags:6 | exc_code:6
-//  w1: node   w2: tid   w3: wake_seq (0 = not queued)
-//  f0, f1: the two outermost frames (mask:16 << 16 | pc:16; mask 0 = finally
-//          frame of timeout epoch pc); frames 2.. live in the per-slot
-//          overflow area fx (TimedT's handler list, TimedT.hs:84,198)
-//  xl, xh: pending async exception value (int64, TimedT.hs:113,359)
-//  r0..r3: int64 registers
-struct Th {
-    uint32_t w0, w1, w2, w3;
-    uint32_t f0, f1, xl, xh;
-    int64_t r0, r1, r2, r3;
-};
-#define FL_SHIFT 20u   // flags field of w0
-#define EXC_SHIFT 26u  // exception-code field of w0
-
-#define F_STARTED 1u
-#define F_MAIN 2u
-#define F_PHANTOM 4u   // LP mode: a delivery record's stand-in for the deliverer's wake pop
-#define F_OWNS 8u      // has bound its node with an owned listener (checked at death)
-#define F_NEARQ 16u    // its live queue entry is in the on-chip near heap
-
-__device__ __forceinline__ uint32_t th_pc(const Th& t) { return t.w0 & 0xFFFFu; }
-__device__ __forceinline__ void th_set_pc(Th& t, uint32_t pc) { t.w0 = (t.w0 & 0xFFFF0000u) | (pc & 0xFFFFu); }
-__device__ __forceinline__ uint32_t th_nfr(const Th& t) { return (t.w0 >> 16) & 15u; }
-__device__ __forceinline__ void th_set_nfr(Th& t, uint32_t n) { t.w0 = (t.w0 & ~(15u << 16)) | (n << 16); }
-__device__ __forceinline__ uint32_t th_flags(const Th& t) { return (t.w0 >> FL_SHIFT) & 0x3Fu; }
-__device__ __forceinline__ void th_or_flags(Th& t, uint32_t f) { t.w0 |= (f & 0x3Fu) << FL_SHIFT; }
-__device__ __forceinline__ void th_clr_flags(Th& t, uint32_t f) { t.w0 &= ~((f & 0x3Fu) << FL_SHIFT); }
-__device__ __forceinline__ uint32_t th_exc(const Th& t) { return t.w0 >> EXC_SHIFT; }
-__device__ __forceinline__ void th_set_exc(Th& t, uint32_t c) {
-    t.w0 = (t.w0 & ((1u << EXC_SHIFT) - 1u)) | (c << EXC_SHIFT);
-}
-__device__ __forceinline__ int64_t th_xval(const Th& t) { return (int64_t)(((uint64_t)t.xh << 32) | t.xl); }
-__device__ __forceinline__ void th_set_xval(Th& t, int64_t v) {
-    t.xl = (uint32_t)v;
-    t.xh = (uint32_t)((uint64_t)v >> 32);
-}
-
-enum {
-    SC_NOW, SC_FINAL_T, SC_EVENTS, SC_DELIVERED, SC_DROPPED, SC_UNDELIV, SC_THREADS, SC_SEQ, SC_TIDC,
-    SC_LIVE, SC_NEAR_N, SC_FAR_N, SC_STATUS, SC_MAIN_EXC, SC_PENDING_MAIN, SC_FREE_N, SC_FTOP, SC_BUMP,
-    SC_TMO_CTR, SC_RH0, SC_RC0 = SC_RH0 + TW_RUNS, SC_TRACE_N = SC_RC0 + TW_RUNS, SC_COUNT
-};
-
-struct Dev {
-    // shape
-    uint32_t R, S, Q, N, L, D, T, Cr;
-    uint32_t n_insns, n_consts, n_sets, n_kinds;
-    int64_t horizon;
-    // scenario (shared by all replicas)
-    const uint2* insns;
-    const int64_t* consts;
-    const uint32_t* lpc;
-    const uint32_t* out_off;
-    const uint32_t* link_dst;
-    const uint32_t* link_rev;
-    const uint32_t* link_table;   // [L*D][R] or null
-    // per-replica scalars: one [field][replica] block of 64-bit words (SC_*)
-    uint64_t* scal;
-    // per-replica arrays
-    uint4* slots;        // [S][R][4]
-    uint32_t* free_stk;  // [S][R] (entries below the register-cached top)
-    uint4* far;          // [Q][R]  {t_lo, t_hi, slot, seq}
-    uint4* runs;         // [TW_RUNS][Cr][R] monotone FIFO runs (ring buffers)
-    uint4* near_spill;   // [NEAR_CAP][R]  near heap between launches
-    uint4* dummy;        // [5][R] per-lane sink of the fixed-shape store tail's unused stores
-    int64_t* nvars;      // [N*4][R]
-    uint64_t* hash;      // [N][R]
-    uint32_t* bind;      // [N][R] 0 or set+1
-    uint32_t* bind_own;  // [N][R] owner tid or 0xFFFFFFFF
-    uint32_t* bind_rel;  // [N][R] tid of the last owner that died (0xFFFFFFFE: none); the
-                         // binding is live iff bind != 0 && bind_own != bind_rel
-    uint32_t* link_ord;  // [L][R]
-    uint8_t* tmo_done;   // [T][R]
-    uint32_t* n_active;  // [1]
-    // node-partitioned (LP) mode: lane r = global node lp0 + r
-    uint32_t lp0, Ntot, IB, out_cap;
-    int64_t lookahead;
-    uint64_t* hash_g;    // [Ntot] this context's additions to every node's hash
-    uint4* inbox;        // [IB][R][2] delivery records addressed to local nodes
-    uint32_t* inbox_n;   // [R]
-    uint4* outbox;       // [out_cap][2] records produced this window
-    uint32_t* out_n;     // [1]
-    uint64_t* next_t;    // [1] min next-event time (atomicMin)
-    uint32_t* lp_err;    // [1] inbox/outbox overflow
-    // LP work lists: a launch serves only the nodes of list act_cur (those with
-    // a live thread or new delivery records); nodes join list act_cur ^ 1 for
-    // the next window at most once (listed[node] == wid)
-    uint32_t* act;       // [2][R]
-    uint32_t* act_n;     // [2]
-    uint32_t* listed;    // [R]
-    uint32_t act_cur, wid;
-    unsigned long long* prof;  // [P_COUNT] diagnostic build only
-    uint4* trace;        // [trace_cap][R][2] TRACE records (tw_set_trace), replica mode
-    uint32_t trace_cap;
-    // handler stack beyond the record's two frames: [S][R][FXQ] quads (frames 2..)
-    uint4* fx;
-    uint32_t FXQ, max_frames;
-    // BinaryP transmission time (tw_scenario_desc.msg_bytes / link_bw)
-    const uint32_t* msg_bytes;  // [n_kinds] or null
-    const uint64_t* link_bw;    // [L] or null
-    uint32_t tie_mode;          // TW_TIE_*: order of equal-timestamp events
-};
-
-// The key an insertion counter value takes in the queues (equal timestamps pop
-// in key order): FIFO (canonical), reverse (LIFO) or a scrambled bijection.
-// Every mode maps 0 to 0 and nothing else to 0 (wake_seq 0 = not queued).
-__device__ __forceinline__ uint32_t seq_key(uint32_t mode, uint32_t s) {
-    if (mode == TW_TIE_FIFO) return s;
-    if (mode == TW_TIE_LIFO) return 0u - s;
-    uint32_t x = s;  // xorshift-multiply: a bijection of u32 with x(0) = 0
-    x ^= x >> 16; x *= 0x7feb352du; x ^= x >> 15; x *= 0x846ca68bu; x ^= x >> 16;
-    return x;
-}
-// BinaryP transmission time of a message of `kind` over `link` (µs, rounded up)
-__device__ __forceinline__ int64_t tx_us(const Dev& c, uint64_t link, uint32_t kind) {
-    if (!c.msg_bytes || !c.link_bw || kind >= c.n_kinds) return 0;
-    const uint64_t bw = gp(c.link_bw)[link];
-    if (!bw) return 0;
-    return (int64_t)(((uint64_t)gp(c.msg_bytes)[kind] * 1000000ull + bw - 1) / bw);
-}
-
-// LP: node r joins the next window's work list (once per window)
-__device__ __forceinline__ void lp_list_next(const Dev& c, uint32_t r) {
-    if (__hip_atomic_exchange(gp(c.listed) + r, c.wid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != c.wid) {
-        const uint32_t nx = c.act_cur ^ 1u;
-        const uint32_t k = __hip_atomic_fetch_add(gp(c.act_n) + nx, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        gp(c.act)[(size_t)nx * c.R + k] = r;
-    }
-}
-
-// ------------------------------------------------------------------ hashing
-__device__ __forceinline__ uint64_t mix64(uint64_t z) {
-#ifdef TW_X_NOMIX
-        return z;
-#endif
-    z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
-    z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
-    return z ^ (z >> 31);
-}
-// == tw_term of include/timewarp.h
-__device__ __forceinline__ uint64_t term(int64_t t, uint32_t kind, int64_t val) {
-    uint64_t v = val ? mix64((uint64_t)val ^ 0x9e3779b97f4a7c15ull) : 0ull;
-    return mix64((((uint64_t)t << 20) | kind) ^ v);
-}
-__device__ __forceinline__ uint64_t term0(int64_t t, uint32_t kind) { return mix64(((uint64_t)t << 20) | kind); }
-
-__device__ __forceinline__ bool tless(int64_t ta, uint32_t sa, int64_t tb, uint32_t sb) {
-    return ta < tb || (ta == tb && sa < sb);
-}
-__device__ __forceinline__ uint4 ent(int64_t t, uint32_t slot, uint32_t seq) {
-    return make_uint4((uint32_t)t, (uint32_t)((uint64_t)t >> 32), slot, seq);
-}
-__device__ __forceinline__ int64_t ent_t(uint4 e) { return (int64_t)(((uint64_t)e.y << 32) | e.x); }
-
+using namespace tw;
 
 // Cold per-lane words in LDS, [CW_*][TW_WG] u32: the far runs' bookkeeping,
 // the far-heap top, rarely-touched counters and the step's spawn/yield
@@ -2528,7 +2355,7 @@ static int digest(tw_ctx* c, std::vector<uint64_t>& h) {
     return TW_OK;
 }
 
-int tw_tie_audit(tw_ctx* c, uint32_t probes, tw_stats* out) {
+int tw_tie_audit(tw_ctx* c, int64_t t_end_us, uint64_t max_events, uint32_t probes, tw_stats* out) {
     if (!c) return TW_ERR_INVALID;
     if (!c->loaded) return TW_ERR_STATE;
     if (c->lp || probes < 1 || probes > 2) return TW_ERR_INVALID;
@@ -2538,7 +2365,7 @@ int tw_tie_audit(tw_ctx* c, uint32_t probes, tw_stats* out) {
     for (uint32_t p = probes; p + 1 > 0 && rc == TW_OK; --p) {  // probes first, the canonical run last
         c->d.tie_mode = p;
         rc = tw_reset(c);
-        if (rc == TW_OK) rc = tw_run(c, INT64_MAX, UINT64_MAX, p == 0 ? out : nullptr);
+        if (rc == TW_OK) rc = tw_run(c, t_end_us, max_events, p == 0 ? out : nullptr);
         if (rc == TW_OK) rc = digest(c, dg[p]);
         if (p == 0) break;
     }

@@ -75,7 +75,7 @@ def load_library(path: Optional[str] = None):
     lib.tw_lp_results.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t]
     lib.tw_set_trace.argtypes = [C.c_void_p, C.c_uint32]
     lib.tw_read_trace.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_size_t, C.POINTER(C.c_uint64)]
-    lib.tw_tie_audit.argtypes = [C.c_void_p, C.c_uint32, C.POINTER(TwStats)]
+    lib.tw_tie_audit.argtypes = [C.c_void_p, C.c_int64, C.c_uint64, C.c_uint32, C.POINTER(TwStats)]
     lib.tw_set_counter_base.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32]
     lib.tw_geometry.argtypes = [C.c_void_p]
     for name in ("tw_create", "tw_load", "tw_reset", "tw_run", "tw_read_results", "tw_read_hashes", "tw_read_final",
@@ -175,14 +175,15 @@ class Engine:
         _check(self.lib.tw_run(self.ctx, t_end, max_events, C.byref(st)), "tw_run")
         return RunStats(**{f: getattr(st, f) for f, _ in TwStats._fields_ if f != "reserved"})
 
-    def tie_audit(self, probes: int = 2) -> RunStats:
+    def tie_audit(self, probes: int = 2, t_end: int = T_INF, max_events: int = UNLIMITED) -> RunStats:
         """Run every replica under `probes` tie-order probes (reverse and
         scrambled order of equal-timestamp events) and then canonically;
         results()['tie_flags'] bit p marks replicas whose outputs differ under
         probe p (they depend on TimedT's pqueue tie order, TimedT.hs:100-104).
         The canonical run's results stay loaded."""
         st = TwStats()
-        _check(self.lib.tw_tie_audit(self.ctx, int(probes), C.byref(st)), "tw_tie_audit")
+        _check(self.lib.tw_tie_audit(self.ctx, int(t_end), int(max_events), int(probes), C.byref(st)),
+               "tw_tie_audit")
         return RunStats(**{f: getattr(st, f) for f, _ in TwStats._fields_ if f != "reserved"})
 
     def set_counter_base(self, seq0: int, tid0: int = 1) -> "Engine":

@@ -431,14 +431,45 @@ class Code:
         self.mov(scratch, link_reg).addi(scratch, state_base)
         return self.nstorex(r, var, scratch)
 
-    def close_conn(self, link_reg: int, state_base: int, scratch: int = 2, zero: int = 3):
-        """``close addr`` / ``closeR`` (MonadTransfer.hs:139-142, 162-163): the
-        connection's socket goes away, so the next one starts from a fresh
-        ``mkState`` -- the state cell of the link is reset to zeros (clobbers
-        `scratch` and `zero`)."""
-        self.mov(scratch, link_reg).addi(scratch, state_base).seti(zero, 0)
-        for var in range(4):
-            self.nstorex(zero, var, scratch)
+    # Connections (MonadTransfer.hs:114-152).  A link carries one connection at
+    # a time; the sender numbers them: node var `epoch_var` of the sending node
+    # is the current connection's number.  Every message is tagged with it
+    # (payload + epoch * CONN_TAG), and the receiving side's state cell for the
+    # link remembers which connection its state belongs to (cell var 3): a
+    # message of a newer connection finds a fresh ``mkState`` (zeros).  So
+    # ``close`` only ends the connection -- data already in flight still
+    # arrives on the old one, like bytes written before a FIN.
+    CONN_TAG = 1 << 16
+
+    def close_conn(self, epoch_var: int, scratch: int = 3):
+        """``close addr`` (MonadTransfer.hs:139-142): the next send opens a new
+        connection (clobbers `scratch`)."""
+        return self.nload(scratch, epoch_var).addi(scratch, 1).nstore(scratch, epoch_var)
+
+    def conn_tag(self, payload_reg: int, epoch_var: int, scratch: int = 3):
+        """Tag a payload (< CONN_TAG) with the sender's current connection number."""
+        return self.nload(scratch, epoch_var).muli(scratch, self.CONN_TAG).add(payload_reg, scratch)
+
+    def conn_accept(self, state_base: int):
+        """Receiving side of a tagged message in a handler (r0 = tagged payload,
+        r1 = incoming link): if it belongs to a newer connection than the link's
+        state cell, reset the cell (``mkState`` for the accepted socket) and
+        record the connection.  Leaves r0 = r3 = the untagged payload, r1 = the
+        link, r2 = the state cell node."""
+        T = self.CONN_TAG
+        self.mov(2, 1).addi(2, state_base)          # r2 = state cell of the link
+        self.mov(3, 0).modi(3, T)                   # r3 = payload
+        self.sub(0, 3)                              # r0 = connection tag
+        self.nloadx(1, 3, 2)                        # r1 = the cell's connection tag
+        same = self.p.label()
+        self.jeq(1, 0, same)
+        self.nstorex(0, 3, 2)                       # a new connection: record it ...
+        self.seti(1, 0)
+        for var in range(3):                        # ... with a fresh state
+            self.nstorex(1, var, 2)
+        self.bind(same)
+        self.mov(0, 3)                              # r0 = payload
+        self.mov(1, 2).addi(1, -state_base)         # r1 = link
         return self
 
     def trace(self, tag: int, r: int = 0):

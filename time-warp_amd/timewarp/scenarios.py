@@ -443,9 +443,13 @@ def socket_state(n_replicas: int = 1, network_delay=(ms(1), ms(5)), seed_base: i
     ``max_rounds``); the reference draws from the global IO generator, which is
     not reproducible.  Main holds the counts in r1..r3 (``main_regs``).
 
-    ``close_every`` > 0: a client ``close``s its connection after every that
-    many pings and reconnects on the next send (MonadTransfer.hs:139-142), so
-    the server's per-connection counter restarts from a fresh state."""
+    Connections (Code.close_conn / conn_tag / conn_accept): a client tags
+    each Ping with its connection number; ``close`` (MonadTransfer.hs:139-142)
+    ends the connection, and the server's state cell for the link starts from
+    a fresh ``mkState`` when a Ping of a newer connection arrives.  With
+    ``close_every`` > 0 a client closes after every that many pings, so the
+    per-connection counter restarts; the final close (:86-87) changes nothing
+    observable (no later connection)."""
     SRV, SYS, STATE = 0, 4, 5
     p = Program()
     K_PING = p.kind("Ping")
@@ -465,6 +469,7 @@ def socket_state(n_replicas: int = 1, network_delay=(ms(1), ms(5)), seed_base: i
     c.end()
 
     c = p.function("on_ping")                         # \(Ping cid) -> do
+    c.conn_accept(STATE)                              #   (the connection's socket state)
     c.user_state_load(3, 0, 1, STATE)                 #   counter <- userStateR
     c.addi(3, 1)                                      #   reqNo <- counter <+= 1
     c.user_state_store(3, 0, 1, STATE)
@@ -479,17 +484,17 @@ def socket_state(n_replicas: int = 1, network_delay=(ms(1), ms(5)), seed_base: i
     done = c.label()
     c.jeqi(0, 0, done)                                # whileM ruskaRuletka $ do
     c.wait(for_(sec(1)))                              #   wait (for 1 sec)
+    c.node(2).conn_tag(2, 0, scratch=3)               #   (on the current connection)
     c.send(1, K_PING, 2)                              #   send (localhost, 4444) $ Ping cid
     c.addi(0, -1)
     if close_every:
         keep = c.label()
         c.mov(3, 0).modi(3, close_every).jnei(3, 0, keep)
-        c.close_conn(1, STATE, scratch=2, zero=3)     #   close (localhost, 4444): fresh socket next time
-        c.node(2)
+        c.close_conn(0, scratch=3)                    #   close (localhost, 4444): a new socket next time
         c.bind(keep)
     c.jmp(top)
     c.bind(done)
-    c.close_conn(1, STATE, scratch=2, zero=3)         # close (localhost, 4444)
+    c.close_conn(0, scratch=3)                        # close (localhost, 4444)
     c.end()
 
     img = p.finalize()
