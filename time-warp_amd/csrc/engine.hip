@@ -1922,6 +1922,7 @@ struct tw_ctx {
     std::vector<hipEvent_t> ev_pool;
     uint32_t act_n_init[2] = {0, 0};
     std::vector<uint32_t> tie_flags;  // tw_tie_audit, per replica
+    Dev* d_dev = nullptr;             // device copy of d (the wave kernel reads it through the scalar cache)
     uint32_t seq0 = 0, tid0 = 1;      // tw_set_counter_base
 };
 
@@ -2085,6 +2086,7 @@ static int load_common(tw_ctx* c, const tw_scenario_desc* s, bool lp, uint32_t l
         if (g && !strcmp(g, "dense")) geo = 0;
         if (g && !strcmp(g, "sparse")) geo = 1;
         if (g && !strcmp(g, "half")) geo = 2;
+        if (g && !strcmp(g, "wave")) geo = 3;
         if (lp) geo = 0;
         if (geo == 1 && fixed_lds_bytes<TW_WG_SPARSE, TW_NEAR_SPARSE>() + prog_lds > 160 * 1024) geo = 0;
         c->geo = geo;
@@ -2092,8 +2094,10 @@ static int load_common(tw_ctx* c, const tw_scenario_desc* s, bool lp, uint32_t l
     c->lds_bytes = (c->geo == 1 ? fixed_lds_bytes<TW_WG_SPARSE, TW_NEAR_SPARSE>()
                                   : fixed_lds_bytes<TW_WG, TW_NEAR_CAP>()) +
                    prog_lds;
+    if (c->geo == 3) c->lds_bytes = 0;  // the wave kernel reads the program image through the scalar cache
     if (c->lds_bytes > 160 * 1024) { free_all(c); return TW_ERR_INVALID; }  // program + constants must fit in LDS
-    if (c->geo == 1)
+    if (c->geo == 3) {
+    } else if (c->geo == 1)
         HIPCHK(hipFuncSetAttribute((const void*)tw_run_kernel<false, TW_WG_SPARSE, TW_NEAR_SPARSE>,
                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)c->lds_bytes));
     else if (c->geo == 2)
@@ -2120,7 +2124,7 @@ static int load_common(tw_ctx* c, const tw_scenario_desc* s, bool lp, uint32_t l
     ALLOC(d.free_stk, (size_t)d.S * R);
     ALLOC(d.far, (size_t)d.Q * R);
     ALLOC(d.runs, (size_t)(d.Cr ? TW_RUNS * (size_t)d.Cr : 1) * R);
-    ALLOC(d.near_spill, (size_t)(c->geo == 1 ? TW_NEAR_SPARSE : TW_NEAR_CAP) * R);
+    ALLOC(d.near_spill, (size_t)(c->geo == 1 ? TW_NEAR_SPARSE : c->geo == 3 ? wave_spill_entries(d.R) : TW_NEAR_CAP) * R);
     ALLOC(d.dummy, (size_t)5 * R);
     ALLOC(d.nvars, (size_t)d.N * 4 * R);
     ALLOC(d.hash, (size_t)d.N * R);
@@ -2130,6 +2134,7 @@ static int load_common(tw_ctx* c, const tw_scenario_desc* s, bool lp, uint32_t l
     ALLOC(d.link_ord, (size_t)(d.L ? d.L : 1) * (lp ? 1 : R));
     ALLOC(d.tmo_done, (size_t)(d.T ? d.T : 1) * R);
     ALLOC(d.n_active, 1);
+    ALLOC(c->d_dev, 1);
     if (d.FXQ) ALLOC(d.fx, (size_t)d.S * R * d.FXQ);
     uint32_t* mbytes = nullptr;
     uint64_t* lbw = nullptr;
@@ -2279,6 +2284,8 @@ int tw_run(tw_ctx* c, int64_t t_end_us, uint64_t max_events, tw_stats* out) {
             HIPCHK(hipEventRecord(c->ev_pool[2 * i], st));
             if (c->lp)
                 launch_run<true, TW_WG, TW_NEAR_CAP>(c, st, t_end_us, limit, budget);
+            else if (c->geo == 3)
+                HIPCHK(wave_launch(c->d, c->d_dev, st, t_end_us, limit, 1u << 16));
             else if (c->geo == 1)
                 launch_run<false, TW_WG_SPARSE, TW_NEAR_SPARSE>(c, st, t_end_us, limit, budget);
             else if (c->geo == 2)

@@ -188,4 +188,10 @@ __device__ __forceinline__ uint4 ent(int64_t t, uint32_t slot, uint32_t seq) {
 __device__ __forceinline__ int64_t ent_t(uint4 e) { return (int64_t)(((uint64_t)e.y << 32) | e.x); }
 
 
+// wave.hip: the wave-per-replica kernel (geometry TW_GEO_WAVE)
+int wave_near_k(uint32_t R);                // near-queue entries per lane it uses for R replicas
+size_t wave_spill_entries(uint32_t R);      // near-queue spill entries per replica
+hipError_t wave_launch(const Dev& d, const Dev* d_dev, hipStream_t st, int64_t t_end, uint64_t limit,
+                       uint32_t budget);
+
 }  // namespace tw
