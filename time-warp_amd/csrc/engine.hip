@@ -2045,6 +2045,69 @@ static int validate(const tw_scenario_desc* s) {
 
 int tw_reset(tw_ctx* c);
 
+// Batch class of every resume pc for the wave kernel (wave.hip PC_*): what the
+// code a thread runs from that pc until its next yield may touch.
+//   1 (LOCAL)   its own record, its own node's vars / binding / out-links, and
+//               forks (whose records and queue entries the batch commit writes);
+//   2 (DELIVER) LOCAL plus the destination node of a delivery (the deliverer stub);
+//   0 (ALONE)   anything that can reach another thread or another node's state
+//               (throwTo, throw, the watchdog's fire, cross-node vars, in-place
+//               handlers): such an event runs as a batch of one.
+// Events in one batch have equal timestamps, consecutive seqs and disjoint node
+// footprints, so running them side by side commits the same effects as
+// TimedT's one-at-a-time loop (TimedT.hs:239-263).  (Sends go over the sender's
+// own out-links, as every lowered scenario's LINK / RLINK links do.)
+static void classify_pcs(const tw_scenario_desc* s, std::vector<uint8_t>& cls) {
+    const uint32_t n = s->n_insns;
+    cls.assign((size_t)n + 1, 0);
+    bool inline_any = false;
+    for (size_t i = 0; i < (size_t)s->n_listener_sets * s->n_msg_kinds; ++i)
+        if (s->listener_pc[i] != TW_PC_NONE && (s->listener_pc[i] & TW_LPC_INLINE)) inline_any = true;
+    std::vector<uint32_t> seen(n, 0xFFFFFFFFu), stk;
+    for (uint32_t p0 = 0; p0 < n; ++p0) {
+        bool alone = false, dlv = false;
+        stk.assign(1, p0);
+        seen[p0] = p0;
+        while (!stk.empty() && !alone) {
+            const uint32_t q = stk.back();
+            stk.pop_back();
+            const uint32_t op = s->insns[q].w0 & 0xFFu;
+            const uint32_t imm = (uint32_t)s->insns[q].imm;
+            uint32_t nx[2] = {0xFFFFFFFFu, 0xFFFFFFFFu};
+            switch (op) {
+            case TW_OP_THROW_TO: case TW_OP_THROW: case TW_OP_TMO_FIRE: case TW_OP_NLOADX: case TW_OP_NSTOREX:
+                alone = true;
+                break;
+            case TW_OP_END: case TW_OP_WAIT_REL: case TW_OP_WAIT_ABS: case TW_OP_WAIT_REG: case TW_OP_FORK:
+            case TW_OP_TMO_BEGIN:
+                break;  // the step ends here
+            case TW_OP_DELIVER:
+                if (inline_any) alone = true;
+                dlv = true;
+                nx[0] = q + 1;  // undeliverable: the deliverer goes on
+                break;
+            case TW_OP_JMP:
+                nx[0] = imm;
+                break;
+            case TW_OP_JEQ: case TW_OP_JNE: case TW_OP_JLT: case TW_OP_JLE: case TW_OP_JEQI: case TW_OP_JNEI:
+                nx[0] = imm;
+                nx[1] = q + 1;
+                break;
+            default:
+                if (op >= TW_OP_COUNT) alone = true;
+                nx[0] = q + 1;  // (SEND: a dropped message lets the sender go on)
+                break;
+            }
+            for (uint32_t x : nx) {
+                if (x == 0xFFFFFFFFu) continue;
+                if (x >= n) { alone = true; break; }
+                if (seen[x] != p0) { seen[x] = p0; stk.push_back(x); }
+            }
+        }
+        cls[p0] = alone ? 0 : dlv ? 2 : 1;
+    }
+}
+
 static int load_common(tw_ctx* c, const tw_scenario_desc* s, bool lp, uint32_t lp_begin, uint32_t lp_count,
                        int64_t lookahead, uint32_t inbox_cap, uint32_t outbox_cap) {
     if (!c) return TW_ERR_INVALID;
@@ -2187,6 +2250,14 @@ static int load_common(tw_ctx* c, const tw_scenario_desc* s, bool lp, uint32_t l
     }
     d.msg_bytes = mbytes;
     d.link_bw = lbw;
+    if (c->geo == 3) {
+        std::vector<uint8_t> cls;
+        classify_pcs(s, cls);
+        uint8_t* pcl = nullptr;
+        if ((e = dalloc(c, &pcl, cls.size())) != TW_OK) { free_all(c); return e; }
+        HIPCHK(hipMemcpy(pcl, cls.data(), cls.size(), hipMemcpyHostToDevice));
+        d.pc_cls = pcl;
+    }
     d.insns = insns; d.consts = consts; d.lpc = lpc; d.out_off = out_off; d.link_dst = ldst; d.link_rev = lrev;
     d.link_table = ltab;
     c->main_pc = s->main_pc;

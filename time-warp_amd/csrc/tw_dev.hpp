@@ -134,6 +134,7 @@ struct Dev {
     const uint32_t* msg_bytes;  // [n_kinds] or null
     const uint64_t* link_bw;    // [L] or null
     uint32_t tie_mode;          // TW_TIE_*: order of equal-timestamp events
+    const uint8_t* pc_cls;      // [n_insns + 1] wave kernel: batch class of each resume pc (classify_pcs)
 };
 
 // The key an insertion counter value takes in the queues (equal timestamps pop
