@@ -288,6 +288,7 @@ def main():
 
     elapsed = 0.0
     events = sends = 0
+    msg = {"delivered": 0, "dropped": 0, "undeliverable": 0}
     kernel_ms = 0.0
     launches = 0
     for _ in range(args.steps):
@@ -301,6 +302,8 @@ def main():
         elapsed += time.perf_counter() - t0
         events += st.events
         sends += st.sends
+        for k in msg:
+            msg[k] += getattr(st, k)
         print(f"[bench] rank {rank} step: {st.events} events in {(time.perf_counter() - t0) * 1e3:.1f} ms",
               file=sys.stderr, flush=True)
         kernel_ms += float(eng.launch_ms().sum())
@@ -354,6 +357,16 @@ def main():
             },
         }
         out["roofline"]["algorithmic_per_event"] = alg_bytes / max(1, events)
+        # what the timed events are (rank 0, per step): message sends, arrivals
+        # (delivered / dropped / no listener), threads forked, and the rest
+        # (waits, wake-ups, kills, timeouts)
+        per = {k: v // args.steps for k, v in msg.items()}
+        per["sends"] = sends // args.steps
+        per["threads_forked"] = int(res["threads"].sum())
+        per["events"] = events // args.steps
+        arrivals = per["delivered"] + per["dropped"] + per["undeliverable"]
+        per["message_path_frac"] = (per["sends"] + arrivals) / max(1, per["events"])
+        out["events_breakdown"] = per
         mt = measured_traffic(args, launches / args.steps, events / args.steps) if world == 1 else None
         if mt:
             out["roofline"].update(mt)

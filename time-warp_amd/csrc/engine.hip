@@ -57,6 +57,18 @@
 // memory waits.
 #define TW_HALF_LANES 32
 #define TW_STEP_CAP (1u << 22)  // instructions per thread step (== oracle kStepCap)
+// store only the record quads an event changed (1), or the whole record of a
+// thread that stays queued (0, the default).  C3, quad-major records, r02:
+// 1 = 72 B written per event at 17.2 G events/s, 0 = 90 B at 17.8 G (the
+// register compares cost more issue than the bytes save: not HBM-bound)
+#ifndef TW_DIRTY_TAIL
+#define TW_DIRTY_TAIL 0
+#endif
+// store-tail sinks: 8 XCD groups x 4 quads x 256 lanes (record quads), then
+// one 16-B word per replica (the hash atomic's, kept apart: atomics to shared
+// addresses would serialise)
+#define TW_DUMMY_Q (8u * 256u)
+#define TW_DUMMY_REC (4u * TW_DUMMY_Q)
 #define TW_TAIL_VMEM 9          // vector-memory ops of every iteration after the record prefetch
 
 #define P_COUNT 28
@@ -188,6 +200,7 @@ struct Lane {
     static constexpr bool PL = LP || WG < 64;
     Dev c;  // by value: kernel arguments stay in SGPRs
     uint32_t r;       // replica
+    uint4 GAS* dmq;   // this lane's record-store sink (TW_DUMMY_REC quads, stride TW_DUMMY_Q)
     // LDS (lane-offset pointers; element j at [j * WG])
     uint64_t LAS* nk;     // near heap keys: (t - nbase) << 32 | seq; a free position holds ~0
     uint32_t LAS* ns;     // near heap slots
@@ -207,6 +220,9 @@ struct Lane {
     // far sources: heap size, and the cached min over the runs and the heap top
     uint32_t far_n;
     bool far_dirty;
+    // the running thread's frames / pending-exception quad changed this step
+    // (the store tail then writes it; otherwise only the quads that changed)
+    bool q1d;
     int fsrc;  // -1 none, 0..TW_RUNS-1 run, TW_RUNS heap
     int64_t fmt;
     uint32_t fms, fmsl;
@@ -739,10 +755,13 @@ struct Lane {
         th.r2 = (int64_t)(((uint64_t)e.y << 32) | e.x);
         th.r3 = (int64_t)(((uint64_t)e.w << 32) | e.z);
     }
-    __device__ __forceinline__ uint4 GAS* hrec(uint32_t slot) const { return gp(c.slots) + ix(slot) * 4; }
+    // quad 0 of a record; quad q is c.RQ further ([quad][slot][replica]: the 64
+    // lanes' same quad of the same slot is one contiguous 1 KiB, so a wave that
+    // writes only its header quads still writes whole lines)
+    __device__ __forceinline__ uint4 GAS* hrec(uint32_t slot) const { return gp(c.slots) + ix(slot); }
     __device__ __forceinline__ void hbm_load(uint32_t slot, Th& th) const {
         const uint4 GAS* p = hrec(slot);
-        unpack(th, p[0], p[1], p[2], p[3]);
+        unpack(th, p[0], p[c.RQ], p[2 * c.RQ], p[3 * c.RQ]);
     }
     __device__ __forceinline__ void peek_rec(uint32_t slot, Th& th) { hbm_load(slot, th); }
     // mode ST_THROUGH: the full record; ST_DEAD: only the header quad (the tid
@@ -757,47 +776,54 @@ struct Lane {
         STAT(K_PUT_HBM);
         uint4 GAS* p = hrec(slot);
         p[0] = make_uint4(th.w0, th.w1, th.w2, th.w3);
-        p[1] = make_uint4(th.f0, th.f1, th.xl, th.xh);
-        p[2] = make_uint4((uint32_t)th.r0, (uint32_t)((uint64_t)th.r0 >> 32), (uint32_t)th.r1,
-                          (uint32_t)((uint64_t)th.r1 >> 32));
-        p[3] = make_uint4((uint32_t)th.r2, (uint32_t)((uint64_t)th.r2 >> 32), (uint32_t)th.r3,
+        p[c.RQ] = make_uint4(th.f0, th.f1, th.xl, th.xh);
+        p[2 * c.RQ] = make_uint4((uint32_t)th.r0, (uint32_t)((uint64_t)th.r0 >> 32), (uint32_t)th.r1,
+                                 (uint32_t)((uint64_t)th.r1 >> 32));
+        p[3 * c.RQ] = make_uint4((uint32_t)th.r2, (uint32_t)((uint64_t)th.r2 >> 32), (uint32_t)th.r3,
                           (uint32_t)((uint64_t)th.r3 >> 32));
     }
-    // The iteration's stores, issued by every lane in the same shape (lanes
-    // with nothing to store write their dummy sink): the parent's record
-    // (full, or only the header of a thread that ended), the forked child's
-    // record.  With no store skipped by a branch, the compiler's vmcnt
-    // bookkeeping stays exact and the next pop waits only for its prefetch,
-    // not for these stores (vector-memory counters retire in issue order).
+    // The iteration's stores: the same NUMBER of vector-memory instructions on
+    // every path (so the next pop's counted vmcnt wait proves the prefetch
+    // landed without waiting for them), but each lane writes to HBM only what
+    // changed: the header quad of its thread (pc, flags, wake seq), the frames /
+    // exception quad when q1d, each register quad when its registers differ
+    // from the record's, and a forked child's whole record.  A quad with
+    // nothing to write goes to the lane's dummy sink (a few L2-resident lines
+    // per lane), so no store sits behind a branch or an exec mask.
     __device__ __forceinline__ void store_tail(uint32_t slot, Th& th, bool full, bool hdr, uint32_t cslot,
                                                const Th& ch) {
-        const uint4 GAS* dm = gp(c.dummy) + (size_t)r;
-        const size_t R5 = c.R;
-        th.r0 = rf[0]; th.r1 = rf[WG]; th.r2 = rf[2 * WG]; th.r3 = rf[3 * WG];
-        uint4 GAS* pr = hrec(full || hdr ? slot : 0);
-        uint4 GAS* p0 = (full || hdr) ? pr : (uint4 GAS*)dm;
-        uint4 GAS* p1 = full ? pr + 1 : (uint4 GAS*)(dm + R5);
-        uint4 GAS* p2 = full ? pr + 2 : (uint4 GAS*)(dm + 2 * R5);
-        uint4 GAS* p3 = full ? pr + 3 : (uint4 GAS*)(dm + 3 * R5);
-        *p0 = make_uint4(th.w0, th.w1, th.w2, th.w3);
-        *p1 = make_uint4(th.f0, th.f1, th.xl, th.xh);
-        *p2 = make_uint4((uint32_t)th.r0, (uint32_t)((uint64_t)th.r0 >> 32), (uint32_t)th.r1,
-                         (uint32_t)((uint64_t)th.r1 >> 32));
-        *p3 = make_uint4((uint32_t)th.r2, (uint32_t)((uint64_t)th.r2 >> 32), (uint32_t)th.r3,
-                         (uint32_t)((uint64_t)th.r3 >> 32));
+        uint4 GAS* dm = dmq;
+        const size_t R5 = TW_DUMMY_Q;
+        const int64_t n0 = rf[0], n1 = rf[WG], n2 = rf[2 * WG], n3 = rf[3 * WG];
+        const bool w0q = full || hdr;
+#if TW_DIRTY_TAIL
+        const bool w1q = full && q1d;
+        const bool w2q = full && (n0 != th.r0 || n1 != th.r1);
+        const bool w3q = full && (n2 != th.r2 || n3 != th.r3);
+#else
+        const bool w1q = full, w2q = full, w3q = full;
+#endif
+        th.r0 = n0; th.r1 = n1; th.r2 = n2; th.r3 = n3;
+        uint4 GAS* pr = hrec(slot);
+        *(w0q ? pr : dm) = make_uint4(th.w0, th.w1, th.w2, th.w3);
+        *(w1q ? pr + c.RQ : dm + R5) = make_uint4(th.f0, th.f1, th.xl, th.xh);
+        *(w2q ? pr + 2 * c.RQ : dm + 2 * R5) =
+            make_uint4((uint32_t)th.r0, (uint32_t)((uint64_t)th.r0 >> 32), (uint32_t)th.r1,
+                       (uint32_t)((uint64_t)th.r1 >> 32));
+        *(w3q ? pr + 3 * c.RQ : dm + 3 * R5) =
+            make_uint4((uint32_t)th.r2, (uint32_t)((uint64_t)th.r2 >> 32), (uint32_t)th.r3,
+                       (uint32_t)((uint64_t)th.r3 >> 32));
         const bool hc = cslot != 0xFFFFFFFFu;
         uint4 GAS* pc0 = hrec(hc ? cslot : 0);
-        uint4 GAS* c0 = hc ? pc0 : (uint4 GAS*)dm;
-        uint4 GAS* c1 = hc ? pc0 + 1 : (uint4 GAS*)(dm + R5);
-        uint4 GAS* c2 = hc ? pc0 + 2 : (uint4 GAS*)(dm + 2 * R5);
-        uint4 GAS* c3 = hc ? pc0 + 3 : (uint4 GAS*)(dm + 3 * R5);
-        *c0 = make_uint4(ch.w0, ch.w1, ch.w2, ch.w3);
-        *c1 = make_uint4(ch.f0, ch.f1, ch.xl, ch.xh);
-        *c2 = make_uint4((uint32_t)ch.r0, (uint32_t)((uint64_t)ch.r0 >> 32), (uint32_t)ch.r1,
-                         (uint32_t)((uint64_t)ch.r1 >> 32));
-        *c3 = make_uint4((uint32_t)ch.r2, (uint32_t)((uint64_t)ch.r2 >> 32), (uint32_t)ch.r3,
-                         (uint32_t)((uint64_t)ch.r3 >> 32));
-        pf_slot = ((full || hdr) && slot == pf_slot) || (hc && cslot == pf_slot) ? 0xFFFFFFFFu : pf_slot;
+        *(hc ? pc0 : dm) = make_uint4(ch.w0, ch.w1, ch.w2, ch.w3);
+        *(hc ? pc0 + c.RQ : dm + R5) = make_uint4(ch.f0, ch.f1, ch.xl, ch.xh);
+        *(hc ? pc0 + 2 * c.RQ : dm + 2 * R5) =
+            make_uint4((uint32_t)ch.r0, (uint32_t)((uint64_t)ch.r0 >> 32), (uint32_t)ch.r1,
+                       (uint32_t)((uint64_t)ch.r1 >> 32));
+        *(hc ? pc0 + 3 * c.RQ : dm + 3 * R5) =
+            make_uint4((uint32_t)ch.r2, (uint32_t)((uint64_t)ch.r2 >> 32), (uint32_t)ch.r3,
+                       (uint32_t)((uint64_t)ch.r3 >> 32));
+        pf_slot = (w0q && slot == pf_slot) || (hc && cslot == pf_slot) ? 0xFFFFFFFFu : pf_slot;
     }
 
     // Issue the HBM load of the record the next pop will most likely need,
@@ -818,11 +844,11 @@ struct Lane {
         // destination, so each quad gets its own global address instead
         asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(p), "s"(pfs_wave)
                      : "memory", "m0");
-        asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(p + 1),
+        asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(p + c.RQ),
                      "s"(pfs_wave + WG * 16) : "memory", "m0");
-        asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(p + 2),
+        asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(p + 2 * c.RQ),
                      "s"(pfs_wave + 2 * WG * 16) : "memory", "m0");
-        asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(p + 3),
+        asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(p + 3 * c.RQ),
                      "s"(pfs_wave + 3 * WG * 16) : "memory", "m0");
         pf_slot = valid ? s : 0xFFFFFFFFu;
     }
@@ -835,7 +861,7 @@ struct Lane {
         if (slot != pf_slot) {
             STAT(K_PEEK_HBM);
             const uint4 GAS* p = hrec(slot);
-            const uint4 a = p[0], b = p[1], d = p[2], e = p[3];
+            const uint4 a = p[0], b = p[c.RQ], d = p[2 * c.RQ], e = p[3 * c.RQ];
             pfs[0] = a; pfs[WG] = b; pfs[2 * WG] = d; pfs[3 * WG] = e;
         } else {
             STAT(K_PEEK_PF);
@@ -889,7 +915,7 @@ struct Lane {
         const bool h = hacc != 0;
         unsigned long long GAS* p = h ? (LP ? (unsigned long long GAS*)(gp(c.hash_g) + hnode)
                                             : (unsigned long long GAS*)(gp(c.hash) + ix(hnode)))
-                                      : (unsigned long long GAS*)(gp(c.dummy) + (size_t)4 * c.R + r);
+                                      : (unsigned long long GAS*)(gp(c.dummy) + TW_DUMMY_REC + r);
         __hip_atomic_fetch_add(p, (unsigned long long)hacc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         hacc = 0;
     }
@@ -938,7 +964,7 @@ struct Lane {
         if (ts >= c.S) return;
         if (ts == self_slot) {  // the running thread: its record lives in registers
             if (self.w2 != tid) return;
-            if (th_exc(self) == 0) { th_set_exc(self, code); th_set_xval(self, val); }
+            if (th_exc(self) == 0) { th_set_exc(self, code); th_set_xval(self, val); q1d = true; }
             return;
         }
         Th t;
@@ -1225,6 +1251,7 @@ struct Lane {
                 const bool ok = me && !bad;
                 th.f0 = (ok && nf == 0) ? fv : th.f0;
                 th.f1 = (ok && nf == 1) ? fv : th.f1;
+                q1d = q1d || (ok && nf < 2);
                 if (ok && nf >= 2) *fxp(slot, nf) = fv;  // deeper frames: the overflow area
                 th.w0 = ok ? (th.w0 & ~(15u << 16)) | ((nf + 1) << 16) : th.w0;
                 break;
@@ -1497,15 +1524,15 @@ __global__ void __launch_bounds__(TW_WG) tw_init_kernel(Dev c, uint32_t main_pc,
     gp(c.scal)[(size_t)SC_STATUS * c.R + r] = TW_REP_RUNNING;
     gp(c.scal)[(size_t)SC_PENDING_MAIN * c.R + r] = has_main ? 1 : 0;
     gp(c.scal)[(size_t)SC_BUMP * c.R + r] = has_main ? 1 : 0;  // slot 0 = main
-    uint4 GAS* p = gp(c.slots) + (size_t)r * 4;  // slot 0
+    uint4 GAS* p = gp(c.slots) + r;  // slot 0, quad-major (Lane::hrec)
     uint32_t w0 = (main_pc & 0xFFFFu) | (F_MAIN << FL_SHIFT);
     p[0] = make_uint4(w0, main_node, has_main ? 0u : 0xFFFFFFFFu, 0u);
-    p[1] = make_uint4(0u, 0u, 0u, 0u);
+    p[c.RQ] = make_uint4(0u, 0u, 0u, 0u);
     int64_t m[4] = {0, 0, 0, 0};
     if (main_regs && !lp_mode)
         for (int i = 0; i < 4; ++i) m[i] = main_regs[(size_t)r * 4 + i];
-    p[2] = make_uint4((uint32_t)m[0], (uint32_t)((uint64_t)m[0] >> 32), (uint32_t)m[1], (uint32_t)((uint64_t)m[1] >> 32));
-    p[3] = make_uint4((uint32_t)m[2], (uint32_t)((uint64_t)m[2] >> 32), (uint32_t)m[3], (uint32_t)((uint64_t)m[3] >> 32));
+    p[2 * c.RQ] = make_uint4((uint32_t)m[0], (uint32_t)((uint64_t)m[0] >> 32), (uint32_t)m[1], (uint32_t)((uint64_t)m[1] >> 32));
+    p[3 * c.RQ] = make_uint4((uint32_t)m[2], (uint32_t)((uint64_t)m[2] >> 32), (uint32_t)m[3], (uint32_t)((uint64_t)m[3] >> 32));
     if (lp_mode) {
         if (nv_init)
             for (uint32_t i = 0; i < 4; ++i) gp(c.nvars)[(size_t)i * c.R + r] = nv_init[(size_t)g * 4 + i];
@@ -1580,6 +1607,9 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
     Lane<LP, WG, NC> L;
     L.c = c;
     L.r = r;
+    // record sinks shared by the workgroups of one XCD (blocks are dealt to the
+    // 8 XCDs round-robin): a few KiB that stay in that XCD's L2
+    L.dmq = gp(c.dummy) + (size_t)(blockIdx.x & 7u) * 256u + li;
     L.nk = s_k + li;
     L.ns = s_s + li;
     L.rf = s_rf + li;
@@ -1722,6 +1752,7 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
             }
         }
         bool popping = alive && !rare;
+        L.q1d = false;
         {
             // PQ.minView: the min of the near root and the far sources
             if (L.far_dirty) L.far_min();
@@ -1770,6 +1801,7 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
                             const int64_t val = th_xval(th);
                             th_set_exc(th, 0);
                             th.xl = th.xh = 0;
+                            L.q1d = true;
                             L.hacc += term0(t, TW_KIND_EXC | exc);
                             if (!(th_flags(th) & (F_STARTED | F_MAIN))) {  // escapes launchTimedT (:252-263)
                                 L.status = TW_REP_ABORTED;
@@ -2124,6 +2156,7 @@ static int load_common(tw_ctx* c, const tw_scenario_desc* s, bool lp, uint32_t l
     c->lp = lp;
     d.R = lp ? lp_count : s->n_replicas;
     d.S = s->max_slots; d.Q = s->queue_capacity;
+    d.RQ = (uint64_t)d.S * d.R;
     d.N = lp ? 1 : s->n_nodes;  // per-lane node arrays
     d.Ntot = s->n_nodes;
     d.lp0 = lp ? lp_begin : 0;
@@ -2188,7 +2221,7 @@ static int load_common(tw_ctx* c, const tw_scenario_desc* s, bool lp, uint32_t l
     ALLOC(d.far, (size_t)d.Q * R);
     ALLOC(d.runs, (size_t)(d.Cr ? TW_RUNS * (size_t)d.Cr : 1) * R);
     ALLOC(d.near_spill, (size_t)(c->geo == 1 ? TW_NEAR_SPARSE : c->geo == 3 ? wave_spill_entries(d.R) : TW_NEAR_CAP) * R);
-    ALLOC(d.dummy, (size_t)5 * R);
+    ALLOC(d.dummy, (size_t)TW_DUMMY_REC + R);
     ALLOC(d.nvars, (size_t)d.N * 4 * R);
     ALLOC(d.hash, (size_t)d.N * R);
     ALLOC(d.bind, (size_t)d.N * R);

@@ -81,6 +81,7 @@ struct Dev {
     uint32_t R, S, Q, N, L, D, T, Cr;
     uint32_t n_insns, n_consts, n_sets, n_kinds;
     int64_t horizon;
+    uint64_t RQ;         // quad stride of the thread records: S * R (records are [quad][slot][replica])
     // scenario (shared by all replicas)
     const uint2* insns;
     const int64_t* consts;
@@ -97,7 +98,7 @@ struct Dev {
     uint4* far;          // [Q][R]  {t_lo, t_hi, slot, seq}
     uint4* runs;         // [TW_RUNS][Cr][R] monotone FIFO runs (ring buffers)
     uint4* near_spill;   // [NEAR_CAP][R]  near heap between launches
-    uint4* dummy;        // [5][R] per-lane sink of the fixed-shape store tail's unused stores
+    uint4* dummy;        // sinks of the fixed-shape store tail's unused stores (engine.hip TW_DUMMY_*)
     int64_t* nvars;      // [N*4][R]
     uint64_t* hash;      // [N][R]
     uint32_t* bind;      // [N][R] 0 or set+1
@@ -166,9 +167,6 @@ __device__ __forceinline__ void lp_list_next(const Dev& c, uint32_t r) {
 
 // ------------------------------------------------------------------ hashing
 __device__ __forceinline__ uint64_t mix64(uint64_t z) {
-#ifdef TW_X_NOMIX
-        return z;
-#endif
     z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
     z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
     return z ^ (z >> 31);
@@ -188,6 +186,34 @@ __device__ __forceinline__ uint4 ent(int64_t t, uint32_t slot, uint32_t seq) {
 }
 __device__ __forceinline__ int64_t ent_t(uint4 e) { return (int64_t)(((uint64_t)e.y << 32) | e.x); }
 
+
+// Stores by a subset of the lanes WITHOUT a branch: exec is narrowed inside
+// one asm block.  A lane-conditional `if` would make the compiler treat every
+// value merged after it as divergent, and the whole wave-uniform event loop
+// would fall into vector registers under exec masking.  Vector-memory ops
+// complete in issue order, so later loads of the same words see these stores.
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void st32(uint32_t GAS* p, uint32_t v, uint64_t mask = 1) {
+    uint64_t sv;
+    asm volatile("s_mov_b64 %0, exec\n\ts_and_b64 exec, exec, %3\n\tglobal_store_dword %1, %2, off\n\t"
+                 "s_mov_b64 exec, %0" : "=&s"(sv) : "v"(p), "v"(v), "s"(mask) : "memory");
+}
+__device__ __forceinline__ void st128(uint4 GAS* p, uint4 v, uint64_t mask = 1) {
+    uint64_t sv;
+    const u32x4 d = {v.x, v.y, v.z, v.w};
+    asm volatile("s_mov_b64 %0, exec\n\ts_and_b64 exec, exec, %3\n\tglobal_store_dwordx4 %1, %2, off\n\t"
+                 "s_mov_b64 exec, %0" : "=&s"(sv) : "v"(p), "v"(d), "s"(mask) : "memory");
+}
+__device__ __forceinline__ void st8(uint8_t GAS* p, uint32_t v, uint64_t mask = 1) {
+    uint64_t sv;
+    asm volatile("s_mov_b64 %0, exec\n\ts_and_b64 exec, exec, %3\n\tglobal_store_byte %1, %2, off\n\t"
+                 "s_mov_b64 exec, %0" : "=&s"(sv) : "v"(p), "v"(v), "s"(mask) : "memory");
+}
+__device__ __forceinline__ void atom_add64(unsigned long long GAS* p, uint64_t v, uint64_t mask = 1) {
+    uint64_t sv;
+    asm volatile("s_mov_b64 %0, exec\n\ts_and_b64 exec, exec, %3\n\tglobal_atomic_add_x2 %1, %2, off\n\t"
+                 "s_mov_b64 exec, %0" : "=&s"(sv) : "v"(p), "v"(v), "s"(mask) : "memory");
+}
 
 // wave.hip: the wave-per-replica kernel (geometry TW_GEO_WAVE)
 int wave_near_k(uint32_t R);                // near-queue entries per lane it uses for R replicas

@@ -85,40 +85,6 @@ __device__ __forceinline__ uint64_t wave_min64(uint64_t v) {
     return m3 < m ? m3 : m;
 }
 
-// Stores by a subset of the lanes WITHOUT a branch: exec is narrowed inside
-// one asm block.  A lane-conditional `if` would make the compiler treat every
-// value merged after it as divergent, and the whole wave-uniform event loop
-// would fall into vector registers under exec masking.  Vector-memory ops
-// complete in issue order, so later loads of the same words see these stores.
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ void st32(uint32_t GAS* p, uint32_t v, uint64_t mask = 1) {
-    uint64_t sv;
-    asm volatile("s_mov_b64 %0, exec\n\ts_and_b64 exec, exec, %3\n\tglobal_store_dword %1, %2, off\n\t"
-                 "s_mov_b64 exec, %0" : "=&s"(sv) : "v"(p), "v"(v), "s"(mask) : "memory");
-}
-__device__ __forceinline__ void st64(uint64_t GAS* p, uint64_t v, uint64_t mask = 1) {
-    uint64_t sv;
-    asm volatile("s_mov_b64 %0, exec\n\ts_and_b64 exec, exec, %3\n\tglobal_store_dwordx2 %1, %2, off\n\t"
-                 "s_mov_b64 exec, %0" : "=&s"(sv) : "v"(p), "v"(v), "s"(mask) : "memory");
-}
-__device__ __forceinline__ void st128(uint4 GAS* p, uint4 v, uint64_t mask = 1) {
-    uint64_t sv;
-    const u32x4 d = {v.x, v.y, v.z, v.w};
-    asm volatile("s_mov_b64 %0, exec\n\ts_and_b64 exec, exec, %3\n\tglobal_store_dwordx4 %1, %2, off\n\t"
-                 "s_mov_b64 exec, %0" : "=&s"(sv) : "v"(p), "v"(d), "s"(mask) : "memory");
-}
-__device__ __forceinline__ void st8(uint8_t GAS* p, uint32_t v, uint64_t mask = 1) {
-    uint64_t sv;
-    asm volatile("s_mov_b64 %0, exec\n\ts_and_b64 exec, exec, %3\n\tglobal_store_byte %1, %2, off\n\t"
-                 "s_mov_b64 exec, %0" : "=&s"(sv) : "v"(p), "v"(v), "s"(mask) : "memory");
-}
-__device__ __forceinline__ void atom_add64(unsigned long long GAS* p, uint64_t v, uint64_t mask = 1) {
-    uint64_t sv;
-    asm volatile("s_mov_b64 %0, exec\n\ts_and_b64 exec, exec, %3\n\tglobal_atomic_add_x2 %1, %2, off\n\t"
-                 "s_mov_b64 exec, %0" : "=&s"(sv) : "v"(p), "v"(v), "s"(mask) : "memory");
-}
-__device__ __forceinline__ void st_i64(int64_t GAS* p, int64_t v) { st64((uint64_t GAS*)p, (uint64_t)v); }
-
 // Read-only tables (program image, constants, topology): constant address
 // space, so uniform-address reads become scalar loads.
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -144,9 +110,9 @@ struct URec {
         r0 = i == 0 ? v : r0; r1 = i == 1 ? v : r1; r2 = i == 2 ? v : r2; r3 = i == 3 ? v : r3;
     }
 };
-__device__ __forceinline__ void urec_load(const uint4 GAS* p, URec& t) {
-    // lanes 0..3 fetch one quad each (one 64-B request); readlane to scalars
-    const uint4 q = p[__lane_id() & 3u];
+__device__ __forceinline__ void urec_load(const uint4 GAS* p, uint64_t qs, URec& t) {
+    // lanes 0..3 fetch one quad each (records are quad-major: stride qs); readlane to scalars
+    const uint4 q = p[(__lane_id() & 3u) * qs];
     t.w0 = rdl(q.x, 0); t.w1 = rdl(q.y, 0); t.w2 = rdl(q.z, 0); t.w3 = rdl(q.w, 0);
     t.f0 = rdl(q.x, 1); t.f1 = rdl(q.y, 1); t.xl = rdl(q.z, 1); t.xh = rdl(q.w, 1);
     t.r0 = (int64_t)(((uint64_t)rdl(q.y, 2) << 32) | rdl(q.x, 2));
@@ -155,21 +121,17 @@ __device__ __forceinline__ void urec_load(const uint4 GAS* p, URec& t) {
     t.r3 = (int64_t)(((uint64_t)rdl(q.w, 3) << 32) | rdl(q.z, 3));
 }
 // store quads [q0, q1) of the record (lanes q0..q1-1, one request)
-__device__ __forceinline__ void urec_store(uint4 GAS* p, const URec& t, uint32_t q0, uint32_t q1) {
+__device__ __forceinline__ void urec_store(uint4 GAS* p, uint64_t qs, const URec& t, uint32_t q0, uint32_t q1) {
     const uint32_t l = __lane_id() & 3u;
     const bool a = l == 0, b = l == 1, c = l == 2;
     const uint4 q = make_uint4(a ? t.w0 : b ? t.f0 : c ? (uint32_t)t.r0 : (uint32_t)t.r2,
                                a ? t.w1 : b ? t.f1 : c ? (uint32_t)((uint64_t)t.r0 >> 32) : (uint32_t)((uint64_t)t.r2 >> 32),
                                a ? t.w2 : b ? t.xl : c ? (uint32_t)t.r1 : (uint32_t)t.r3,
                                a ? t.w3 : b ? t.xh : c ? (uint32_t)((uint64_t)t.r1 >> 32) : (uint32_t)((uint64_t)t.r3 >> 32));
-    st128(p + l, q, ((1ull << q1) - 1) & ~((1ull << q0) - 1));
+    st128(p + l * qs, q, ((1ull << q1) - 1) & ~((1ull << q0) - 1));
 }
-__device__ __forceinline__ uint32_t u_pc(const URec& t) { return t.w0 & 0xFFFFu; }
-__device__ __forceinline__ uint32_t u_nfr(const URec& t) { return (t.w0 >> 16) & 15u; }
 __device__ __forceinline__ uint32_t u_flags(const URec& t) { return (t.w0 >> FL_SHIFT) & 0x3Fu; }
 __device__ __forceinline__ uint32_t u_exc(const URec& t) { return t.w0 >> EXC_SHIFT; }
-__device__ __forceinline__ void u_set_pc(URec& t, uint32_t pc) { t.w0 = (t.w0 & 0xFFFF0000u) | (pc & 0xFFFFu); }
-__device__ __forceinline__ void u_set_nfr(URec& t, uint32_t n) { t.w0 = (t.w0 & ~(15u << 16)) | (n << 16); }
 __device__ __forceinline__ void u_set_exc(URec& t, uint32_t c) {
     t.w0 = (t.w0 & ((1u << EXC_SHIFT) - 1u)) | (c << EXC_SHIFT);
 }
@@ -462,7 +424,7 @@ struct Wave {
     }
 
     // ----------------------------------------------------- thread records
-    __device__ __forceinline__ uint4 GAS* hrec(uint32_t slot) const { return gp(dv->slots) + ix(slot) * 4; }
+    __device__ __forceinline__ uint4 GAS* hrec(uint32_t slot) const { return gp(dv->slots) + ix(slot); }
     __device__ __forceinline__ uint32_t alloc_slot() {
         if (free_n) {
             const uint32_t s = ftop;
@@ -497,7 +459,7 @@ struct Wave {
         const uint32_t ts = (uint32_t)ref, tid = (uint32_t)((uint64_t)ref >> 32);
         if (ts >= dv->S) return;
         URec t;
-        urec_load(hrec(ts), t);
+        urec_load(hrec(ts), dv->RQ, t);
         if (t.w2 != tid) return;  // dead: the map entry is unobservable
         if (t.w3 != 0) {
             bool on_chip = (u_flags(t) & F_NEARQ) != 0;
@@ -515,7 +477,7 @@ struct Wave {
             t.xl = (uint32_t)val;
             t.xh = (uint32_t)((uint64_t)val >> 32);
         }
-        urec_store(hrec(ts), t, 0, 2);
+        urec_store(hrec(ts), dv->RQ, t, 0, 2);
     }
     // (uniform) pop the global minimum (near or far); false if none
     __device__ __forceinline__ bool peek_min(int64_t& t, uint32_t& sq, int& src) {
@@ -562,22 +524,23 @@ struct LRec {
     __device__ __forceinline__ void set_nfr(uint32_t n) { w0 = (w0 & ~(15u << 16)) | (n << 16); }
     __device__ __forceinline__ void set_exc(uint32_t c) { w0 = (w0 & ((1u << EXC_SHIFT) - 1u)) | (c << EXC_SHIFT); }
 };
-__device__ __forceinline__ void lrec_load(const uint4 GAS* p, LRec& t) {
-    const uint4 a = p[0], b = p[1], d = p[2], e = p[3];
+__device__ __forceinline__ void lrec_load(const uint4 GAS* p, uint64_t qs, LRec& t) {
+    const uint4 a = p[0], b = p[qs], d = p[2 * qs], e = p[3 * qs];
     t.w0 = a.x; t.w1 = a.y; t.w2 = a.z; t.w3 = a.w;
     t.f0 = b.x; t.f1 = b.y; t.xl = b.z; t.xh = b.w;
     t.r0 = (int64_t)(((uint64_t)d.y << 32) | d.x); t.r1 = (int64_t)(((uint64_t)d.w << 32) | d.z);
     t.r2 = (int64_t)(((uint64_t)e.y << 32) | e.x); t.r3 = (int64_t)(((uint64_t)e.w << 32) | e.z);
 }
 // the lanes of `mask` store quads [q0, q1) of their records (one instruction per quad)
-__device__ __forceinline__ void lrec_store(uint4 GAS* p, const LRec& t, uint64_t mask, uint32_t q0, uint32_t q1) {
+__device__ __forceinline__ void lrec_store(uint4 GAS* p, uint64_t qs, const LRec& t, uint64_t mask, uint32_t q0,
+                                           uint32_t q1) {
     if (q0 <= 0 && 0 < q1) st128(p, make_uint4(t.w0, t.w1, t.w2, t.w3), mask);
-    if (q0 <= 1 && 1 < q1) st128(p + 1, make_uint4(t.f0, t.f1, t.xl, t.xh), mask);
+    if (q0 <= 1 && 1 < q1) st128(p + qs, make_uint4(t.f0, t.f1, t.xl, t.xh), mask);
     if (q0 <= 2 && 2 < q1)
-        st128(p + 2, make_uint4((uint32_t)t.r0, (uint32_t)((uint64_t)t.r0 >> 32), (uint32_t)t.r1,
+        st128(p + 2 * qs, make_uint4((uint32_t)t.r0, (uint32_t)((uint64_t)t.r0 >> 32), (uint32_t)t.r1,
                                 (uint32_t)((uint64_t)t.r1 >> 32)), mask);
     if (q0 <= 3 && 3 < q1)
-        st128(p + 3, make_uint4((uint32_t)t.r2, (uint32_t)((uint64_t)t.r2 >> 32), (uint32_t)t.r3,
+        st128(p + 3 * qs, make_uint4((uint32_t)t.r2, (uint32_t)((uint64_t)t.r2 >> 32), (uint32_t)t.r3,
                                 (uint32_t)((uint64_t)t.r3 >> 32)), mask);
 }
 
@@ -611,7 +574,7 @@ struct LaneCtx {
     uint32_t tmo0, trn0;       // counters before the batch (singletons read them)
     uint32_t GAS* thr_n;       // deferred throws (singletons): LDS list
     __device__ __forceinline__ size_t ix(size_t i) const { return i * dv->R + r; }
-    __device__ __forceinline__ uint4 GAS* hrec(uint32_t slot) const { return gp(dv->slots) + ix(slot) * 4; }
+    __device__ __forceinline__ uint4 GAS* hrec(uint32_t slot) const { return gp(dv->slots) + ix(slot); }
     __device__ __forceinline__ uint32_t GAS* fxp(uint32_t slot, uint32_t i) const {
         return (uint32_t GAS*)(gp(dv->fx) + ((size_t)slot * dv->R + r) * dv->FXQ) + (i - 2);
     }
@@ -1006,7 +969,7 @@ __global__ void __launch_bounds__(64) tw_wave_kernel(const Dev* dptr, int64_t t_
         const bool cand = lane < n;
         // ---- 2. records, liveness, class, footprint (loads for every lane: no branch)
         LRec th;
-        lrec_load(W.hrec(cand ? cslot : 0u), th);
+        lrec_load(W.hrec(cand ? cslot : 0u), dv->RQ, th);
         const bool live_ev = cand && (is_main || th.w3 == csq);  // else superseded by a throwTo re-stamp
         uint32_t cls = PC_LOCAL, fnode2 = 0xFFFFFFFFu;
         {
@@ -1200,13 +1163,13 @@ __global__ void __launch_bounds__(64) tw_wave_kernel(const Dev* dptr, int64_t t_
             ch.w1 = e.cnode; ch.w2 = tid; ch.w3 = ckey;
             ch.f0 = ch.f1 = ch.xl = ch.xh = 0;
             ch.r0 = e.q0; ch.r1 = e.q1; ch.r2 = e.q2; ch.r3 = e.q3;
-            lrec_store(W.hrec(sp ? csl : 0u), ch, spm, 0, 4);
+            lrec_store(W.hrec(sp ? csl : 0u), dv->RQ, ch, spm, 0, 4);
             const uint64_t fullm = __builtin_amdgcn_ballot_w64(cm && (yl || e.fin == W_STOP));
-            lrec_store(W.hrec(cslot), th, fullm, 0, 4);
+            lrec_store(W.hrec(cslot), dv->RQ, th, fullm, 0, 4);
             const bool ends = cm && (e.fin == W_EXIT || e.fin == W_DIED);
             if (cm && e.fin == W_EXIT) X.die(th, e);
             const uint64_t endm = __builtin_amdgcn_ballot_w64(ends);
-            lrec_store(W.hrec(cslot), th, endm, 0, 1);
+            lrec_store(W.hrec(cslot), dv->RQ, th, endm, 0, 1);
             uint64_t fm = endm;
             while (fm) {
                 const uint32_t l = (uint32_t)__builtin_ctzll(fm);

@@ -32,9 +32,11 @@ for s in "$@"; do
     benchq_c2) step benchq_c2 300 python bench.py --config ping_pong --steps 2 --warmup 1 --no-cpu-baseline ;;
     geo=*) export TW_GEOMETRY=${s#geo=}; SFX=_${s#geo=} ;;
     pytest_geo) step pytest_geo 600 python -u -m pytest tests/ -q -m gpu -x --timeout 120 --timeout-method thread -k "$TW_GEOMETRY" ;;
+    lib=default) unset TW_LIB; SFX="" ;;
     lib=*) export TW_LIB=$PWD/time-warp_amd/lib/libtimewarp_${s#lib=}.so; SFX=_${s#lib=} ;;
     pmcq_c3_8k) bash tools/pmc_passes.sh gpurun_out/pmcq_c3_8k$SFX --replicas 8192 > gpurun_out/pmcq_c3_8k$SFX.log 2>&1; rc=$?; echo "pmcq_c3_8k=$rc"; [ $rc -eq 0 ] || exit $rc ;;
     pmcq_c3) bash tools/pmc_passes.sh gpurun_out/pmcq_c3$SFX > gpurun_out/pmcq_c3$SFX.log 2>&1; rc=$?; echo "pmcq_c3=$rc"; [ $rc -eq 0 ] || exit $rc ;;
+    pmct_c3) PMC_SET=traffic bash tools/pmc_passes.sh gpurun_out/pmct_c3$SFX > gpurun_out/pmct_c3$SFX.log 2>&1; rc=$?; echo "pmct_c3=$rc"; [ $rc -eq 0 ] || exit $rc ;;
     pmc) bash tools/pmc.sh gpurun_out/pmc$SFX > gpurun_out/pmc$SFX.log 2>&1; rc=$?; echo "pmc=$rc"; [ $rc -eq 0 ] || exit $rc ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac

@@ -1,13 +1,15 @@
 #!/bin/bash
-# Two quick PMC passes (instruction mix, wait/issue cycles) over a 1-step bench
+# Two quick PMC passes (instruction mix, wait/issue cycles; PMC_SET=traffic:
+# FETCH_SIZE and WRITE_SIZE) over a 1-step bench
 # run; prints per-dispatch sums for the event kernels.
 # usage: tools/pmc_passes.sh OUTDIR [bench args...]   (env TW_GEOMETRY etc. pass through)
 OUT=$1; shift
 mkdir -p $OUT
 export TMPDIR=/tmp
 i=0
-for P in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVE_CYCLES" \
-         "SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_BRANCH SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA SQ_BUSY_CYCLES GRBM_GUI_ACTIVE"; do
+if [ "$PMC_SET" = traffic ]; then SETS=("FETCH_SIZE" "WRITE_SIZE"); else SETS=("SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVE_CYCLES" \
+         "SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_BRANCH SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA SQ_BUSY_CYCLES GRBM_GUI_ACTIVE"); fi
+for P in "${SETS[@]}"; do
   i=$((i+1))
   timeout -s KILL 240 rocprofv3 --pmc $P --kernel-trace --output-format csv -d $OUT/q$i -o run -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline "$@" > $OUT/q$i.log 2>&1
   rc=$?
