@@ -373,6 +373,56 @@ int tw_lp_inject(tw_ctx* ctx, const tw_lp_record* recs, size_t n, int64_t* next_
  * the scenario's hashes are the sum over contexts mod 2^64). */
 int tw_lp_results(tw_ctx* ctx, tw_replica_result* agg, uint64_t* node_hashes, size_t n_nodes);
 
+/* ---- device-driven windows (no host round trip per window)
+ * The window loop above costs several host synchronisations per window.  Here
+ * the device keeps the window start T, the work lists and the window count,
+ * and advances T itself.  One "tick" is: the event kernel over window
+ * [T, T + lookahead), the local delivery of this context's records, and the
+ * packing of foreign records into fixed per-rank blocks; then, between
+ * ranks, an all-to-all of those blocks and an all-reduce(min) of two int64
+ * words; then the advance: when no rank has work left in the window, T := the
+ * global next-event time (INT64_MAX: done), else the same window runs again.
+ * Records are drained into node queues only at a window's first tick, so the
+ * result does not depend on how many ticks a window took.  Every kernel goes
+ * on the context's stream (tw_set_stream: the caller's, e.g. the stream its
+ * RCCL collectives run on), so a caller enqueues many ticks and synchronises
+ * once (tw_lp_progress).  Replaces the MonadDialog send path's cross-node hop
+ * (MonadDialog.hs:149-166) with an on-device exchange.
+ *
+ * Block layout (send and recv, world blocks of (cap + 1) tw_lp_records):
+ * record 0 of block g is a header whose first uint32 is the record count, then
+ * up to cap records.  red: 2 device int64 {next event time, -(lanes active)},
+ * all-reduced with MIN between tw_lp_tick_import and tw_lp_tick_end. */
+typedef struct tw_lp_state {
+    uint64_t windows;   /* windows completed                                 */
+    uint64_t ticks;     /* ticks run (>= windows)                            */
+    int64_t  t;         /* current window start (INT64_MAX when done)        */
+    uint32_t done;      /* 1: every queue is empty everywhere                */
+    uint32_t err;       /* inbox / outbox / exchange-block overflow bits     */
+} tw_lp_state;
+/* Use the caller's HIP stream (hipStream_t) for every later call; NULL = the
+ * context's own stream. */
+int tw_set_stream(tw_ctx* ctx, void* hip_stream);
+/* world == 1: send/recv/red may be NULL (the context keeps its own red).
+ * starts: host array of world + 1 node boundaries (rank g owns nodes
+ * [starts[g], starts[g+1])).  send/recv: device buffers of
+ * world * (cap + 1) * 32 bytes; red: device int64[2]. */
+int tw_lp_exchange_setup(tw_ctx* ctx, uint32_t world, uint32_t rank, const uint32_t* starts, void* send,
+                         void* recv, uint32_t cap, int64_t* red);
+/* Start the device loop at T = 0 (after tw_reset). */
+int tw_lp_loop_begin(tw_ctx* ctx);
+/* Enqueue a tick's first half: event kernel + local delivery + packing. */
+int tw_lp_tick(tw_ctx* ctx);
+/* After the all-to-all: deliver recv's records; fill red. */
+int tw_lp_tick_import(tw_ctx* ctx);
+/* After the all-reduce of red: advance the window or rerun it. */
+int tw_lp_tick_end(tw_ctx* ctx);
+/* Synchronise the stream once and read the loop's state. */
+int tw_lp_progress(tw_ctx* ctx, tw_lp_state* out);
+/* Single context (world 1): enqueue ticks in batches of 16 with one host
+ * synchronisation per batch until done or max_ticks. */
+int tw_lp_run_windows(tw_ctx* ctx, uint64_t max_ticks, tw_lp_state* out);
+
 /* ---------------------------------------------------------------- hashing
  * Per-node trace hash (made fully commutative): every
  * committed event / trace / delivery at node n adds term(t, kind, val) to

@@ -12,6 +12,7 @@ pytestmark = pytest.mark.gpu
 FIELDS = ["final_t", "events", "delivered", "dropped", "undeliverable", "status", "main_exc", "threads"]
 
 
+@pytest.mark.one_geometry  # LP mode: the replica geometries do not apply
 @pytest.mark.parametrize("n,parts,drop", [(64, 1, 0), (1000, 1, 0), (1000, 4, 0), (5000, 3, 4), (50000, 8, 0)])
 def test_gossip_partitioned_equals_oracle(engine_mod, oracle_mod, n, parts, drop):
     scn = scenarios.gossip(n, drop_log2=drop, seed=n)
@@ -23,6 +24,7 @@ def test_gossip_partitioned_equals_oracle(engine_mod, oracle_mod, n, parts, drop
     assert windows > 1
 
 
+@pytest.mark.one_geometry  # LP mode: the replica geometries do not apply
 @pytest.mark.parametrize("parts", [1, 4])
 def test_gossip_inline_handlers_partitioned(engine_mod, oracle_mod, parts):
     """In-place handler dispatch (MonadDialog.hs:114-117) on the LP engine: the
@@ -45,6 +47,7 @@ def test_gossip_replica_engine(engine_mod, oracle_mod):
     assert np.array_equal(h[0], o.hashes)
 
 
+@pytest.mark.one_geometry  # LP mode: the replica geometries do not apply
 def test_lookahead_violation_is_an_error(engine_mod):
     """token-ring's observer links have 0 µs delay (examples/token-ring/Main.hs:75-76):
     no conservative window exists, and the LP engine must say so instead of
@@ -54,3 +57,20 @@ def test_lookahead_violation_is_an_error(engine_mod):
     scn = scenarios.token_ring(n_nodes=8, n_replicas=1, launch_duration=20_000_000)
     agg, hashes, windows = engine_mod.run_partitioned(scn, parts=2, lookahead_us=1000, max_windows=100000)
     assert int(agg["status"]) == isa.REP_ERR_INSN
+
+
+@pytest.mark.one_geometry
+@pytest.mark.parametrize("n,parts,drop", [(1000, 1, 0), (5000, 3, 4), (50000, 8, 0)])
+def test_gossip_device_windows_equal_oracle(engine_mod, oracle_mod, n, parts, drop):
+    """The device-driven window loop (tw_lp_tick / tw_lp_run_windows: the
+    window start, the work lists and the record exchange stay on the device)
+    gives the sequential oracle's counters and node hashes, and runs the same
+    windows as the host-driven loop."""
+    scn = scenarios.gossip(n, drop_log2=drop, seed=n)
+    agg, hashes, windows, ticks = engine_mod.run_partitioned_device(scn, parts=parts)
+    o = oracle_mod.run(scn, trace_cap=0)
+    for f in FIELDS:
+        assert int(agg[f]) == int(o.result[f]), (f, int(agg[f]), o.result[f])
+    assert np.array_equal(hashes, o.hashes)
+    _, _, host_windows = engine_mod.run_partitioned(scn, parts=parts)
+    assert windows == host_windows and ticks >= windows

@@ -1568,6 +1568,20 @@ __host__ __device__ constexpr size_t fixed_lds_bytes() {
 template <bool LP, int WG, int NC, int TPW = 64>
 __global__ void __launch_bounds__(WG * 64 / TPW) __attribute__((amdgpu_waves_per_eu((WG * 64 / TPW + 255) / 256, 2)))
 tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
+    // device-driven windows: the window, its work list and whether this is the
+    // window's first tick (the only one that drains inboxes) come from the device
+    bool fresh = true;
+    if (LP && c.win) {
+        const int64_t GAS* w = gp(c.win);
+        const int64_t fl = w[WN_FLAGS];
+        if (fl & WN_DONE) return;
+        t_end = w[WN_T] + w[WN_L] - 1;
+        c.act_cur = (uint32_t)w[WN_ACT];
+        c.wid = (uint32_t)w[WN_WID];
+        fresh = (fl & WN_FRESH) != 0;
+    }
+    // LP: workgroups past the window's work list leave before staging the program
+    if (LP && blockIdx.x * WG >= gp(c.act_n)[c.act_cur]) return;
     extern __shared__ __attribute__((aligned(16))) uint64_t lds_raw[];
     uint4 LAS* s_pf = (uint4 LAS*)lds_raw;
     uint4 LAS* s_rq = s_pf + 5 * WG;
@@ -1602,7 +1616,7 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
     // LP: a node with no live thread and an empty inbox has nothing to do in
     // this window (every live thread holds its one queued event; a superseded
     // entry left behind pops without effect whenever the node wakes again)
-    if (LP && sc[SC_LIVE * R] == 0 && sc[SC_PENDING_MAIN * R] == 0 && gp(c.inbox_n)[r] == 0) return;
+    if (LP && sc[SC_LIVE * R] == 0 && sc[SC_PENDING_MAIN * R] == 0 && (!fresh || gp(c.inbox_n)[r] == 0)) return;
 
     Lane<LP, WG, NC> L;
     L.c = c;
@@ -1673,7 +1687,7 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
         L.push_far(ent_t(e), e.w, e.z);  // the thread's F_NEARQ hint only speeds up throwTo
     }
 
-    if (LP) {
+    if (LP && fresh) {
         // delivery records addressed to this node become phantom deliverer
         // threads, inserted in (t, link, payload, src) order so queue seqs are
         // deterministic whatever order the records arrived in
@@ -1881,9 +1895,25 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
 }
 
 
+// A delivery record for local node dst: claim an inbox slot (the drain at the
+// window's first tick sorts them), lower *tmin to its time, list the node for
+// the next window.
+__device__ __forceinline__ void lp_deliver(const Dev& c, uint4 a, uint4 b, uint64_t GAS* tmin) {
+    const uint32_t lp = b.w - c.lp0;
+    const uint32_t k = __hip_atomic_fetch_add(gp(c.inbox_n) + lp, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (k >= c.IB) {
+        __hip_atomic_fetch_or(gp(c.lp_err), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return;
+    }
+    uint4 GAS* q = gp(c.inbox) + ((size_t)k * c.R + lp) * 2;
+    q[0] = a;
+    q[1] = b;
+    __hip_atomic_fetch_min(tmin, (uint64_t)ent_t(a), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    lp_list_next(c, lp);
+}
+
 // Delivery records -> inboxes of local nodes (or the foreign buffer for the
-// host exchange).  One thread per record; the per-node inbox slot is claimed
-// with an atomic, and the drain at the next window start sorts them.
+// host exchange).  One thread per record.
 __global__ void __launch_bounds__(256) tw_lp_scatter(Dev c, const uint4* recs, uint32_t n, uint4* foreign,
                                                      uint32_t* n_foreign, uint32_t foreign_cap) {
     uint32_t i = blockIdx.x * 256 + threadIdx.x;
@@ -1891,18 +1921,7 @@ __global__ void __launch_bounds__(256) tw_lp_scatter(Dev c, const uint4* recs, u
     uint4 a = gp(recs)[(size_t)i * 2], b = gp(recs)[(size_t)i * 2 + 1];
     uint32_t dst = b.w;
     if (dst >= c.lp0 && dst < c.lp0 + c.R) {
-        uint32_t lp = dst - c.lp0;
-        uint32_t k = __hip_atomic_fetch_add(gp(c.inbox_n) + lp, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (k >= c.IB) {
-            __hip_atomic_fetch_or(gp(c.lp_err), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            return;
-        }
-        uint4 GAS* q = gp(c.inbox) + ((size_t)k * c.R + lp) * 2;
-        q[0] = a;
-        q[1] = b;
-        int64_t ta = ent_t(a);
-        __hip_atomic_fetch_min(gp(c.next_t), (uint64_t)ta, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        lp_list_next(c, lp);
+        lp_deliver(c, a, b, gp(c.next_t));
     } else if (foreign) {
         uint32_t k = __hip_atomic_fetch_add(gp(n_foreign), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (k >= foreign_cap) {
@@ -1914,6 +1933,125 @@ __global__ void __launch_bounds__(256) tw_lp_scatter(Dev c, const uint4* recs, u
     } else {
         __hip_atomic_fetch_or(gp(c.lp_err), 4u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
+}
+
+// ---- device-driven windows (tw_lp_tick / tw_lp_tick_import / tw_lp_tick_end)
+// The window's state is read from c.win by every kernel; a finished loop makes
+// them all return at once.
+__device__ __forceinline__ bool win_enter(Dev& c) {
+    const int64_t GAS* w = gp(c.win);
+    if (w[WN_FLAGS] & WN_DONE) return false;
+    c.act_cur = (uint32_t)w[WN_ACT];
+    c.wid = (uint32_t)w[WN_WID];
+    return true;
+}
+// this tick's records: local ones into inboxes, foreign ones into the send
+// block of their owner rank (starts[g] <= dst < starts[g + 1])
+__global__ void __launch_bounds__(256) tw_lp_pack(Dev c, uint4* send, const uint32_t* starts, uint32_t world,
+                                                  uint32_t cap) {
+    if (!win_enter(c)) return;
+    uint32_t n = *gp(c.out_n);
+    n = n < c.out_cap ? n : c.out_cap;
+    uint64_t GAS* tmin = (uint64_t GAS*)(gp(c.win) + WN_REC_MIN);
+    for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
+        const uint4 a = gp(c.outbox)[(size_t)i * 2], b = gp(c.outbox)[(size_t)i * 2 + 1];
+        const uint32_t dst = b.w;
+        if (dst >= c.lp0 && dst < c.lp0 + c.R) {
+            lp_deliver(c, a, b, tmin);
+        } else if (send && world > 1) {
+            uint32_t lo = 0, hi = world;
+            while (hi - lo > 1) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (gp(starts)[mid] <= dst) lo = mid; else hi = mid;
+            }
+            uint4 GAS* blk = gp(send) + (size_t)lo * (cap + 1) * 2;
+            const uint32_t k = __hip_atomic_fetch_add((uint32_t GAS*)blk, 1u, __ATOMIC_RELAXED,
+                                                      __HIP_MEMORY_SCOPE_AGENT);
+            if (k >= cap) {
+                __hip_atomic_fetch_or(gp(c.lp_err), 8u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                continue;
+            }
+            blk[(size_t)(k + 1) * 2] = a;
+            blk[(size_t)(k + 1) * 2 + 1] = b;
+        } else {
+            __hip_atomic_fetch_or(gp(c.lp_err), 4u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+}
+// the records other ranks sent this tick
+__global__ void __launch_bounds__(256) tw_lp_import(Dev c, const uint4* recv, uint32_t world, uint32_t cap) {
+    if (!win_enter(c)) return;
+    uint64_t GAS* tmin = (uint64_t GAS*)(gp(c.win) + WN_REC_MIN);
+    const uint32_t total = world * cap;
+    for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < total; i += gridDim.x * 256) {
+        const uint32_t g = i / cap, k = i - g * cap;
+        const uint4 GAS* blk = gp(recv) + (size_t)g * (cap + 1) * 2;
+        const uint32_t cnt = blk[0].x;
+        if (k >= (cnt < cap ? cnt : cap)) continue;
+        const uint4 a = blk[(size_t)(k + 1) * 2], b = blk[(size_t)(k + 1) * 2 + 1];
+        if (b.w >= c.lp0 && b.w < c.lp0 + c.R) lp_deliver(c, a, b, tmin);
+        else __hip_atomic_fetch_or(gp(c.lp_err), 4u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+// red = {this rank's next event time (lanes' queues, records delivered this
+// window), -(lanes still active in the window)}, for an all-reduce(min)
+__global__ void tw_lp_fill(Dev c, int64_t* red) {
+    const int64_t GAS* w = gp(c.win);
+    if (w[WN_FLAGS] & WN_DONE) {
+        gp(red)[0] = INT64_MAX;
+        gp(red)[1] = 0;
+        return;
+    }
+    const uint64_t a = *gp(c.next_t), b = (uint64_t)w[WN_REC_MIN];
+    const uint64_t m = a < b ? a : b;
+    gp(red)[0] = m >= (uint64_t)INT64_MAX ? INT64_MAX : (int64_t)m;
+    gp(red)[1] = -(int64_t)*gp(c.n_active);
+}
+// advance: every rank idle in this window -> T := the global next time (a
+// fresh window: flip the work lists), else rerun the window
+__global__ void tw_lp_ctl(Dev c, const int64_t* red, uint4* send, uint32_t world, uint32_t cap) {
+    int64_t GAS* w = gp(c.win);
+    if (w[WN_FLAGS] & WN_DONE) return;
+    w[WN_TICKS] += 1;
+    *gp(c.out_n) = 0;
+    for (uint32_t g = 0; send && g < world; ++g) gp(send)[(size_t)g * (cap + 1) * 2].x = 0;
+    *gp(c.n_active) = 0;
+    *gp(c.next_t) = ~0ull;
+    if (gp(red)[1] < 0) {
+        w[WN_FLAGS] &= ~WN_FRESH;
+        return;
+    }
+    w[WN_WINDOWS] += 1;
+    const int64_t t = gp(red)[0];
+    if (t == INT64_MAX) {
+        w[WN_T] = INT64_MAX;
+        w[WN_FLAGS] = WN_DONE;
+        return;
+    }
+    w[WN_T] = t;
+    const uint32_t act = (uint32_t)w[WN_ACT] ^ 1u;
+    w[WN_ACT] = act;
+    w[WN_WID] += 1;
+    gp(c.act_n)[act ^ 1u] = 0;
+    w[WN_REC_MIN] = (int64_t)~0ull;
+    w[WN_FLAGS] = WN_FRESH;
+}
+// loop start after tw_reset: the first window serves every node (list 1), as
+// the host loop's first tw_lp_window does
+__global__ void tw_lp_begin(Dev c, int64_t lookahead) {
+    int64_t GAS* w = gp(c.win);
+    w[WN_T] = 0;
+    w[WN_L] = lookahead;
+    w[WN_REC_MIN] = (int64_t)~0ull;
+    w[WN_WINDOWS] = 0;
+    w[WN_TICKS] = 0;
+    w[WN_FLAGS] = WN_FRESH;
+    w[WN_ACT] = 1;
+    w[WN_WID] = 1;
+    gp(c.act_n)[0] = 0;
+    *gp(c.out_n) = 0;
+    *gp(c.n_active) = 0;
+    *gp(c.next_t) = ~0ull;
 }
 
 // Per-replica digest of the results and node hashes (tw_tie_audit compares
@@ -1956,6 +2094,21 @@ struct tw_ctx {
     std::vector<uint32_t> tie_flags;  // tw_tie_audit, per replica
     Dev* d_dev = nullptr;             // device copy of d (the wave kernel reads it through the scalar cache)
     uint32_t seq0 = 0, tid0 = 1;      // tw_set_counter_base
+    hipStream_t own_stream = nullptr; // the context's stream (tw_set_stream may replace `stream`)
+    // device-driven windows (tw_lp_exchange_setup)
+    uint32_t ex_world = 1, ex_rank = 0, ex_cap = 0;
+    uint32_t* ex_starts = nullptr;    // device, world + 1
+    uint4* ex_send = nullptr;         // caller's device buffers
+    uint4* ex_recv = nullptr;
+    int64_t* ex_red = nullptr;        // caller's (or red_own)
+    int64_t* red_own = nullptr;
+    int64_t* win_buf = nullptr;       // the device loop's WN_* words
+    bool loop_ready = false;
+    Dev dwin() const {                // the descriptor the device loop's kernels get
+        Dev x = d;
+        x.win = win_buf;
+        return x;
+    }
 };
 
 namespace {
@@ -1990,6 +2143,14 @@ void free_all(tw_ctx* c) {
     if (c->d.trace) (void)hipFree(c->d.trace);
     c->d.trace = nullptr;
     c->d.trace_cap = 0;
+    if (c->ex_starts) (void)hipFree(c->ex_starts);
+    c->ex_starts = nullptr;
+    c->ex_send = c->ex_recv = nullptr;
+    c->ex_red = c->red_own = nullptr;
+    c->win_buf = nullptr;
+    c->ex_world = 1;
+    c->ex_rank = c->ex_cap = 0;
+    c->loop_ready = false;
     c->loaded = false;
 }
 
@@ -2041,6 +2202,7 @@ int tw_create(int device, tw_ctx** out) {
         delete c;
         return TW_ERR_HIP;
     }
+    c->own_stream = c->stream;
     *out = c;
     return TW_OK;
 }
@@ -2052,7 +2214,7 @@ void tw_destroy(tw_ctx* c) {
     free_all(c);
     for (hipEvent_t e : c->ev_pool) (void)hipEventDestroy(e);
     if (c->h_active) (void)hipHostFree(c->h_active);
-    if (c->stream) (void)hipStreamDestroy(c->stream);
+    if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
     delete c;
 }
 
@@ -2256,6 +2418,8 @@ static int load_common(tw_ctx* c, const tw_scenario_desc* s, bool lp, uint32_t l
         ALLOC(c->foreign, (size_t)d.out_cap * 2);
         ALLOC(c->n_foreign, 1);
         ALLOC(c->staging, (size_t)d.out_cap * 2);
+        ALLOC(c->win_buf, WN_COUNT);  // d.win stays null: the host-driven loop
+        ALLOC(c->red_own, 2);
     }
     int64_t *mregs = nullptr, *nvi = nullptr;
     if (s->main_regs && !lp) ALLOC(mregs, R * 4);
@@ -2631,6 +2795,140 @@ int tw_lp_results(tw_ctx* c, tw_replica_result* agg, uint64_t* node_hashes, size
         HIPCHK(hipStreamSynchronize(c->stream));
     }
     return TW_OK;
+}
+
+int tw_set_stream(tw_ctx* c, void* hs) {
+    if (!c) return TW_ERR_INVALID;
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipStreamSynchronize(c->stream));  // finish what was queued on the old one
+    c->stream = hs ? (hipStream_t)hs : c->own_stream;
+    return TW_OK;
+}
+
+int tw_lp_exchange_setup(tw_ctx* c, uint32_t world, uint32_t rank, const uint32_t* starts, void* send, void* recv,
+                         uint32_t cap, int64_t* red) {
+    if (!c || world == 0 || rank >= world || !starts) return TW_ERR_INVALID;
+    if (!c->loaded || !c->lp) return TW_ERR_STATE;
+    if (world > 1 && (!send || !recv || !red || cap == 0)) return TW_ERR_INVALID;
+    for (uint32_t g = 0; g < world; ++g)
+        if (starts[g] > starts[g + 1]) return TW_ERR_INVALID;
+    if (starts[rank] != c->d.lp0 || starts[rank + 1] != c->d.lp0 + c->d.R) return TW_ERR_INVALID;
+    HIPCHK(hipSetDevice(c->device));
+    if (c->ex_starts) {
+        HIPCHK(hipStreamSynchronize(c->stream));
+        HIPCHK(hipFree(c->ex_starts));
+        c->ex_starts = nullptr;
+    }
+    HIPCHK(hipMalloc((void**)&c->ex_starts, 4ull * (world + 1)));
+    HIPCHK(hipMemcpy(c->ex_starts, starts, 4ull * (world + 1), hipMemcpyHostToDevice));
+    c->ex_world = world;
+    c->ex_rank = rank;
+    c->ex_cap = world > 1 ? cap : 0;
+    c->ex_send = world > 1 ? (uint4*)send : nullptr;
+    c->ex_recv = world > 1 ? (uint4*)recv : nullptr;
+    c->ex_red = world > 1 ? red : c->red_own;
+    if (world > 1) HIPCHK(hipMemsetAsync(send, 0, 32ull * world * (cap + 1), c->stream));
+    return TW_OK;
+}
+
+int tw_lp_loop_begin(tw_ctx* c) {
+    if (!c) return TW_ERR_INVALID;
+    if (!c->loaded || !c->lp) return TW_ERR_STATE;
+    HIPCHK(hipSetDevice(c->device));
+    if (!c->ex_red) c->ex_red = c->red_own;  // world 1 without an explicit setup
+    c->d.act_cur = 0;
+    c->d.wid = 0;
+    hipLaunchKernelGGL(tw_lp_begin, dim3(1), dim3(1), 0, c->stream, c->dwin(), c->d.lookahead);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemsetAsync(c->d.lp_err, 0, 4, c->stream));
+    c->loop_ready = true;
+    return TW_OK;
+}
+
+static uint32_t lp_grid(uint32_t n) {
+    const uint32_t b = (n + 255) / 256;
+    return b < 1 ? 1 : b > 2048 ? 2048 : b;
+}
+
+int tw_lp_tick(tw_ctx* c) {
+    if (!c) return TW_ERR_INVALID;
+    if (!c->loaded || !c->lp || !c->loop_ready) return TW_ERR_STATE;
+    HIPCHK(hipSetDevice(c->device));
+    hipStream_t st = c->stream;
+    const Dev d = c->dwin();
+    // the window comes from the device (tw_run_kernel reads c.win); launch
+    // arguments are captured at enqueue, so d.win is set only around it
+    c->d.win = c->win_buf;
+    launch_run<true, TW_WG, TW_NEAR_CAP>(c, st, 0, UINT64_MAX, 1u << 14);
+    c->d.win = nullptr;
+    HIPCHK(hipGetLastError());
+    hipLaunchKernelGGL(tw_lp_pack, dim3(lp_grid(d.out_cap)), dim3(256), 0, st, d, c->ex_send,
+                       (const uint32_t*)c->ex_starts, c->ex_world, c->ex_cap);
+    HIPCHK(hipGetLastError());
+    return TW_OK;
+}
+
+int tw_lp_tick_import(tw_ctx* c) {
+    if (!c) return TW_ERR_INVALID;
+    if (!c->loaded || !c->lp || !c->loop_ready) return TW_ERR_STATE;
+    HIPCHK(hipSetDevice(c->device));
+    hipStream_t st = c->stream;
+    if (c->ex_world > 1) {
+        hipLaunchKernelGGL(tw_lp_import, dim3(lp_grid(c->ex_world * c->ex_cap)), dim3(256), 0, st, c->dwin(),
+                           (const uint4*)c->ex_recv, c->ex_world, c->ex_cap);
+        HIPCHK(hipGetLastError());
+    }
+    hipLaunchKernelGGL(tw_lp_fill, dim3(1), dim3(1), 0, st, c->dwin(), c->ex_red);
+    HIPCHK(hipGetLastError());
+    return TW_OK;
+}
+
+int tw_lp_tick_end(tw_ctx* c) {
+    if (!c) return TW_ERR_INVALID;
+    if (!c->loaded || !c->lp || !c->loop_ready) return TW_ERR_STATE;
+    HIPCHK(hipSetDevice(c->device));
+    hipLaunchKernelGGL(tw_lp_ctl, dim3(1), dim3(1), 0, c->stream, c->dwin(), (const int64_t*)c->ex_red, c->ex_send,
+                       c->ex_world, c->ex_cap);
+    HIPCHK(hipGetLastError());
+    return TW_OK;
+}
+
+int tw_lp_progress(tw_ctx* c, tw_lp_state* out) {
+    if (!c || !out) return TW_ERR_INVALID;
+    if (!c->loaded || !c->lp || !c->loop_ready) return TW_ERR_STATE;
+    HIPCHK(hipSetDevice(c->device));
+    int64_t w[WN_COUNT];
+    uint32_t err = 0;
+    HIPCHK(hipMemcpyAsync(w, c->win_buf, sizeof(w), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipMemcpyAsync(&err, c->d.lp_err, 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    out->windows = (uint64_t)w[WN_WINDOWS];
+    out->ticks = (uint64_t)w[WN_TICKS];
+    out->t = w[WN_T];
+    out->done = (w[WN_FLAGS] & WN_DONE) ? 1u : 0u;
+    out->err = err;
+    return TW_OK;
+}
+
+int tw_lp_run_windows(tw_ctx* c, uint64_t max_ticks, tw_lp_state* out) {
+    if (!c || !out) return TW_ERR_INVALID;
+    if (!c->loaded || !c->lp || !c->loop_ready) return TW_ERR_STATE;
+    if (c->ex_world != 1) return TW_ERR_STATE;
+    for (uint64_t done_ticks = 0; done_ticks < max_ticks;) {
+        const uint64_t batch = max_ticks - done_ticks < 16 ? max_ticks - done_ticks : 16;
+        for (uint64_t i = 0; i < batch; ++i) {
+            int rc = tw_lp_tick(c);
+            if (!rc) rc = tw_lp_tick_import(c);
+            if (!rc) rc = tw_lp_tick_end(c);
+            if (rc) return rc;
+        }
+        done_ticks += batch;
+        int rc = tw_lp_progress(c, out);
+        if (rc) return rc;
+        if (out->err) return TW_ERR_REPLICA;
+        if (out->done) return TW_OK;
+    }
+    return TW_ERR_INCOMPLETE;
 }
 
 #ifdef TW_STATS

@@ -125,6 +125,9 @@ struct Dev {
     uint32_t* act_n;     // [2]
     uint32_t* listed;    // [R]
     uint32_t act_cur, wid;
+    // device-driven windows (tw_lp_tick): the loop state, WN_* words; null
+    // for the host-driven loop (tw_lp_window)
+    int64_t* win;
     unsigned long long* prof;  // [P_COUNT] diagnostic build only
     uint4* trace;        // [trace_cap][R][2] TRACE records (tw_set_trace), replica mode
     uint32_t trace_cap;
@@ -157,6 +160,9 @@ __device__ __forceinline__ int64_t tx_us(const Dev& c, uint64_t link, uint32_t k
 }
 
 // LP: node r joins the next window's work list (once per window)
+enum { WN_T, WN_L, WN_REC_MIN, WN_WINDOWS, WN_TICKS, WN_FLAGS, WN_ACT, WN_WID, WN_COUNT };
+enum : int64_t { WN_FRESH = 1, WN_DONE = 2 };
+
 __device__ __forceinline__ void lp_list_next(const Dev& c, uint32_t r) {
     if (__hip_atomic_exchange(gp(c.listed) + r, c.wid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != c.wid) {
         const uint32_t nx = c.act_cur ^ 1u;

@@ -29,7 +29,6 @@
 #include "tw_dev.hpp"
 
 #define TW_STEP_CAP (1u << 22)  // instructions per thread step (== oracle kStepCap, engine.hip)
-#define TW_WAVE_THROWS 256      // deferred throwTo's of one thread step (a longer burst: TW_REP_ERR_QUEUE)
 
 namespace tw {
 namespace {
@@ -53,22 +52,6 @@ __device__ __forceinline__ uint32_t dpp_shr(uint32_t v, int n) {
     default: return (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x118, 0xF, 0xF, false);
     }
 }
-__device__ __forceinline__ int64_t rdl64s(int64_t v, uint32_t l) { return (int64_t)rdl64((uint64_t)v, l); }
-// sum over the 64 lanes (wave-uniform result): row prefix sums by DPP row_shr
-// 1/2/4/8 (a lane whose source is outside its row adds 0), then the row sums
-__device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, false);
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, false);
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, false);
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, false);
-    return rdl(v, 15) + rdl(v, 31) + rdl(v, 47) + rdl(v, 63);
-}
-// value of lane (this lane + d) (d wave-uniform; lanes past 63 read 0)
-__device__ __forceinline__ uint32_t lane_down(uint32_t v, uint32_t d) {
-    const uint32_t src = __lane_id() + d;
-    const uint32_t x = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((src & 63u) << 2), (int)v);
-    return src < 64 ? x : 0u;
-}
 // min over the 64 lanes of a 64-bit value (wave-uniform result): row prefix-min
 // by DPP row_shr 1/2/4/8 (a lane whose source is outside its row keeps its own
 // value), then the four row minima by readlane.
@@ -84,6 +67,14 @@ __device__ __forceinline__ uint64_t wave_min64(uint64_t v) {
     m = m2 < m ? m2 : m;
     return m3 < m ? m3 : m;
 }
+
+// (branch-free masked stores st32/st128/st8/atom_add64: tw_dev.hpp)
+__device__ __forceinline__ void st64(uint64_t GAS* p, uint64_t v, uint64_t mask = 1) {
+    uint64_t sv;
+    asm volatile("s_mov_b64 %0, exec\n\ts_and_b64 exec, exec, %3\n\tglobal_store_dwordx2 %1, %2, off\n\t"
+                 "s_mov_b64 exec, %0" : "=&s"(sv) : "v"(p), "v"(v), "s"(mask) : "memory");
+}
+__device__ __forceinline__ void st_i64(int64_t GAS* p, int64_t v) { st64((uint64_t GAS*)p, (uint64_t)v); }
 
 // Read-only tables (program image, constants, topology): constant address
 // space, so uniform-address reads become scalar loads.
@@ -130,8 +121,12 @@ __device__ __forceinline__ void urec_store(uint4 GAS* p, uint64_t qs, const URec
                                a ? t.w3 : b ? t.xh : c ? (uint32_t)((uint64_t)t.r1 >> 32) : (uint32_t)((uint64_t)t.r3 >> 32));
     st128(p + l * qs, q, ((1ull << q1) - 1) & ~((1ull << q0) - 1));
 }
+__device__ __forceinline__ uint32_t u_pc(const URec& t) { return t.w0 & 0xFFFFu; }
+__device__ __forceinline__ uint32_t u_nfr(const URec& t) { return (t.w0 >> 16) & 15u; }
 __device__ __forceinline__ uint32_t u_flags(const URec& t) { return (t.w0 >> FL_SHIFT) & 0x3Fu; }
 __device__ __forceinline__ uint32_t u_exc(const URec& t) { return t.w0 >> EXC_SHIFT; }
+__device__ __forceinline__ void u_set_pc(URec& t, uint32_t pc) { t.w0 = (t.w0 & 0xFFFF0000u) | (pc & 0xFFFFu); }
+__device__ __forceinline__ void u_set_nfr(URec& t, uint32_t n) { t.w0 = (t.w0 & ~(15u << 16)) | (n << 16); }
 __device__ __forceinline__ void u_set_exc(URec& t, uint32_t c) {
     t.w0 = (t.w0 & ((1u << EXC_SHIFT) - 1u)) | (c << EXC_SHIFT);
 }
@@ -451,13 +446,66 @@ struct Wave {
         hash_atomic(hnode, hacc);
         hacc = 0;
     }
-    // (uniform) throwTo of a deferred throw (TimedT.hs:357-368): the target's
-    // queued event is re-stamped to now with a fresh seq, the first pending
-    // exception wins.  The target is never the running thread (that case is
-    // handled in the thread's own lane).
-    __device__ void throw_to(int64_t ref, uint32_t code, int64_t val) {
+    __device__ __forceinline__ uint32_t GAS* fxp(uint32_t slot, uint32_t i) const {
+        return (uint32_t GAS*)(gp(dv->fx) + ((size_t)slot * dv->R + r) * dv->FXQ) + (i - 2);
+    }
+    __device__ __forceinline__ uint32_t frame(const URec& t, uint32_t slot, uint32_t i) const {
+        if (i < 2) return i == 0 ? t.f0 : t.f1;
+        return rfl(*fxp(slot, i));
+    }
+    __device__ __forceinline__ void trace_rec(uint32_t node, int32_t tag, int64_t val) {
+        const uint32_t n = rfl(cw->trn);
+        cw->trn = n + 1;
+        if (n < dv->trace_cap) {
+            uint4 GAS* q = gp(dv->trace) + ((size_t)n * dv->R + r) * 2;
+            const bool l0 = (lane & 1u) == 0;
+            st128(q + (lane & 1u), l0 ? make_uint4((uint32_t)now, (uint32_t)((uint64_t)now >> 32), node, (uint32_t)tag)
+                                      : make_uint4((uint32_t)val, (uint32_t)((uint64_t)val >> 32), 0u, 0u), 3);
+        }
+    }
+
+    // Thread ends: owned listener released, refs invalidated, slot freed; the
+    // header quad is stored by the caller.
+    __device__ __forceinline__ void die(URec& th, uint32_t slot) {
+        if (u_flags(th) & F_OWNS) st32(gp(dv->bind_rel) + ix(th.w1), th.w2);
+        th.w2 = 0xFFFFFFFFu;
+        th.w3 = 0;
+        free_slot(slot);
+    }
+    // Raise `code` in the running thread (TimedT.hs:183-204): innermost frame
+    // first; finally frames set their timeout's done flag (TimedT.hs:376).
+    __device__ bool unwind(URec& th, uint32_t slot, uint32_t code, int64_t val) {
+        for (int i = (int)u_nfr(th) - 1; i >= 0; --i) {
+            const uint32_t f = frame(th, slot, (uint32_t)i);
+            const uint32_t mask = f >> 16;
+            if (mask == 0) {
+                const uint32_t e = f & 0xFFFFu;
+                if (e < dv->T) st8(gp(dv->tmo_done) + ix(e), 1);
+            } else if (mask & (1u << code)) {
+                u_set_nfr(th, (uint32_t)i);
+                u_set_pc(th, f & 0xFFFFu);
+                th.r0 = val;
+                th.r3 = (int64_t)code;
+                return true;
+            }
+        }
+        u_set_nfr(th, 0);
+        if (u_flags(th) & F_MAIN) cw->main_exc = code;
+        die(th, slot);
+        urec_store(hrec(slot), dv->RQ, th, 0, 1);
+        return false;
+    }
+
+    // throwTo (TimedT.hs:357-368): the target's queued event is re-stamped to
+    // now with a fresh seq; the first pending exception wins; no yield.
+    __device__ void throw_to(URec& self, uint32_t self_slot, int64_t ref, uint32_t code, int64_t val) {
         const uint32_t ts = (uint32_t)ref, tid = (uint32_t)((uint64_t)ref >> 32);
         if (ts >= dv->S) return;
+        if (ts == self_slot) {
+            if (self.w2 != tid) return;
+            if (u_exc(self) == 0) { u_set_exc(self, code); self.xl = (uint32_t)val; self.xh = (uint32_t)((uint64_t)val >> 32); }
+            return;
+        }
         URec t;
         urec_load(hrec(ts), dv->RQ, t);
         if (t.w2 != tid) return;  // dead: the map entry is unobservable
@@ -479,225 +527,85 @@ struct Wave {
         }
         urec_store(hrec(ts), dv->RQ, t, 0, 2);
     }
-    // (uniform) pop the global minimum (near or far); false if none
-    __device__ __forceinline__ bool peek_min(int64_t& t, uint32_t& sq, int& src) {
-        if (far_dirty) far_min();
-        const bool use_near = near_n != 0;
-        const int64_t tn = nbase + (int64_t)(gmin >> 32);
-        const bool use_far = fm_src >= 0 && (!use_near || tless(fm_t, fm_s, tn, (uint32_t)gmin));
-        if (!use_near && !use_far) return false;
-        t = use_far ? fm_t : tn;
-        sq = use_far ? fm_s : (uint32_t)gmin;
-        src = use_far ? fm_src : -1;
+
+    // Create a thread queued at now (fork, TimedT.hs:326-339); its record is stored here.
+    __device__ bool spawn(uint32_t pc, uint32_t node, int64_t q0, int64_t q1, int64_t q2, int64_t q3, int64_t& ref) {
+        const uint32_t s = alloc_slot();
+        if (s == 0xFFFFFFFFu) return false;
+        if (tidc == 0xFFFFFFFFu) { fail(TW_REP_ERR_COUNTER); return false; }
+        const uint32_t tid = tidc++;
+        cw->d_th = rfl(cw->d_th) + 1;
+        URec ch;
+        ch.w0 = pc & 0xFFFFu; ch.w1 = node; ch.w2 = tid; ch.w3 = 0;
+        ch.f0 = ch.f1 = ch.xl = ch.xh = 0;
+        ch.r0 = q0; ch.r1 = q1; ch.r2 = q2; ch.r3 = q3;
+        enqueue(ch, s, now);
+        urec_store(hrec(s), dv->RQ, ch, 0, 4);
+        ref = (int64_t)(((uint64_t)tid << 32) | s);
         return true;
     }
-    __device__ __forceinline__ uint32_t pop_min(int src) {
-        if (src < 0) return near_pop();
-        const uint32_t sl = fm_sl;
-        if (src == TW_RUNS) heap_pop();
-        else run_pop(src);
-        return sl;
-    }
-    // (uniform) put a popped entry back (same key)
-    __device__ __forceinline__ void push_back(int64_t t, uint32_t sq, uint32_t slot) {
-        if (near_fits(t)) near_push(t, sq, slot);
-        else if (!run_push(t, sq, slot)) heap_push(t, sq, slot);
-    }
-};
 
-// ------------------------------------------------- per-lane thread steps
-// A thread record in one lane's vector registers.
-struct LRec {
-    uint32_t w0, w1, w2, w3, f0, f1, xl, xh;
-    int64_t r0, r1, r2, r3;
-    __device__ __forceinline__ int64_t reg(uint32_t i) const {
-        return i == 0 ? r0 : i == 1 ? r1 : i == 2 ? r2 : r3;
-    }
-    __device__ __forceinline__ void set_reg(uint32_t i, int64_t v) {
-        r0 = i == 0 ? v : r0; r1 = i == 1 ? v : r1; r2 = i == 2 ? v : r2; r3 = i == 3 ? v : r3;
-    }
-    __device__ __forceinline__ uint32_t pc() const { return w0 & 0xFFFFu; }
-    __device__ __forceinline__ uint32_t nfr() const { return (w0 >> 16) & 15u; }
-    __device__ __forceinline__ uint32_t flags() const { return (w0 >> FL_SHIFT) & 0x3Fu; }
-    __device__ __forceinline__ uint32_t exc() const { return w0 >> EXC_SHIFT; }
-    __device__ __forceinline__ void set_pc(uint32_t p) { w0 = (w0 & 0xFFFF0000u) | (p & 0xFFFFu); }
-    __device__ __forceinline__ void set_nfr(uint32_t n) { w0 = (w0 & ~(15u << 16)) | (n << 16); }
-    __device__ __forceinline__ void set_exc(uint32_t c) { w0 = (w0 & ((1u << EXC_SHIFT) - 1u)) | (c << EXC_SHIFT); }
-};
-__device__ __forceinline__ void lrec_load(const uint4 GAS* p, uint64_t qs, LRec& t) {
-    const uint4 a = p[0], b = p[qs], d = p[2 * qs], e = p[3 * qs];
-    t.w0 = a.x; t.w1 = a.y; t.w2 = a.z; t.w3 = a.w;
-    t.f0 = b.x; t.f1 = b.y; t.xl = b.z; t.xh = b.w;
-    t.r0 = (int64_t)(((uint64_t)d.y << 32) | d.x); t.r1 = (int64_t)(((uint64_t)d.w << 32) | d.z);
-    t.r2 = (int64_t)(((uint64_t)e.y << 32) | e.x); t.r3 = (int64_t)(((uint64_t)e.w << 32) | e.z);
-}
-// the lanes of `mask` store quads [q0, q1) of their records (one instruction per quad)
-__device__ __forceinline__ void lrec_store(uint4 GAS* p, uint64_t qs, const LRec& t, uint64_t mask, uint32_t q0,
-                                           uint32_t q1) {
-    if (q0 <= 0 && 0 < q1) st128(p, make_uint4(t.w0, t.w1, t.w2, t.w3), mask);
-    if (q0 <= 1 && 1 < q1) st128(p + qs, make_uint4(t.f0, t.f1, t.xl, t.xh), mask);
-    if (q0 <= 2 && 2 < q1)
-        st128(p + 2 * qs, make_uint4((uint32_t)t.r0, (uint32_t)((uint64_t)t.r0 >> 32), (uint32_t)t.r1,
-                                (uint32_t)((uint64_t)t.r1 >> 32)), mask);
-    if (q0 <= 3 && 3 < q1)
-        st128(p + 3 * qs, make_uint4((uint32_t)t.r2, (uint32_t)((uint64_t)t.r2 >> 32), (uint32_t)t.r3,
-                                (uint32_t)((uint64_t)t.r3 >> 32)), mask);
-}
-
-// What a thread step leaves for the batch commit (all per lane).
-struct Eff {
-    uint32_t fin;          // W_*
-    int64_t yt;            // yield time
-    uint32_t cpc, cnode, cra;  // spawned child (fin == W_SPAWN)
-    int64_t q0, q1, q2, q3;
-    uint32_t tmo_a;        // TMO_BEGIN: register receiving the fresh epoch (4: none)
-    uint32_t hn0, hn1;     // nodes of the two hash accumulators (hn1 = 0xFFFFFFFF: unused)
-    uint64_t h0, h1;
-    uint32_t dl, dr, ud;   // delivered / dropped / undeliverable
-    uint32_t st;           // error status of this event (TW_REP_RUNNING: none)
-    uint32_t mexc;         // main thread's uncaught exception code (0: none)
-    uint32_t ntr;          // TRACE records emitted (singletons only)
-    bool freed;            // the thread ended: its slot is freed
-};
-
-// Class of a resume pc (tw_load's static analysis, engine.hip classify_pcs):
-// 0 = may touch another thread or node (throwTo, throw, watchdog fire,
-// cross-node vars, in-place handlers): runs alone; 1 = own node only; 2 = the
-// deliverer's DELIVER: its own node plus the destination node.
-enum { PC_ALONE = 0, PC_LOCAL = 1, PC_DELIVER = 2 };
-
-template <int K>
-struct LaneCtx {
-    const Dev CAS* dv;
-    uint32_t r, lane;
-    int64_t now;
-    uint32_t tmo0, trn0;       // counters before the batch (singletons read them)
-    uint32_t GAS* thr_n;       // deferred throws (singletons): LDS list
-    __device__ __forceinline__ size_t ix(size_t i) const { return i * dv->R + r; }
-    __device__ __forceinline__ uint4 GAS* hrec(uint32_t slot) const { return gp(dv->slots) + ix(slot); }
-    __device__ __forceinline__ uint32_t GAS* fxp(uint32_t slot, uint32_t i) const {
-        return (uint32_t GAS*)(gp(dv->fx) + ((size_t)slot * dv->R + r) * dv->FXQ) + (i - 2);
-    }
-    __device__ __forceinline__ uint32_t frame(const LRec& t, uint32_t slot, uint32_t i) const {
-        if (i < 2) return i == 0 ? t.f0 : t.f1;
-        return *fxp(slot, i);
-    }
-    __device__ __forceinline__ void hadd(Eff& e, uint32_t node, uint64_t v) const {
-        if (node == e.hn0) { e.h0 += v; return; }
-        if (e.hn1 == 0xFFFFFFFFu || node == e.hn1) { e.hn1 = node; e.h1 += v; return; }
-        atomicAdd((unsigned long long*)(dv->hash + ix(node)), (unsigned long long)v);  // (singletons only)
-    }
-    __device__ __forceinline__ void fail(Eff& e, uint32_t s) const {
-        if (e.st == TW_REP_RUNNING) e.st = s;
-    }
-    // the thread ends: owned listener released, refs invalidated
-    __device__ __forceinline__ void die(LRec& th, Eff& e) const {
-        if (th.flags() & F_OWNS) gp(dv->bind_rel)[ix(th.w1)] = th.w2;
-        th.w2 = 0xFFFFFFFFu;
-        th.w3 = 0;
-        e.freed = true;
-    }
-    // raise `code` (TimedT.hs:183-204): innermost frame first, finally frames set
-    // their timeout's done flag (TimedT.hs:376); true if a catch frame took it
-    __device__ bool unwind(LRec& th, uint32_t slot, uint32_t code, int64_t val, Eff& e) const {
-        for (int i = (int)th.nfr() - 1; i >= 0; --i) {
-            const uint32_t f = frame(th, slot, (uint32_t)i);
-            const uint32_t mask = f >> 16;
-            if (mask == 0) {
-                const uint32_t ep = f & 0xFFFFu;
-                if (ep < dv->T) gp(dv->tmo_done)[ix(ep)] = 1;
-            } else if (mask & (1u << code)) {
-                th.set_nfr((uint32_t)i);
-                th.set_pc(f & 0xFFFFu);
-                th.r0 = val;
-                th.r3 = (int64_t)code;
-                return true;
-            }
-        }
-        th.set_nfr(0);
-        if (th.flags() & F_MAIN) e.mexc = code;
-        die(th, e);
-        return false;
-    }
-    __device__ __forceinline__ void trace_rec(Eff& e, uint32_t node, int32_t tag, int64_t val) const {
-        const uint32_t n = trn0 + e.ntr++;
-        if (n < dv->trace_cap) {
-            uint4 GAS* q = gp(dv->trace) + ((size_t)n * dv->R + r) * 2;
-            q[0] = make_uint4((uint32_t)now, (uint32_t)((uint64_t)now >> 32), node, (uint32_t)tag);
-            q[1] = make_uint4((uint32_t)val, (uint32_t)((uint64_t)val >> 32), 0u, 0u);
-        }
-    }
-
-    // Run the thread's continuation until it yields or ends (TimedT.hs:343-355),
-    // in this lane; effects on shared replica state are left in `e` (or, for a
-    // lone event's throwTo, in the LDS throw list).
-    __device__ void step(LRec& th, uint32_t slot, Eff& e, int64_t LAS* thr) const {
+    // Run the thread's continuation until it yields or ends (TimedT.hs:343-355).
+    __device__ void step(URec& th, uint32_t slot) {
         th.w0 |= F_STARTED << FL_SHIFT;
-        uint32_t pc = th.pc();
-        const tw_insn* P = (const tw_insn*)dv->insns;
-        const int64_t* KP = dv->consts;
+        uint32_t pc = u_pc(th);
+        uint32_t fin = W_NONE;
+        int64_t yt = 0;
+        uint32_t cpc = 0, cnode = 0, cra = 4;
+        int64_t q0 = 0, q1 = 0, q2 = 0, q3 = 0;  // the spawned child's registers
+        const uint2 CAS* P = cp((const uint2*)dv->insns);
+        const int64_t CAS* KP = cp(dv->consts);
         for (uint32_t n = 0;; ++n) {
-            if (pc >= dv->n_insns || n >= TW_STEP_CAP) { fail(e, TW_REP_ERR_INSN); e.fin = W_STOP; break; }
-            const tw_insn in = P[pc];
-            const uint32_t w = in.w0, op = w & 0xFFu, a = (w >> 8) & 3u, b = w >> 16;
-            const int32_t imm = in.imm;
-            const int64_t ra = th.reg(a), rb = th.reg(b & 3u);
+            if (pc >= dv->n_insns || n >= TW_STEP_CAP) { fail(TW_REP_ERR_INSN); fin = W_STOP; break; }
+            const uint2 in = P[pc];
+            const uint32_t w = in.x, op = w & 0xFFu, a = (w >> 8) & 3u, b = w >> 16;
+            const int32_t imm = (int32_t)in.y;
+            const int64_t ra = th.reg(a);
+            const int64_t rb = th.reg(b & 3u);
             uint32_t npc = pc + 1;
-            bool wr = false;
+            bool wr = false;        // the op writes r[a] := wv
             int64_t wv = 0;
+            bool thr = false;
+            int64_t tref = 0, tval = 0;
+            uint32_t tcode = 0;
             switch (op) {
             case TW_OP_NOP: break;
-            case TW_OP_END: e.fin = W_EXIT; break;
-            case TW_OP_WAIT_REL: e.yt = now + KP[imm]; e.fin = W_YIELD; break;
-            case TW_OP_WAIT_ABS: { const int64_t k = KP[imm]; e.yt = k > now ? k : now; e.fin = W_YIELD; break; }
-            case TW_OP_WAIT_REG: e.yt = now + (ra > 0 ? ra : 0); e.fin = W_YIELD; break;
+            case TW_OP_END: fin = W_EXIT; break;
+            case TW_OP_WAIT_REL: yt = now + KP[imm]; fin = W_YIELD; break;
+            case TW_OP_WAIT_ABS: { const int64_t k = KP[imm]; yt = k > now ? k : now; fin = W_YIELD; break; }
+            case TW_OP_WAIT_REG: yt = now + (ra > 0 ? ra : 0); fin = W_YIELD; break;
             case TW_OP_FORK: {
                 const uint32_t node = b == 0xFFFFu ? th.w1 : (uint32_t)rb;
-                if (node >= dv->N) { fail(e, TW_REP_ERR_INSN); e.fin = W_STOP; break; }
-                e.cpc = (uint32_t)imm; e.cnode = node; e.cra = a;
-                e.q0 = th.r0; e.q1 = th.r1; e.q2 = th.r2; e.q3 = th.r3;
-                e.fin = W_SPAWN;
+                if (node >= dv->N) { fail(TW_REP_ERR_INSN); fin = W_STOP; break; }
+                cpc = (uint32_t)imm; cnode = node; cra = a;
+                q0 = th.r0; q1 = th.r1; q2 = th.r2; q3 = th.r3;
+                fin = W_SPAWN;
                 break;
             }
             case TW_OP_MYTID: wr = true; wv = (int64_t)(((uint64_t)th.w2 << 32) | slot); break;
-            case TW_OP_THROW_TO: {  // (a lone event: deferred to the commit, in program order)
-                const int64_t ref = ra;
-                const uint32_t code = b & 0xFFu;
-                const int64_t val = th.reg((b >> 8) & 3u);
-                const uint32_t ts = (uint32_t)ref, tid = (uint32_t)((uint64_t)ref >> 32);
-                if (ts == slot) {  // the running thread: its record is in this lane
-                    if (th.w2 == tid && th.exc() == 0) {
-                        th.set_exc(code);
-                        th.xl = (uint32_t)val; th.xh = (uint32_t)((uint64_t)val >> 32);
-                    }
-                } else if (ts < dv->S) {
-                    const uint32_t k = (uint32_t)thr[0];
-                    if (k >= TW_WAVE_THROWS) { fail(e, TW_REP_ERR_QUEUE); e.fin = W_STOP; break; }
-                    thr[1 + 3 * k] = ref; thr[2 + 3 * k] = code; thr[3 + 3 * k] = val;
-                    thr[0] = k + 1;
-                }
+            case TW_OP_THROW_TO:
+                thr = true; tref = ra; tcode = b & 0xFFu; tval = th.reg((b >> 8) & 3u);
                 break;
-            }
             case TW_OP_THROW:
-                th.set_pc(pc + 1);
-                if (unwind(th, slot, b & 0xFFu, th.reg((b >> 8) & 3u), e)) npc = th.pc();
-                else e.fin = W_DIED;
+                u_set_pc(th, pc + 1);
+                if (unwind(th, slot, b & 0xFFu, th.reg((b >> 8) & 3u))) npc = u_pc(th);
+                else fin = W_DIED;
                 break;
             case TW_OP_CATCH:
             case TW_OP_TMO_PUSH: {
-                const uint32_t nf = th.nfr();
-                if (nf >= dv->max_frames) { fail(e, TW_REP_ERR_FRAMES); e.fin = W_STOP; break; }
+                const uint32_t nf = u_nfr(th);
+                if (nf >= dv->max_frames) { fail(TW_REP_ERR_FRAMES); fin = W_STOP; break; }
                 const uint32_t fv = op == TW_OP_CATCH ? (b << 16) | ((uint32_t)imm & 0xFFFFu) : (uint32_t)ra & 0xFFFFu;
                 if (nf == 0) th.f0 = fv;
                 else if (nf == 1) th.f1 = fv;
-                else *fxp(slot, nf) = fv;
-                th.set_nfr(nf + 1);
+                else st32(fxp(slot, nf), fv);
+                u_set_nfr(th, nf + 1);
                 break;
             }
             case TW_OP_UNCATCH: {
-                const uint32_t nf = th.nfr();
-                if (nf == 0 || (frame(th, slot, nf - 1) >> 16) == 0) { fail(e, TW_REP_ERR_INSN); e.fin = W_STOP; break; }
-                th.set_nfr(nf - 1);
+                const uint32_t nf = u_nfr(th);
+                if (nf == 0 || (frame(th, slot, nf - 1) >> 16) == 0) { fail(TW_REP_ERR_INSN); fin = W_STOP; break; }
+                u_set_nfr(th, nf - 1);
                 break;
             }
             case TW_OP_SETI: wr = true; wv = imm; break;
@@ -717,136 +625,149 @@ struct LaneCtx {
             case TW_OP_JNEI: if (ra != (int64_t)(int16_t)b) npc = (uint32_t)imm; break;
             case TW_OP_NOW: wr = true; wv = now; break;
             case TW_OP_NODE: wr = true; wv = th.w1; break;
-            case TW_OP_NLOAD: wr = true; wv = gp(dv->nvars)[ix((size_t)th.w1 * 4 + (b & 3u))]; break;
-            case TW_OP_NSTORE: gp(dv->nvars)[ix((size_t)th.w1 * 4 + (b & 3u))] = ra; break;
+            case TW_OP_NLOAD: wr = true; wv = rfl64s(gp(dv->nvars)[ix((size_t)th.w1 * 4 + (b & 3u))]); break;
+            case TW_OP_NSTORE: st_i64(gp(dv->nvars) + ix((size_t)th.w1 * 4 + (b & 3u)), ra); break;
             case TW_OP_NLOADX:
             case TW_OP_NSTOREX: {
                 const uint64_t node = (uint64_t)th.reg((b >> 8) & 3u);
-                if (node >= dv->N) { fail(e, TW_REP_ERR_INSN); e.fin = W_STOP; break; }
+                if (node >= dv->N) { fail(TW_REP_ERR_INSN); fin = W_STOP; break; }
                 int64_t GAS* v = &gp(dv->nvars)[ix((size_t)node * 4 + (b & 3u))];
-                if (op == TW_OP_NLOADX) { wr = true; wv = *v; }
-                else *v = ra;
+                if (op == TW_OP_NLOADX) { wr = true; wv = rfl64s(*v); }
+                else st_i64(v, ra);
                 break;
             }
-            case TW_OP_LINK: wr = true; wv = (int64_t)dv->out_off[th.w1] + imm; break;
+            case TW_OP_LINK: wr = true; wv = (int64_t)cp(dv->out_off)[th.w1] + imm; break;
             case TW_OP_RLINK:
-                if ((uint64_t)rb >= dv->L) { fail(e, TW_REP_ERR_INSN); e.fin = W_STOP; break; }
-                wr = true; wv = (int64_t)dv->link_rev[rb];
+                if ((uint64_t)rb >= dv->L) { fail(TW_REP_ERR_INSN); fin = W_STOP; break; }
+                wr = true; wv = (int64_t)cp(dv->link_rev)[rb];
                 break;
             case TW_OP_SEND: {  // schedule (after d) (deliver ..) unless the link drops it
                 const uint64_t link = (uint64_t)ra;
-                if (link >= dv->L) { fail(e, TW_REP_ERR_INSN); e.fin = W_STOP; break; }
+                if (link >= dv->L) { fail(TW_REP_ERR_INSN); fin = W_STOP; break; }
                 const uint32_t kind = b & 0xFFu;
                 const int64_t payload = th.reg((b >> 8) & 3u);
                 uint32_t GAS* op_ = gp(dv->link_ord) + ix(link);
-                const uint32_t ord = *op_;
-                *op_ = ord + 1;
-                const uint32_t lt = dv->link_table ? gp(dv->link_table)[ix((size_t)link * dv->D + ord % dv->D)] : 0u;
-                if (lt & TW_LINK_DROP) {
-                    ++e.dr;
-                    hadd(e, th.w1, term(now, TW_KIND_DROP | kind, payload));
+                const uint32_t ord = rfl(*op_);
+                st32(op_, ord + 1);
+                const uint32_t e = dv->link_table ? rfl(gp(dv->link_table)[ix((size_t)link * dv->D + ord % dv->D)]) : 0u;
+                if (e & TW_LINK_DROP) {
+                    cw->dr = rfl(cw->dr) + 1;
+                    hash_add(th.w1, term(now, TW_KIND_DROP | kind, payload));
                 } else {
-                    e.cpc = TW_PC_DELIVER_STUB; e.cnode = th.w1; e.cra = 4;
-                    e.q0 = payload; e.q1 = (int64_t)link;
-                    e.q2 = (int64_t)(lt & 0x7FFFFFFFu) + tx_us_w(dv, link, kind);
-                    e.q3 = (int64_t)kind;
-                    e.fin = W_SPAWN;
+                    cpc = TW_PC_DELIVER_STUB; cnode = th.w1; cra = 4;
+                    q0 = payload; q1 = (int64_t)link; q2 = (int64_t)(e & 0x7FFFFFFFu) + tx_us_w(dv, link, kind);
+                    q3 = (int64_t)kind;
+                    fin = W_SPAWN;
                 }
                 break;
             }
             case TW_OP_DELIVER: {  // listener dispatch, ForkStrategy fork_ (MonadDialog.hs:232-256,317)
                 const uint64_t link = (uint64_t)th.r1;
                 const uint32_t kind = (uint32_t)th.r3;
-                const uint32_t dst = dv->link_dst[link];
-                const uint32_t set0 = gp(dv->bind)[ix(dst)];
-                const uint32_t own = gp(dv->bind_own)[ix(dst)], rel = gp(dv->bind_rel)[ix(dst)];
+                const uint32_t dst = cp(dv->link_dst)[link];
+                const uint32_t set0 = rfl(gp(dv->bind)[ix(dst)]);
+                const uint32_t own = rfl(gp(dv->bind_own)[ix(dst)]), rel = rfl(gp(dv->bind_rel)[ix(dst)]);
                 const uint32_t set = own == rel ? 0u : set0;  // owner died: released
                 uint32_t lpc = TW_PC_NONE;
-                if (set && kind < dv->n_kinds) lpc = dv->lpc[(size_t)(set - 1) * dv->n_kinds + kind];
+                if (set && kind < dv->n_kinds) lpc = cp(dv->lpc)[(size_t)(set - 1) * dv->n_kinds + kind];
                 const int64_t p0 = th.r0;
                 if (lpc == TW_PC_NONE) {
-                    ++e.ud;
-                    hadd(e, dst, term(now, TW_KIND_UNDELIV | kind, p0));
+                    cw->ud = rfl(cw->ud) + 1;
+                    hash_add(dst, term(now, TW_KIND_UNDELIV | kind, p0));
                 } else if (lpc & TW_LPC_INLINE) {  // ForkStrategy `const id` (MonadDialog.hs:114-117)
-                    ++e.dl;
-                    hadd(e, dst, term(now, TW_KIND_RECV | kind, p0));
+                    cw->dl = rfl(cw->dl) + 1;
+                    hash_add(dst, term(now, TW_KIND_RECV | kind, p0));
+                    hash_flush();
                     th.r0 = p0; th.r1 = (int64_t)link; th.r2 = (int64_t)th.w1; th.r3 = (int64_t)kind;
+                    hnode = dst;
                     th.w1 = dst;
                     npc = lpc & ~TW_LPC_INLINE;
                 } else {
-                    ++e.dl;
-                    hadd(e, dst, term(now, TW_KIND_RECV | kind, p0));
-                    e.cpc = lpc; e.cnode = dst; e.cra = 4;
-                    e.q0 = p0; e.q1 = (int64_t)link; e.q2 = (int64_t)th.w1; e.q3 = (int64_t)kind;
-                    e.fin = W_SPAWN;
+                    cw->dl = rfl(cw->dl) + 1;
+                    hash_add(dst, term(now, TW_KIND_RECV | kind, p0));
+                    cpc = lpc; cnode = dst; cra = 4;
+                    q0 = p0; q1 = (int64_t)link; q2 = (int64_t)th.w1; q3 = (int64_t)kind;
+                    fin = W_SPAWN;
                 }
                 break;
             }
             case TW_OP_LISTEN:
-                if ((uint32_t)imm >= dv->n_sets) { fail(e, TW_REP_ERR_INSN); e.fin = W_STOP; break; }
-                gp(dv->bind)[ix(th.w1)] = (uint32_t)imm + 1;
-                gp(dv->bind_own)[ix(th.w1)] = b ? th.w2 : 0xFFFFFFFFu;
+                if ((uint32_t)imm >= dv->n_sets) { fail(TW_REP_ERR_INSN); fin = W_STOP; break; }
+                st32(gp(dv->bind) + ix(th.w1), (uint32_t)imm + 1);
+                st32(gp(dv->bind_own) + ix(th.w1), b ? th.w2 : 0xFFFFFFFFu);
                 if (b) th.w0 |= F_OWNS << FL_SHIFT;
                 break;
             case TW_OP_UNLISTEN:
-                gp(dv->bind)[ix(th.w1)] = 0;
-                gp(dv->bind_own)[ix(th.w1)] = 0xFFFFFFFFu;
+                st32(gp(dv->bind) + ix(th.w1), 0);
+                st32(gp(dv->bind_own) + ix(th.w1), 0xFFFFFFFFu);
                 break;
             case TW_OP_TRACE:
-                hadd(e, th.w1, term(now, TW_KIND_TRACE | ((uint32_t)imm & 0xFFFFu), ra));
-                if (dv->trace_cap) trace_rec(e, th.w1, imm, ra);
+                hacc += term(now, TW_KIND_TRACE | ((uint32_t)imm & 0xFFFFu), ra);
+                if (dv->trace_cap) trace_rec(th.w1, imm, ra);
                 break;
-            case TW_OP_TMO_BEGIN:  // schedule (after t) watchdog (TimedT.hs:373-375); epoch at commit
-                e.tmo_a = a;
-                e.cpc = TW_PC_WATCHDOG_STUB; e.cnode = th.w1; e.cra = 4;
-                e.q0 = (int64_t)(((uint64_t)th.w2 << 32) | slot); e.q1 = 0; e.q2 = KP[imm]; e.q3 = 0;
-                e.fin = W_SPAWN;
-                break;
-            case TW_OP_TMO_END: {
-                const uint32_t nf = th.nfr();
-                const uint32_t fr = nf ? frame(th, slot, nf - 1) : 0u;
-                if (nf == 0 || (fr >> 16) != 0) { fail(e, TW_REP_ERR_INSN); e.fin = W_STOP; break; }
-                th.set_nfr(nf - 1);
-                if ((fr & 0xFFFFu) < dv->T) gp(dv->tmo_done)[ix(fr & 0xFFFFu)] = 1;
+            case TW_OP_TMO_BEGIN: {  // schedule (after t) watchdog (TimedT.hs:373-375)
+                const uint32_t tmo = rfl(cw->tmo);
+                if (tmo >= dv->T) { fail(TW_REP_ERR_INSN); fin = W_STOP; break; }
+                st8(gp(dv->tmo_done) + ix(tmo), 0);
+                th.set_reg(a, tmo);
+                cpc = TW_PC_WATCHDOG_STUB; cnode = th.w1; cra = 4;
+                q0 = (int64_t)(((uint64_t)th.w2 << 32) | slot); q1 = (int64_t)tmo; q2 = KP[imm]; q3 = 0;
+                cw->tmo = tmo + 1;
+                fin = W_SPAWN;
                 break;
             }
-            case TW_OP_TMO_FIRE: {  // unless done: throwTo owner MTTimeoutError (deferred, a lone event)
-                const uint64_t ep = (uint64_t)th.r1;
-                if (ep < dv->T && !gp(dv->tmo_done)[ix(ep)]) {
-                    const int64_t ref = th.r0;
-                    const uint32_t ts = (uint32_t)ref;
-                    if (ts != slot && ts < dv->S) {
-                        const uint32_t k = (uint32_t)thr[0];
-                        if (k >= TW_WAVE_THROWS) { fail(e, TW_REP_ERR_QUEUE); e.fin = W_STOP; break; }
-                        thr[1 + 3 * k] = ref; thr[2 + 3 * k] = TW_EXC_TIMEOUT; thr[3 + 3 * k] = 0;
-                        thr[0] = k + 1;
-                    }
-                }
+            case TW_OP_TMO_END: {
+                const uint32_t nf = u_nfr(th);
+                const uint32_t fr = nf ? frame(th, slot, nf - 1) : 0u;
+                if (nf == 0 || (fr >> 16) != 0) { fail(TW_REP_ERR_INSN); fin = W_STOP; break; }
+                u_set_nfr(th, nf - 1);
+                if ((fr & 0xFFFFu) < dv->T) st8(gp(dv->tmo_done) + ix(fr & 0xFFFFu), 1);
+                break;
+            }
+            case TW_OP_TMO_FIRE: {
+                const uint64_t e = (uint64_t)th.r1;
+                thr = e < dv->T && !rfl(gp(dv->tmo_done)[ix(e < dv->T ? e : 0)]);
+                tref = th.r0; tcode = TW_EXC_TIMEOUT; tval = 0;
                 break;
             }
             default:
-                fail(e, TW_REP_ERR_INSN);
-                e.fin = W_STOP;
+                fail(TW_REP_ERR_INSN);
+                fin = W_STOP;
                 break;
             }
             if (wr) th.set_reg(a, wv);
-            if (e.fin != W_NONE) {
-                if (e.fin != W_DIED && e.fin != W_STOP) pc = npc;
+            if (thr) throw_to(th, slot, tref, tcode, tval);
+            if (fin != W_NONE) {
+                if (fin != W_DIED && fin != W_STOP) pc = npc;
                 break;
             }
             pc = npc;
-            if (e.st != TW_REP_RUNNING) { e.fin = W_STOP; break; }
-            if (pc >= dv->n_insns) { fail(e, TW_REP_ERR_INSN); e.fin = W_STOP; break; }
+            if (status != TW_REP_RUNNING) { fin = W_STOP; break; }
+            if (pc >= dv->n_insns) { fail(TW_REP_ERR_INSN); fin = W_STOP; break; }
         }
-        if (e.fin != W_DIED) th.set_pc(pc);
+        if (fin != W_DIED) u_set_pc(th, pc);
+        // terminal actions: fork's child is queued at now, then the parent waits 1 µs
+        if (fin == W_SPAWN) {
+            int64_t ref = 0;
+            if (!spawn(cpc, cnode, q0, q1, q2, q3, ref)) {
+                fin = W_STOP;
+            } else {
+                if (cra < 4) th.set_reg(cra, ref);
+                yt = now + 1;
+                fin = W_YIELD;
+            }
+        }
+        if (fin == W_YIELD) {
+            enqueue(th, slot, yt);
+            urec_store(hrec(slot), dv->RQ, th, 0, 4);
+        } else if (fin == W_EXIT) {
+            die(th, slot);
+            urec_store(hrec(slot), dv->RQ, th, 0, 1);
+        } else if (fin == W_STOP) {
+            urec_store(hrec(slot), dv->RQ, th, 0, 4);
+        }
     }
 };
-
-// exclusive prefix count of `mask` below this lane
-__device__ __forceinline__ uint32_t below(uint64_t mask) {
-    return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
-}
-__device__ __forceinline__ uint32_t pc64(uint64_t m) { return (uint32_t)__builtin_popcountll(m); }
 
 template <int K>
 __global__ void __launch_bounds__(64) tw_wave_kernel(const Dev* dptr, int64_t t_end, uint64_t max_events,
@@ -859,10 +780,6 @@ __global__ void __launch_bounds__(64) tw_wave_kernel(const Dev* dptr, int64_t t_
     const uint32_t status0 = (uint32_t)rfl64(sc[SC_STATUS * R]);
     if (status0 != TW_REP_RUNNING) return;
     Wave<K> W(dv, r);
-    __shared__ WCold cold;
-    __shared__ int64_t thr[1 + 3 * TW_WAVE_THROWS];  // deferred throws of a lone event
-    __shared__ uint32_t ftab[257];                   // batch footprint table (node hash -> lowest lane; 256: none)
-    W.cw = (WCold LAS*)&cold;
     W.status = status0;
     W.now = rfl64s((int64_t)sc[SC_NOW * R]);
     W.final_t = rfl64s((int64_t)sc[SC_FINAL_T * R]);
@@ -874,6 +791,8 @@ __global__ void __launch_bounds__(64) tw_wave_kernel(const Dev* dptr, int64_t t_
     W.free_n = rfl((uint32_t)sc[SC_FREE_N * R]);
     W.ftop = rfl((uint32_t)sc[SC_FTOP * R]);
     W.bump = rfl((uint32_t)sc[SC_BUMP * R]);
+    __shared__ WCold cold;
+    W.cw = (WCold LAS*)&cold;
     cold.main_exc = rfl((uint32_t)sc[SC_MAIN_EXC * R]);
     cold.tmo = rfl((uint32_t)sc[SC_TMO_CTR * R]);
     cold.trn = rfl((uint32_t)sc[SC_TRACE_N * R]);
@@ -924,271 +843,71 @@ __global__ void __launch_bounds__(64) tw_wave_kernel(const Dev* dptr, int64_t t_
         W.near_n = near_n0;
         W.gmin = wave_min64(W.lmk);
     }
-    const uint32_t lane = W.lane;
-    const uint64_t me_bit = 1ull << lane;
-    const bool batching = dv->trace_cap == 0;  // TRACE records are appended in execution order
-    const uint32_t S = dv->S;
 
-    // Candidate buffer: the next events of the schedule, in (t, seq) order, one
-    // per lane (cslot/csq), all at time tbuf.  Events a batch could not take
-    // stay here for the next iteration (they remain the queue's minimum: any
-    // later push at tbuf carries a larger seq).
-    uint32_t cslot = 0, csq = 0, nbuf = 0;
-    int64_t tbuf = 0;
-    const uint32_t cap = batching ? 64u : 1u;
-    for (uint32_t it = 0; it < budget && W.status == TW_REP_RUNNING; ++it) {
-        // ---- 1. candidates: the events at the minimum time
-        bool is_main = false;
-        int64_t t = 0;
-        if (pending_main) {  // runInSandbox main (TimedT.hs:237): runs at t=0 without a pop
+    bool alive = true;
+    for (uint32_t it = 0; it < budget && alive; ++it) {
+        URec th;
+        uint32_t slot = 0;
+        bool run = false;
+        if (pending_main) {  // runInSandbox main (TimedT.hs:237): runs at t=0, not a pop
             pending_main = 0;
-            is_main = true;
-            t = W.now;
-            cslot = 0;
-            nbuf = 1;
+            urec_load(W.hrec(0), dv->RQ, th);
+            W.hnode = th.w1;
+            run = true;
         } else {
-            if (W.live == 0) { nbuf = 0; W.status = TW_REP_DONE; break; }  // whileM_ notDone
-            if (W.d_ev >= ev_room) break;                                 // this call's event cap
-            uint32_t sq;
-            int src;
-            if (nbuf) t = tbuf;
-            else if (!W.peek_min(t, sq, src)) break;
-            if (t > t_end) break;                                         // parked beyond t_end
-            int64_t t2;
-            while (nbuf < cap && W.peek_min(t2, sq, src) && t2 == t) {
-                const uint32_t sl = W.pop_min(src);
-                cslot = lane == nbuf ? sl : cslot;
-                csq = lane == nbuf ? sq : csq;
-                ++nbuf;
+            if (W.live == 0) { W.status = TW_REP_DONE; break; }  // whileM_ notDone
+            if (W.d_ev >= ev_room) break;                        // this call's event cap
+            // PQ.minView: the near minimum or the far minimum
+            if (W.far_dirty) W.far_min();
+            const int src = W.fm_src;
+            const int64_t ft = W.fm_t;
+            const uint32_t fs = W.fm_s, fsl = W.fm_sl;
+            const bool use_near = W.near_n != 0;
+            const int64_t tn = W.nbase + (int64_t)(W.gmin >> 32);
+            const bool use_far = src >= 0 && (!use_near || tless(ft, fs, tn, (uint32_t)W.gmin));
+            if (!use_near && !use_far) break;
+            const int64_t t = use_far ? ft : tn;
+            const uint32_t sq = use_far ? fs : (uint32_t)W.gmin;
+            if (t > t_end) break;  // parked beyond t_end
+            if (use_far) {
+                slot = fsl;
+                if (src == TW_RUNS) W.heap_pop();
+                else W.run_pop(src);
+            } else {
+                slot = W.near_pop();
             }
-            tbuf = t;
-            W.now = t;  // curTime .= timestamp (TimedT.hs:241-247)
+            urec_load(W.hrec(slot), dv->RQ, th);
+            if (th.w3 != sq) continue;  // superseded by a throwTo re-stamp
+            th.w3 = 0;
+            --W.live;
+            W.now = t;                  // curTime .= timestamp (TimedT.hs:241-247)
             if (t - W.nbase > (int64_t)0x7FFFFFFF) W.near_rebase(t);
-        }
-        const uint32_t n = nbuf;
-        const bool cand = lane < n;
-        // ---- 2. records, liveness, class, footprint (loads for every lane: no branch)
-        LRec th;
-        lrec_load(W.hrec(cand ? cslot : 0u), dv->RQ, th);
-        const bool live_ev = cand && (is_main || th.w3 == csq);  // else superseded by a throwTo re-stamp
-        uint32_t cls = PC_LOCAL, fnode2 = 0xFFFFFFFFu;
-        {
-            uint32_t rpc = th.pc();
-            const uint32_t ex = is_main ? 0u : th.exc();
-            bool alone = false;
-            if (ex) {
-                alone = !(th.flags() & (F_STARTED | F_MAIN));  // escapes launchTimedT: ABORTED
-                uint32_t hp = 0xFFFFFFFFu;                     // no catching frame: the thread dies
-                const uint32_t nf = live_ev ? th.nfr() : 0u;
-                for (uint32_t i = nf; i-- > 0;) {
-                    const uint32_t f = i < 2 ? (i == 0 ? th.f0 : th.f1)
-                                             : *((uint32_t GAS*)(gp(dv->fx) + ((size_t)cslot * R + r) * dv->FXQ) + (i - 2));
-                    if ((f >> 16) & (1u << ex)) { hp = f & 0xFFFFu; break; }
-                }
-                rpc = hp;
-            }
-            const uint32_t c = rpc == 0xFFFFFFFFu ? (uint32_t)PC_LOCAL
-                             : rpc < dv->n_insns ? (uint32_t)gp(dv->pc_cls)[rpc] : (uint32_t)PC_ALONE;
-            cls = alone ? (uint32_t)PC_ALONE : c;
-            const uint64_t l = (uint64_t)th.r1;
-            fnode2 = (live_ev && cls == PC_DELIVER) ? (l < dv->L ? dv->link_dst[l] : th.w1) : 0xFFFFFFFFu;
-        }
-        const uint64_t live_m = __builtin_amdgcn_ballot_w64(live_ev);
-        uint32_t B = n;
-        if (live_m && n > 1) {
-            const uint32_t first = (uint32_t)__builtin_ctzll(live_m);
-            uint64_t brk = __builtin_amdgcn_ballot_w64(live_ev && lane > first && cls == PC_ALONE);
-            // footprints: the lowest lane claiming each node hash; a lane colliding
-            // with an earlier live lane ends the batch (hash collisions only shorten it)
-            const bool two = fnode2 != 0xFFFFFFFFu;
-            const uint32_t h1 = live_ev ? (th.w1 * 0x9E3779B1u) >> 24 : 256u;
-            const uint32_t h2 = two ? (fnode2 * 0x9E3779B1u) >> 24 : 256u;
-            ftab[h1] = 0xFFFFFFFFu;
-            ftab[h2] = 0xFFFFFFFFu;
-            __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
-            atomicMin(&ftab[h1], lane);
-            atomicMin(&ftab[h2], lane);
-            __builtin_amdgcn_s_waitcnt(0xC07F);
-            const bool coll = live_ev && (ftab[h1] < lane || (two && ftab[h2] < lane));
-            brk |= __builtin_amdgcn_ballot_w64(coll);
-            B = brk ? (uint32_t)__builtin_ctzll(brk) : n;
-            // capacity for the batch's worst case (every event forks and yields): else one event
-            const uint32_t nl = pc64(live_m & (B >= 64 ? ~0ull : (1ull << B) - 1));
-            const bool room = (S - W.bump) + W.free_n >= nl && W.tidc <= 0xFFFFFFFFu - nl &&
-                              W.seq <= 0xFFFFFFFFu - 2 * nl && rfl(cold.tmo) + nl <= dv->T &&
-                              W.d_ev + nl <= ev_room;
-            if (!room) B = first + 1;
-        }
-        const bool mine = live_ev && lane < B;
-        // ---- 3. the batch's thread steps, one per lane (divergent)
-        Eff e;
-        e.fin = W_NONE; e.yt = 0; e.cpc = e.cnode = 0; e.cra = 4; e.q0 = e.q1 = e.q2 = e.q3 = 0; e.tmo_a = 4;
-        e.hn0 = th.w1; e.hn1 = 0xFFFFFFFFu; e.h0 = e.h1 = 0; e.dl = e.dr = e.ud = 0;
-        e.st = TW_REP_RUNNING; e.mexc = 0; e.ntr = 0; e.freed = false;
-        thr[0] = 0;
-        LaneCtx<K> X{dv, r, lane, t, rfl(cold.tmo), rfl(cold.trn), nullptr};
-        if (mine) {
-            bool run = true;
-            if (!is_main) {
-                th.w3 = 0;
-                const uint32_t ex = th.exc();  // asyncExceptions . at tid <<.= Nothing (:252)
-                if (ex) {
-                    const int64_t val = (int64_t)(((uint64_t)th.xh << 32) | th.xl);
-                    th.set_exc(0);
-                    th.xl = th.xh = 0;
-                    e.h0 += term0(t, TW_KIND_EXC | ex);
-                    if (!(th.flags() & (F_STARTED | F_MAIN))) {  // escapes launchTimedT (:252-263)
-                        e.st = TW_REP_ABORTED;
-                        e.mexc = ex;
-                        e.fin = W_STOP;
-                        run = false;
-                    } else {
-                        run = X.unwind(th, cslot, ex, val, e);
-                        if (!run) e.fin = W_DIED;
-                    }
+            W.hnode = th.w1;
+            W.final_t = t;
+            ++W.d_ev;
+            const uint32_t exc = u_exc(th);  // asyncExceptions . at tid <<.= Nothing (:252)
+            if (exc) {
+                const int64_t val = (int64_t)(((uint64_t)th.xh << 32) | th.xl);
+                u_set_exc(th, 0);
+                th.xl = th.xh = 0;
+                W.hacc += term0(t, TW_KIND_EXC | exc);
+                if (!(u_flags(th) & (F_STARTED | F_MAIN))) {  // escapes launchTimedT (:252-263)
+                    W.status = TW_REP_ABORTED;
+                    cold.main_exc = exc;
+                    urec_store(W.hrec(slot), dv->RQ, th, 0, 4);
                 } else {
-                    e.h0 += term0(t, TW_KIND_RESUME | th.pc());
+                    run = W.unwind(th, slot, exc, val);
                 }
-            }
-            if (run) X.step(th, cslot, e, (int64_t LAS*)thr);
-        }
-        // ---- 4. commit in (t, seq) order: lanes up to the first event that failed
-        uint64_t bm = __builtin_amdgcn_ballot_w64(mine);
-        {
-            const uint64_t errm = __builtin_amdgcn_ballot_w64(mine && e.st != TW_REP_RUNNING);
-            if (errm) {
-                const uint32_t fl = (uint32_t)__builtin_ctzll(errm);
-                bm &= fl >= 63 ? ~0ull : (2ull << fl) - 1;
-                W.fail(rdl(e.st, fl));
+            } else {
+                W.hacc += term0(t, TW_KIND_RESUME | u_pc(th));
+                run = true;
             }
         }
-        const bool cm = (bm & me_bit) != 0;
-        const uint32_t nev = is_main ? 0u : pc64(bm);
-        W.d_ev += nev;
-        W.live -= nev;
-        if (nev) W.final_t = t;
-        cold.dl = rfl(cold.dl) + wave_sum(cm ? e.dl : 0u);
-        cold.dr = rfl(cold.dr) + wave_sum(cm ? e.dr : 0u);
-        cold.ud = rfl(cold.ud) + wave_sum(cm ? e.ud : 0u);
-        {
-            const uint64_t mx = __builtin_amdgcn_ballot_w64(cm && e.mexc);
-            if (mx) cold.main_exc = rdl(e.mexc, 63u - (uint32_t)__builtin_clzll(mx));
-            cold.trn = rfl(cold.trn) + wave_sum(cm ? e.ntr : 0u);
-        }
-        // deferred throws of a lone event, in program order, before its own pushes
-        if (bm) {
-            const uint32_t nthr = (uint32_t)rfl64s(thr[0]);
-            for (uint32_t k = 0; k < nthr; ++k)
-                W.throw_to(rfl64s(thr[1 + 3 * k]), (uint32_t)rfl64s(thr[2 + 3 * k]), rfl64s(thr[3 + 3 * k]));
-        }
-        // forks: slot, tid and timeout epoch, in lane order (a batch of more than
-        // one event was checked for room; a lone event fails like the sequential loop)
-        bool sp = cm && e.fin == W_SPAWN;
-        uint32_t csl = 0xFFFFFFFFu;
-        {
-            uint64_t m = __builtin_amdgcn_ballot_w64(sp);
-            while (m) {
-                const uint32_t l = (uint32_t)__builtin_ctzll(m);
-                m &= m - 1;
-                uint32_t s = 0xFFFFFFFFu;
-                const bool tm = rdl(e.tmo_a, l) < 4;
-                if (tm && rfl(cold.tmo) >= dv->T) W.fail(TW_REP_ERR_INSN);      // TMO_BEGIN: no epoch left
-                else if ((s = W.alloc_slot()) != 0xFFFFFFFFu && W.tidc == 0xFFFFFFFFu) {
-                    W.fail(TW_REP_ERR_COUNTER);                                 // getNextThreadId would wrap
-                    s = 0xFFFFFFFFu;
-                }
-                if (s != 0xFFFFFFFFu && tm) {
-                    const uint32_t ep = rfl(cold.tmo);
-                    cold.tmo = ep + 1;
-                    if (lane == l) { th.set_reg(e.tmo_a, ep); e.q1 = ep; }
-                    st8(gp(dv->tmo_done) + W.ix(ep), 0);
-                }
-                csl = lane == l ? s : csl;
-            }
-        }
-        if (sp && csl == 0xFFFFFFFFu) { sp = false; e.fin = W_STOP; }  // the fork failed (status set)
-        const uint64_t spm = __builtin_amdgcn_ballot_w64(sp);
-        const uint32_t tid = W.tidc + below(spm);
-        W.tidc += pc64(spm);
-        cold.d_th = rfl(cold.d_th) + pc64(spm);
-        const bool yl = cm && (e.fin == W_YIELD || sp);
-        if (sp) {
-            if (e.cra < 4) th.set_reg(e.cra, (int64_t)(((uint64_t)tid << 32) | csl));
-            e.yt = t + 1;  // the parent waits 1 µs (TimedT.hs:340)
-        }
-        // queue pushes in (t, seq) order: each forking lane's child, then its own wake
-        {
-            const uint64_t ym = __builtin_amdgcn_ballot_w64(yl);
-            const uint32_t tot = pc64(spm) + pc64(ym);
-            const uint32_t sbase = W.seq;
-            if (tot && sbase > 0xFFFFFFFFu - tot) W.fail(TW_REP_ERR_COUNTER);  // (a lone event near the top)
-            const uint32_t cnt = (sp ? 1u : 0u) + (yl ? 1u : 0u);
-            const uint32_t pre = below(spm) + below(ym);
-            uint32_t child_seq = sbase + pre + 1, own_seq = sbase + pre + cnt;
-            child_seq = child_seq < sbase ? 0xFFFFFFFFu : child_seq;
-            own_seq = own_seq < sbase ? 0xFFFFFFFFu : own_seq;
-            W.seq = sbase > 0xFFFFFFFFu - tot ? 0xFFFFFFFFu : sbase + tot;
-            const uint32_t mode = dv->tie_mode;
-            const uint32_t ckey = mode ? seq_key(mode, child_seq) : child_seq;
-            const uint32_t okey = mode ? seq_key(mode, own_seq) : own_seq;
-            bool c_on = false, o_on = false;
-            uint64_t m = spm | ym;
-            while (m) {
-                const uint32_t l = (uint32_t)__builtin_ctzll(m);
-                m &= m - 1;
-                if ((spm >> l) & 1) {
-                    const uint32_t k = rdl(ckey, l), s = rdl(csl, l);
-                    const bool on = W.near_fits(t);
-                    if (on) W.near_push(t, k, s);
-                    else if (!W.run_push(t, k, s)) W.heap_push(t, k, s);
-                    c_on = lane == l ? on : c_on;
-                }
-                if ((ym >> l) & 1) {
-                    const int64_t yt = rdl64s(e.yt, l);
-                    const uint32_t k = rdl(okey, l), s = rdl(cslot, l);
-                    const bool on = W.near_fits(yt);
-                    if (on) W.near_push(yt, k, s);
-                    else if (!W.run_push(yt, k, s)) W.heap_push(yt, k, s);
-                    o_on = lane == l ? on : o_on;
-                }
-            }
-            W.live += tot;
-            if (yl) {
-                th.w3 = okey;
-                th.w0 = o_on ? th.w0 | (F_NEARQ << FL_SHIFT) : th.w0 & ~(F_NEARQ << FL_SHIFT);
-            }
-            // records: children (whole), parents (whole, or the header of a thread that ended)
-            LRec ch;
-            ch.w0 = (e.cpc & 0xFFFFu) | (c_on ? F_NEARQ << FL_SHIFT : 0u);
-            ch.w1 = e.cnode; ch.w2 = tid; ch.w3 = ckey;
-            ch.f0 = ch.f1 = ch.xl = ch.xh = 0;
-            ch.r0 = e.q0; ch.r1 = e.q1; ch.r2 = e.q2; ch.r3 = e.q3;
-            lrec_store(W.hrec(sp ? csl : 0u), dv->RQ, ch, spm, 0, 4);
-            const uint64_t fullm = __builtin_amdgcn_ballot_w64(cm && (yl || e.fin == W_STOP));
-            lrec_store(W.hrec(cslot), dv->RQ, th, fullm, 0, 4);
-            const bool ends = cm && (e.fin == W_EXIT || e.fin == W_DIED);
-            if (cm && e.fin == W_EXIT) X.die(th, e);
-            const uint64_t endm = __builtin_amdgcn_ballot_w64(ends);
-            lrec_store(W.hrec(cslot), dv->RQ, th, endm, 0, 1);
-            uint64_t fm = endm;
-            while (fm) {
-                const uint32_t l = (uint32_t)__builtin_ctzll(fm);
-                fm &= fm - 1;
-                W.free_slot(rdl(cslot, l));
-            }
-        }
-        // hash terms (commutative sums), per lane
-        atom_add64((unsigned long long GAS*)(gp(dv->hash) + W.ix(e.hn0)), e.h0,
-                   __builtin_amdgcn_ballot_w64(cm && e.h0));
-        atom_add64((unsigned long long GAS*)(gp(dv->hash) + W.ix(e.hn1 == 0xFFFFFFFFu ? 0 : e.hn1)), e.h1,
-                   __builtin_amdgcn_ballot_w64(cm && e.hn1 != 0xFFFFFFFFu && e.h1));
-        // the candidates the batch did not take move down to lanes 0..
-        cslot = lane_down(cslot, B);
-        csq = lane_down(csq, B);
-        nbuf = n - B;
+        if (run) W.step(th, slot);
+        W.hash_flush();
+        alive = W.status == TW_REP_RUNNING;
     }
-    // candidates still buffered go back to the queue (same keys)
-    for (uint32_t l = 0; l < nbuf; ++l) W.push_back(tbuf, rdl(csq, l), rdl(cslot, l));
+    W.hash_flush();
     if (W.status == TW_REP_RUNNING && W.live == 0 && !pending_main) W.status = TW_REP_DONE;
 
     uint64_t* so = gp(dv->scal) + r;

@@ -73,6 +73,17 @@ class TwStats(C.Structure):
 
 
 # the fields a run produces (tie_flags is set by tw_tie_audit only)
+class TwLpState(C.Structure):
+    """tw_lp_state: the device-driven window loop's progress."""
+    _fields_ = [
+        ("windows", C.c_uint64),
+        ("ticks", C.c_uint64),
+        ("t", C.c_int64),
+        ("done", C.c_uint32),
+        ("err", C.c_uint32),
+    ]
+
+
 RESULT_FIELDS = ["final_t", "events", "delivered", "dropped", "undeliverable", "status", "main_exc", "threads"]
 
 # numpy dtype with the same layout as tw_replica_result (for bulk reads)

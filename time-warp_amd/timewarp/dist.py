@@ -143,6 +143,49 @@ def lp_loop(eng, starts: np.ndarray, lookahead_us: int, device=None, distributed
     return windows, kms
 
 
+def lp_loop_device(eng, world: int, rank: int, starts: np.ndarray, device=None, cap: int = 1 << 16,
+                   check_every: int = 16, max_ticks: int = 1 << 22):
+    """The device-driven window loop of one rank (tw_lp_tick ...): per tick the
+    event kernel + local delivery + packing, an all-to-all of fixed-size record
+    blocks, the import, an all-reduce(min) of {next time, -active lanes}, and
+    the device-side advance.  The host enqueues `check_every` ticks between
+    synchronisations (tw_lp_progress); no record ever goes through host memory.
+    `starts` has world + 1 entries.  Over the "nccl" backend the collectives
+    are RCCL on xGMI on the same stream as the engine's kernels.  Returns the
+    final tw_lp_state."""
+    import torch
+    import torch.distributed as dist
+
+    starts = np.asarray(starts, dtype=np.uint32)
+    if world == 1:
+        if device is not None:
+            eng.set_stream(torch.cuda.current_stream(device).cuda_stream)
+        eng.exchange_setup(1, 0, starts)
+        eng.loop_begin()
+        return eng.run_windows(max_ticks)
+    blk = (cap + 1) * 32
+    send = torch.zeros(world * blk, dtype=torch.uint8, device=device)
+    recv = torch.zeros_like(send)
+    red = torch.zeros(2, dtype=torch.int64, device=device)
+    eng.exchange_tensors(world, rank, starts, send, recv, cap, red)
+    eng.loop_begin()
+    ticks, st = 0, None
+    while ticks < max_ticks:
+        for _ in range(check_every):
+            eng.tick()
+            dist.all_to_all_single(recv, send)   # equal splits: block g -> rank g
+            eng.tick_import()
+            dist.all_reduce(red, op=dist.ReduceOp.MIN)
+            eng.tick_end()
+        ticks += check_every
+        st = eng.progress()
+        if st.err:
+            raise RuntimeError(f"device window loop: overflow bits {st.err} on rank {rank}")
+        if st.done:
+            break
+    return st
+
+
 def run_partitioned_dist(scn, lookahead_us=None, device_index: int = 0, max_windows: int = 1 << 20):
     """One scenario partitioned by node over all ranks (one GPU each):
     conservative windows [T, T+L), records exchanged by all-to-all, next T by

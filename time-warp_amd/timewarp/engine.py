@@ -16,7 +16,7 @@ from typing import Optional
 
 import numpy as np
 
-from .abi import RESULT_DTYPE, TwStats
+from .abi import RESULT_DTYPE, TwLpState, TwStats
 from .scenario import Scenario
 
 _PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -27,7 +27,9 @@ T_INF = (1 << 63) - 1
 EXPORTS = ["tw_create", "tw_load", "tw_reset", "tw_run", "tw_read_results", "tw_read_hashes", "tw_read_final",
            "tw_last_launch_ms", "tw_destroy", "tw_strerror", "tw_version",
            "tw_lp_load", "tw_lp_window", "tw_lp_take_outbox", "tw_lp_inject", "tw_lp_results",
-           "tw_set_trace", "tw_read_trace", "tw_tie_audit", "tw_set_counter_base", "tw_geometry"]
+           "tw_set_trace", "tw_read_trace", "tw_tie_audit", "tw_set_counter_base", "tw_geometry",
+           "tw_set_stream", "tw_lp_exchange_setup", "tw_lp_loop_begin", "tw_lp_tick", "tw_lp_tick_import",
+           "tw_lp_tick_end", "tw_lp_progress", "tw_lp_run_windows"]
 GEOMETRIES = ("dense", "sparse", "half", "wave", "lp")  # TW_GEO_* order
 
 # tw_trace_rec (include/timewarp.h)
@@ -55,6 +57,15 @@ def load_library(path: Optional[str] = None):
     p = path or os.environ.get("TW_LIB") or LIB_PATH
     if not os.path.exists(p):
         raise EngineError(f"HIP engine library missing: {p} (run __graft_entry__.build())")
+    # One HIP runtime per process: torch's wheel bundles libamdhip64.so.7 under
+    # the same soname as /opt/rocm's.  Loading torch first makes this library
+    # bind to that copy, so torch streams/tensors (tw_set_stream, the RCCL
+    # exchange buffers) and the engine share one runtime; loading the engine
+    # first would leave torch without a usable device.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     lib = C.CDLL(p)
     lib.tw_create.argtypes = [C.c_int, C.POINTER(C.c_void_p)]
     lib.tw_load.argtypes = [C.c_void_p, C.c_void_p]
@@ -78,10 +89,18 @@ def load_library(path: Optional[str] = None):
     lib.tw_tie_audit.argtypes = [C.c_void_p, C.c_int64, C.c_uint64, C.c_uint32, C.POINTER(TwStats)]
     lib.tw_set_counter_base.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32]
     lib.tw_geometry.argtypes = [C.c_void_p]
+    lib.tw_set_stream.argtypes = [C.c_void_p, C.c_void_p]
+    lib.tw_lp_exchange_setup.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p,
+                                         C.c_uint32, C.c_void_p]
+    for name in ("tw_lp_loop_begin", "tw_lp_tick", "tw_lp_tick_import", "tw_lp_tick_end"):
+        getattr(lib, name).argtypes = [C.c_void_p]
+    lib.tw_lp_progress.argtypes = [C.c_void_p, C.POINTER(TwLpState)]
+    lib.tw_lp_run_windows.argtypes = [C.c_void_p, C.c_uint64, C.POINTER(TwLpState)]
     for name in ("tw_create", "tw_load", "tw_reset", "tw_run", "tw_read_results", "tw_read_hashes", "tw_read_final",
                  "tw_last_launch_ms", "tw_lp_load", "tw_lp_window", "tw_lp_take_outbox", "tw_lp_inject",
                  "tw_lp_results", "tw_set_trace", "tw_read_trace", "tw_tie_audit", "tw_set_counter_base",
-                 "tw_geometry"):
+                 "tw_geometry", "tw_set_stream", "tw_lp_exchange_setup", "tw_lp_loop_begin", "tw_lp_tick",
+                 "tw_lp_tick_import", "tw_lp_tick_end", "tw_lp_progress", "tw_lp_run_windows"):
         getattr(lib, name).restype = C.c_int
     if path is None:
         _lib = lib
@@ -262,6 +281,56 @@ class LPEngine(Engine):
                                      C.byref(nt)), "tw_lp_inject")
         return nt.value
 
+    # ---- device-driven windows (tw_lp_tick ...): no host round trip per window
+    def set_stream(self, hip_stream: int):
+        """Run every later kernel on the caller's HIP stream (0: the context's own)."""
+        _check(self.lib.tw_set_stream(self.ctx, C.c_void_p(hip_stream or None)), "tw_set_stream")
+        return self
+
+    def exchange_setup(self, world: int, rank: int, starts, send_ptr: int = 0, recv_ptr: int = 0, cap: int = 0,
+                       red_ptr: int = 0):
+        """starts: world + 1 node boundaries; buffers are device pointers
+        (world * (cap + 1) * 32 bytes each; red: 2 int64)."""
+        st = np.ascontiguousarray(starts, dtype=np.uint32)
+        _check(self.lib.tw_lp_exchange_setup(self.ctx, world, rank, st.ctypes.data, C.c_void_p(send_ptr or None),
+                                             C.c_void_p(recv_ptr or None), cap, C.c_void_p(red_ptr or None)),
+               "tw_lp_exchange_setup")
+        return self
+
+    def exchange_tensors(self, world: int, rank: int, starts, send, recv, cap: int, red):
+        """exchange_setup over torch device tensors (the RCCL buffers); the
+        engine then runs on torch's current stream, where the collectives go."""
+        import torch
+
+        self.set_stream(torch.cuda.current_stream(send.device).cuda_stream)
+        self._ex_keep = (send, recv, red)  # the library holds raw pointers
+        return self.exchange_setup(world, rank, starts, send.data_ptr(), recv.data_ptr(), cap, red.data_ptr())
+
+    def loop_begin(self):
+        _check(self.lib.tw_lp_loop_begin(self.ctx), "tw_lp_loop_begin")
+        return self
+
+    def tick(self):
+        _check(self.lib.tw_lp_tick(self.ctx), "tw_lp_tick")
+
+    def tick_import(self):
+        _check(self.lib.tw_lp_tick_import(self.ctx), "tw_lp_tick_import")
+
+    def tick_end(self):
+        _check(self.lib.tw_lp_tick_end(self.ctx), "tw_lp_tick_end")
+
+    def progress(self) -> TwLpState:
+        st = TwLpState()
+        _check(self.lib.tw_lp_progress(self.ctx, C.byref(st)), "tw_lp_progress")
+        return st
+
+    def run_windows(self, max_ticks: int = 1 << 20) -> TwLpState:
+        """Single context: the whole window loop on the device, one host
+        synchronisation per 16 ticks."""
+        st = TwLpState()
+        _check(self.lib.tw_lp_run_windows(self.ctx, max_ticks, C.byref(st)), "tw_lp_run_windows")
+        return st
+
     def lp_results(self):
         agg = np.zeros(1, RESULT_DTYPE)
         h = np.zeros(self.scn.n_nodes, np.uint64)
@@ -276,6 +345,23 @@ def lp_scenario(scn: Scenario, max_slots: int = 32, queue_capacity: int = 64) ->
     s = copy.copy(scn)
     s.max_slots, s.queue_capacity, s.run_capacity = max_slots, queue_capacity, 0
     return s
+
+
+def _combine(engines, n_nodes: int):
+    """Aggregate of the contexts' results: max times, summed counts, summed hashes."""
+    agg, hashes = None, np.zeros(n_nodes, np.uint64)
+    for e in engines:
+        a, h = e.lp_results()
+        hashes += h
+        if agg is None:
+            agg = a.copy()
+        else:
+            agg["final_t"] = max(agg["final_t"], a["final_t"])
+            for f in ("events", "delivered", "dropped", "undeliverable", "threads"):
+                agg[f] += a[f]
+            agg["main_exc"] = max(agg["main_exc"], a["main_exc"])
+            agg["status"] = max(agg["status"], a["status"])
+    return agg, hashes
 
 
 def run_partitioned(scn: Scenario, parts: int = 1, lookahead_us: Optional[int] = None, device: int = 0,
@@ -308,19 +394,72 @@ def run_partitioned(scn: Scenario, parts: int = 1, lookahead_us: Optional[int] =
                         nexts[i] = min(nexts[i], e.inject(mine))
             T = min(nexts)
             windows += 1
-        agg, hashes = None, np.zeros(N, np.uint64)
-        for e in engines:
-            a, h = e.lp_results()
-            hashes += h
-            if agg is None:
-                agg = a.copy()
-            else:
-                agg["final_t"] = max(agg["final_t"], a["final_t"])
-                for f in ("events", "delivered", "dropped", "undeliverable", "threads"):
-                    agg[f] += a[f]
-                agg["main_exc"] = max(agg["main_exc"], a["main_exc"])
-                agg["status"] = max(agg["status"], a["status"])
+        agg, hashes = _combine(engines, N)
         return agg, hashes, windows
     finally:
         for e in engines:
+            e.close()
+
+
+def run_partitioned_device(scn: Scenario, parts: int = 1, lookahead_us: Optional[int] = None, device: int = 0,
+                           cap: int = 1 << 16, check_every: int = 16, max_ticks: int = 1 << 20):
+    """The device-driven window loop (tw_lp_tick ...) over `parts` contexts of
+    one process on one GPU.  Between the contexts' ticks, the block exchange an
+    RCCL all-to-all does between GPUs is done with device copies, and the
+    all-reduce(min) of the reduction words with a device min: everything stays
+    on one stream, with one host synchronisation per `check_every` ticks.
+    parts == 1 uses tw_lp_run_windows.  Returns (aggregate, node hashes,
+    windows, ticks)."""
+    import torch
+
+    L = int(lookahead_us if lookahead_us is not None else scn.meta["lookahead_us"])
+    s = lp_scenario(scn)
+    N = scn.n_nodes
+    bounds = [(i * N // parts, (i + 1) * N // parts) for i in range(parts)]
+    starts = np.array([b0 for b0, _ in bounds] + [N], dtype=np.uint32)
+    engines = [LPEngine(s, b0, b1 - b0, L, device) for b0, b1 in bounds]
+    try:
+        for e in engines:
+            e.reset()
+        if parts == 1:
+            e = engines[0].loop_begin()
+            st = e.run_windows(max_ticks)
+            agg, hashes = _combine(engines, N)
+            return agg, hashes, st.windows, st.ticks
+        dev = torch.device("cuda", device)
+        stream = torch.cuda.current_stream(dev)
+        blk = (cap + 1) * 32
+        send = [torch.zeros(parts * blk, dtype=torch.uint8, device=dev) for _ in range(parts)]
+        recv = [torch.zeros(parts * blk, dtype=torch.uint8, device=dev) for _ in range(parts)]
+        red = [torch.zeros(2, dtype=torch.int64, device=dev) for _ in range(parts)]
+        for g, e in enumerate(engines):
+            e.set_stream(stream.cuda_stream)
+            e.exchange_setup(parts, g, starts, send[g].data_ptr(), recv[g].data_ptr(), cap, red[g].data_ptr())
+            e.loop_begin()
+        ticks = 0
+        while ticks < max_ticks:
+            for _ in range(check_every):
+                for e in engines:
+                    e.tick()
+                for g in range(parts):        # all-to-all: block g of src -> block src of g
+                    for src in range(parts):
+                        recv[g][src * blk:(src + 1) * blk].copy_(send[src][g * blk:(g + 1) * blk])
+                for e in engines:
+                    e.tick_import()
+                m = torch.stack(red).min(dim=0).values   # all-reduce(min)
+                for r in red:
+                    r.copy_(m)
+                for e in engines:
+                    e.tick_end()
+            ticks += check_every
+            st = engines[0].progress()
+            if st.err or any(e.progress().err for e in engines[1:]):
+                raise EngineError(f"device window loop: overflow bits {st.err}")
+            if st.done:
+                break
+        agg, hashes = _combine(engines, N)
+        return agg, hashes, st.windows, st.ticks
+    finally:
+        for e in engines:
+            e.set_stream(0) if e.ctx else None
             e.close()

@@ -26,6 +26,9 @@ for s in "$@"; do
     benchq) step benchq 300 python bench.py --steps 2 --no-cpu-baseline ;;
     bench_c2) step bench_c2 400 python bench.py --config ping_pong ;;
     bench_c4) step bench_c4 500 python bench.py --config gossip ;;
+    benchq_c4) step benchq_c4 300 python bench.py --config gossip --steps 2 --warmup 1 --no-cpu-baseline ;;
+    benchq_c4h) step benchq_c4h 300 python bench.py --config gossip --steps 2 --warmup 1 --no-cpu-baseline --host-windows ;;
+    gossip) step gossip 400 python -u -m pytest tests/test_gpu_gossip.py -q -m gpu -x --timeout 120 --timeout-method thread ;;
     bench_c5) step bench_c5 400 python bench.py --config hotspot ;;
     benchq_c5) step benchq_c5 400 python bench.py --config hotspot --steps 2 --warmup 1 --no-cpu-baseline ;;
     benchq_c3_8k) step benchq_c3_8k 300 python bench.py --replicas 8192 --steps 2 --warmup 1 --no-cpu-baseline ;;
