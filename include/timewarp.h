@@ -317,13 +317,15 @@ int tw_tie_audit(tw_ctx* ctx, int64_t t_end_us, uint64_t max_events, uint32_t pr
 int tw_set_counter_base(tw_ctx* ctx, uint32_t seq0, uint32_t tid0);
 
 /* Kernel geometry of the loaded scenario, chosen by tw_load from the replica
- * count (environment TW_GEOMETRY=dense|sparse|half|wave overrides):
+ * count (environment TW_GEOMETRY=dense|sparse|half|wave|narrow overrides):
  *   DENSE  one lane per replica, 256 replicas per workgroup (many replicas);
  *   SPARSE one lane per replica, 16 per workgroup, large on-chip queue;
  *   HALF   the dense layout as two 32-lane waves per SIMD (an experiment);
  *   WAVE   one wavefront per replica: lane-parallel queue (few replicas);
+ *   NARROW the dense layout with 8 replicas per wave (few replicas: one
+ *          wave per SIMD);
  *   LP     node-partitioned mode (tw_lp_load). */
-enum { TW_GEO_DENSE = 0, TW_GEO_SPARSE = 1, TW_GEO_HALF = 2, TW_GEO_WAVE = 3, TW_GEO_LP = 4 };
+enum { TW_GEO_DENSE = 0, TW_GEO_SPARSE = 1, TW_GEO_HALF = 2, TW_GEO_WAVE = 3, TW_GEO_LP = 4, TW_GEO_NARROW = 5 };
 int tw_geometry(tw_ctx* ctx);
 
 /* Duration (ms) of every event-kernel launch of the last tw_run, measured with

@@ -56,6 +56,12 @@
 // one wave's scalar, LDS and branch issue overlaps the other's VALU and
 // memory waits.
 #define TW_HALF_LANES 32
+// narrow geometry (few replicas, e.g. C3 sharded 8 ways = 8192 per GPU): the
+// dense layout and near heap with TW_NARROW replicas per workgroup, one wave of
+// TW_NARROW active lanes, so the replicas spread one wave per SIMD
+#ifndef TW_NARROW
+#define TW_NARROW 8
+#endif
 #define TW_STEP_CAP (1u << 22)  // instructions per thread step (== oracle kStepCap)
 // store only the record quads an event changed (1), or the whole record of a
 // thread that stays queued (0, the default).  C3, quad-major records, r02:
@@ -1540,8 +1546,7 @@ __global__ void __launch_bounds__(TW_WG) tw_init_kernel(Dev c, uint32_t main_pc,
         gp(c.bind_rel)[r] = 0xFFFFFFFEu;
         if (listen_init) gp(c.bind)[r] = listen_init[g];
         gp(c.inbox_n)[r] = 0;
-        gp(c.listed)[r] = 0;
-        gp(c.act)[(size_t)c.R + r] = r;  // list 1 = every node: the first window scans them all
+        gp(c.listed)[r] = 0;  // marked for the first window: it serves every node
         return;
     }
     if (nv_init)
@@ -1658,7 +1663,9 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
         uint32_t rh4[TW_RUNS];
 #pragma unroll
         for (int j = 0; j < TW_RUNS; ++j) {
-            const uint32_t rh = (uint32_t)sc[(SC_RH0 + j) * R], rn = (uint32_t)sc[(SC_RC0 + j) * R];
+            // (no far runs configured, e.g. LP nodes: nothing to load)
+            const uint32_t rh = c.Cr ? (uint32_t)sc[(SC_RH0 + j) * R] : 0u;
+            const uint32_t rn = c.Cr ? (uint32_t)sc[(SC_RC0 + j) * R] : 0u;
             rh4[j] = rh;
             uint4 h = make_uint4(0, 0, 0, 0), s2 = h, u = h;
             if (rn) {
@@ -1869,7 +1876,7 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
     sc[SC_EVENTS * R] = events0 + L.d_ev;
     sc[SC_DELIVERED * R] += L.cg(CW_DL); sc[SC_DROPPED * R] += L.cg(CW_DR);
     sc[SC_UNDELIV * R] += L.cg(CW_UD); sc[SC_THREADS * R] += L.d_th;
-    {
+    if (c.Cr) {
         const uint4 ix4 = *L.rqp(RQ_IDX);
 #pragma unroll
         for (int j = 0; j < TW_RUNS; ++j) {
@@ -2032,12 +2039,61 @@ __global__ void tw_lp_ctl(Dev c, const int64_t* red, uint4* send, uint32_t world
     const uint32_t act = (uint32_t)w[WN_ACT] ^ 1u;
     w[WN_ACT] = act;
     w[WN_WID] += 1;
-    gp(c.act_n)[act ^ 1u] = 0;
+    gp(c.act_n)[act] = 0;  // tw_lp_compact builds it next
     w[WN_REC_MIN] = (int64_t)~0ull;
     w[WN_FLAGS] = WN_FRESH;
 }
-// loop start after tw_reset: the first window serves every node (list 1), as
-// the host loop's first tw_lp_window does
+// The window's work list: every node marked during the previous window
+// (listed[r] == mark), in node order inside each block of TW_CPT * 256 nodes
+// (so the lanes' [field][node] state accesses coalesce); one atomic per block
+// claims its span of the list.  Device loop (c.win): only at a window's first
+// tick, with mark/list from the window words.
+#define TW_CPT 16
+__global__ void __launch_bounds__(256) tw_lp_compact(Dev c, uint32_t mark, uint32_t dst) {
+    if (c.win) {
+        const int64_t GAS* w = gp(c.win);
+        const int64_t fl = w[WN_FLAGS];
+        if (!(fl & WN_FRESH) || (fl & WN_DONE)) return;
+        mark = (uint32_t)w[WN_WID] - 1u;
+        dst = (uint32_t)w[WN_ACT];
+    }
+    __shared__ uint32_t cnt[TW_CPT * 4];
+    __shared__ uint32_t base;
+    const uint32_t wv = threadIdx.x >> 6;
+    const size_t r0 = (size_t)blockIdx.x * TW_CPT * 256 + threadIdx.x;
+    uint64_t ms[TW_CPT];
+#pragma unroll
+    for (int i = 0; i < TW_CPT; ++i) {
+        const size_t r = r0 + (size_t)i * 256;
+        ms[i] = __builtin_amdgcn_ballot_w64(r < c.R && gp(c.listed)[r] == mark);
+        if (__lane_id() == 0) cnt[i * 4 + wv] = (uint32_t)__builtin_popcountll(ms[i]);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t run = 0;
+        for (int k = 0; k < TW_CPT * 4; ++k) {
+            const uint32_t n = cnt[k];
+            cnt[k] = run;
+            run += n;
+        }
+        base = run ? __hip_atomic_fetch_add(gp(c.act_n) + dst, run, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+    }
+    __syncthreads();
+    const uint32_t b0 = base;
+#pragma unroll
+    for (int i = 0; i < TW_CPT; ++i) {
+        const uint64_t m = ms[i];
+        if ((m >> __lane_id()) & 1ull) {
+            const uint32_t below =
+                __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+            gp(c.act)[(size_t)dst * c.R + b0 + cnt[i * 4 + wv] + below] = (uint32_t)(r0 + (size_t)i * 256);
+        }
+    }
+}
+static uint32_t compact_blocks(uint32_t R) { return (R + TW_CPT * 256 - 1) / (TW_CPT * 256); }
+
+// loop start after tw_reset: the window words; the first window's list
+// (every node: tw_reset marks them all 0) is compacted next
 __global__ void tw_lp_begin(Dev c, int64_t lookahead) {
     int64_t GAS* w = gp(c.win);
     w[WN_T] = 0;
@@ -2048,7 +2104,7 @@ __global__ void tw_lp_begin(Dev c, int64_t lookahead) {
     w[WN_FLAGS] = WN_FRESH;
     w[WN_ACT] = 1;
     w[WN_WID] = 1;
-    gp(c.act_n)[0] = 0;
+    gp(c.act_n)[1] = 0;
     *gp(c.out_n) = 0;
     *gp(c.n_active) = 0;
     *gp(c.next_t) = ~0ull;
@@ -2090,7 +2146,6 @@ struct tw_ctx {
     uint4* staging = nullptr;      // inject staging [out_cap][2]
     std::vector<double> launch_ms;
     std::vector<hipEvent_t> ev_pool;
-    uint32_t act_n_init[2] = {0, 0};
     std::vector<uint32_t> tie_flags;  // tw_tie_audit, per replica
     Dev* d_dev = nullptr;             // device copy of d (the wave kernel reads it through the scalar cache)
     uint32_t seq0 = 0, tid0 = 1;      // tw_set_counter_base
@@ -2345,11 +2400,13 @@ static int load_common(tw_ctx* c, const tw_scenario_desc* s, bool lp, uint32_t l
         if (g && !strcmp(g, "sparse")) geo = 1;
         if (g && !strcmp(g, "half")) geo = 2;
         if (g && !strcmp(g, "wave")) geo = 3;
+        if (g && !strcmp(g, "narrow")) geo = 5;
         if (lp) geo = 0;
         if (geo == 1 && fixed_lds_bytes<TW_WG_SPARSE, TW_NEAR_SPARSE>() + prog_lds > 160 * 1024) geo = 0;
         c->geo = geo;
     }
-    c->lds_bytes = (c->geo == 1 ? fixed_lds_bytes<TW_WG_SPARSE, TW_NEAR_SPARSE>()
+    c->lds_bytes = (c->geo == 1   ? fixed_lds_bytes<TW_WG_SPARSE, TW_NEAR_SPARSE>()
+                    : c->geo == 5 ? fixed_lds_bytes<TW_NARROW, TW_NEAR_CAP>()
                                   : fixed_lds_bytes<TW_WG, TW_NEAR_CAP>()) +
                    prog_lds;
     if (c->geo == 3) c->lds_bytes = 0;  // the wave kernel reads the program image through the scalar cache
@@ -2360,6 +2417,9 @@ static int load_common(tw_ctx* c, const tw_scenario_desc* s, bool lp, uint32_t l
                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)c->lds_bytes));
     else if (c->geo == 2)
         HIPCHK(hipFuncSetAttribute((const void*)tw_run_kernel<false, TW_WG, TW_NEAR_CAP, TW_HALF_LANES>,
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)c->lds_bytes));
+    else if (c->geo == 5)
+        HIPCHK(hipFuncSetAttribute((const void*)tw_run_kernel<false, TW_NARROW, TW_NEAR_CAP, TW_NARROW>,
                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)c->lds_bytes));
     else if (lp)
         HIPCHK(hipFuncSetAttribute((const void*)tw_run_kernel<true, TW_WG, TW_NEAR_CAP>,
@@ -2495,9 +2555,7 @@ int tw_reset(tw_ctx* c) {
         HIPCHK(hipMemsetAsync(c->n_foreign, 0, 4, st));
         c->d.act_cur = 0;
         c->d.wid = 0;
-        c->act_n_init[0] = 0;
-        c->act_n_init[1] = (uint32_t)R;
-        HIPCHK(hipMemcpyAsync(d.act_n, c->act_n_init, 8, hipMemcpyHostToDevice, st));
+        HIPCHK(hipMemsetAsync(d.act_n, 0, 8, st));
     }
     uint32_t blocks = (uint32_t)((R + TW_WG - 1) / TW_WG);
     hipLaunchKernelGGL(tw_init_kernel, dim3(blocks), dim3(TW_WG), 0, st, d, c->main_pc, c->main_node,
@@ -2529,8 +2587,10 @@ int tw_run(tw_ctx* c, int64_t t_end_us, uint64_t max_events, tw_stats* out) {
         // a new window: serve the list built since the last call (nodes with a
         // live thread or new records); start an empty one for the next call
         c->d.act_cur ^= 1u;
+        HIPCHK(hipMemsetAsync(d.act_n + c->d.act_cur, 0, 4, st));
+        hipLaunchKernelGGL(tw_lp_compact, dim3(compact_blocks(d.R)), dim3(256), 0, st, c->d, c->d.wid, c->d.act_cur);
+        HIPCHK(hipGetLastError());
         c->d.wid += 1u;
-        HIPCHK(hipMemsetAsync(d.act_n + (c->d.act_cur ^ 1u), 0, 4, st));
     }
     const uint32_t budget = 1u << 14;  // pops per lane per launch: bounded kernel time
     // launches between host checks: a replica run needs several budgets; an LP
@@ -2558,6 +2618,8 @@ int tw_run(tw_ctx* c, int64_t t_end_us, uint64_t max_events, tw_stats* out) {
                 launch_run<false, TW_WG_SPARSE, TW_NEAR_SPARSE>(c, st, t_end_us, limit, budget);
             else if (c->geo == 2)
                 launch_run<false, TW_WG, TW_NEAR_CAP, TW_HALF_LANES>(c, st, t_end_us, limit, budget);
+            else if (c->geo == 5)
+                launch_run<false, TW_NARROW, TW_NEAR_CAP, TW_NARROW>(c, st, t_end_us, limit, budget);
             else
                 launch_run<false, TW_WG, TW_NEAR_CAP>(c, st, t_end_us, limit, budget);
             HIPCHK(hipGetLastError());
@@ -2840,6 +2902,8 @@ int tw_lp_loop_begin(tw_ctx* c) {
     c->d.wid = 0;
     hipLaunchKernelGGL(tw_lp_begin, dim3(1), dim3(1), 0, c->stream, c->dwin(), c->d.lookahead);
     HIPCHK(hipGetLastError());
+    hipLaunchKernelGGL(tw_lp_compact, dim3(compact_blocks(c->d.R)), dim3(256), 0, c->stream, c->dwin(), 0u, 0u);
+    HIPCHK(hipGetLastError());
     HIPCHK(hipMemsetAsync(c->d.lp_err, 0, 4, c->stream));
     c->loop_ready = true;
     return TW_OK;
@@ -2889,6 +2953,8 @@ int tw_lp_tick_end(tw_ctx* c) {
     HIPCHK(hipSetDevice(c->device));
     hipLaunchKernelGGL(tw_lp_ctl, dim3(1), dim3(1), 0, c->stream, c->dwin(), (const int64_t*)c->ex_red, c->ex_send,
                        c->ex_world, c->ex_cap);
+    HIPCHK(hipGetLastError());
+    hipLaunchKernelGGL(tw_lp_compact, dim3(compact_blocks(c->d.R)), dim3(256), 0, c->stream, c->dwin(), 0u, 0u);
     HIPCHK(hipGetLastError());
     return TW_OK;
 }

@@ -119,8 +119,9 @@ struct Dev {
     uint64_t* next_t;    // [1] min next-event time (atomicMin)
     uint32_t* lp_err;    // [1] inbox/outbox overflow
     // LP work lists: a launch serves only the nodes of list act_cur (those with
-    // a live thread or new delivery records); nodes join list act_cur ^ 1 for
-    // the next window at most once (listed[node] == wid)
+    // a live thread or new delivery records); during window wid a node is
+    // marked listed[node] = wid, and the next window's list is compacted from
+    // the marks (tw_lp_compact)
     uint32_t* act;       // [2][R]
     uint32_t* act_n;     // [2]
     uint32_t* listed;    // [R]
@@ -159,16 +160,14 @@ __device__ __forceinline__ int64_t tx_us(const Dev& c, uint64_t link, uint32_t k
     return (int64_t)(((uint64_t)gp(c.msg_bytes)[kind] * 1000000ull + bw - 1) / bw);
 }
 
-// LP: node r joins the next window's work list (once per window)
+// LP device-driven window words (Dev::win)
 enum { WN_T, WN_L, WN_REC_MIN, WN_WINDOWS, WN_TICKS, WN_FLAGS, WN_ACT, WN_WID, WN_COUNT };
 enum : int64_t { WN_FRESH = 1, WN_DONE = 2 };
 
+// mark node r for the next window's work list (tw_lp_compact builds the list
+// from the marks, in node order within each wave: coalesced node state)
 __device__ __forceinline__ void lp_list_next(const Dev& c, uint32_t r) {
-    if (__hip_atomic_exchange(gp(c.listed) + r, c.wid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != c.wid) {
-        const uint32_t nx = c.act_cur ^ 1u;
-        const uint32_t k = __hip_atomic_fetch_add(gp(c.act_n) + nx, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        gp(c.act)[(size_t)nx * c.R + k] = r;
-    }
+    gp(c.listed)[r] = c.wid;
 }
 
 // ------------------------------------------------------------------ hashing

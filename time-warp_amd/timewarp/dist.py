@@ -158,11 +158,13 @@ def lp_loop_device(eng, world: int, rank: int, starts: np.ndarray, device=None, 
 
     starts = np.asarray(starts, dtype=np.uint32)
     if world == 1:
-        if device is not None:
-            eng.set_stream(torch.cuda.current_stream(device).cuda_stream)
-        eng.exchange_setup(1, 0, starts)
+        eng.exchange_setup(1, 0, starts)  # the context's own stream; run_windows synchronises it
         eng.loop_begin()
         return eng.run_windows(max_ticks)
+    if device is not None and torch.cuda.current_stream(device).cuda_stream == 0:
+        # the engine and the collectives need one ordered, non-default stream
+        with torch.cuda.stream(torch.cuda.Stream(device)):
+            return lp_loop_device(eng, world, rank, starts, device, cap, check_every, max_ticks)
     blk = (cap + 1) * 32
     send = torch.zeros(world * blk, dtype=torch.uint8, device=device)
     recv = torch.zeros_like(send)

@@ -30,7 +30,7 @@ EXPORTS = ["tw_create", "tw_load", "tw_reset", "tw_run", "tw_read_results", "tw_
            "tw_set_trace", "tw_read_trace", "tw_tie_audit", "tw_set_counter_base", "tw_geometry",
            "tw_set_stream", "tw_lp_exchange_setup", "tw_lp_loop_begin", "tw_lp_tick", "tw_lp_tick_import",
            "tw_lp_tick_end", "tw_lp_progress", "tw_lp_run_windows"]
-GEOMETRIES = ("dense", "sparse", "half", "wave", "lp")  # TW_GEO_* order
+GEOMETRIES = ("dense", "sparse", "half", "wave", "lp", "narrow")  # TW_GEO_* order
 
 # tw_trace_rec (include/timewarp.h)
 TRACE_DTYPE = np.dtype([("t", np.int64), ("val", np.int64), ("node", np.uint32), ("tag", np.uint32)])
@@ -164,7 +164,7 @@ class Engine:
         d = scn.desc()
         old = os.environ.get("TW_GEOMETRY")
         if geometry is not None:
-            if geometry not in ("dense", "sparse", "half", "wave"):
+            if geometry not in ("dense", "sparse", "half", "wave", "narrow"):
                 raise ValueError(f"geometry must be 'dense', 'sparse', 'half' or 'wave', not {geometry!r}")
             os.environ["TW_GEOMETRY"] = geometry
         try:
@@ -302,7 +302,12 @@ class LPEngine(Engine):
         engine then runs on torch's current stream, where the collectives go."""
         import torch
 
-        self.set_stream(torch.cuda.current_stream(send.device).cuda_stream)
+        cur = torch.cuda.current_stream(send.device).cuda_stream
+        if not cur:
+            # the legacy default stream: tw_set_stream(NULL) would mean the
+            # context's own (non-blocking) stream, unordered with torch's work
+            raise EngineError("exchange_tensors: run under a non-default torch stream (torch.cuda.stream(s))")
+        self.set_stream(cur)
         self._ex_keep = (send, recv, red)  # the library holds raw pointers
         return self.exchange_setup(world, rank, starts, send.data_ptr(), recv.data_ptr(), cap, red.data_ptr())
 
@@ -427,7 +432,9 @@ def run_partitioned_device(scn: Scenario, parts: int = 1, lookahead_us: Optional
             agg, hashes = _combine(engines, N)
             return agg, hashes, st.windows, st.ticks
         dev = torch.device("cuda", device)
-        stream = torch.cuda.current_stream(dev)
+        stream = torch.cuda.Stream(dev)  # not the legacy default stream (cuda_stream 0)
+        ctx = torch.cuda.stream(stream)
+        ctx.__enter__()
         blk = (cap + 1) * 32
         send = [torch.zeros(parts * blk, dtype=torch.uint8, device=dev) for _ in range(parts)]
         recv = [torch.zeros(parts * blk, dtype=torch.uint8, device=dev) for _ in range(parts)]
@@ -457,9 +464,10 @@ def run_partitioned_device(scn: Scenario, parts: int = 1, lookahead_us: Optional
                 raise EngineError(f"device window loop: overflow bits {st.err}")
             if st.done:
                 break
+        stream.synchronize()
+        ctx.__exit__(None, None, None)
         agg, hashes = _combine(engines, N)
         return agg, hashes, st.windows, st.ticks
     finally:
         for e in engines:
-            e.set_stream(0) if e.ctx else None
             e.close()

@@ -28,6 +28,8 @@ for s in "$@"; do
     bench_c4) step bench_c4 500 python bench.py --config gossip ;;
     benchq_c4) step benchq_c4 300 python bench.py --config gossip --steps 2 --warmup 1 --no-cpu-baseline ;;
     benchq_c4h) step benchq_c4h 300 python bench.py --config gossip --steps 2 --warmup 1 --no-cpu-baseline --host-windows ;;
+    prof_c4) step prof_c4 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_c4 -o run -- python3 bench.py --config gossip --steps 2 --warmup 1 --no-cpu-baseline ;;
+    prof_c3) step prof_c3 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_c3 -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline ;;
     gossip) step gossip 400 python -u -m pytest tests/test_gpu_gossip.py -q -m gpu -x --timeout 120 --timeout-method thread ;;
     bench_c5) step bench_c5 400 python bench.py --config hotspot ;;
     benchq_c5) step benchq_c5 400 python bench.py --config hotspot --steps 2 --warmup 1 --no-cpu-baseline ;;
