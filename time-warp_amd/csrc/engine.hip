@@ -56,11 +56,13 @@
 // one wave's scalar, LDS and branch issue overlaps the other's VALU and
 // memory waits.
 #define TW_HALF_LANES 32
-// narrow geometry (few replicas, e.g. C3 sharded 8 ways = 8192 per GPU): the
-// dense layout and near heap with TW_NARROW replicas per workgroup, one wave of
-// TW_NARROW active lanes, so the replicas spread one wave per SIMD
+// narrow geometry (fewer replicas than fill the GPU, e.g. C3 sharded 8 ways =
+// 8192 per GPU): the dense layout and near heap with TW_NARROW replicas per
+// workgroup and one wave per workgroup, so the waves spread over all CUs.
+// C3 at 8192 replicas, G events/s by lanes per wave: 8: 1.47, 16: 1.88,
+// 32: 2.19, 64: 2.51 (dense, 4 waves per workgroup: 2.35)
 #ifndef TW_NARROW
-#define TW_NARROW 8
+#define TW_NARROW 64
 #endif
 #define TW_STEP_CAP (1u << 22)  // instructions per thread step (== oracle kStepCap)
 // store only the record quads an event changed (1), or the whole record of a
@@ -1682,16 +1684,35 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
         *L.rqp(RQ_IDX) = make_uint4(rh4[0], rh4[1], rh4[2], rh4[3]);
     }
     L.far_min();
-    // near heap: re-inserted from the spill area (keys are relative to this launch's base)
+    // near heap: the spill area holds heap positions [0, near_n) verbatim with
+    // absolute times; re-keyed to this launch's base (a common shift keeps the
+    // heap order) they go back in place, without sifting.  An entry too far
+    // ahead for a 32-bit key (or an oversized spill) takes the pushing path.
     L.nbase = L.now;
     L.near_init();
-    for (uint32_t j = 0; j < near_n0; ++j) {
-        uint4 e = gp(c.near_spill)[(size_t)j * R + r];
-        if (L.near_n < NC && (uint64_t)(ent_t(e) - L.nbase) < 0xFFFFFFFFull) {
-            L.near_push(ent_t(e), e.w, e.z);
-            continue;
+    {
+        bool fits = near_n0 <= (uint32_t)NC;
+        for (uint32_t j = 0; j < near_n0 && fits; ++j)
+            fits = (uint64_t)(ent_t(gp(c.near_spill)[(size_t)j * R + r]) - L.nbase) < 0xFFFFFFFFull;
+        if (fits) {
+            for (uint32_t j = 0; j < near_n0; ++j) {
+                const uint4 e = gp(c.near_spill)[(size_t)j * R + r];
+                L.nk[j * WG] = L.nkey(ent_t(e), e.w);
+                L.ns[j * WG] = e.z;
+            }
+            L.near_n = near_n0;
+            L.nrk = L.nk[0];
+            L.nrs = L.ns[0];
+        } else {
+            for (uint32_t j = 0; j < near_n0; ++j) {
+                uint4 e = gp(c.near_spill)[(size_t)j * R + r];
+                if (L.near_n < NC && (uint64_t)(ent_t(e) - L.nbase) < 0xFFFFFFFFull) {
+                    L.near_push(ent_t(e), e.w, e.z);
+                    continue;
+                }
+                L.push_far(ent_t(e), e.w, e.z);  // the thread's F_NEARQ hint only speeds up throwTo
+            }
         }
-        L.push_far(ent_t(e), e.w, e.z);  // the thread's F_NEARQ hint only speeds up throwTo
     }
 
     if (LP && fresh) {
@@ -2391,11 +2412,13 @@ static int load_common(tw_ctx* c, const tw_scenario_desc* s, bool lp, uint32_t l
     const size_t R = d.R;
     const size_t Rt = s->n_replicas;  // replica dimension of the host tables
     const size_t prog_lds = 12ull * (d.n_insns + 1) + 8ull * d.n_consts;
-    // geometry: sparse when the replicas fill at most ~2 workgroups per CU of
-    // the sparse layout (TW_GEOMETRY=dense|sparse overrides; LP mode is dense)
+    // geometry by replica count (TW_GEOMETRY overrides; LP mode is dense):
+    // <= 4096: a wavefront per replica (C5: 0.32 G events/s vs 0.25 sparse,
+    // 0.20 narrow); < 65536: narrow (C3 at 8192: 2.5 vs 0.99 sparse, 0.74
+    // wave); else dense (one workgroup of 256 per CU)
     {
         const char* g = getenv("TW_GEOMETRY");
-        int geo = (!lp && R <= 8192) ? 1 : 0;
+        int geo = lp ? 0 : R <= 4096 ? 3 : R < 65536 ? 5 : 0;
         if (g && !strcmp(g, "dense")) geo = 0;
         if (g && !strcmp(g, "sparse")) geo = 1;
         if (g && !strcmp(g, "half")) geo = 2;

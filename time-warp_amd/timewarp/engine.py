@@ -157,15 +157,17 @@ class Engine:
 
     def load(self, scn: Scenario, geometry: Optional[str] = None) -> "Engine":
         """Upload the scenario.  `geometry` picks the kernel layout: "dense"
-        (256 replicas per workgroup, 16-entry on-chip queue), "sparse" (16
-        replicas per workgroup, 768-entry on-chip queue), "half" (the dense
-        layout as two 32-lane waves per SIMD; an experiment) or None = the
-        library's choice (sparse for <= 8192 replicas; env TW_GEOMETRY)."""
+        (256 replicas per workgroup, 16-entry on-chip queue), "narrow" (the
+        dense layout, one 64-replica wave per workgroup), "sparse" (16
+        replicas per workgroup, 768-entry on-chip queue), "wave" (a
+        wavefront per replica), "half" (the dense layout as two 32-lane waves
+        per SIMD; an experiment) or None = the library's choice (wave for <=
+        4096 replicas, narrow below 65536, else dense; env TW_GEOMETRY)."""
         d = scn.desc()
         old = os.environ.get("TW_GEOMETRY")
         if geometry is not None:
             if geometry not in ("dense", "sparse", "half", "wave", "narrow"):
-                raise ValueError(f"geometry must be 'dense', 'sparse', 'half' or 'wave', not {geometry!r}")
+                raise ValueError(f"geometry must be 'dense', 'sparse', 'half', 'wave' or 'narrow', not {geometry!r}")
             os.environ["TW_GEOMETRY"] = geometry
         try:
             _check(self.lib.tw_load(self.ctx, C.addressof(d)), "tw_load")
