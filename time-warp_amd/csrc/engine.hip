@@ -56,6 +56,9 @@
 // one wave's scalar, LDS and branch issue overlaps the other's VALU and
 // memory waits.
 #define TW_HALF_LANES 32
+// LP mode (node-partitioned C4): 128 nodes per workgroup and no far-run LDS
+// (LP nodes queue few events), so three workgroups share a CU's LDS
+#define TW_WG_LP 128
 // narrow geometry (fewer replicas than fill the GPU, e.g. C3 sharded 8 ways =
 // 8192 per GPU): the dense layout and near heap with TW_NARROW replicas per
 // workgroup and one wave per workgroup, so the waves spread over all CUs.
@@ -646,6 +649,7 @@ struct Lane {
         }
     }
     __device__ __forceinline__ bool run_push(int64_t t, uint32_t sq, uint32_t slot) {
+        if constexpr (LP) return false;  // LP nodes have no far runs (no LDS for them either)
         if (c.Cr == 0) return false;
         uint4 tl[TW_RUNS];
 #pragma unroll
@@ -684,6 +688,7 @@ struct Lane {
     // The head moves to the second entry; the entry after it is loaded now, by
     // LDS-DMA into staging quad 4, and committed before the store tail.
     __device__ __forceinline__ void run_pop(int sel) {
+        if constexpr (LP) return;  // unreachable: fsrc is never a run in LP mode
         run_commit();
         far_dirty = true;
         uint4 ix4 = *rqp(RQ_IDX);
@@ -706,12 +711,13 @@ struct Lane {
     }
     __device__ __forceinline__ void far_min() {  // heads only: a pending second entry is not needed
         far_dirty = false;
-        uint4 hd[TW_RUNS], tl[TW_RUNS];
-#pragma unroll
-        for (int j = 0; j < TW_RUNS; ++j) { hd[j] = *rqp(RQ_HEAD + j); tl[j] = *rqp(RQ_TAIL + j); }
         fsrc = -1;
         fmt = 0; fms = 0; fmsl = 0;
         if (far_n) { fsrc = TW_RUNS; fmt = cg64(CW_FTL, CW_FTH); fms = cg(CW_FS); fmsl = cg(CW_FSL); }
+        if constexpr (LP) return;  // no far runs
+        uint4 hd[TW_RUNS], tl[TW_RUNS];
+#pragma unroll
+        for (int j = 0; j < TW_RUNS; ++j) { hd[j] = *rqp(RQ_HEAD + j); tl[j] = *rqp(RQ_TAIL + j); }
 #pragma unroll
         for (int j = 0; j < TW_RUNS; ++j) {
             const int64_t t = ent_t(hd[j]);
@@ -1564,16 +1570,16 @@ __global__ void __launch_bounds__(TW_WG) tw_init_kernel(Dev c, uint32_t main_pc,
 // LDS per workgroup: near heap keys + slots, the running threads' register
 // files, the cold words, then the program image and constant pool, so
 // instruction fetch and time constants never leave the CU.
-template <int WG, int NC>
+template <int WG, int NC, bool LP = false>
 __host__ __device__ constexpr size_t fixed_lds_bytes() {
-    return (size_t)5 * WG * 16 + (size_t)RQ_COUNT * WG * 16 + (size_t)NC * WG * 12 +
+    return (size_t)5 * WG * 16 + (size_t)(LP ? 0 : RQ_COUNT) * WG * 16 + (size_t)NC * WG * 12 +
            (size_t)4 * WG * 8 + (size_t)CW_COUNT * WG * 4;
 }
 
 // WG replicas per workgroup share its LDS; TPW of each wave's 64 lanes carry a
 // replica (64, or TW_HALF_LANES for the half geometry: twice the waves).
 template <bool LP, int WG, int NC, int TPW = 64>
-__global__ void __launch_bounds__(WG * 64 / TPW) __attribute__((amdgpu_waves_per_eu((WG * 64 / TPW + 255) / 256, 2)))
+__global__ void __launch_bounds__(WG * 64 / TPW) __attribute__((amdgpu_waves_per_eu(LP ? 2 : (WG * 64 / TPW + 255) / 256, 2)))
 tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
     // device-driven windows: the window, its work list and whether this is the
     // window's first tick (the only one that drains inboxes) come from the device
@@ -1592,7 +1598,7 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
     extern __shared__ __attribute__((aligned(16))) uint64_t lds_raw[];
     uint4 LAS* s_pf = (uint4 LAS*)lds_raw;
     uint4 LAS* s_rq = s_pf + 5 * WG;
-    uint64_t LAS* s_k = (uint64_t LAS*)(s_rq + RQ_COUNT * WG);
+    uint64_t LAS* s_k = (uint64_t LAS*)(s_rq + (LP ? 0 : RQ_COUNT) * WG);
     int64_t LAS* s_rf = (int64_t LAS*)(s_k + NC * WG);
     uint32_t LAS* s_s = (uint32_t LAS*)(s_rf + 4 * WG);
     uint32_t LAS* s_cw = s_s + NC * WG;
@@ -1661,7 +1667,7 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
     L.d_ev = 0;
     L.d_th = 0;
     if (L.far_n) L.set_ftop(L.far_ld(0));
-    {
+    if constexpr (!LP) {
         uint32_t rh4[TW_RUNS];
 #pragma unroll
         for (int j = 0; j < TW_RUNS; ++j) {
@@ -1897,7 +1903,7 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
     sc[SC_EVENTS * R] = events0 + L.d_ev;
     sc[SC_DELIVERED * R] += L.cg(CW_DL); sc[SC_DROPPED * R] += L.cg(CW_DR);
     sc[SC_UNDELIV * R] += L.cg(CW_UD); sc[SC_THREADS * R] += L.d_th;
-    if (c.Cr) {
+    if (!LP && c.Cr) {
         const uint4 ix4 = *L.rqp(RQ_IDX);
 #pragma unroll
         for (int j = 0; j < TW_RUNS; ++j) {
@@ -2405,6 +2411,7 @@ static int load_common(tw_ctx* c, const tw_scenario_desc* s, bool lp, uint32_t l
     d.n_insns = s->n_insns; d.n_consts = s->n_consts; d.n_sets = s->n_listener_sets; d.n_kinds = s->n_msg_kinds;
     d.horizon = s->near_horizon_us;
     d.Cr = s->run_capacity;
+    if (lp) d.Cr = 0;  // LP nodes keep no far runs (tw_run_kernel<true> has no LDS for them)
     d.max_frames = s->max_frames ? s->max_frames : 2u;
     d.FXQ = d.max_frames > 2 ? (d.max_frames - 2 + 3) / 4 : 0u;
     d.tie_mode = TW_TIE_FIFO;
@@ -2428,7 +2435,8 @@ static int load_common(tw_ctx* c, const tw_scenario_desc* s, bool lp, uint32_t l
         if (geo == 1 && fixed_lds_bytes<TW_WG_SPARSE, TW_NEAR_SPARSE>() + prog_lds > 160 * 1024) geo = 0;
         c->geo = geo;
     }
-    c->lds_bytes = (c->geo == 1   ? fixed_lds_bytes<TW_WG_SPARSE, TW_NEAR_SPARSE>()
+    c->lds_bytes = (lp            ? fixed_lds_bytes<TW_WG_LP, TW_NEAR_CAP, true>()
+                    : c->geo == 1 ? fixed_lds_bytes<TW_WG_SPARSE, TW_NEAR_SPARSE>()
                     : c->geo == 5 ? fixed_lds_bytes<TW_NARROW, TW_NEAR_CAP>()
                                   : fixed_lds_bytes<TW_WG, TW_NEAR_CAP>()) +
                    prog_lds;
@@ -2445,7 +2453,7 @@ static int load_common(tw_ctx* c, const tw_scenario_desc* s, bool lp, uint32_t l
         HIPCHK(hipFuncSetAttribute((const void*)tw_run_kernel<false, TW_NARROW, TW_NEAR_CAP, TW_NARROW>,
                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)c->lds_bytes));
     else if (lp)
-        HIPCHK(hipFuncSetAttribute((const void*)tw_run_kernel<true, TW_WG, TW_NEAR_CAP>,
+        HIPCHK(hipFuncSetAttribute((const void*)tw_run_kernel<true, TW_WG_LP, TW_NEAR_CAP>,
                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)c->lds_bytes));
     else
         HIPCHK(hipFuncSetAttribute((const void*)tw_run_kernel<false, TW_WG, TW_NEAR_CAP>,
@@ -2634,7 +2642,7 @@ int tw_run(tw_ctx* c, int64_t t_end_us, uint64_t max_events, tw_stats* out) {
             if (c->lp) HIPCHK(hipMemsetAsync(d.next_t, 0xFF, 8, st));
             HIPCHK(hipEventRecord(c->ev_pool[2 * i], st));
             if (c->lp)
-                launch_run<true, TW_WG, TW_NEAR_CAP>(c, st, t_end_us, limit, budget);
+                launch_run<true, TW_WG_LP, TW_NEAR_CAP>(c, st, t_end_us, limit, budget);
             else if (c->geo == 3)
                 HIPCHK(wave_launch(c->d, c->d_dev, st, t_end_us, limit, 1u << 16));
             else if (c->geo == 1)
@@ -2946,7 +2954,7 @@ int tw_lp_tick(tw_ctx* c) {
     // the window comes from the device (tw_run_kernel reads c.win); launch
     // arguments are captured at enqueue, so d.win is set only around it
     c->d.win = c->win_buf;
-    launch_run<true, TW_WG, TW_NEAR_CAP>(c, st, 0, UINT64_MAX, 1u << 14);
+    launch_run<true, TW_WG_LP, TW_NEAR_CAP>(c, st, 0, UINT64_MAX, 1u << 14);
     c->d.win = nullptr;
     HIPCHK(hipGetLastError());
     hipLaunchKernelGGL(tw_lp_pack, dim3(lp_grid(d.out_cap)), dim3(256), 0, st, d, c->ex_send,

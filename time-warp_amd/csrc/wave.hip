@@ -111,15 +111,6 @@ __device__ __forceinline__ void urec_load(const uint4 GAS* p, uint64_t qs, URec&
     t.r2 = (int64_t)(((uint64_t)rdl(q.y, 3) << 32) | rdl(q.x, 3));
     t.r3 = (int64_t)(((uint64_t)rdl(q.w, 3) << 32) | rdl(q.z, 3));
 }
-// the record from a quad-per-lane register (lanes 0..3) loaded earlier
-__device__ __forceinline__ void urec_unpack(uint4 q, URec& t) {
-    t.w0 = rdl(q.x, 0); t.w1 = rdl(q.y, 0); t.w2 = rdl(q.z, 0); t.w3 = rdl(q.w, 0);
-    t.f0 = rdl(q.x, 1); t.f1 = rdl(q.y, 1); t.xl = rdl(q.z, 1); t.xh = rdl(q.w, 1);
-    t.r0 = (int64_t)(((uint64_t)rdl(q.y, 2) << 32) | rdl(q.x, 2));
-    t.r1 = (int64_t)(((uint64_t)rdl(q.w, 2) << 32) | rdl(q.z, 2));
-    t.r2 = (int64_t)(((uint64_t)rdl(q.y, 3) << 32) | rdl(q.x, 3));
-    t.r3 = (int64_t)(((uint64_t)rdl(q.w, 3) << 32) | rdl(q.z, 3));
-}
 // store quads [q0, q1) of the record (lanes q0..q1-1, one request)
 __device__ __forceinline__ void urec_store(uint4 GAS* p, uint64_t qs, const URec& t, uint32_t q0, uint32_t q1) {
     const uint32_t l = __lane_id() & 3u;
@@ -173,7 +164,6 @@ struct Wave {
     uint32_t ns[K];
     uint64_t lmk;    // this lane's minimum key
     uint32_t lmj;    // ... and its entry index
-    uint32_t lms;    // ... and its slot (the next pop's record is prefetched by slot)
     uint32_t lcnt;   // entries held by this lane
     // wave-uniform state
     uint64_t gmin;   // minimum near key (~0: near queue empty)
@@ -209,20 +199,19 @@ struct Wave {
     __device__ __forceinline__ void near_init() {
 #pragma unroll
         for (int j = 0; j < K; ++j) { nk[j] = ~0ull; ns[j] = 0; }
-        lmk = ~0ull; lmj = 0; lms = 0; lcnt = 0;
+        lmk = ~0ull; lmj = 0; lcnt = 0;
         gmin = ~0ull; near_n = 0; rot = 0;
     }
     __device__ __forceinline__ void lane_rescan() {
         uint64_t m = ~0ull;
-        uint32_t mj = 0, ms = 0;
+        uint32_t mj = 0;
 #pragma unroll
         for (int j = 0; j < K; ++j) {
             const bool b = nk[j] < m;
             m = b ? nk[j] : m;
             mj = b ? (uint32_t)j : mj;
-            ms = b ? ns[j] : ms;
         }
-        lmk = m; lmj = mj; lms = ms;
+        lmk = m; lmj = mj;
     }
     __device__ __forceinline__ bool near_fits(int64_t t) const {
         return near_n < 64u * K && t - now < dv->horizon && (uint64_t)(t - nbase) < 0xFFFFFFFFull;
@@ -242,7 +231,6 @@ struct Wave {
             nk[j] = take ? key : nk[j];
             ns[j] = take ? slot : ns[j];
             lmj = (take && key < lmk) ? (uint32_t)j : lmj;
-            lms = (take && key < lmk) ? slot : lms;
             done = done || take;
         }
         lmk = (me && key < lmk) ? key : lmk;
@@ -251,19 +239,6 @@ struct Wave {
         gmin = key < gmin ? key : gmin;
     }
     // remove the minimum (key gmin); returns its slot
-    // Load the record of the event the next pop will take (the queue minimum
-    // now: nothing between here and that pop writes records or pushes events).
-    __device__ __forceinline__ void prefetch(uint32_t& pfs, uint4& pq) {
-        if (far_dirty) far_min();
-        const bool use_near = near_n != 0;
-        const int64_t tn = nbase + (int64_t)(gmin >> 32);
-        const bool use_far = fm_src >= 0 && (!use_near || tless(fm_t, fm_s, tn, (uint32_t)gmin));
-        if (!use_near && !use_far) return;
-        uint32_t s2 = fm_sl;
-        if (!use_far) s2 = rdl(lms, rfl((uint32_t)__builtin_ctzll(__builtin_amdgcn_ballot_w64(lmk == gmin))));
-        pfs = s2;
-        pq = (gp(dv->slots) + ix(s2))[(size_t)(lane & 3u) * dv->RQ];
-    }
     __device__ __forceinline__ uint32_t near_pop() {
         const uint32_t wl = rfl((uint32_t)__builtin_ctzll(__builtin_amdgcn_ballot_w64(lmk == gmin)));
         uint32_t s = 0;
@@ -870,10 +845,6 @@ __global__ void __launch_bounds__(64) tw_wave_kernel(const Dev* dptr, int64_t t_
     }
 
     bool alive = true;
-    // the next pop's record, loaded at the end of the previous iteration (after
-    // its stores) so the load overlaps the queue pop; lanes 0..3 hold a quad each
-    uint32_t pf_slot = 0xFFFFFFFFu;
-    uint4 pq = make_uint4(0, 0, 0, 0);
     for (uint32_t it = 0; it < budget && alive; ++it) {
         URec th;
         uint32_t slot = 0;
@@ -905,10 +876,8 @@ __global__ void __launch_bounds__(64) tw_wave_kernel(const Dev* dptr, int64_t t_
             } else {
                 slot = W.near_pop();
             }
-            if (slot == pf_slot) urec_unpack(pq, th);
-            else urec_load(W.hrec(slot), dv->RQ, th);
-            pf_slot = 0xFFFFFFFFu;
-            if (th.w3 != sq) { W.prefetch(pf_slot, pq); continue; }  // superseded by a throwTo re-stamp
+            urec_load(W.hrec(slot), dv->RQ, th);
+            if (th.w3 != sq) continue;  // superseded by a throwTo re-stamp
             th.w3 = 0;
             --W.live;
             W.now = t;                  // curTime .= timestamp (TimedT.hs:241-247)
@@ -937,7 +906,6 @@ __global__ void __launch_bounds__(64) tw_wave_kernel(const Dev* dptr, int64_t t_
         if (run) W.step(th, slot);
         W.hash_flush();
         alive = W.status == TW_REP_RUNNING;
-        if (alive && !pending_main) W.prefetch(pf_slot, pq);
     }
     W.hash_flush();
     if (W.status == TW_REP_RUNNING && W.live == 0 && !pending_main) W.status = TW_REP_DONE;
@@ -986,7 +954,7 @@ __global__ void __launch_bounds__(64) tw_wave_kernel(const Dev* dptr, int64_t t_
 int wave_near_k(uint32_t R) {
     // registers per lane hold K queue entries: few replicas per SIMD leave
     // room for a deep on-chip queue (C5's hotspot receiver keeps 1-2k events)
-    return R <= 4096 ? 24 : 4;
+    return R <= 4096 ? 32 : 4;
 }
 size_t wave_spill_entries(uint32_t R) { return 64u * (size_t)wave_near_k(R); }
 
@@ -996,8 +964,8 @@ hipError_t wave_launch(const Dev& d, const Dev* d_dev, hipStream_t st, int64_t t
     // not from kernel arguments held in scalar registers for the whole launch
     hipError_t e = hipMemcpyAsync((void*)d_dev, &d, sizeof(Dev), hipMemcpyHostToDevice, st);
     if (e != hipSuccess) return e;
-    if (wave_near_k(d.R) == 24)
-        hipLaunchKernelGGL((tw_wave_kernel<24>), dim3(d.R), dim3(64), 0, st, d_dev, t_end, limit, budget);
+    if (wave_near_k(d.R) == 32)
+        hipLaunchKernelGGL((tw_wave_kernel<32>), dim3(d.R), dim3(64), 0, st, d_dev, t_end, limit, budget);
     else
         hipLaunchKernelGGL((tw_wave_kernel<4>), dim3(d.R), dim3(64), 0, st, d_dev, t_end, limit, budget);
     return hipGetLastError();
