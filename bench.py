@@ -387,7 +387,9 @@ def main():
         per["threads_forked"] = int(res["threads"].sum())
         per["events"] = events // args.steps
         arrivals = per["delivered"] + per["dropped"] + per["undeliverable"]
-        per["message_path_frac"] = (per["sends"] + arrivals) / max(1, per["events"])
+        # arrival pops over all pops (each delivered message also forks a
+        # handler thread and wakes its receiver: DESIGN.md section 6)
+        per["arrivals_frac"] = arrivals / max(1, per["events"])
         out["events_breakdown"] = per
         mt = measured_traffic(args, launches / args.steps, events / args.steps) if world == 1 else None
         if mt:

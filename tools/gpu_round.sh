@@ -31,6 +31,9 @@ for s in "$@"; do
     prof_c4) step prof_c4 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_c4 -o run -- python3 bench.py --config gossip --steps 2 --warmup 1 --no-cpu-baseline ;;
     prof_c3) step prof_c3 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_c3 -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline ;;
     gossip) step gossip 400 python -u -m pytest tests/test_gpu_gossip.py -q -m gpu -x --timeout 120 --timeout-method thread ;;
+    bench_msg) step bench_msg 500 python bench.py --duration-s 24576 --drop-log2 16 --steps 2 --warmup 1 ;;
+    pmct_msg) PMC_SET=traffic bash tools/pmc_passes.sh gpurun_out/pmct_msg$SFX --duration-s 24576 --drop-log2 16 > gpurun_out/pmct_msg$SFX.log 2>&1; rc=$?; echo "pmct_msg=$rc"; [ $rc -eq 0 ] || exit $rc ;;
+    pmc_full) bash tools/pmc.sh gpurun_out/pmc_full > gpurun_out/pmc_full.log 2>&1; rc=$?; echo "pmc_full=$rc"; [ $rc -eq 0 ] || exit $rc ;;
     bench_c5) step bench_c5 400 python bench.py --config hotspot ;;
     benchq_c5) step benchq_c5 400 python bench.py --config hotspot --steps 2 --warmup 1 --no-cpu-baseline ;;
     benchq_c3_8k) step benchq_c3_8k 300 python bench.py --replicas 8192 --steps 2 --warmup 1 --no-cpu-baseline ;;
