@@ -2185,6 +2185,7 @@ struct tw_ctx {
     int64_t* ex_red = nullptr;        // caller's (or red_own)
     int64_t* red_own = nullptr;
     int64_t* win_buf = nullptr;       // the device loop's WN_* words
+    int64_t* h_win = nullptr;         // pinned host copy of them + lp_err (tw_lp_progress)
     bool loop_ready = false;
     Dev dwin() const {                // the descriptor the device loop's kernels get
         Dev x = d;
@@ -2296,6 +2297,7 @@ void tw_destroy(tw_ctx* c) {
     free_all(c);
     for (hipEvent_t e : c->ev_pool) (void)hipEventDestroy(e);
     if (c->h_active) (void)hipHostFree(c->h_active);
+    if (c->h_win) (void)hipHostFree(c->h_win);
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
     delete c;
 }
@@ -2994,11 +2996,13 @@ int tw_lp_progress(tw_ctx* c, tw_lp_state* out) {
     if (!c || !out) return TW_ERR_INVALID;
     if (!c->loaded || !c->lp || !c->loop_ready) return TW_ERR_STATE;
     HIPCHK(hipSetDevice(c->device));
-    int64_t w[WN_COUNT];
-    uint32_t err = 0;
-    HIPCHK(hipMemcpyAsync(w, c->win_buf, sizeof(w), hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(hipMemcpyAsync(&err, c->d.lp_err, 4, hipMemcpyDeviceToHost, c->stream));
+    if (!c->h_win) HIPCHK(hipHostMalloc((void**)&c->h_win, 8 * (WN_COUNT + 1)));
+    int64_t* w = c->h_win;  // pinned: plain DMA copies, no staging blit
+    w[WN_COUNT] = 0;        // lp_err fills its low 4 bytes
+    HIPCHK(hipMemcpyAsync(w, c->win_buf, 8 * WN_COUNT, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipMemcpyAsync(w + WN_COUNT, c->d.lp_err, 4, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
+    const uint32_t err = (uint32_t)w[WN_COUNT];
     out->windows = (uint64_t)w[WN_WINDOWS];
     out->ticks = (uint64_t)w[WN_TICKS];
     out->t = w[WN_T];
