@@ -211,7 +211,6 @@ struct Lane {
     static constexpr bool PL = LP || WG < 64;
     Dev c;  // by value: kernel arguments stay in SGPRs
     uint32_t r;       // replica
-    uint4 GAS* dmq;   // this lane's record-store sink (TW_DUMMY_REC quads, stride TW_DUMMY_Q)
     // LDS (lane-offset pointers; element j at [j * WG])
     uint64_t LAS* nk;     // near heap keys: (t - nbase) << 32 | seq; a free position holds ~0
     uint32_t LAS* ns;     // near heap slots
@@ -806,7 +805,10 @@ struct Lane {
     // per lane), so no store sits behind a branch or an exec mask.
     __device__ __forceinline__ void store_tail(uint32_t slot, Th& th, bool full, bool hdr, uint32_t cslot,
                                                const Th& ch) {
-        uint4 GAS* dm = dmq;
+        // the record sinks are shared by the workgroups of one XCD (blocks are
+        // dealt to the 8 XCDs round-robin): a few KiB that stay in that XCD's L2
+        // (recomputed here rather than held in registers)
+        uint4 GAS* dm = gp(c.dummy) + (size_t)(blockIdx.x & 7u) * 256u + (threadIdx.x & 255u);
         const size_t R5 = TW_DUMMY_Q;
         const int64_t n0 = rf[0], n1 = rf[WG], n2 = rf[2 * WG], n3 = rf[3 * WG];
         const bool w0q = full || hdr;
@@ -1634,9 +1636,6 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
     Lane<LP, WG, NC> L;
     L.c = c;
     L.r = r;
-    // record sinks shared by the workgroups of one XCD (blocks are dealt to the
-    // 8 XCDs round-robin): a few KiB that stay in that XCD's L2
-    L.dmq = gp(c.dummy) + (size_t)(blockIdx.x & 7u) * 256u + li;
     L.nk = s_k + li;
     L.ns = s_s + li;
     L.rf = s_rf + li;

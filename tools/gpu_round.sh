@@ -45,6 +45,8 @@ for s in "$@"; do
     pmcq_c3_8k) bash tools/pmc_passes.sh gpurun_out/pmcq_c3_8k$SFX --replicas 8192 > gpurun_out/pmcq_c3_8k$SFX.log 2>&1; rc=$?; echo "pmcq_c3_8k=$rc"; [ $rc -eq 0 ] || exit $rc ;;
     pmcq_c3) bash tools/pmc_passes.sh gpurun_out/pmcq_c3$SFX > gpurun_out/pmcq_c3$SFX.log 2>&1; rc=$?; echo "pmcq_c3=$rc"; [ $rc -eq 0 ] || exit $rc ;;
     pmct_c3) PMC_SET=traffic bash tools/pmc_passes.sh gpurun_out/pmct_c3$SFX > gpurun_out/pmct_c3$SFX.log 2>&1; rc=$?; echo "pmct_c3=$rc"; [ $rc -eq 0 ] || exit $rc ;;
+    pmcq_c5) bash tools/pmc_passes.sh gpurun_out/pmcq_c5$SFX --config hotspot > gpurun_out/pmcq_c5$SFX.log 2>&1; rc=$?; echo "pmcq_c5=$rc"; [ $rc -eq 0 ] || exit $rc ;;
+    calib) mkdir -p gpurun_out/calib && timeout -k 10 120 ./tools/ubench/pmc_calib > gpurun_out/calib/run.log 2>&1 && timeout -s KILL 60 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d gpurun_out/calib/f -o run -- ./tools/ubench/pmc_calib > gpurun_out/calib/f.log 2>&1 && timeout -s KILL 60 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d gpurun_out/calib/w -o run -- ./tools/ubench/pmc_calib > gpurun_out/calib/w.log 2>&1 && python3 tools/pmc_calib.py gpurun_out/calib/pmc_calibration.json gpurun_out/calib/run.log gpurun_out/calib/f gpurun_out/calib/w > gpurun_out/calib/summary.log 2>&1; rc=$?; echo "calib=$rc"; [ $rc -eq 0 ] || exit $rc ;;
     pmc) bash tools/pmc.sh gpurun_out/pmc$SFX > gpurun_out/pmc$SFX.log 2>&1; rc=$?; echo "pmc=$rc"; [ $rc -eq 0 ] || exit $rc ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac

@@ -7,10 +7,13 @@ usage: pmc_summary.py OUT.json KERNEL_STATS_DIR [PMC_DIR ...]
 * PMC passes (tools/pmc.sh): `*counter_collection.csv`, one row per dispatch x counter.
 HBM traffic per dispatch: bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024.  The
 factor 2 on FETCH_SIZE: on gfx950 FETCH_SIZE counts 64 B per 128-B read request
-of a wide coalesced stream, i.e. half the bytes (the MI355X microarchitecture
-guide's HBM section; checked on this engine's own record-read pattern by
-tools/ubench/pmc_calib.hip, profiles/pmc_calibration.json).  FETCH_SIZE and
-WRITE_SIZE are reported raw beside the derived value.
+of a wide coalesced stream, i.e. half the bytes, while WRITE_SIZE counts written
+bytes exactly.  Measured here, not assumed: tools/ubench/pmc_calib.hip streams
+2 GiB with 16 B per lane (the engine's record access shape) and
+profiles/pmc_calibration.json holds the result: bytes read / (FETCH_SIZE x 1024)
+= 2.000, bytes written / (WRITE_SIZE x 1024) = 1.000 (raw counter CSVs in
+profiles/r02c/calib/).  FETCH_SIZE and WRITE_SIZE are reported raw beside the
+derived value.
 """
 import csv
 import glob
