@@ -59,6 +59,7 @@
 // LP mode (node-partitioned C4): 128 nodes per workgroup and no far-run LDS
 // (LP nodes queue few events), so three workgroups share a CU's LDS
 #define TW_WG_LP 128
+#define TW_NEAR_LP 8      // an LP node queues few events: 8 on chip (4 workgroups per CU)
 // narrow geometry (fewer replicas than fill the GPU, e.g. C3 sharded 8 ways =
 // 8192 per GPU): the dense layout and near heap with TW_NARROW replicas per
 // workgroup and one wave per workgroup, so the waves spread over all CUs.
@@ -80,6 +81,12 @@
 // addresses would serialise)
 #define TW_DUMMY_Q (8u * 256u)
 #define TW_DUMMY_REC (4u * TW_DUMMY_Q)
+// cold words (CW_*) in registers (1) or in the LDS cold-word array (0, the
+// default): in registers the dense kernel needs 68 AGPRs of spill space and
+// ran C3 at 16.5 vs 17.9 G events/s (r02)
+#ifndef TW_CW_REGS
+#define TW_CW_REGS 0
+#endif
 #define TW_TAIL_VMEM 9          // vector-memory ops of every iteration after the record prefetch
 
 #define P_COUNT 28
@@ -217,7 +224,12 @@ struct Lane {
     int64_t LAS* rf;      // the running thread's registers r0..r3 during its step
     uint4 LAS* pfs;       // prefetch staging: quad q of the next pop's record at [q * WG]
     uint32_t pfs_wave;    // LDS byte address of this wave's staging (quad 0), wave-uniform
-    uint32_t LAS* cw;     // cold words [CW_*]
+    uint32_t LAS* cw;     // cold words [CW_*] in LDS (TW_CW_REGS=0)
+    // cold words in registers (replica kernels): every index is a constant, so no
+    // LDS round trip; the allocator parks them in AGPRs when tight.  The LP
+    // kernel runs two waves per SIMD (no AGPR room) and keeps them in LDS.
+    static constexpr bool CWR = TW_CW_REGS && !LP;
+    uint32_t cwr[CW_COUNT];
     uint4 LAS* rq;        // far runs' bookkeeping quads [RQ_*]
     const uint2 LAS* P;   // program image
     const uint32_t LAS* PU;  // its uop flags
@@ -265,16 +277,22 @@ struct Lane {
         return LP ? i : ix(i);
     }
     // cold words
-    __device__ __forceinline__ uint32_t cg(int w) const { return cw[w * WG]; }
-    __device__ __forceinline__ void cs(int w, uint32_t v) const { cw[w * WG] = v; }
+    __device__ __forceinline__ uint32_t cg(int w) const {
+        if constexpr (CWR) return cwr[w];
+        else return cw[w * WG];
+    }
+    __device__ __forceinline__ void cs(int w, uint32_t v) {
+        if constexpr (CWR) cwr[w] = v;
+        else cw[w * WG] = v;
+    }
     __device__ __forceinline__ int64_t cg64(int wl, int wh) const {
-        return (int64_t)(((uint64_t)cw[wh * WG] << 32) | cw[wl * WG]);
+        return (int64_t)(((uint64_t)cg(wh) << 32) | cg(wl));
     }
-    __device__ __forceinline__ void cs64(int wl, int wh, int64_t v) const {
-        cw[wl * WG] = (uint32_t)v;
-        cw[wh * WG] = (uint32_t)((uint64_t)v >> 32);
+    __device__ __forceinline__ void cs64(int wl, int wh, int64_t v) {
+        cs(wl, (uint32_t)v);
+        cs(wh, (uint32_t)((uint64_t)v >> 32));
     }
-    __device__ __forceinline__ void cinc(int w) const { cw[w * WG] += 1; }
+    __device__ __forceinline__ void cinc(int w) { cs(w, cg(w) + 1); }
 
     __device__ __forceinline__ void fail(uint32_t st) {
         if (status == TW_REP_RUNNING) status = st;
@@ -298,7 +316,7 @@ struct Lane {
         return d;
     }
     static constexpr int ND = near_depth();  // levels below the root
-    static_assert(NC >= 16, "near heap too small");
+    static_assert(NC >= 8, "near heap too small");
     __device__ __forceinline__ uint64_t nkey(int64_t t, uint32_t s) const {
         return ((uint64_t)(t - nbase) << 32) | s;
     }
@@ -505,7 +523,7 @@ struct Lane {
     // ------------------------------------------------------ far heap (HBM, 4-ary)
     __device__ __forceinline__ uint4 far_ld(uint32_t i) const { return gp(c.far)[ix(i)]; }
     __device__ __forceinline__ void far_st(uint32_t i, uint4 e) const { gp(c.far)[ix(i)] = e; }
-    __device__ __forceinline__ void set_ftop(uint4 e) const {
+    __device__ __forceinline__ void set_ftop(uint4 e) {
         cs(CW_FTL, e.x); cs(CW_FTH, e.y); cs(CW_FS, e.w); cs(CW_FSL, e.z);
     }
     // Heaps of up to TW_FAR_FAST entries are at most TW_FAR_D levels deep below
@@ -1079,7 +1097,10 @@ struct Lane {
         status = (cond && status == TW_REP_RUNNING) ? st : status;
     }
     // predicated cold-word store: idle lanes write a dummy word (no branch)
-    __device__ __forceinline__ void csp(bool p, int w, uint32_t v) const { cw[(p ? w : CW_DUMMY) * WG] = v; }
+    __device__ __forceinline__ void csp(bool p, int w, uint32_t v) {
+        if constexpr (CWR) cwr[w] = p ? v : cwr[w];
+        else cw[(p ? w : CW_DUMMY) * WG] = v;  // idle lanes write a dummy word (no branch)
+    }
 
     enum { T_NONE, T_YIELD, T_SPAWN, T_EXIT, T_STOP, T_DIED };
 
@@ -1574,7 +1595,7 @@ __global__ void __launch_bounds__(TW_WG) tw_init_kernel(Dev c, uint32_t main_pc,
 // instruction fetch and time constants never leave the CU.
 template <int WG, int NC, bool LP = false>
 __host__ __device__ constexpr size_t fixed_lds_bytes() {
-    return (size_t)5 * WG * 16 + (size_t)(LP ? 0 : RQ_COUNT) * WG * 16 + (size_t)NC * WG * 12 +
+    return (size_t)(LP ? 4 : 5) * WG * 16 + (size_t)(LP ? 0 : RQ_COUNT) * WG * 16 + (size_t)NC * WG * 12 +
            (size_t)4 * WG * 8 + (size_t)CW_COUNT * WG * 4;
 }
 
@@ -1599,7 +1620,7 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
     if (LP && blockIdx.x * WG >= gp(c.act_n)[c.act_cur]) return;
     extern __shared__ __attribute__((aligned(16))) uint64_t lds_raw[];
     uint4 LAS* s_pf = (uint4 LAS*)lds_raw;
-    uint4 LAS* s_rq = s_pf + 5 * WG;
+    uint4 LAS* s_rq = s_pf + (LP ? 4 : 5) * WG;  // (staging quad 4 holds a far run's next entry: no runs in LP)
     uint64_t LAS* s_k = (uint64_t LAS*)(s_rq + (LP ? 0 : RQ_COUNT) * WG);
     int64_t LAS* s_rf = (int64_t LAS*)(s_k + NC * WG);
     uint32_t LAS* s_s = (uint32_t LAS*)(s_rf + 4 * WG);
@@ -1656,6 +1677,7 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
     L.far_n = (uint32_t)sc[SC_FAR_N * R];
     L.status = (uint32_t)sc[SC_STATUS * R];
     L.free_n = (uint32_t)sc[SC_FREE_N * R]; L.ftop = (uint32_t)sc[SC_FTOP * R]; L.bump = (uint32_t)sc[SC_BUMP * R];
+#pragma unroll
     for (int w = 0; w < CW_COUNT; ++w) L.cs(w, 0);
     L.cs(CW_MAINEXC, (uint32_t)sc[SC_MAIN_EXC * R]);
     L.cs(CW_TMO, (uint32_t)sc[SC_TMO_CTR * R]);
@@ -2436,7 +2458,7 @@ static int load_common(tw_ctx* c, const tw_scenario_desc* s, bool lp, uint32_t l
         if (geo == 1 && fixed_lds_bytes<TW_WG_SPARSE, TW_NEAR_SPARSE>() + prog_lds > 160 * 1024) geo = 0;
         c->geo = geo;
     }
-    c->lds_bytes = (lp            ? fixed_lds_bytes<TW_WG_LP, TW_NEAR_CAP, true>()
+    c->lds_bytes = (lp            ? fixed_lds_bytes<TW_WG_LP, TW_NEAR_LP, true>()
                     : c->geo == 1 ? fixed_lds_bytes<TW_WG_SPARSE, TW_NEAR_SPARSE>()
                     : c->geo == 5 ? fixed_lds_bytes<TW_NARROW, TW_NEAR_CAP>()
                                   : fixed_lds_bytes<TW_WG, TW_NEAR_CAP>()) +
@@ -2454,7 +2476,7 @@ static int load_common(tw_ctx* c, const tw_scenario_desc* s, bool lp, uint32_t l
         HIPCHK(hipFuncSetAttribute((const void*)tw_run_kernel<false, TW_NARROW, TW_NEAR_CAP, TW_NARROW>,
                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)c->lds_bytes));
     else if (lp)
-        HIPCHK(hipFuncSetAttribute((const void*)tw_run_kernel<true, TW_WG_LP, TW_NEAR_CAP>,
+        HIPCHK(hipFuncSetAttribute((const void*)tw_run_kernel<true, TW_WG_LP, TW_NEAR_LP>,
                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)c->lds_bytes));
     else
         HIPCHK(hipFuncSetAttribute((const void*)tw_run_kernel<false, TW_WG, TW_NEAR_CAP>,
@@ -2643,7 +2665,7 @@ int tw_run(tw_ctx* c, int64_t t_end_us, uint64_t max_events, tw_stats* out) {
             if (c->lp) HIPCHK(hipMemsetAsync(d.next_t, 0xFF, 8, st));
             HIPCHK(hipEventRecord(c->ev_pool[2 * i], st));
             if (c->lp)
-                launch_run<true, TW_WG_LP, TW_NEAR_CAP>(c, st, t_end_us, limit, budget);
+                launch_run<true, TW_WG_LP, TW_NEAR_LP>(c, st, t_end_us, limit, budget);
             else if (c->geo == 3)
                 HIPCHK(wave_launch(c->d, c->d_dev, st, t_end_us, limit, 1u << 16));
             else if (c->geo == 1)
@@ -2955,10 +2977,10 @@ int tw_lp_tick(tw_ctx* c) {
     // the window comes from the device (tw_run_kernel reads c.win); launch
     // arguments are captured at enqueue, so d.win is set only around it
     c->d.win = c->win_buf;
-    launch_run<true, TW_WG_LP, TW_NEAR_CAP>(c, st, 0, UINT64_MAX, 1u << 14);
+    launch_run<true, TW_WG_LP, TW_NEAR_LP>(c, st, 0, UINT64_MAX, 1u << 14);
     c->d.win = nullptr;
     HIPCHK(hipGetLastError());
-    hipLaunchKernelGGL(tw_lp_pack, dim3(lp_grid(d.out_cap)), dim3(256), 0, st, d, c->ex_send,
+    hipLaunchKernelGGL(tw_lp_pack, dim3(lp_grid(d.out_cap) < 512 ? lp_grid(d.out_cap) : 512), dim3(256), 0, st, d, c->ex_send,
                        (const uint32_t*)c->ex_starts, c->ex_world, c->ex_cap);
     HIPCHK(hipGetLastError());
     return TW_OK;
