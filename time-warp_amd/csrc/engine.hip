@@ -60,6 +60,12 @@
 // (LP nodes queue few events), so three workgroups share a CU's LDS
 #define TW_WG_LP 128
 #define TW_NEAR_LP 8      // an LP node queues few events: 8 on chip (4 workgroups per CU)
+// work-list buckets by pending delivery records (tw_lp_compact).  Measured
+// with 4 buckets: C4 1.45 vs 1.58 G events/s -- pending records do not predict
+// a node's events in the window (most arrive for later windows) -- so 1.
+#ifndef TW_LP_NB
+#define TW_LP_NB 1
+#endif
 // narrow geometry (fewer replicas than fill the GPU, e.g. C3 sharded 8 ways =
 // 8192 per GPU): the dense layout and near heap with TW_NARROW replicas per
 // workgroup and one wave per workgroup, so the waves spread over all CUs.
@@ -89,7 +95,7 @@
 #endif
 #define TW_TAIL_VMEM 9          // vector-memory ops of every iteration after the record prefetch
 
-#define P_COUNT 28
+#define P_COUNT 29
 // Diagnostic build (-DTW_STATS, lib/libtimewarp_stats.so): per-lane event-path
 // counters summed into Dev::prof at kernel end (tools/stats_probe.py).  The
 // product build compiles every STAT to nothing.
@@ -103,7 +109,7 @@
 enum { K_POP, K_SUPERSEDED, K_PEEK_PF, K_PEEK_HBM, K_PUT_HBM, K_PUT_DEAD, K_PF_ISSUE, K_HASH_IMM, K_HASH_FLUSH,
        K_NEAR_PUSH, K_RUN_PUSH, K_FAR_PUSH, K_INSN, K_CYC_POP, K_CYC_INTERP, K_CYC_TAIL,
        K_CYC_SEL, K_CYC_FETCH, K_CYC_QPOP, K_CYC_COMMIT, K_CYC_PF, K_CYC_TERM, K_CYC_STORE, K_CYC_HASH,
-       K_CYC_SPAWN, K_CYC_ENQ, K_SPAWN, K_ALLOC_LD };
+       K_CYC_SPAWN, K_CYC_ENQ, K_SPAWN, K_ALLOC_LD, K_ITER };
 #ifdef TW_STATS
 #define STIME(v) const uint64_t v = __builtin_amdgcn_s_memtime()
 #define STADD(i, v) (st[(i)] += (uint32_t)(v))
@@ -261,6 +267,8 @@ struct Lane {
     int64_t now, final_t;
     uint32_t seq, tidc, live, status;
     uint32_t d_ev, d_th;  // this launch's event and thread counts
+    int64_t t_end;        // this launch's bound (LP: the window's last µs)
+    uint32_t ev_room;     // events this launch may still commit
 #ifdef TW_STATS
     uint32_t st[P_COUNT];
 #endif
@@ -1490,6 +1498,40 @@ struct Lane {
             tc = capped ? (uint32_t)T_STOP : tc;
             tc = (tc == T_NONE && (status != TW_REP_RUNNING || oob)) ? (uint32_t)T_STOP : tc;
 #endif
+            if constexpr (LP) {
+                // Inline continuation: a thread that yields to a time before every
+                // event in its node's queue is the next pop (PQ.minView,
+                // TimedT.hs:242), so it resumes here -- the pop's count, clock,
+                // insertion-counter step and trace term as if it had been queued
+                // and popped, without the queue round trip or a loop iteration.
+                // (An LP node runs a few such yields per window -- every send
+                // yields 1 µs -- and a wave waits for its busiest lane.)
+                const bool y = me && tc == T_YIELD && !(th_flags(th) & F_PHANTOM) && status == TW_REP_RUNNING &&
+                               seq != 0xFFFFFFFFu;
+                if (__builtin_amdgcn_ballot_w64(y)) {
+                    if (far_dirty) far_min();
+                    const uint32_t sn = c.tie_mode ? seq_key(c.tie_mode, seq + 1) : seq + 1;
+                    bool has = near_n != 0;
+                    int64_t qt = nbase + (int64_t)(nrk >> 32);
+                    uint32_t qs = (uint32_t)nrk;
+                    const bool uf = fsrc >= 0 && (!has || tless(fmt, fms, qt, qs));
+                    qt = uf ? fmt : qt;
+                    qs = uf ? fms : qs;
+                    has = has || fsrc >= 0;
+                    const bool inl = y && yt <= t_end && d_ev < ev_room && (!has || tless(yt, sn, qt, qs));
+                    if (inl) {
+                        STAT(K_POP);
+                        ++seq;                       // the seq its queue entry would have taken
+                        now = yt;                    // curTime .= timestamp
+                        ++d_ev;
+                        final_t = yt > final_t ? yt : final_t;
+                        hacc += term0(yt, TW_KIND_RESUME | (pc & 0xFFFFu));
+                        n = 0;                       // TW_STEP_CAP counts per pop
+                        tc = T_NONE;
+                        if (now - nbase > (int64_t)0x7FFFFFFF) near_rebase(now);
+                    }
+                }
+            }
             fin = at ? tc : fin;
             running = running && !(at && tc != T_NONE);
         }
@@ -1616,8 +1658,23 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
         c.wid = (uint32_t)w[WN_WID];
         fresh = (fl & WN_FRESH) != 0;
     }
-    // LP: workgroups past the window's work list leave before staging the program
-    if (LP && blockIdx.x * WG >= gp(c.act_n)[c.act_cur]) return;
+    // LP: workgroup -> (bucket, span) of the window's work list, the busiest
+    // bucket first, each bucket padded to whole workgroups; workgroups past the
+    // list leave before staging the program
+    uint32_t lp_k = 0, lp_i = 0, lp_n = 0;
+    if (LP) {
+        uint32_t blk = blockIdx.x;
+        int k = TW_LP_NB - 1;
+        for (; k >= 0; --k) {
+            lp_n = gp(c.act_n)[c.act_cur * TW_LP_NB + k];
+            const uint32_t nb = (lp_n + WG - 1) / WG;
+            if (blk < nb) break;
+            blk -= nb;
+        }
+        if (k < 0) return;
+        lp_k = (uint32_t)k;
+        lp_i = blk * WG;
+    }
     extern __shared__ __attribute__((aligned(16))) uint64_t lds_raw[];
     uint4 LAS* s_pf = (uint4 LAS*)lds_raw;
     uint4 LAS* s_rq = s_pf + (LP ? 4 : 5) * WG;  // (staging quad 4 holds a far run's next entry: no runs in LP)
@@ -1642,8 +1699,9 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
     const uint32_t li = wbase + (threadIdx.x & 63u);
     uint32_t r = blockIdx.x * WG + li;
     if (LP) {
-        if (r >= gp(c.act_n)[c.act_cur]) return;
-        r = gp(c.act)[(size_t)c.act_cur * c.R + r];
+        const uint32_t i = lp_i + li;
+        if (i >= lp_n) return;
+        r = gp(c.act)[((size_t)c.act_cur * TW_LP_NB + lp_k) * c.R + i];
     }
     if (r >= c.R) return;
     uint64_t* sc = gp(c.scal) + r;
@@ -1685,6 +1743,8 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
     const uint64_t events0 = sc[SC_EVENTS * R];
     const uint64_t ev_room64 = max_events > events0 ? max_events - events0 : 0;
     const uint32_t ev_room = ev_room64 > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)ev_room64;
+    L.t_end = t_end;
+    L.ev_room = ev_room;
     L.d_ev = 0;
     L.d_th = 0;
     if (L.far_n) L.set_ftop(L.far_ld(0));
@@ -1801,6 +1861,7 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
     for (uint32_t it = 0; it < budget; ++it) {
         if (!__builtin_amdgcn_ballot_w64(alive)) break;
         STIME(tl0);
+        STATL(K_ITER);  // lane-iterations, idle lanes included (pops / this = lane efficiency)
         Th th;
         uint32_t slot = 0;
         bool run = false;
@@ -2087,15 +2148,17 @@ __global__ void tw_lp_ctl(Dev c, const int64_t* red, uint4* send, uint32_t world
     const uint32_t act = (uint32_t)w[WN_ACT] ^ 1u;
     w[WN_ACT] = act;
     w[WN_WID] += 1;
-    gp(c.act_n)[act] = 0;  // tw_lp_compact builds it next
+    for (int k = 0; k < TW_LP_NB; ++k) gp(c.act_n)[act * TW_LP_NB + k] = 0;  // tw_lp_compact builds it next
     w[WN_REC_MIN] = (int64_t)~0ull;
     w[WN_FLAGS] = WN_FRESH;
 }
 // The window's work list: every node marked during the previous window
-// (listed[r] == mark), in node order inside each block of TW_CPT * 256 nodes
-// (so the lanes' [field][node] state accesses coalesce); one atomic per block
-// claims its span of the list.  Device loop (c.win): only at a window's first
-// tick, with mark/list from the window words.
+// (listed[r] == mark), split into TW_LP_NB buckets by the node's pending
+// delivery records (min(inbox_n, NB-1): a wave runs until its busiest lane is
+// done, so lanes with alike work share waves), in node order inside each
+// block of TW_CPT * 256 nodes (so the lanes' [field][node] state accesses
+// coalesce); one atomic per block and bucket claims its span.  Device loop
+// (c.win): only at a window's first tick, with mark/list from the window words.
 #define TW_CPT 16
 __global__ void __launch_bounds__(256) tw_lp_compact(Dev c, uint32_t mark, uint32_t dst) {
     if (c.win) {
@@ -2105,36 +2168,48 @@ __global__ void __launch_bounds__(256) tw_lp_compact(Dev c, uint32_t mark, uint3
         mark = (uint32_t)w[WN_WID] - 1u;
         dst = (uint32_t)w[WN_ACT];
     }
-    __shared__ uint32_t cnt[TW_CPT * 4];
-    __shared__ uint32_t base;
+    __shared__ uint32_t cnt[TW_LP_NB][TW_CPT * 4];
+    __shared__ uint32_t base[TW_LP_NB];
     const uint32_t wv = threadIdx.x >> 6;
     const size_t r0 = (size_t)blockIdx.x * TW_CPT * 256 + threadIdx.x;
-    uint64_t ms[TW_CPT];
+    uint32_t key[TW_CPT];
 #pragma unroll
     for (int i = 0; i < TW_CPT; ++i) {
         const size_t r = r0 + (size_t)i * 256;
-        ms[i] = __builtin_amdgcn_ballot_w64(r < c.R && gp(c.listed)[r] == mark);
-        if (__lane_id() == 0) cnt[i * 4 + wv] = (uint32_t)__builtin_popcountll(ms[i]);
+        const bool b = r < c.R && gp(c.listed)[r] == mark;
+        const uint32_t n_in = (TW_LP_NB > 1 && b) ? gp(c.inbox_n)[r] : 0u;
+        key[i] = b ? (n_in < TW_LP_NB - 1 ? n_in : TW_LP_NB - 1) : 0xFFu;
+#pragma unroll
+        for (int k = 0; k < TW_LP_NB; ++k) {
+            const uint64_t m = __builtin_amdgcn_ballot_w64(key[i] == (uint32_t)k);
+            if (__lane_id() == 0) cnt[k][i * 4 + wv] = (uint32_t)__builtin_popcountll(m);
+        }
     }
     __syncthreads();
-    if (threadIdx.x == 0) {
+    if (threadIdx.x < TW_LP_NB) {
+        const uint32_t k = threadIdx.x;
         uint32_t run = 0;
-        for (int k = 0; k < TW_CPT * 4; ++k) {
-            const uint32_t n = cnt[k];
-            cnt[k] = run;
+        for (int j = 0; j < TW_CPT * 4; ++j) {
+            const uint32_t n = cnt[k][j];
+            cnt[k][j] = run;
             run += n;
         }
-        base = run ? __hip_atomic_fetch_add(gp(c.act_n) + dst, run, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+        base[k] = run ? __hip_atomic_fetch_add(gp(c.act_n) + dst * TW_LP_NB + k, run, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT)
+                      : 0u;
     }
     __syncthreads();
-    const uint32_t b0 = base;
 #pragma unroll
     for (int i = 0; i < TW_CPT; ++i) {
-        const uint64_t m = ms[i];
-        if ((m >> __lane_id()) & 1ull) {
-            const uint32_t below =
-                __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-            gp(c.act)[(size_t)dst * c.R + b0 + cnt[i * 4 + wv] + below] = (uint32_t)(r0 + (size_t)i * 256);
+#pragma unroll
+        for (int k = 0; k < TW_LP_NB; ++k) {
+            const uint64_t m = __builtin_amdgcn_ballot_w64(key[i] == (uint32_t)k);
+            if (key[i] == (uint32_t)k) {
+                const uint32_t below =
+                    __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+                gp(c.act)[((size_t)dst * TW_LP_NB + k) * c.R + base[k] + cnt[k][i * 4 + wv] + below] =
+                    (uint32_t)(r0 + (size_t)i * 256);
+            }
         }
     }
 }
@@ -2152,7 +2227,7 @@ __global__ void tw_lp_begin(Dev c, int64_t lookahead) {
     w[WN_FLAGS] = WN_FRESH;
     w[WN_ACT] = 1;
     w[WN_WID] = 1;
-    gp(c.act_n)[1] = 0;
+    for (int k = 0; k < TW_LP_NB; ++k) gp(c.act_n)[TW_LP_NB + k] = 0;
     *gp(c.out_n) = 0;
     *gp(c.n_active) = 0;
     *gp(c.next_t) = ~0ull;
@@ -2262,7 +2337,7 @@ void free_all(tw_ctx* c) {
 
 template <bool LP, int WG, int NC, int TPW = 64>
 static void launch_run(tw_ctx* c, hipStream_t st, int64_t t_end, uint64_t limit, uint32_t budget) {
-    const uint32_t blocks = (uint32_t)((c->d.R + WG - 1) / WG);
+    const uint32_t blocks = (uint32_t)((c->d.R + WG - 1) / WG) + (LP ? TW_LP_NB : 0);  // LP: bucket padding
     hipLaunchKernelGGL((tw_run_kernel<LP, WG, NC, TPW>), dim3(blocks), dim3(WG * 64 / TPW), c->lds_bytes, st, c->d, t_end, limit,
                        budget);
 }
@@ -2526,8 +2601,8 @@ static int load_common(tw_ctx* c, const tw_scenario_desc* s, bool lp, uint32_t l
         ALLOC(d.out_n, 1);
         ALLOC(d.next_t, 1);
         ALLOC(d.lp_err, 1);
-        ALLOC(d.act, 2 * R);
-        ALLOC(d.act_n, 2);
+        ALLOC(d.act, 2 * TW_LP_NB * R);
+        ALLOC(d.act_n, 2 * TW_LP_NB);
         ALLOC(d.listed, R);
         ALLOC(c->foreign, (size_t)d.out_cap * 2);
         ALLOC(c->n_foreign, 1);
@@ -2609,7 +2684,7 @@ int tw_reset(tw_ctx* c) {
         HIPCHK(hipMemsetAsync(c->n_foreign, 0, 4, st));
         c->d.act_cur = 0;
         c->d.wid = 0;
-        HIPCHK(hipMemsetAsync(d.act_n, 0, 8, st));
+        HIPCHK(hipMemsetAsync(d.act_n, 0, 8 * TW_LP_NB, st));
     }
     uint32_t blocks = (uint32_t)((R + TW_WG - 1) / TW_WG);
     hipLaunchKernelGGL(tw_init_kernel, dim3(blocks), dim3(TW_WG), 0, st, d, c->main_pc, c->main_node,
@@ -2641,7 +2716,7 @@ int tw_run(tw_ctx* c, int64_t t_end_us, uint64_t max_events, tw_stats* out) {
         // a new window: serve the list built since the last call (nodes with a
         // live thread or new records); start an empty one for the next call
         c->d.act_cur ^= 1u;
-        HIPCHK(hipMemsetAsync(d.act_n + c->d.act_cur, 0, 4, st));
+        HIPCHK(hipMemsetAsync(d.act_n + c->d.act_cur * TW_LP_NB, 0, 4 * TW_LP_NB, st));
         hipLaunchKernelGGL(tw_lp_compact, dim3(compact_blocks(d.R)), dim3(256), 0, st, c->d, c->d.wid, c->d.act_cur);
         HIPCHK(hipGetLastError());
         c->d.wid += 1u;

@@ -122,8 +122,8 @@ struct Dev {
     // a live thread or new delivery records); during window wid a node is
     // marked listed[node] = wid, and the next window's list is compacted from
     // the marks (tw_lp_compact)
-    uint32_t* act;       // [2][R]
-    uint32_t* act_n;     // [2]
+    uint32_t* act;       // [2][TW_LP_NB][R]
+    uint32_t* act_n;     // [2][TW_LP_NB]
     uint32_t* listed;    // [R]
     uint32_t act_cur, wid;
     // device-driven windows (tw_lp_tick): the loop state, WN_* words; null

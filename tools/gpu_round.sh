@@ -20,6 +20,7 @@ for s in "$@"; do
     micro)  step micro 300 python tools/micro_probe.py 65536 8 ;;
     probe)  step probe 300 env TW_LIB=$PWD/time-warp_amd/lib/libtimewarp_prof.so python tools/kernel_probe.py 65536 4096 ;;
     stats) step stats 300 env TW_LIB=$PWD/time-warp_amd/lib/libtimewarp_stats.so python tools/stats_probe.py 65536 4096 ;;
+    stats_c4) step stats_c4 300 env TW_LIB=$PWD/time-warp_amd/lib/libtimewarp_stats.so python -u tools/stats_probe.py gossip ;;
     stats_c5) step stats_c5 400 env TW_LIB=$PWD/time-warp_amd/lib/libtimewarp_stats.so python -u tools/stats_probe.py hotspot 4096 256 ;;
     probe2) step probe2 300 env TW_LIB=$PWD/time-warp_amd/lib/libtimewarp_prof2.so python tools/kernel_probe.py 65536 4096 ;;
     bench)  step bench 500 python bench.py ;;

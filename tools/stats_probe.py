@@ -23,7 +23,7 @@ from timewarp.engine import Engine  # noqa: E402
 NAMES = ["pop", "superseded", "peek_pf", "peek_hbm", "put_hbm", "put_dead", "pf_issue", "hash_imm", "hash_flush",
          "near_push", "run_push", "far_push", "insn", "cyc_pop", "cyc_interp", "cyc_step_and_flush",
          "cyc_select", "cyc_fetch", "cyc_qpop", "cyc_commit", "cyc_prefetch", "cyc_terminal", "cyc_store", "cyc_hash",
-         "cyc_spawn", "cyc_enqueue", "spawn", "alloc_ld"]
+         "cyc_spawn", "cyc_enqueue", "spawn", "alloc_ld", "iter"]
 
 
 def read(eng):
@@ -37,6 +37,25 @@ def read(eng):
 
 
 def main():
+    if len(sys.argv) > 1 and sys.argv[1] == "gossip":  # config 4 on the device window loop, one context
+        import numpy as np
+
+        from timewarp.engine import LPEngine, lp_scenario
+
+        N = int(sys.argv[2]) if len(sys.argv) > 2 else 1 << 20
+        scn = scenarios.gossip(N, seed=0)
+        eng = LPEngine(lp_scenario(scn), 0, N, int(scn.meta["lookahead_us"]), 0)
+        read(eng)
+        eng.reset()
+        eng.exchange_setup(1, 0, np.array([0, N]))
+        eng.loop_begin()
+        st = eng.run_windows()
+        d = read(eng)
+        pops = max(d["pop"], 1)
+        print(json.dumps({"phase": "gossip", "windows": st.windows, "ticks": st.ticks,
+                          "lane_efficiency": d["pop"] / max(d["iter"], 1),
+                          "per_pop": {k: round(v / pops, 4) for k, v in d.items() if k != "pop"}, "counters": d}))
+        return
     if len(sys.argv) > 1 and sys.argv[1] == "hotspot":  # config 5: one phase per 0.25 s of virtual time
         R = int(sys.argv[2]) if len(sys.argv) > 2 else 4096
         S = int(sys.argv[3]) if len(sys.argv) > 3 else 256
