@@ -950,11 +950,15 @@ __global__ void __launch_bounds__(64) tw_wave_kernel(const Dev* dptr, int64_t t_
 
 }  // namespace
 
+// near-queue entries per lane for few replicas (<= 4096)
+#ifndef TW_WAVE_K_FEW
+#define TW_WAVE_K_FEW 32
+#endif
 // Host launcher (engine.hip's tw_run): one 64-lane workgroup per replica.
 int wave_near_k(uint32_t R) {
     // registers per lane hold K queue entries: few replicas per SIMD leave
     // room for a deep on-chip queue (C5's hotspot receiver keeps 1-2k events)
-    return R <= 4096 ? 32 : 4;
+    return R <= 4096 ? TW_WAVE_K_FEW : 4;
 }
 size_t wave_spill_entries(uint32_t R) { return 64u * (size_t)wave_near_k(R); }
 
@@ -964,8 +968,8 @@ hipError_t wave_launch(const Dev& d, const Dev* d_dev, hipStream_t st, int64_t t
     // not from kernel arguments held in scalar registers for the whole launch
     hipError_t e = hipMemcpyAsync((void*)d_dev, &d, sizeof(Dev), hipMemcpyHostToDevice, st);
     if (e != hipSuccess) return e;
-    if (wave_near_k(d.R) == 32)
-        hipLaunchKernelGGL((tw_wave_kernel<32>), dim3(d.R), dim3(64), 0, st, d_dev, t_end, limit, budget);
+    if (wave_near_k(d.R) == TW_WAVE_K_FEW)
+        hipLaunchKernelGGL((tw_wave_kernel<TW_WAVE_K_FEW>), dim3(d.R), dim3(64), 0, st, d_dev, t_end, limit, budget);
     else
         hipLaunchKernelGGL((tw_wave_kernel<4>), dim3(d.R), dim3(64), 0, st, d_dev, t_end, limit, budget);
     return hipGetLastError();
