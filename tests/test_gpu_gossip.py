@@ -74,3 +74,19 @@ def test_gossip_device_windows_equal_oracle(engine_mod, oracle_mod, n, parts, dr
     assert np.array_equal(hashes, o.hashes)
     _, _, host_windows = engine_mod.run_partitioned(scn, parts=parts)
     assert windows == host_windows and ticks >= windows
+
+
+@pytest.mark.one_geometry
+@pytest.mark.parametrize("parts", [1, 3])
+def test_gossip_device_windows_rerun_ticks(engine_mod, oracle_mod, monkeypatch, parts):
+    """Windows that take several ticks (a lane budget of 2 pops per tick): the
+    device loop reruns the window, drains inboxes only at its first tick, and
+    the result is still the oracle's."""
+    monkeypatch.setenv("TW_LP_TICK_BUDGET", "2")
+    scn = scenarios.gossip(3000, drop_log2=4, seed=7)
+    agg, hashes, windows, ticks = engine_mod.run_partitioned_device(scn, parts=parts)
+    o = oracle_mod.run(scn, trace_cap=0)
+    for f in FIELDS:
+        assert int(agg[f]) == int(o.result[f]), (f, int(agg[f]), o.result[f])
+    assert np.array_equal(hashes, o.hashes)
+    assert ticks > windows

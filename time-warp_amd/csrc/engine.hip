@@ -2283,6 +2283,9 @@ struct tw_ctx {
     int64_t* win_buf = nullptr;       // the device loop's WN_* words
     int64_t* h_win = nullptr;         // pinned host copy of them + lp_err (tw_lp_progress)
     bool loop_ready = false;
+    // pops per lane per tick of the device loop (TW_LP_TICK_BUDGET overrides it,
+    // for tests: a small budget makes windows take several ticks)
+    uint32_t lp_budget = 1u << 14;
     Dev dwin() const {                // the descriptor the device loop's kernels get
         Dev x = d;
         x.win = win_buf;
@@ -3025,6 +3028,10 @@ int tw_lp_exchange_setup(tw_ctx* c, uint32_t world, uint32_t rank, const uint32_
 int tw_lp_loop_begin(tw_ctx* c) {
     if (!c) return TW_ERR_INVALID;
     if (!c->loaded || !c->lp) return TW_ERR_STATE;
+    if (const char* b = getenv("TW_LP_TICK_BUDGET")) {
+        const long v = strtol(b, nullptr, 10);
+        c->lp_budget = v >= 1 && v <= (1 << 20) ? (uint32_t)v : (1u << 14);
+    }
     HIPCHK(hipSetDevice(c->device));
     if (!c->ex_red) c->ex_red = c->red_own;  // world 1 without an explicit setup
     c->d.act_cur = 0;
@@ -3052,7 +3059,7 @@ int tw_lp_tick(tw_ctx* c) {
     // the window comes from the device (tw_run_kernel reads c.win); launch
     // arguments are captured at enqueue, so d.win is set only around it
     c->d.win = c->win_buf;
-    launch_run<true, TW_WG_LP, TW_NEAR_LP>(c, st, 0, UINT64_MAX, 1u << 14);
+    launch_run<true, TW_WG_LP, TW_NEAR_LP>(c, st, 0, UINT64_MAX, c->lp_budget);
     c->d.win = nullptr;
     HIPCHK(hipGetLastError());
     hipLaunchKernelGGL(tw_lp_pack, dim3(lp_grid(d.out_cap) < 512 ? lp_grid(d.out_cap) : 512), dim3(256), 0, st, d, c->ex_send,
