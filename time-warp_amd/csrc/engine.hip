@@ -1151,12 +1151,8 @@ struct Lane {
             const bool hot = !(fl & U_FX);
             const bool at = PL ? (running & ((hot & !(lfl & U_FX)) | (!hot & ((in.x & 0xFFu) == op))))
                                : (running && (in.x & 0xFFu) == op);
-#ifndef TW_X_NOCAP
             n += at ? 1u : 0u;
             const bool capped = at && n > TW_STEP_CAP;  // TW_REP_ERR_INSN before executing it
-#else
-            const bool capped = false;
-#endif
             const bool me = at && !capped;
             const uint32_t uw = in.x;
             const int32_t imm = (int32_t)in.y;
@@ -1491,13 +1487,11 @@ struct Lane {
             }
             // per-lane epilogue of the pass
             pc = me ? tgt : pc;
-#ifndef TW_X_NOEPI
             pfail(capped, TW_REP_ERR_INSN);
             const bool oob = tc == T_NONE && pc >= c.n_insns;
             pfail(me && oob, TW_REP_ERR_INSN);
             tc = capped ? (uint32_t)T_STOP : tc;
             tc = (tc == T_NONE && (status != TW_REP_RUNNING || oob)) ? (uint32_t)T_STOP : tc;
-#endif
             if constexpr (LP) {
                 // Inline continuation: a thread that yields to a time before every
                 // event in its node's queue is the next pop (PQ.minView,
@@ -2348,7 +2342,8 @@ static void launch_run(tw_ctx* c, hipStream_t st, int64_t t_end, uint64_t limit,
 extern "C" {
 
 const char* tw_version(void) {
-    return "timewarp-mi355x 0.3 (gfx950; lane-per-replica dense/sparse kernels, node-partitioned LP kernel; ABI 2)";
+    return "timewarp-mi355x 0.4 (gfx950; lane-per-replica dense/narrow/sparse kernels, wavefront-per-replica kernel, "
+           "node-partitioned LP kernel with device-driven windows; ABI 2)";
 }
 
 const char* tw_strerror(int code) {
