@@ -159,7 +159,8 @@ def measured_traffic(args, launches_per_step: float, events_per_step: float):
 
 def workload_key(args) -> str:
     return (f"{args.config}:nodes={args.nodes}:replicas={args.replicas}:weak={int(args.weak)}:"
-            f"dur={args.duration_s}:drop={args.drop_log2}:rt={args.round_trips}:msgs={args.msg_num}")
+            f"dur={args.duration_s}:drop={args.drop_log2}:rt={args.round_trips}:msgs={args.msg_num}"
+            + (f":geo={args.geometry}" if getattr(args, "geometry", None) else ""))
 
 
 def bench_gossip(args, scn, workload, world, rank, local, dist_on, barrier):
@@ -267,6 +268,9 @@ def main():
     ap.add_argument("--msg-num", type=int, default=1000)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--geometry", default=None, choices=["dense", "sparse", "half", "wave", "narrow", "lpb"],
+                    help="replica configs: kernel geometry (default: the library's choice by replica count); "
+                         "lpb = every (node, replica) a logical process in one window loop")
     ap.add_argument("--host-windows", action="store_true",
                     help="gossip: the host-driven window loop (round-1 path) instead of the device loop")
     ap.add_argument("--workload-key", action="store_true",
@@ -302,7 +306,7 @@ def main():
     scn, workload = build_scenario(args, rank, world)
     if args.config == "gossip":
         return bench_gossip(args, scn, workload, world, rank, local, dist_on, barrier)
-    eng = Engine(local).load(scn)
+    eng = Engine(local).load(scn, geometry=args.geometry)
 
     for _ in range(args.warmup):
         eng.reset()
@@ -372,7 +376,7 @@ def main():
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS,
                 "traffic": None,
-                "kernel": "tw_run_kernel",
+                "kernel": "tw_run_kernel" if eng.geometry() != "lpb" else "tw_run_kernel<LP> window loop",
                 "launches": launches,
                 "avg_launch_ms": kernel_ms / max(1, launches),
                 "algorithmic_bytes": "64 B/event + 8 B/send (SURVEY.md 8d)",

@@ -324,8 +324,10 @@ int tw_set_counter_base(tw_ctx* ctx, uint32_t seq0, uint32_t tid0);
  *   WAVE   one wavefront per replica: lane-parallel queue (few replicas);
  *   NARROW the dense layout with 8 replicas per wave (few replicas: one
  *          wave per SIMD);
- *   LP     node-partitioned mode (tw_lp_load). */
-enum { TW_GEO_DENSE = 0, TW_GEO_SPARSE = 1, TW_GEO_HALF = 2, TW_GEO_WAVE = 3, TW_GEO_LP = 4, TW_GEO_NARROW = 5 };
+ *   LP     node-partitioned mode (tw_lp_load);
+ *   LPB    batched node-partitioned mode (tw_lpb_load). */
+enum { TW_GEO_DENSE = 0, TW_GEO_SPARSE = 1, TW_GEO_HALF = 2, TW_GEO_WAVE = 3, TW_GEO_LP = 4, TW_GEO_NARROW = 5,
+       TW_GEO_LPB = 6 };
 int tw_geometry(tw_ctx* ctx);
 
 /* Duration (ms) of every event-kernel launch of the last tw_run, measured with
@@ -374,6 +376,28 @@ int tw_lp_inject(tw_ctx* ctx, const tw_lp_record* recs, size_t n, int64_t* next_
  * worst) and this context's additions to every node's hash (length n_nodes;
  * the scenario's hashes are the sum over contexts mod 2^64). */
 int tw_lp_results(tw_ctx* ctx, tw_replica_result* agg, uint64_t* node_hashes, size_t n_nodes);
+
+/* ---- batched node-partitioned mode (intra-replica parallelism)
+ * R replicas of a scenario whose nodes interact only through sends of at
+ * least lookahead_us (plus forks onto other nodes issued before any node runs
+ * past the fork time, e.g. a main thread that starts the node daemons):
+ * every (node, replica) pair is a lane, a logical process with its own queue,
+ * and the replicas share one device-driven window loop.  A replica's events
+ * then run in parallel across its nodes instead of in one sequential chain
+ * (a hotspot receiver's backlog is sorted per window by tw_lp_due instead of
+ * being queued).  After tw_lpb_load the replica API applies unchanged:
+ * tw_reset, tw_run (t_end_us = INT64_MAX, max_events = UINT64_MAX only: the
+ * whole window loop), tw_read_results / tw_read_hashes per replica, with
+ * results equal to runTimedT's (TimedT.hs:293-304) for scenarios whose outputs
+ * do not depend on equal-timestamp order (the oracle's tie audit).  The
+ * replica count must be a power of two; node_inbox_cap[n] (NULL: inbox_cap
+ * for every node, each <= 2048) bounds the delivery records pending at node n
+ * of one replica; outbox_cap bounds the records of one tick.  A fork's ref to
+ * a child on another node is opaque (-1). */
+int tw_lpb_load(tw_ctx* ctx, const tw_scenario_desc* desc, int64_t lookahead_us, const uint32_t* node_inbox_cap,
+                uint32_t inbox_cap, uint32_t outbox_cap);
+/* Windows and ticks of the last tw_run in batched mode. */
+int tw_lpb_windows(tw_ctx* ctx, uint64_t* windows, uint64_t* ticks);
 
 /* ---- device-driven windows (no host round trip per window)
  * The window loop above costs several host synchronisations per window.  Here

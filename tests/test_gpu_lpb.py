@@ -1,0 +1,85 @@
+"""Batched node-partitioned mode (tw_lpb_load) vs the oracle (canonical mode).
+
+Every (node, replica) pair is a logical process; the replicas share one
+device-driven window loop.  The sequential TimedT run of each replica
+(oracle/timedt_oracle.cpp, TimedT.hs:234-304) must come out bit-exact: every
+result field and every per-node trace hash.  Main's forks onto the node
+daemons travel as spawn records; a hotspot receiver with more than TW_LIGHT
+records pending takes the tw_lp_due path (its due run, sorted per window)."""
+import numpy as np
+import pytest
+
+from timewarp import scenarios
+from timewarp.abi import RESULT_FIELDS
+
+pytestmark = [pytest.mark.gpu, pytest.mark.one_geometry]
+
+
+def _compare_lpb(scn, engine_mod, oracle_mod, threads=8):
+    with engine_mod.Engine(0) as e:
+        e.load(scn, geometry="lpb")
+        assert e.geometry() == "lpb"
+        e.reset()
+        st = e.run()
+        res, hashes = e.results(), e.hashes()
+        windows, ticks = e.lpb_windows()
+    ores, ohashes = oracle_mod.run_batch(scn, threads=threads)
+    bad = {}
+    for f in RESULT_FIELDS:
+        if f == "tie_flags":
+            continue
+        m = np.nonzero(res[f] != ores[f])[0]
+        if m.size:
+            bad[f] = (m[:5].tolist(), res[f][m[:5]].tolist(), ores[f][m[:5]].tolist())
+    hm = np.nonzero((hashes != ohashes).any(axis=1))[0]
+    if hm.size:
+        bad["hashes"] = (hm[:5].tolist(), np.nonzero(hashes[hm[0]] != ohashes[hm[0]])[0][:8].tolist())
+    assert not bad, f"{scn.name}: LPB != oracle: {bad}"
+    assert st.events == int(ores["events"].sum())
+    assert windows > 0 and ticks >= windows
+    return st, ores, windows
+
+
+def test_lpb_hotspot_light(engine_mod, oracle_mod):
+    # 8 senders: the receiver's inbox stays light (<= 32 pending)
+    scn = scenarios.hotspot(n_senders=8, n_replicas=64, msg_num=30)
+    _compare_lpb(scn, engine_mod, oracle_mod)
+
+
+def test_lpb_hotspot_heavy_receiver(engine_mod, oracle_mod):
+    # 64 senders at 1 msg/ms with 1-5 ms delays: ~300 pings pending at the
+    # receiver, so its records go through tw_lp_due every window
+    scn = scenarios.hotspot(n_senders=64, n_replicas=32, msg_num=60)
+    st, ores, windows = _compare_lpb(scn, engine_mod, oracle_mod)
+    assert ores["delivered"].sum() == 2 * 64 * 60 * 32
+
+
+def test_lpb_hotspot_inline(engine_mod, oracle_mod):
+    # ForkStrategy `const id`: the handler runs in the phantom deliverer
+    scn = scenarios.hotspot(n_senders=48, n_replicas=16, msg_num=40, fork_strategy="inline")
+    _compare_lpb(scn, engine_mod, oracle_mod)
+
+
+def test_lpb_hotspot_full_senders(engine_mod, oracle_mod):
+    # the C5 shape (256 senders), few replicas and messages
+    scn = scenarios.hotspot(n_senders=256, n_replicas=4, msg_num=12)
+    _compare_lpb(scn, engine_mod, oracle_mod)
+
+
+def test_lpb_ping_pong(engine_mod, oracle_mod):
+    scn = scenarios.ping_pong(n_replicas=256, round_trips=30)
+    _compare_lpb(scn, engine_mod, oracle_mod)
+
+
+def test_lpb_gossip_single_replica(engine_mod, oracle_mod):
+    # one replica: the classic partitioned scenario through the batched path
+    scn = scenarios.gossip(n_nodes=4096, fanout=4)
+    _compare_lpb(scn, engine_mod, oracle_mod, threads=1)
+
+
+def test_lpb_rejects_zero_lookahead(engine_mod):
+    # token ring's observer links have 0 µs delay: no conservative window exists
+    scn = scenarios.token_ring(n_nodes=8, n_replicas=4, launch_duration=5_000_000)
+    with engine_mod.Engine(0) as e:
+        with pytest.raises(engine_mod.EngineError):
+            e.load(scn, geometry="lpb")

@@ -149,6 +149,9 @@ enum {
     CW_DUMMY,                                          // target of idle lanes' predicated stores
     CW_COUNT
 };
+// LP-only cold words, after the CW_* block: the due run of a heavy lane
+// (head | count << 16, seq base, head time) and its inbox base index
+enum { DW_HN, DW_SQ0, DW_TL, DW_TH, DW_IB, DW_COUNT };
 
 // Pre-decoded instruction class ("uop" flags, built once per launch in the
 // kernel prologue from the program image): the interpreter's hot pass computes
@@ -279,11 +282,21 @@ struct Lane {
         return LP ? ix(var) : ix((size_t)node * 4 + var);
     }
     __device__ __forceinline__ size_t bix(uint32_t node) const { return LP ? ix(0) : ix(node); }
-    __device__ __forceinline__ size_t lix(uint64_t link) const { return LP ? (size_t)link : ix(link); }
+    // LP: the replica this lane's node belongs to (0 for one partitioned
+    // scenario), and the global lane of another node of that replica
+    __device__ __forceinline__ uint32_t rho() const { return (c.lp0 + r) & ((1u << c.rep_lg) - 1u); }
+    __device__ __forceinline__ uint32_t lane_of(uint32_t node) const { return (node << c.rep_lg) | rho(); }
+    // link arrays: [link][replica] ([link] x replicas batched, LP)
+    __device__ __forceinline__ size_t lix(uint64_t link) const {
+        return LP ? ((size_t)link << c.rep_lg) + rho() : ix(link);
+    }
     __device__ __forceinline__ size_t tix(uint64_t link, uint32_t ord) const {
         size_t i = (size_t)link * c.D + ord % c.D;
-        return LP ? i : ix(i);
+        return LP ? (i << c.rep_lg) + rho() : ix(i);
     }
+    // LP cold words (DW_*)
+    __device__ __forceinline__ uint32_t dg(int w) const { return cw[(CW_COUNT + w) * WG]; }
+    __device__ __forceinline__ void ds(int w, uint32_t v) { cw[(CW_COUNT + w) * WG] = v; }
     // cold words
     __device__ __forceinline__ uint32_t cg(int w) const {
         if constexpr (CWR) return cwr[w];
@@ -739,7 +752,17 @@ struct Lane {
         fsrc = -1;
         fmt = 0; fms = 0; fmsl = 0;
         if (far_n) { fsrc = TW_RUNS; fmt = cg64(CW_FTL, CW_FTH); fms = cg(CW_FS); fmsl = cg(CW_FSL); }
-        if constexpr (LP) return;  // no far runs
+        if constexpr (LP) {
+            // no far runs; the due run of a heavy lane is source 0 (its seqs were
+            // reserved at the window's start, in the run's order)
+            const uint32_t hn = dg(DW_HN), h = hn & 0xFFFFu;
+            if (h < (hn >> 16)) {
+                const int64_t t = (int64_t)(((uint64_t)dg(DW_TH) << 32) | dg(DW_TL));
+                const uint32_t sq = dg(DW_SQ0) + 1u + h;
+                if (fsrc < 0 || tless(t, sq, fmt, fms)) { fsrc = 0; fmt = t; fms = sq; fmsl = 0xFFFFFFFFu; }
+            }
+            return;
+        }
         uint4 hd[TW_RUNS], tl[TW_RUNS];
 #pragma unroll
         for (int j = 0; j < TW_RUNS; ++j) { hd[j] = *rqp(RQ_HEAD + j); tl[j] = *rqp(RQ_TAIL + j); }
@@ -939,7 +962,7 @@ struct Lane {
     // added once at the end of the iteration, after the step's loads were issued
     // (a load waits for every older store/atomic of the wave: vmcnt is in order).
     __device__ __forceinline__ void hash_atomic(uint32_t node, uint64_t v) {
-        unsigned long long GAS* h = LP ? (unsigned long long GAS*)(gp(c.hash_g) + node)
+        unsigned long long GAS* h = LP ? (unsigned long long GAS*)(gp(c.hash_g) + lane_of(node))
                                        : (unsigned long long GAS*)(gp(c.hash) + ix(node));
         __hip_atomic_fetch_add(h, (unsigned long long)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
@@ -955,7 +978,7 @@ struct Lane {
     // term): one unconditional vector-memory op for the store tail's shape
     __device__ __forceinline__ void hash_flush_all() {
         const bool h = hacc != 0;
-        unsigned long long GAS* p = h ? (LP ? (unsigned long long GAS*)(gp(c.hash_g) + hnode)
+        unsigned long long GAS* p = h ? (LP ? (unsigned long long GAS*)(gp(c.hash_g) + lane_of(hnode))
                                             : (unsigned long long GAS*)(gp(c.hash) + ix(hnode)))
                                       : (unsigned long long GAS*)(gp(c.dummy) + TW_DUMMY_REC + r);
         __hip_atomic_fetch_add(p, (unsigned long long)hacc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -976,6 +999,51 @@ struct Lane {
         o[0] = make_uint4((uint32_t)ta, (uint32_t)((uint64_t)ta >> 32), (uint32_t)payload,
                           (uint32_t)((uint64_t)payload >> 32));
         o[1] = make_uint4(link, kind, src, dst);
+    }
+    // Batched LP: a fork onto another node of this replica.  The child is
+    // queued at t on that node's lane (TimedT.hs:326-339) by the spawn record
+    // pair this appends (tw_lp_pack hands it over; the lane creates the thread
+    // at its next tick, before running anything later than t).
+    __device__ __forceinline__ void emit_spawn(int64_t t, uint32_t pc, uint32_t dst, int64_t q0, int64_t q1,
+                                               int64_t q2, int64_t q3) {
+        uint32_t i = __hip_atomic_fetch_add(gp(c.out_n), 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (i + 1 >= c.out_cap) {
+            __hip_atomic_fetch_or(gp(c.lp_err), 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            return;
+        }
+        uint4 GAS* o = gp(c.outbox) + (size_t)i * 2;
+        o[0] = make_uint4((uint32_t)t, (uint32_t)((uint64_t)t >> 32), (uint32_t)q0, (uint32_t)((uint64_t)q0 >> 32));
+        o[1] = make_uint4(pc, TW_SPAWN_KIND, 0u, dst);
+        o[2] = make_uint4((uint32_t)q1, (uint32_t)((uint64_t)q1 >> 32), (uint32_t)q2, (uint32_t)((uint64_t)q2 >> 32));
+        o[3] = make_uint4((uint32_t)q3, TW_SPAWN_CONT, (uint32_t)((uint64_t)q3 >> 32), dst);
+    }
+    // LP: pop the head of the due run.  The record becomes the deliverer's
+    // phantom thread (its wake pop, counted by the sender) in a fresh slot,
+    // exactly as if it had been queued at the window's start.
+    __device__ __forceinline__ void due_pop(Th& th, uint32_t& slot, uint32_t sq) {
+        const uint32_t hn = dg(DW_HN), h = hn & 0xFFFFu, n = hn >> 16;
+        const size_t ib = dg(DW_IB), st = ib_stride(c);
+        const uint4 GAS* q = gp(c.due) + (ib + (size_t)h * st) * 2;
+        const uint4 a = q[0], b = q[1];
+        const uint4 nx = gp(c.due)[(ib + (size_t)(h + 1 < n ? h + 1 : h) * st) * 2];
+        tw_vm_drain();
+        ds(DW_HN, hn + 1);
+        ds(DW_TL, nx.x);
+        ds(DW_TH, nx.y);
+        far_dirty = true;
+        const uint32_t s = alloc_slot();
+        const bool ok = s != 0xFFFFFFFFu;
+        th.w0 = ((TW_PC_DELIVER_STUB + 1) & 0xFFFFu) | ((F_STARTED | F_PHANTOM) << FL_SHIFT);
+        th.w1 = (c.lp0 + r) >> c.rep_lg;
+        th.w2 = 0xFFFFFFFEu;      // never a throwTo target
+        th.w3 = ok ? sq : sq + 1; // no slot (the lane has failed): a pop without effect
+        th.f0 = th.f1 = th.xl = th.xh = 0;
+        th.r0 = (int64_t)(((uint64_t)a.w << 32) | a.z);  // payload
+        th.r1 = b.x;                                     // link
+        th.r2 = b.z;                                     // sending node
+        th.r3 = b.y;                                     // kind
+        live += ok ? 1u : 0u;
+        slot = ok ? s : 0u;
     }
 
     // Create a thread queued at now (fork, TimedT.hs:326-339): its record is
@@ -1238,7 +1306,7 @@ struct Lane {
                     if (need(tk == TK_FORK)) {
                         const bool fk = tk == TK_FORK;
                         const uint32_t node = b == 0xFFFFu ? th.w1 : (uint32_t)rb;
-                        const bool bad = fk && (LP ? node != th.w1 : node >= c.N);
+                        const bool bad = fk && (LP ? (c.lpb ? node >= c.Ntot : node != th.w1) : node >= c.N);
                         pfail(me && bad, TW_REP_ERR_INSN);
                         tc = fk ? (bad ? (uint32_t)T_STOP : (uint32_t)T_SPAWN) : tc;
                         const bool p = me && fk && !bad;
@@ -1360,7 +1428,7 @@ struct Lane {
                                 d_ev += 2;
                                 ++d_th;
                                 final_t = ta > final_t ? ta : final_t;
-                                emit(ta, payload, (uint32_t)link, kind, th.w1, gp(c.link_dst)[link]);
+                                emit(ta, payload, (uint32_t)link, kind, th.w1, lane_of(gp(c.link_dst)[link]));
                                 yt = now + 1;
                                 tc = T_YIELD;
                             }
@@ -1544,7 +1612,14 @@ struct Lane {
             const uint32_t cdel = cg(CW_CDEL), cra = cg(CW_CRA);
             int64_t ref;
             bool ok;
-            if (cdel & 2u)
+            if (LP && c.lpb && (cdel & 2u) && cg(CW_CNODE) != th.w1) {
+                // a fork onto another node (batched LP): a spawn record; the ref is
+                // opaque (-1: refs name engine slots, and a cross-node throwTo is
+                // outside LP mode anyway)
+                emit_spawn(now, cg(CW_CPC), lane_of(cg(CW_CNODE)), rf[0], rf[WG], rf[2 * WG], rf[3 * WG]);
+                ref = -1;
+                ok = true;
+            } else if (cdel & 2u)
                 ok = spawn(cg(CW_CPC), cg(CW_CNODE), rf[0], rf[WG], rf[2 * WG], rf[3 * WG], ref, ch, cslot);
             else
                 ok = spawn(cg(CW_CPC), cg(CW_CNODE), cg64(CW_Q0, CW_Q0 + 1), cg64(CW_Q0 + 2, CW_Q0 + 3),
@@ -1587,8 +1662,10 @@ __global__ void __launch_bounds__(TW_WG) tw_init_kernel(Dev c, uint32_t main_pc,
                                                        uint32_t tid0) {
     uint32_t r = blockIdx.x * TW_WG + threadIdx.x;
     if (r >= c.R) return;
-    // LP mode: lane r is global node g; only the main node's lane holds the main thread
-    const uint32_t g = lp_mode ? c.lp0 + r : 0u;
+    // LP mode: lane r runs global node g (of replica rho, batched mode); only
+    // the main node's lane holds the main thread
+    const uint32_t g = lp_mode ? (c.lp0 + r) >> c.rep_lg : 0u;
+    const uint32_t rho = lp_mode ? (c.lp0 + r) & ((1u << c.rep_lg) - 1u) : r;
     const bool has_main = !lp_mode || g == main_node;
     for (uint32_t f = 0; f < SC_COUNT; ++f) gp(c.scal)[(size_t)f * c.R + r] = 0;
     gp(c.scal)[(size_t)SC_THREADS * c.R + r] = has_main ? 1 : 0;
@@ -1602,8 +1679,8 @@ __global__ void __launch_bounds__(TW_WG) tw_init_kernel(Dev c, uint32_t main_pc,
     p[0] = make_uint4(w0, main_node, has_main ? 0u : 0xFFFFFFFFu, 0u);
     p[c.RQ] = make_uint4(0u, 0u, 0u, 0u);
     int64_t m[4] = {0, 0, 0, 0};
-    if (main_regs && !lp_mode)
-        for (int i = 0; i < 4; ++i) m[i] = main_regs[(size_t)r * 4 + i];
+    if (main_regs && has_main)
+        for (int i = 0; i < 4; ++i) m[i] = main_regs[(size_t)rho * 4 + i];
     p[2 * c.RQ] = make_uint4((uint32_t)m[0], (uint32_t)((uint64_t)m[0] >> 32), (uint32_t)m[1], (uint32_t)((uint64_t)m[1] >> 32));
     p[3 * c.RQ] = make_uint4((uint32_t)m[2], (uint32_t)((uint64_t)m[2] >> 32), (uint32_t)m[3], (uint32_t)((uint64_t)m[3] >> 32));
     if (lp_mode) {
@@ -1613,6 +1690,7 @@ __global__ void __launch_bounds__(TW_WG) tw_init_kernel(Dev c, uint32_t main_pc,
         gp(c.bind_rel)[r] = 0xFFFFFFFEu;
         if (listen_init) gp(c.bind)[r] = listen_init[g];
         gp(c.inbox_n)[r] = 0;
+        if (c.lpb) gp(c.spawn_n)[r] = 0;
         gp(c.listed)[r] = 0;  // marked for the first window: it serves every node
         return;
     }
@@ -1632,7 +1710,7 @@ __global__ void __launch_bounds__(TW_WG) tw_init_kernel(Dev c, uint32_t main_pc,
 template <int WG, int NC, bool LP = false>
 __host__ __device__ constexpr size_t fixed_lds_bytes() {
     return (size_t)(LP ? 4 : 5) * WG * 16 + (size_t)(LP ? 0 : RQ_COUNT) * WG * 16 + (size_t)NC * WG * 12 +
-           (size_t)4 * WG * 8 + (size_t)CW_COUNT * WG * 4;
+           (size_t)4 * WG * 8 + (size_t)(CW_COUNT + (LP ? DW_COUNT : 0)) * WG * 4;
 }
 
 // WG replicas per workgroup share its LDS; TPW of each wave's 64 lanes carry a
@@ -1676,7 +1754,7 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
     int64_t LAS* s_rf = (int64_t LAS*)(s_k + NC * WG);
     uint32_t LAS* s_s = (uint32_t LAS*)(s_rf + 4 * WG);
     uint32_t LAS* s_cw = s_s + NC * WG;
-    uint2 LAS* s_p = (uint2 LAS*)(s_cw + CW_COUNT * WG);
+    uint2 LAS* s_p = (uint2 LAS*)(s_cw + (CW_COUNT + (LP ? DW_COUNT : 0)) * WG);
     int64_t LAS* s_c = (int64_t LAS*)(s_p + c.n_insns + 1);
     uint32_t LAS* s_u = (uint32_t LAS*)(s_c + c.n_consts);
     {
@@ -1701,10 +1779,20 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
     uint64_t* sc = gp(c.scal) + r;
     const size_t R = c.R;
     if (sc[SC_STATUS * R] != TW_REP_RUNNING) return;
-    // LP: a node with no live thread and an empty inbox has nothing to do in
-    // this window (every live thread holds its one queued event; a superseded
-    // entry left behind pops without effect whenever the node wakes again)
-    if (LP && sc[SC_LIVE * R] == 0 && sc[SC_PENDING_MAIN * R] == 0 && (!fresh || gp(c.inbox_n)[r] == 0)) return;
+    // LP: a node with no live thread, nothing to drain, no due run and no
+    // spawn record has nothing to do in this window (every live thread holds
+    // its one queued event; a superseded entry left behind pops without effect
+    // whenever the node wakes again).  A light inbox (<= TW_LIGHT records) is
+    // drained into the queue at the window's first tick; a heavy one was
+    // sorted by tw_lp_due into this window's due run and the records due later.
+    uint32_t n_in = 0;
+    if (LP) {
+        n_in = gp(c.inbox_n)[r];
+        const bool drain = fresh && n_in != 0 && n_in <= TW_LIGHT;
+        if (sc[SC_LIVE * R] == 0 && sc[SC_PENDING_MAIN * R] == 0 && !drain && sc[SC_DUE_H * R] >= sc[SC_DUE_N * R] &&
+            !(c.lpb && gp(c.spawn_n)[r]))
+            return;
+    }
 
     Lane<LP, WG, NC> L;
     L.c = c;
@@ -1742,6 +1830,17 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
     L.d_ev = 0;
     L.d_th = 0;
     if (L.far_n) L.set_ftop(L.far_ld(0));
+    if constexpr (LP) {
+        const uint32_t dn = (uint32_t)sc[SC_DUE_N * R], dh = (uint32_t)sc[SC_DUE_H * R];
+        const size_t ib = ib_base(c, r);
+        L.ds(DW_IB, (uint32_t)ib);
+        L.ds(DW_HN, dh | (dn << 16));
+        L.ds(DW_SQ0, (uint32_t)sc[SC_DUE_SEQ * R]);
+        uint4 h = make_uint4(0, 0, 0, 0);
+        if (dh < dn) h = gp(c.due)[(ib + (size_t)dh * ib_stride(c)) * 2];
+        L.ds(DW_TL, h.x);
+        L.ds(DW_TH, h.y);
+    }
     if constexpr (!LP) {
         uint32_t rh4[TW_RUNS];
 #pragma unroll
@@ -1796,22 +1895,18 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
         }
     }
 
-    if (LP && fresh) {
+    if (LP && fresh && n_in != 0 && n_in <= TW_LIGHT) {
         // delivery records addressed to this node become phantom deliverer
         // threads, inserted in (t, link, payload, src) order so queue seqs are
         // deterministic whatever order the records arrived in
-        uint32_t n_in = gp(c.inbox_n)[r];
-        if (n_in > c.IB) {
-            L.fail(TW_REP_ERR_QUEUE);
-            n_in = c.IB;
-        }
-        uint32_t used = 0;  // bitmask, IB <= 32
+        const size_t ib = ib_base(c, r), ist = ib_stride(c);
+        uint32_t used = 0;  // bitmask, n_in <= TW_LIGHT = 32
         for (uint32_t k = 0; k < n_in && L.status == TW_REP_RUNNING; ++k) {
             int best = -1;
             uint4 ba = make_uint4(0, 0, 0, 0), bb = ba;
             for (uint32_t j = 0; j < n_in; ++j) {
                 if (used & (1u << j)) continue;
-                const uint4 GAS* q = gp(c.inbox) + ((size_t)j * R + r) * 2;
+                const uint4 GAS* q = gp(c.inbox) + (ib + (size_t)j * ist) * 2;
                 uint4 ea = q[0], eb = q[1];
                 bool less = best < 0;
                 if (!less) {
@@ -1827,7 +1922,7 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
             if (s == 0xFFFFFFFFu) break;
             Th ph;
             ph.w0 = ((TW_PC_DELIVER_STUB + 1) & 0xFFFFu) | ((F_STARTED | F_PHANTOM) << FL_SHIFT);
-            ph.w1 = c.lp0 + r;
+            ph.w1 = (c.lp0 + r) >> c.rep_lg;
             ph.w2 = 0xFFFFFFFEu;  // never a throwTo target
             ph.w3 = 0;
             ph.f0 = ph.f1 = ph.xl = ph.xh = 0;
@@ -1839,6 +1934,46 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
             L.put_rec(s, ph);
         }
         gp(c.inbox_n)[r] = 0;
+    }
+    if (LP && c.lpb) {
+        // batched LP: children forked onto this node by another node of the
+        // replica (emit_spawn), queued at their fork time
+        uint32_t nsp = gp(c.spawn_n)[r];
+        if (nsp) {
+            if (nsp > TW_SPN) {
+                L.fail(TW_REP_ERR_QUEUE);
+                nsp = TW_SPN;
+            }
+            for (uint32_t k = 0; k < nsp && L.status == TW_REP_RUNNING; ++k) {
+                const uint4 GAS* q = gp(c.spawn) + ((size_t)k * R + r) * 4;
+                const uint4 a = q[0], b = q[1], d = q[2], e = q[3];
+                const int64_t t = ent_t(a);
+                if (t < L.now) {  // the lane already ran past the fork time: not conservative
+                    L.fail(TW_REP_ERR_INSN);
+                    break;
+                }
+                const uint32_t s = L.alloc_slot();
+                if (s == 0xFFFFFFFFu) break;
+                if (L.tidc == 0xFFFFFFFFu) {
+                    L.fail(TW_REP_ERR_COUNTER);
+                    break;
+                }
+                Th ch;
+                ch.w0 = b.x & 0xFFFFu;
+                ch.w1 = (c.lp0 + r) >> c.rep_lg;
+                ch.w2 = L.tidc++;
+                ch.w3 = 0;
+                ch.f0 = ch.f1 = ch.xl = ch.xh = 0;
+                ch.r0 = (int64_t)(((uint64_t)a.w << 32) | a.z);
+                ch.r1 = (int64_t)(((uint64_t)d.y << 32) | d.x);
+                ch.r2 = (int64_t)(((uint64_t)d.w << 32) | d.z);
+                ch.r3 = (int64_t)(((uint64_t)e.z << 32) | e.x);
+                ++L.d_th;
+                L.enqueue(ch, s, t);
+                L.put_rec(s, ch);
+            }
+            gp(c.spawn_n)[r] = 0;
+        }
     }
 
 #ifdef TW_STATS
@@ -1894,10 +2029,13 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
             popping = popping && !parked;
             if (popping) {
                 {
-                    L.fetch_rec(slot, th);  // prefetched copy or HBM
+                    const bool due = LP && use_far && L.fsrc == 0;
+                    if (due) L.due_pop(th, slot, sq);
+                    else L.fetch_rec(slot, th);  // prefetched copy or HBM
                     STIME(ts2);
                     STADDL(K_CYC_FETCH, ts2 - ts1);
-                    if (!use_far) L.near_pop();
+                    if (due) {
+                    } else if (!use_far) L.near_pop();
                     else if (L.fsrc == TW_RUNS) L.far_pop();
                     else L.run_pop(L.fsrc);
                     STIME(ts3);
@@ -1977,6 +2115,7 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
     sc[SC_TMO_CTR * R] = L.cg(CW_TMO);
     sc[SC_TRACE_N * R] = L.cg(CW_TRN);
     sc[SC_EVENTS * R] = events0 + L.d_ev;
+    if (LP) sc[SC_DUE_H * R] = L.dg(DW_HN) & 0xFFFFu;
     sc[SC_DELIVERED * R] += L.cg(CW_DL); sc[SC_DROPPED * R] += L.cg(CW_DR);
     sc[SC_UNDELIV * R] += L.cg(CW_UD); sc[SC_THREADS * R] += L.d_th;
     if (!LP && c.Cr) {
@@ -2011,13 +2150,43 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
 __device__ __forceinline__ void lp_deliver(const Dev& c, uint4 a, uint4 b, uint64_t GAS* tmin) {
     const uint32_t lp = b.w - c.lp0;
     const uint32_t k = __hip_atomic_fetch_add(gp(c.inbox_n) + lp, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (k >= c.IB) {
+    const uint32_t cap = ib_cap(c, lp);
+    if (k >= cap) {
         __hip_atomic_fetch_or(gp(c.lp_err), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         return;
     }
-    uint4 GAS* q = gp(c.inbox) + ((size_t)k * c.R + lp) * 2;
+    uint4 GAS* q = gp(c.inbox) + (ib_base(c, lp) + (size_t)k * ib_stride(c)) * 2;
     q[0] = a;
     q[1] = b;
+    __hip_atomic_fetch_min(tmin, (uint64_t)ent_t(a), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // the record that makes the inbox heavy lists the lane for tw_lp_due at the
+    // next window's start (device loop; the list of window wid + 1)
+    if (k == TW_LIGHT && c.win) {
+        const uint32_t l = (c.wid + 1u) & 1u;
+        const uint32_t i = __hip_atomic_fetch_add(gp(c.heavy_n) + l, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        gp(c.heavy)[(size_t)l * c.R + i] = lp;
+    }
+    lp_list_next(c, lp);
+}
+// Batched LP: a spawn record pair (Lane::emit_spawn) for a local lane.
+__device__ __forceinline__ void lp_spawn(const Dev& c, const uint4 GAS* o, uint64_t GAS* tmin) {
+    const uint4 a = o[0], b = o[1], d = o[2], e = o[3];
+    const uint32_t dst = b.w;
+    if (dst < c.lp0 || dst >= c.lp0 + c.R) {
+        __hip_atomic_fetch_or(gp(c.lp_err), 4u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return;
+    }
+    const uint32_t lp = dst - c.lp0;
+    const uint32_t k = __hip_atomic_fetch_add(gp(c.spawn_n) + lp, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (k >= TW_SPN) {
+        __hip_atomic_fetch_or(gp(c.lp_err), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return;
+    }
+    uint4 GAS* q = gp(c.spawn) + ((size_t)k * c.R + lp) * 4;
+    q[0] = a;
+    q[1] = b;
+    q[2] = d;
+    q[3] = e;
     __hip_atomic_fetch_min(tmin, (uint64_t)ent_t(a), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     lp_list_next(c, lp);
 }
@@ -2066,6 +2235,11 @@ __global__ void __launch_bounds__(256) tw_lp_pack(Dev c, uint4* send, const uint
     for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
         const uint4 a = gp(c.outbox)[(size_t)i * 2], b = gp(c.outbox)[(size_t)i * 2 + 1];
         const uint32_t dst = b.w;
+        if (b.y == TW_SPAWN_CONT) continue;  // second half of a spawn pair
+        if (b.y == TW_SPAWN_KIND) {
+            lp_spawn(c, gp(c.outbox) + (size_t)i * 2, tmin);
+            continue;
+        }
         if (dst >= c.lp0 && dst < c.lp0 + c.R) {
             lp_deliver(c, a, b, tmin);
         } else if (send && world > 1) {
@@ -2112,8 +2286,9 @@ __global__ void tw_lp_fill(Dev c, int64_t* red) {
         gp(red)[1] = 0;
         return;
     }
-    const uint64_t a = *gp(c.next_t), b = (uint64_t)w[WN_REC_MIN];
-    const uint64_t m = a < b ? a : b;
+    const uint64_t a = *gp(c.next_t), b = (uint64_t)w[WN_REC_MIN], p = *gp(c.pend_min);
+    uint64_t m = a < b ? a : b;
+    m = p < m ? p : m;
     gp(red)[0] = m >= (uint64_t)INT64_MAX ? INT64_MAX : (int64_t)m;
     gp(red)[1] = -(int64_t)*gp(c.n_active);
 }
@@ -2142,6 +2317,9 @@ __global__ void tw_lp_ctl(Dev c, const int64_t* red, uint4* send, uint32_t world
     const uint32_t act = (uint32_t)w[WN_ACT] ^ 1u;
     w[WN_ACT] = act;
     w[WN_WID] += 1;
+    // tw_lp_due serves heavy list wid & 1 now; the other one collects this window's
+    *gp(c.pend_min) = ~0ull;
+    gp(c.heavy_n)[(w[WN_WID] + 1) & 1] = 0;
     for (int k = 0; k < TW_LP_NB; ++k) gp(c.act_n)[act * TW_LP_NB + k] = 0;  // tw_lp_compact builds it next
     w[WN_REC_MIN] = (int64_t)~0ull;
     w[WN_FLAGS] = WN_FRESH;
@@ -2225,6 +2403,139 @@ __global__ void tw_lp_begin(Dev c, int64_t lookahead) {
     *gp(c.out_n) = 0;
     *gp(c.n_active) = 0;
     *gp(c.next_t) = ~0ull;
+    *gp(c.pend_min) = ~0ull;
+    gp(c.heavy_n)[0] = gp(c.heavy_n)[1] = 0;
+}
+
+// Heavy inboxes at a window's first tick (device loop).  A lane with more than
+// TW_LIGHT pending records (a hotspot receiver: hundreds of messages in flight)
+// would otherwise hold every one of them as a phantom thread in its queue.
+// Here one workgroup per heavy lane stages the records in LDS, keeps the ones
+// due in this window [T, T + L) as the lane's due run, sorted by (t, link,
+// payload, src, kind) -- the order the light drain inserts them in -- with
+// their queue seqs reserved now, as if they had been queued at the window's
+// start; the rest stay in the inbox (their earliest time bounds the next
+// window).  Lanes still heavy afterwards are listed for the next window's pass.
+#define TW_DUE_GRID 1024  // tw_lp_due workgroups (each serves heavy lanes in turn)
+__device__ __forceinline__ bool rec_less(uint4 a, uint4 b, uint4 c, uint4 d) {
+    const int64_t t1 = ent_t(a), t2 = ent_t(c);
+    if (t1 != t2) return t1 < t2;
+    if (b.x != d.x) return b.x < d.x;
+    const uint64_t p1 = ((uint64_t)a.w << 32) | a.z, p2 = ((uint64_t)c.w << 32) | c.z;
+    if (p1 != p2) return p1 < p2;
+    if (b.z != d.z) return b.z < d.z;
+    return b.y < d.y;
+}
+__global__ void __launch_bounds__(256) tw_lp_due(Dev c) {
+    const int64_t GAS* w = gp(c.win);
+    const int64_t fl = w[WN_FLAGS];
+    if (!(fl & WN_FRESH) || (fl & WN_DONE)) return;
+    const uint32_t wid = (uint32_t)w[WN_WID];
+    const int64_t tend = w[WN_T] + w[WN_L] - 1;
+    const uint32_t lst = wid & 1u;
+    const uint32_t nh = gp(c.heavy_n)[lst];
+    __shared__ uint4 ea[TW_HEAVY_CAP], eb[TW_HEAVY_CAP];
+    __shared__ uint16_t dix[TW_HEAVY_CAP];  // entry index of the i-th due record (arrival order)
+    __shared__ uint32_t cnt[257];           // exclusive scan of the due counts per thread; [256] = total
+    __shared__ unsigned long long smin;
+    static_assert(TW_HEAVY_CAP == 256 * 8, "eight entries per thread");
+    const uint32_t tid = threadIdx.x;
+    const size_t st = ib_stride(c);
+    for (uint32_t hi = blockIdx.x; hi < nh; hi += gridDim.x) {
+        const uint32_t r = gp(c.heavy)[(size_t)lst * c.R + hi];
+        uint32_t n = gp(c.inbox_n)[r];
+        const uint32_t cap = ib_cap(c, r);
+        n = n < cap ? n : cap;
+        const size_t ib = ib_base(c, r);
+        for (uint32_t k = tid; k < n; k += 256) {
+            const uint4 GAS* q = gp(c.inbox) + (ib + (size_t)k * st) * 2;
+            ea[k] = q[0];
+            eb[k] = q[1];
+        }
+        if (tid == 0) smin = ~0ull;
+        __syncthreads();
+        // thread tid owns entries [8 tid, 8 tid + 8): due flags, then a scan
+        uint32_t my = 0;
+        for (uint32_t j = 0; j < 8; ++j) {
+            const uint32_t k = tid * 8 + j;
+            my += (k < n && ent_t(ea[k]) <= tend) ? 1u : 0u;
+        }
+        cnt[tid] = my;
+        __syncthreads();
+        if (tid == 0) {
+            uint32_t run = 0;
+            for (int i = 0; i < 256; ++i) {
+                const uint32_t v = cnt[i];
+                cnt[i] = run;
+                run += v;
+            }
+            cnt[256] = run;
+        }
+        __syncthreads();
+        const uint32_t nd = cnt[256];
+        // due records -> dix (arrival order); the rest compacted back into the
+        // inbox in arrival order (every record is staged in LDS already)
+        uint32_t before = cnt[tid];
+        unsigned long long mn = ~0ull;
+        for (uint32_t j = 0; j < 8; ++j) {
+            const uint32_t k = tid * 8 + j;
+            if (k >= n) break;
+            const int64_t t = ent_t(ea[k]);
+            if (t <= tend) {
+                dix[before++] = (uint16_t)k;
+            } else {
+                uint4 GAS* q = gp(c.inbox) + (ib + (size_t)(k - before) * st) * 2;
+                q[0] = ea[k];
+                q[1] = eb[k];
+                mn = (unsigned long long)t < mn ? (unsigned long long)t : mn;
+            }
+        }
+        if (mn != ~0ull) atomicMin(&smin, mn);
+        __syncthreads();
+        // rank of every due record among the due ones (ties by arrival) = its
+        // position in the due run
+        for (uint32_t i = tid; i < nd; i += 256) {
+            const uint32_t k = dix[i];
+            const uint4 a = ea[k], b = eb[k];
+            uint32_t rank = 0;
+            for (uint32_t j = 0; j < nd; ++j) {
+                const uint32_t m = dix[j];
+                rank += (rec_less(ea[m], eb[m], a, b) || (j < i && !rec_less(a, b, ea[m], eb[m]))) ? 1u : 0u;
+            }
+            uint4 GAS* q = gp(c.due) + (ib + (size_t)rank * st) * 2;
+            q[0] = a;
+            q[1] = b;
+        }
+        if (tid == 0) {
+            const uint32_t left = n - nd;
+            gp(c.inbox_n)[r] = left;
+            uint64_t* sc = gp(c.scal) + r;
+            const size_t R = c.R;
+            const uint64_t s0 = sc[SC_SEQ * R];
+            if (s0 + nd >= 0xFFFFFFFFull) {
+                if (sc[SC_STATUS * R] == TW_REP_RUNNING) sc[SC_STATUS * R] = TW_REP_ERR_COUNTER;
+            } else {
+                sc[SC_SEQ * R] = s0 + nd;  // the due run's queue seqs: s0 + 1 .. s0 + nd
+            }
+            sc[SC_DUE_SEQ * R] = s0;
+            sc[SC_DUE_N * R] = nd;
+            sc[SC_DUE_H * R] = 0;
+            if (smin != ~0ull)
+                __hip_atomic_fetch_min(gp(c.pend_min), (uint64_t)smin, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            // due now: this window's list (compacted next, from mark wid - 1);
+            // only records due later and few enough for the light drain: the
+            // next window's list; still heavy: the next window's pass
+            if (nd) gp(c.listed)[r] = wid - 1u;
+            else if (left && left <= TW_LIGHT && gp(c.listed)[r] != wid - 1u) gp(c.listed)[r] = wid;
+            if (left > TW_LIGHT) {
+                const uint32_t l = lst ^ 1u;
+                const uint32_t i = __hip_atomic_fetch_add(gp(c.heavy_n) + l, 1u, __ATOMIC_RELAXED,
+                                                          __HIP_MEMORY_SCOPE_AGENT);
+                gp(c.heavy)[(size_t)l * c.R + i] = r;
+            }
+        }
+        __syncthreads();
+    }
 }
 
 // Per-replica digest of the results and node hashes (tw_tie_audit compares
@@ -2258,6 +2569,10 @@ struct tw_ctx {
     int geo = 0;  // 0: dense (TW_WG, TW_NEAR_CAP); 1: sparse (TW_WG_SPARSE, TW_NEAR_SPARSE); 2: half (TW_WG, TW_NEAR_CAP, TW_HALF_LANES lanes per wave)
     // LP mode
     bool lp = false;
+    bool lpb = false;               // batched LP (tw_lpb_load): R = nodes x replicas
+    uint32_t n_rep = 1;             // replicas batched per node
+    bool heavy_ok = false;          // some node's inbox can exceed TW_LIGHT (tw_lp_due runs)
+    uint64_t lpb_windows = 0, lpb_ticks = 0;  // of the last batched-LP tw_run
     uint4* foreign = nullptr;      // [out_cap][2]
     uint32_t* n_foreign = nullptr;
     uint4* staging = nullptr;      // inject staging [out_cap][2]
@@ -2481,19 +2796,42 @@ static void classify_pcs(const tw_scenario_desc* s, std::vector<uint8_t>& cls) {
 }
 
 static int load_common(tw_ctx* c, const tw_scenario_desc* s, bool lp, uint32_t lp_begin, uint32_t lp_count,
-                       int64_t lookahead, uint32_t inbox_cap, uint32_t outbox_cap) {
+                       int64_t lookahead, uint32_t inbox_cap, uint32_t outbox_cap, bool lpb = false,
+                       const uint32_t* node_caps = nullptr) {
     if (!c) return TW_ERR_INVALID;
     int v = validate(s);
     if (v) return v;
-    if (lp && (s->n_replicas != 1 || lp_count == 0 || (uint64_t)lp_begin + lp_count > s->n_nodes ||
-               inbox_cap == 0 || inbox_cap > 32 || outbox_cap == 0 || lookahead < 1))
+    uint32_t rep_lg = 0;
+    if (lpb) {
+        // every replica's nodes as lanes (node-major): a power-of-two replica count
+        while ((1u << rep_lg) < s->n_replicas) ++rep_lg;
+        if ((1u << rep_lg) != s->n_replicas || rep_lg > 16 || (uint64_t)s->n_nodes << rep_lg > 0x7FFFFFFFull ||
+            outbox_cap < 2 || lookahead < 1)
+            return TW_ERR_INVALID;
+        uint64_t tot = 0;
+        for (uint32_t n = 0; n < s->n_nodes; ++n) {
+            const uint32_t k = node_caps ? node_caps[n] : inbox_cap;
+            if (k == 0 || k > TW_HEAVY_CAP) return TW_ERR_INVALID;
+            tot += k;
+        }
+        if ((tot << rep_lg) > 0xFFFFFFFFull) return TW_ERR_INVALID;
+        lp_begin = 0;
+        lp_count = s->n_nodes << rep_lg;
+    } else if (lp && (s->n_replicas != 1 || lp_count == 0 || (uint64_t)lp_begin + lp_count > s->n_nodes ||
+                      inbox_cap == 0 || inbox_cap > TW_LIGHT || outbox_cap == 0 || lookahead < 1)) {
         return TW_ERR_INVALID;
+    }
     HIPCHK(hipSetDevice(c->device));
     HIPCHK(hipStreamSynchronize(c->stream));
     free_all(c);
     Dev& d = c->d;
     d = Dev{};
     c->lp = lp;
+    c->lpb = lpb;
+    c->n_rep = lpb ? s->n_replicas : 1u;
+    c->heavy_ok = false;
+    d.rep_lg = rep_lg;
+    d.lpb = lpb ? 1u : 0u;
     d.R = lp ? lp_count : s->n_replicas;
     d.S = s->max_slots; d.Q = s->queue_capacity;
     d.RQ = (uint64_t)d.S * d.R;
@@ -2576,7 +2914,7 @@ static int load_common(tw_ctx* c, const tw_scenario_desc* s, bool lp, uint32_t l
     ALLOC(d.bind, (size_t)d.N * R);
     ALLOC(d.bind_own, (size_t)d.N * R);
     ALLOC(d.bind_rel, (size_t)d.N * R);
-    ALLOC(d.link_ord, (size_t)(d.L ? d.L : 1) * (lp ? 1 : R));
+    ALLOC(d.link_ord, (size_t)(d.L ? d.L : 1) * (lp ? (size_t)1 << rep_lg : R));
     ALLOC(d.tmo_done, (size_t)(d.T ? d.T : 1) * R);
     ALLOC(d.n_active, 1);
     ALLOC(c->d_dev, 1);
@@ -2591,9 +2929,30 @@ static int load_common(tw_ctx* c, const tw_scenario_desc* s, bool lp, uint32_t l
     ALLOC(d.prof, P_COUNT);
     HIPCHK(hipMemsetAsync(d.prof, 0, 8 * P_COUNT, c->stream));
 #endif
+    uint32_t* iboff = nullptr;
+    std::vector<uint32_t> h_iboff;
     if (lp) {
-        ALLOC(d.hash_g, (size_t)d.Ntot);
-        ALLOC(d.inbox, (size_t)d.IB * R * 2);
+        size_t ib_entries = (size_t)d.IB * R;
+        if (lpb) {
+            h_iboff.resize((size_t)s->n_nodes + 1);
+            h_iboff[0] = 0;
+            for (uint32_t n = 0; n < s->n_nodes; ++n) {
+                const uint32_t k = node_caps ? node_caps[n] : inbox_cap;
+                h_iboff[n + 1] = h_iboff[n] + k;
+                if (k > TW_LIGHT) c->heavy_ok = true;
+            }
+            ib_entries = (size_t)h_iboff[s->n_nodes] << rep_lg;
+            d.IB = 0;
+            ALLOC(iboff, h_iboff.size());
+            ALLOC(d.spawn, (size_t)TW_SPN * R * 4);
+            ALLOC(d.spawn_n, R);
+        }
+        ALLOC(d.hash_g, (size_t)d.Ntot << rep_lg);
+        ALLOC(d.inbox, ib_entries * 2);
+        ALLOC(d.due, c->heavy_ok ? ib_entries * 2 : 2);
+        ALLOC(d.heavy, c->heavy_ok ? 2 * R : 2);
+        ALLOC(d.heavy_n, 2);
+        ALLOC(d.pend_min, 1);
         ALLOC(d.inbox_n, R);
         ALLOC(d.outbox, (size_t)d.out_cap * 2);
         ALLOC(d.out_n, 1);
@@ -2609,7 +2968,7 @@ static int load_common(tw_ctx* c, const tw_scenario_desc* s, bool lp, uint32_t l
         ALLOC(c->red_own, 2);
     }
     int64_t *mregs = nullptr, *nvi = nullptr;
-    if (s->main_regs && !lp) ALLOC(mregs, R * 4);
+    if (s->main_regs && (!lp || lpb)) ALLOC(mregs, (size_t)s->n_replicas * 4);
     if (s->node_vars) ALLOC(nvi, (size_t)d.Ntot * 4);
     uint32_t* lsi = nullptr;
     if (s->node_listen) ALLOC(lsi, (size_t)d.Ntot);
@@ -2625,7 +2984,9 @@ static int load_common(tw_ctx* c, const tw_scenario_desc* s, bool lp, uint32_t l
         HIPCHK(hipMemcpyAsync(lrev, s->link_rev, 4ull * d.L, hipMemcpyHostToDevice, st));
     }
     if (ltab) HIPCHK(hipMemcpyAsync(ltab, s->link_table, 4ull * d.L * d.D * Rt, hipMemcpyHostToDevice, st));
-    if (mregs) HIPCHK(hipMemcpyAsync(mregs, s->main_regs, 32ull * R, hipMemcpyHostToDevice, st));
+    if (mregs) HIPCHK(hipMemcpyAsync(mregs, s->main_regs, 32ull * s->n_replicas, hipMemcpyHostToDevice, st));
+    if (iboff) HIPCHK(hipMemcpy(iboff, h_iboff.data(), 4 * h_iboff.size(), hipMemcpyHostToDevice));
+    d.ib_off = iboff;
     if (nvi) HIPCHK(hipMemcpyAsync(nvi, s->node_vars, 32ull * d.Ntot, hipMemcpyHostToDevice, st));
     if (lsi) HIPCHK(hipMemcpyAsync(lsi, s->node_listen, 4ull * d.Ntot, hipMemcpyHostToDevice, st));
     if (mbytes) {
@@ -2663,6 +3024,11 @@ int tw_lp_load(tw_ctx* c, const tw_scenario_desc* s, uint32_t lp_begin, uint32_t
     return load_common(c, s, true, lp_begin, lp_count, lookahead_us, inbox_cap, outbox_cap);
 }
 
+int tw_lpb_load(tw_ctx* c, const tw_scenario_desc* s, int64_t lookahead_us, const uint32_t* node_inbox_cap,
+                uint32_t inbox_cap, uint32_t outbox_cap) {
+    return load_common(c, s, true, 0, 0, lookahead_us, inbox_cap, outbox_cap, true, node_inbox_cap);
+}
+
 int tw_reset(tw_ctx* c) {
     if (!c) return TW_ERR_INVALID;
     if (!c->loaded) return TW_ERR_STATE;
@@ -2673,10 +3039,12 @@ int tw_reset(tw_ctx* c) {
     HIPCHK(hipMemsetAsync(d.nvars, 0, 32ull * d.N * R, st));
     HIPCHK(hipMemsetAsync(d.hash, 0, 8ull * d.N * R, st));
     HIPCHK(hipMemsetAsync(d.bind, 0, 4ull * d.N * R, st));
-    HIPCHK(hipMemsetAsync(d.link_ord, 0, 4ull * (d.L ? d.L : 1) * (c->lp ? 1 : R), st));
+    HIPCHK(hipMemsetAsync(d.link_ord, 0, 4ull * (d.L ? d.L : 1) * (c->lp ? (size_t)1 << d.rep_lg : R), st));
     HIPCHK(hipMemsetAsync(d.tmo_done, 0, (size_t)(d.T ? d.T : 1) * R, st));
     if (c->lp) {
-        HIPCHK(hipMemsetAsync(d.hash_g, 0, 8ull * d.Ntot, st));
+        HIPCHK(hipMemsetAsync(d.hash_g, 0, 8ull * ((size_t)d.Ntot << d.rep_lg), st));
+        HIPCHK(hipMemsetAsync(d.heavy_n, 0, 8, st));
+        HIPCHK(hipMemsetAsync(d.pend_min, 0xFF, 8, st));
         HIPCHK(hipMemsetAsync(d.out_n, 0, 4, st));
         HIPCHK(hipMemsetAsync(d.lp_err, 0, 4, st));
         HIPCHK(hipMemsetAsync(c->n_foreign, 0, 4, st));
@@ -2693,9 +3061,16 @@ int tw_reset(tw_ctx* c) {
 }
 
 
+static int lpb_run(tw_ctx* c, tw_stats* out);
+
 int tw_run(tw_ctx* c, int64_t t_end_us, uint64_t max_events, tw_stats* out) {
     if (!c) return TW_ERR_INVALID;
     if (!c->loaded) return TW_ERR_STATE;
+    if (c->lpb) {
+        // the batched window loop runs every replica to quiescence
+        if (t_end_us != INT64_MAX || max_events != UINT64_MAX) return TW_ERR_INVALID;
+        return lpb_run(c, out);
+    }
     auto w0 = std::chrono::steady_clock::now();
     HIPCHK(hipSetDevice(c->device));
     hipStream_t st = c->stream;
@@ -2789,12 +3164,33 @@ int tw_read_results(tw_ctx* c, tw_replica_result* out, size_t n) {
     if (!c || !out) return TW_ERR_INVALID;
     if (!c->loaded) return TW_ERR_STATE;
     const Dev& d = c->d;
-    if (n < d.R) return TW_ERR_INVALID;
+    if (n < (c->lpb ? c->n_rep : d.R)) return TW_ERR_INVALID;
     HIPCHK(hipSetDevice(c->device));
     std::vector<uint64_t> sc((size_t)SC_COUNT * d.R);
     HIPCHK(hipMemcpyAsync(sc.data(), d.scal, 8ull * SC_COUNT * d.R, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
     auto F = [&](int f, uint32_t i) { return sc[(size_t)f * d.R + i]; };
+    if (c->lpb) {
+        // per replica: the sum over its nodes' lanes (lane = node << rep_lg | replica);
+        // final time = the latest, status = the worst error, else done
+        const uint32_t nr = c->n_rep;
+        if (n < nr) return TW_ERR_INVALID;
+        for (uint32_t q = 0; q < nr; ++q) {
+            tw_replica_result& o = out[q];
+            std::memset(&o, 0, sizeof(o));
+            o.status = TW_REP_DONE;
+            for (uint32_t nd = 0; nd < d.Ntot; ++nd) {
+                const uint32_t i = (nd << d.rep_lg) | q;
+                if ((int64_t)F(SC_FINAL_T, i) > o.final_t) o.final_t = (int64_t)F(SC_FINAL_T, i);
+                o.events += F(SC_EVENTS, i); o.delivered += F(SC_DELIVERED, i); o.dropped += F(SC_DROPPED, i);
+                o.undeliverable += F(SC_UNDELIV, i); o.threads += F(SC_THREADS, i);
+                if (F(SC_MAIN_EXC, i)) o.main_exc = (uint32_t)F(SC_MAIN_EXC, i);
+                const uint32_t stt = (uint32_t)F(SC_STATUS, i);
+                if (stt >= TW_REP_ABORTED && stt > o.status) o.status = stt;
+            }
+        }
+        return TW_OK;
+    }
     for (uint32_t i = 0; i < d.R; ++i) {
         out[i].final_t = (int64_t)F(SC_FINAL_T, i); out[i].events = F(SC_EVENTS, i);
         out[i].delivered = F(SC_DELIVERED, i); out[i].dropped = F(SC_DROPPED, i);
@@ -2845,7 +3241,7 @@ int tw_tie_audit(tw_ctx* c, int64_t t_end_us, uint64_t max_events, uint32_t prob
 int tw_geometry(tw_ctx* c) {
     if (!c) return TW_ERR_INVALID;
     if (!c->loaded) return TW_ERR_STATE;
-    return c->lp ? TW_GEO_LP : c->geo;
+    return c->lpb ? TW_GEO_LPB : c->lp ? TW_GEO_LP : c->geo;
 }
 
 int tw_set_counter_base(tw_ctx* c, uint32_t seq0, uint32_t tid0) {
@@ -2861,6 +3257,14 @@ int tw_read_hashes(tw_ctx* c, uint64_t* out, size_t n) {
     const Dev& d = c->d;
     if (n < (size_t)d.R * d.N) return TW_ERR_INVALID;
     HIPCHK(hipSetDevice(c->device));
+    if (c->lpb) {  // hash_g is [node][replica] over the batch too
+        std::vector<uint64_t> tmp((size_t)d.Ntot << d.rep_lg);
+        HIPCHK(hipMemcpyAsync(tmp.data(), d.hash_g, 8 * tmp.size(), hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+        for (uint32_t node = 0; node < d.Ntot; ++node)
+            for (uint32_t q = 0; q < c->n_rep; ++q) out[(size_t)q * d.Ntot + node] = tmp[((size_t)node << d.rep_lg) | q];
+        return TW_OK;
+    }
     std::vector<uint64_t> tmp((size_t)d.R * d.N);  // device layout [node][replica]
     HIPCHK(hipMemcpyAsync(tmp.data(), d.hash, 8ull * d.R * d.N, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
@@ -3033,6 +3437,10 @@ int tw_lp_loop_begin(tw_ctx* c) {
     c->d.wid = 0;
     hipLaunchKernelGGL(tw_lp_begin, dim3(1), dim3(1), 0, c->stream, c->dwin(), c->d.lookahead);
     HIPCHK(hipGetLastError());
+    if (c->heavy_ok) {
+        hipLaunchKernelGGL(tw_lp_due, dim3(TW_DUE_GRID), dim3(256), 0, c->stream, c->dwin());
+        HIPCHK(hipGetLastError());
+    }
     hipLaunchKernelGGL(tw_lp_compact, dim3(compact_blocks(c->d.R)), dim3(256), 0, c->stream, c->dwin(), 0u, 0u);
     HIPCHK(hipGetLastError());
     HIPCHK(hipMemsetAsync(c->d.lp_err, 0, 4, c->stream));
@@ -3085,6 +3493,10 @@ int tw_lp_tick_end(tw_ctx* c) {
     hipLaunchKernelGGL(tw_lp_ctl, dim3(1), dim3(1), 0, c->stream, c->dwin(), (const int64_t*)c->ex_red, c->ex_send,
                        c->ex_world, c->ex_cap);
     HIPCHK(hipGetLastError());
+    if (c->heavy_ok) {
+        hipLaunchKernelGGL(tw_lp_due, dim3(TW_DUE_GRID), dim3(256), 0, c->stream, c->dwin());
+        HIPCHK(hipGetLastError());
+    }
     hipLaunchKernelGGL(tw_lp_compact, dim3(compact_blocks(c->d.R)), dim3(256), 0, c->stream, c->dwin(), 0u, 0u);
     HIPCHK(hipGetLastError());
     return TW_OK;
@@ -3128,6 +3540,63 @@ int tw_lp_run_windows(tw_ctx* c, uint64_t max_ticks, tw_lp_state* out) {
         if (out->done) return TW_OK;
     }
     return TW_ERR_INCOMPLETE;
+}
+
+// Batched LP: tw_run = the whole device window loop (one host sync per 16 ticks)
+static int lpb_run(tw_ctx* c, tw_stats* out) {
+    auto w0 = std::chrono::steady_clock::now();
+    std::vector<tw_replica_result> before;
+    if (out) {
+        before.resize(c->n_rep);
+        int rc = tw_read_results(c, before.data(), before.size());
+        if (rc) return rc;
+    }
+    while (c->ev_pool.size() < 2) {
+        hipEvent_t e;
+        HIPCHK(hipEventCreate(&e));
+        c->ev_pool.push_back(e);
+    }
+    int rc = tw_lp_loop_begin(c);
+    if (rc) return rc;
+    HIPCHK(hipEventRecord(c->ev_pool[0], c->stream));
+    tw_lp_state ls{};
+    rc = tw_lp_run_windows(c, 1ull << 40, &ls);
+    HIPCHK(hipEventRecord(c->ev_pool[1], c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    float ms = 0.f;
+    HIPCHK(hipEventElapsedTime(&ms, c->ev_pool[0], c->ev_pool[1]));
+    c->launch_ms.assign(1, ms);
+    c->lpb_windows = ls.windows;
+    c->lpb_ticks = ls.ticks;
+    if (rc) return rc;
+    if (out) {
+        std::memset(out, 0, sizeof(*out));
+        std::vector<tw_replica_result> rr(c->n_rep);
+        rc = tw_read_results(c, rr.data(), rr.size());
+        if (rc) return rc;
+        for (uint32_t i = 0; i < c->n_rep; ++i) {
+            out->events += rr[i].events - before[i].events;
+            out->delivered += rr[i].delivered - before[i].delivered;
+            out->dropped += rr[i].dropped - before[i].dropped;
+            out->undeliverable += rr[i].undeliverable - before[i].undeliverable;
+            if (rr[i].final_t > out->max_final_t) out->max_final_t = rr[i].final_t;
+            if (rr[i].status == TW_REP_DONE) ++out->replicas_done;
+            if (rr[i].status >= TW_REP_ERR_SLOTS) ++out->replicas_error;
+        }
+        out->sends = out->delivered + out->dropped + out->undeliverable;
+        out->launches = (uint32_t)ls.ticks;
+        out->kernel_ms = ms;
+        out->wall_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - w0).count();
+    }
+    return TW_OK;
+}
+
+int tw_lpb_windows(tw_ctx* c, uint64_t* windows, uint64_t* ticks) {
+    if (!c) return TW_ERR_INVALID;
+    if (!c->loaded || !c->lpb) return TW_ERR_STATE;
+    if (windows) *windows = c->lpb_windows;
+    if (ticks) *ticks = c->lpb_ticks;
+    return TW_OK;
 }
 
 #ifdef TW_STATS

@@ -73,7 +73,9 @@ __device__ __forceinline__ void th_set_xval(Th& t, int64_t v) {
 enum {
     SC_NOW, SC_FINAL_T, SC_EVENTS, SC_DELIVERED, SC_DROPPED, SC_UNDELIV, SC_THREADS, SC_SEQ, SC_TIDC,
     SC_LIVE, SC_NEAR_N, SC_FAR_N, SC_STATUS, SC_MAIN_EXC, SC_PENDING_MAIN, SC_FREE_N, SC_FTOP, SC_BUMP,
-    SC_TMO_CTR, SC_RH0, SC_RC0 = SC_RH0 + TW_RUNS, SC_TRACE_N = SC_RC0 + TW_RUNS, SC_COUNT
+    SC_TMO_CTR, SC_RH0, SC_RC0 = SC_RH0 + TW_RUNS, SC_TRACE_N = SC_RC0 + TW_RUNS,
+    // LP: this window's due run of a heavy lane (tw_lp_due): count, head, seq base
+    SC_DUE_N, SC_DUE_H, SC_DUE_SEQ, SC_COUNT
 };
 
 struct Dev {
@@ -108,12 +110,24 @@ struct Dev {
     uint32_t* link_ord;  // [L][R]
     uint8_t* tmo_done;   // [T][R]
     uint32_t* n_active;  // [1]
-    // node-partitioned (LP) mode: lane r = global node lp0 + r
+    // node-partitioned (LP) mode: global lane g = lp0 + r runs node g >> rep_lg of
+    // replica g & (2^rep_lg - 1) (node-major; rep_lg = 0 for one partitioned
+    // scenario, > 0 for the batched mode tw_lpb_load, where cross-node forks
+    // travel as spawn records)
     uint32_t lp0, Ntot, IB, out_cap;
+    uint32_t rep_lg, lpb;
     int64_t lookahead;
-    uint64_t* hash_g;    // [Ntot] this context's additions to every node's hash
-    uint4* inbox;        // [IB][R][2] delivery records addressed to local nodes
+    uint64_t* hash_g;    // [Ntot << rep_lg] this context's additions to every node's hash
+    uint4* inbox;        // delivery records addressed to local lanes: entry k of lane r at
+                         // ib_base(r) + k * ib_stride (x2 quads); [IB][R] without ib_off
     uint32_t* inbox_n;   // [R]
+    const uint32_t* ib_off;  // batched mode: [Nloc + 1] per-node capacity prefix (records), or null
+    uint4* due;          // same layout: a heavy lane's records due in this window, sorted
+    uint4* spawn;        // [TW_SPN][R][4] spawn records (batched mode)
+    uint32_t* spawn_n;   // [R]
+    uint32_t* heavy;     // [2][R] lanes with more than TW_LIGHT pending records
+    uint32_t* heavy_n;   // [2]
+    uint64_t* pend_min;  // [1] min time of records left pending by tw_lp_due
     uint4* outbox;       // [out_cap][2] records produced this window
     uint32_t* out_n;     // [1]
     uint64_t* next_t;    // [1] min next-event time (atomicMin)
@@ -162,7 +176,26 @@ __device__ __forceinline__ int64_t tx_us(const Dev& c, uint64_t link, uint32_t k
 
 // LP device-driven window words (Dev::win)
 enum { WN_T, WN_L, WN_REC_MIN, WN_WINDOWS, WN_TICKS, WN_FLAGS, WN_ACT, WN_WID, WN_COUNT };
+// spawn record markers in the kind field of an outbox entry pair (message kinds are < 256)
+#define TW_SPAWN_KIND 0xFFFFFFFFu
+#define TW_SPAWN_CONT 0xFFFFFFFEu
 enum : int64_t { WN_FRESH = 1, WN_DONE = 2 };
+
+// LP inbox addressing (see Dev::inbox)
+#define TW_LIGHT 32u   // a lane with at most this many pending records drains them in the event kernel
+#define TW_SPN 4u      // spawn records per lane per tick
+#define TW_HEAVY_CAP 2048u  // largest per-node inbox (tw_lp_due stages a lane's records in LDS)
+__device__ __forceinline__ size_t ib_base(const Dev& c, uint32_t r) {
+    if (!c.ib_off) return r;
+    const uint32_t g = c.lp0 + r, n = (g >> c.rep_lg) - (c.lp0 >> c.rep_lg);
+    return ((size_t)gp(c.ib_off)[n] << c.rep_lg) + (g & ((1u << c.rep_lg) - 1u));
+}
+__device__ __forceinline__ size_t ib_stride(const Dev& c) { return c.ib_off ? (size_t)1 << c.rep_lg : (size_t)c.R; }
+__device__ __forceinline__ uint32_t ib_cap(const Dev& c, uint32_t r) {
+    if (!c.ib_off) return c.IB;
+    const uint32_t n = ((c.lp0 + r) >> c.rep_lg) - (c.lp0 >> c.rep_lg);
+    return gp(c.ib_off)[n + 1] - gp(c.ib_off)[n];
+}
 
 // mark node r for the next window's work list (tw_lp_compact builds the list
 // from the marks, in node order within each wave: coalesced node state)

@@ -29,8 +29,8 @@ EXPORTS = ["tw_create", "tw_load", "tw_reset", "tw_run", "tw_read_results", "tw_
            "tw_lp_load", "tw_lp_window", "tw_lp_take_outbox", "tw_lp_inject", "tw_lp_results",
            "tw_set_trace", "tw_read_trace", "tw_tie_audit", "tw_set_counter_base", "tw_geometry",
            "tw_set_stream", "tw_lp_exchange_setup", "tw_lp_loop_begin", "tw_lp_tick", "tw_lp_tick_import",
-           "tw_lp_tick_end", "tw_lp_progress", "tw_lp_run_windows"]
-GEOMETRIES = ("dense", "sparse", "half", "wave", "lp", "narrow")  # TW_GEO_* order
+           "tw_lp_tick_end", "tw_lp_progress", "tw_lp_run_windows", "tw_lpb_load", "tw_lpb_windows"]
+GEOMETRIES = ("dense", "sparse", "half", "wave", "lp", "narrow", "lpb")  # TW_GEO_* order
 
 # tw_trace_rec (include/timewarp.h)
 TRACE_DTYPE = np.dtype([("t", np.int64), ("val", np.int64), ("node", np.uint32), ("tag", np.uint32)])
@@ -96,11 +96,14 @@ def load_library(path: Optional[str] = None):
         getattr(lib, name).argtypes = [C.c_void_p]
     lib.tw_lp_progress.argtypes = [C.c_void_p, C.POINTER(TwLpState)]
     lib.tw_lp_run_windows.argtypes = [C.c_void_p, C.c_uint64, C.POINTER(TwLpState)]
+    lib.tw_lpb_load.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p, C.c_uint32, C.c_uint32]
+    lib.tw_lpb_windows.argtypes = [C.c_void_p, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
     for name in ("tw_create", "tw_load", "tw_reset", "tw_run", "tw_read_results", "tw_read_hashes", "tw_read_final",
                  "tw_last_launch_ms", "tw_lp_load", "tw_lp_window", "tw_lp_take_outbox", "tw_lp_inject",
                  "tw_lp_results", "tw_set_trace", "tw_read_trace", "tw_tie_audit", "tw_set_counter_base",
                  "tw_geometry", "tw_set_stream", "tw_lp_exchange_setup", "tw_lp_loop_begin", "tw_lp_tick",
-                 "tw_lp_tick_import", "tw_lp_tick_end", "tw_lp_progress", "tw_lp_run_windows"):
+                 "tw_lp_tick_import", "tw_lp_tick_end", "tw_lp_progress", "tw_lp_run_windows", "tw_lpb_load",
+                 "tw_lpb_windows"):
         getattr(lib, name).restype = C.c_int
     if path is None:
         _lib = lib
@@ -161,8 +164,11 @@ class Engine:
         dense layout, one 64-replica wave per workgroup), "sparse" (16
         replicas per workgroup, 768-entry on-chip queue), "wave" (a
         wavefront per replica), "half" (the dense layout as two 32-lane waves
-        per SIMD; an experiment) or None = the library's choice (wave for <=
+        per SIMD; an experiment), "lpb" (every (node, replica) a logical
+        process: `load_lpb`) or None = the library's choice (wave for <=
         4096 replicas, narrow below 65536, else dense; env TW_GEOMETRY)."""
+        if geometry == "lpb":
+            return self.load_lpb(scn)
         d = scn.desc()
         old = os.environ.get("TW_GEOMETRY")
         if geometry is not None:
@@ -179,6 +185,42 @@ class Engine:
                     os.environ["TW_GEOMETRY"] = old
         self.scn = scn
         return self
+
+    def load_lpb(self, scn: Scenario, lookahead_us: Optional[int] = None, node_inbox_cap=None,
+                 outbox_cap: Optional[int] = None) -> "Engine":
+        """Batched node-partitioned mode (tw_lpb_load): the replicas' nodes run
+        as logical processes in conservative windows of `lookahead_us` (default:
+        the smallest link delay of the table), so a replica's events run in
+        parallel across its nodes.  Per-lane capacities come from the
+        scenario's meta (lp_max_slots, lp_queue_capacity, lp_inbox_cap: one
+        value or one per node, lp_outbox_cap), like `lp_scenario`."""
+        import copy
+
+        if scn.link_table is None:
+            raise EngineError("load_lpb: the scenario needs a link table (its smallest delay is the lookahead)")
+        if lookahead_us is None:
+            lookahead_us = int((scn.link_table & np.uint32(0x7FFFFFFF)).min())
+        m = scn.meta
+        s = copy.copy(scn)
+        s.max_slots = int(m.get("lp_max_slots", 64))
+        s.queue_capacity = int(m.get("lp_queue_capacity", 128))
+        s.run_capacity = 0
+        cap = node_inbox_cap if node_inbox_cap is not None else m.get("lp_inbox_cap", 32)
+        caps = np.ascontiguousarray(np.broadcast_to(np.asarray(cap, np.uint32), (scn.n_nodes,)), dtype=np.uint32)
+        if outbox_cap is None:
+            outbox_cap = int(m.get("lp_outbox_cap", min(1 << 27, max(1 << 16, 8 * scn.n_nodes * scn.n_replicas))))
+        d = s.desc()
+        _check(self.lib.tw_lpb_load(self.ctx, C.addressof(d), int(lookahead_us), caps.ctypes.data, 32,
+                                    int(outbox_cap)), "tw_lpb_load")
+        self.scn = scn
+        self.lookahead_us = int(lookahead_us)
+        return self
+
+    def lpb_windows(self):
+        """(windows, ticks) of the last batched-LP run."""
+        w, t = C.c_uint64(), C.c_uint64()
+        _check(self.lib.tw_lpb_windows(self.ctx, C.byref(w), C.byref(t)), "tw_lpb_windows")
+        return int(w.value), int(t.value)
 
     def geometry(self) -> str:
         """The kernel geometry tw_load chose (GEOMETRIES)."""
@@ -244,10 +286,11 @@ class Engine:
         return buf[:n].copy()
 
 
-def run_scenario(scn: Scenario, device: int = 0, t_end: int = T_INF, max_events: int = UNLIMITED):
+def run_scenario(scn: Scenario, device: int = 0, t_end: int = T_INF, max_events: int = UNLIMITED,
+                 geometry: Optional[str] = None):
     """Load + run to quiescence; returns (stats, results, hashes)."""
     with Engine(device) as e:
-        e.load(scn)
+        e.load(scn, geometry=geometry)
         st = e.run(t_end, max_events)
         return st, e.results(), e.hashes()
 

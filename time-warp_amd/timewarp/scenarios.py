@@ -327,7 +327,15 @@ def hotspot(n_senders: int = 256, n_replicas: int = 1, msg_num: int = 1000, msg_
         main_pc=img.pc_of("main"), main_node=SYS, link_table=table,
         max_slots=_capped(max_slots), queue_capacity=_capped(2 * max_slots + 256),
         run_capacity=_capped(2 * S + 64), near_horizon_us=near_horizon_us,
-        meta=dict(config="hotspot", n_senders=S, msg_num=msg_num, msg_rate=msg_rate, payload_bytes=payload_bytes),
+        meta=dict(config="hotspot", n_senders=S, msg_num=msg_num, msg_rate=msg_rate, payload_bytes=payload_bytes,
+                  # batched node-partitioned mode (Engine.load_lpb): per-lane capacities;
+                  # the receiver holds every ping in flight (<= max_delay / sendDelay + 2
+                  # per sender), a sender its pongs, and a tick's records per replica are
+                  # <= a ping and a pong per sender and window plus main's spawn pairs
+                  lp_inbox_cap=np.array([32] * S + [min(2048, S * (max_delay // max(1, send_delay) + 2) + 64), 4],
+                                        np.uint32),
+                  lp_max_slots=64, lp_queue_capacity=128,
+                  lp_outbox_cap=min(1 << 27, (8 * S + 2 * (S + 1) + 64) * n_replicas)),
     )
 
 
