@@ -280,6 +280,10 @@ def main():
         args.nodes = {"token_ring": 4096, "hotspot": 256, "gossip": 1 << 20}.get(args.config, 2)
     if args.replicas is None:
         args.replicas = {"token_ring": 65536, "ping_pong": 1 << 20, "hotspot": 4096}.get(args.config, 1)
+    if args.geometry is None and args.config == "hotspot":
+        # C5: a replica is one long chain in the replica geometries (0.32 G
+        # events/s, wave); its nodes as logical processes run it in parallel
+        args.geometry = "lpb"
     if args.workload_key:
         print(json.dumps({"bench_workload": workload_key(args), "engine_sha": engine_sha()}))
         return

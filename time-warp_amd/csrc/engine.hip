@@ -1788,7 +1788,7 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
     uint32_t n_in = 0;
     if (LP) {
         n_in = gp(c.inbox_n)[r];
-        const bool drain = fresh && n_in != 0 && n_in <= TW_LIGHT;
+        const bool drain = fresh && n_in != 0 && ib_cap(c, r) <= TW_LIGHT;
         if (sc[SC_LIVE * R] == 0 && sc[SC_PENDING_MAIN * R] == 0 && !drain && sc[SC_DUE_H * R] >= sc[SC_DUE_N * R] &&
             !(c.lpb && gp(c.spawn_n)[r]))
             return;
@@ -1895,7 +1895,7 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
         }
     }
 
-    if (LP && fresh && n_in != 0 && n_in <= TW_LIGHT) {
+    if (LP && fresh && n_in != 0 && ib_cap(c, r) <= TW_LIGHT) {
         // delivery records addressed to this node become phantom deliverer
         // threads, inserted in (t, link, payload, src) order so queue seqs are
         // deterministic whatever order the records arrived in
@@ -2159,9 +2159,10 @@ __device__ __forceinline__ void lp_deliver(const Dev& c, uint4 a, uint4 b, uint6
     q[0] = a;
     q[1] = b;
     __hip_atomic_fetch_min(tmin, (uint64_t)ent_t(a), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    // the record that makes the inbox heavy lists the lane for tw_lp_due at the
-    // next window's start (device loop; the list of window wid + 1)
-    if (k == TW_LIGHT && c.win) {
+    // a lane whose node may hold more than TW_LIGHT records is served by
+    // tw_lp_due: its first pending record lists it for the next window's pass
+    // (device loop; the list of window wid + 1)
+    if (k == 0 && cap > TW_LIGHT && c.win) {
         const uint32_t l = (c.wid + 1u) & 1u;
         const uint32_t i = __hip_atomic_fetch_add(gp(c.heavy_n) + l, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         gp(c.heavy)[(size_t)l * c.R + i] = lp;
@@ -2407,15 +2408,16 @@ __global__ void tw_lp_begin(Dev c, int64_t lookahead) {
     gp(c.heavy_n)[0] = gp(c.heavy_n)[1] = 0;
 }
 
-// Heavy inboxes at a window's first tick (device loop).  A lane with more than
-// TW_LIGHT pending records (a hotspot receiver: hundreds of messages in flight)
-// would otherwise hold every one of them as a phantom thread in its queue.
-// Here one workgroup per heavy lane stages the records in LDS, keeps the ones
-// due in this window [T, T + L) as the lane's due run, sorted by (t, link,
-// payload, src, kind) -- the order the light drain inserts them in -- with
-// their queue seqs reserved now, as if they had been queued at the window's
-// start; the rest stay in the inbox (their earliest time bounds the next
-// window).  Lanes still heavy afterwards are listed for the next window's pass.
+// Heavy inboxes at a window's first tick (device loop).  A lane whose node may
+// hold more than TW_LIGHT pending records (a hotspot receiver: hundreds of
+// messages in flight) would otherwise hold every one of them as a phantom
+// thread, with a slot, in its queue.  Here one workgroup per such lane with
+// records stages them in LDS, keeps the ones due in this window [T, T + L) as
+// the lane's due run, sorted by (t, link, payload, src, kind) -- the order the
+// light drain inserts them in -- with their queue seqs reserved now, as if
+// they had been queued at the window's start; the rest stay in the inbox
+// (their earliest time bounds the next window) and the lane is listed for the
+// next window's pass.
 #define TW_DUE_GRID 1024  // tw_lp_due workgroups (each serves heavy lanes in turn)
 __device__ __forceinline__ bool rec_less(uint4 a, uint4 b, uint4 c, uint4 d) {
     const int64_t t1 = ent_t(a), t2 = ent_t(c);
@@ -2523,11 +2525,9 @@ __global__ void __launch_bounds__(256) tw_lp_due(Dev c) {
             if (smin != ~0ull)
                 __hip_atomic_fetch_min(gp(c.pend_min), (uint64_t)smin, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             // due now: this window's list (compacted next, from mark wid - 1);
-            // only records due later and few enough for the light drain: the
-            // next window's list; still heavy: the next window's pass
+            // records left for later windows: the next window's pass
             if (nd) gp(c.listed)[r] = wid - 1u;
-            else if (left && left <= TW_LIGHT && gp(c.listed)[r] != wid - 1u) gp(c.listed)[r] = wid;
-            if (left > TW_LIGHT) {
+            if (left) {
                 const uint32_t l = lst ^ 1u;
                 const uint32_t i = __hip_atomic_fetch_add(gp(c.heavy_n) + l, 1u, __ATOMIC_RELAXED,
                                                           __HIP_MEMORY_SCOPE_AGENT);
