@@ -338,6 +338,8 @@ def main():
               file=sys.stderr, flush=True)
         kernel_ms += float(eng.launch_ms().sum())
         launches += st.launches
+        if eng.geometry() == "lpb":
+            lpb_wt = eng.lpb_windows()
         if st.replicas_error:
             raise SystemExit(f"{st.replicas_error} replicas ended in an error status")
 
@@ -387,6 +389,12 @@ def main():
             },
         }
         out["roofline"]["algorithmic_per_event"] = alg_bytes / max(1, events)
+        if eng.geometry() == "lpb":
+            out["config"]["parallelism"] = (f"replica-sharded x{world}; inside a GPU every (node, replica) pair is a "
+                                            "logical process: one device window loop, lookahead = min link delay")
+            out["config"]["windows"], out["config"]["ticks"] = lpb_wt
+            out["roofline"]["kernel_ms_note"] = ("one launch = the whole device window loop (event kernels + "
+                                                 "due/pack/compact/advance kernels), HIP events")
         # what the timed events are (rank 0, per step): message sends, arrivals
         # (delivered / dropped / no listener), threads forked, and the rest
         # (waits, wake-ups, kills, timeouts)

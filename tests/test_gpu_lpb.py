@@ -77,9 +77,33 @@ def test_lpb_gossip_single_replica(engine_mod, oracle_mod):
     _compare_lpb(scn, engine_mod, oracle_mod, threads=1)
 
 
-def test_lpb_rejects_zero_lookahead(engine_mod):
-    # token ring's observer links have 0 µs delay: no conservative window exists
-    scn = scenarios.token_ring(n_nodes=8, n_replicas=4, launch_duration=5_000_000)
+def test_lpb_token_ring_two_phase(engine_mod, oracle_mod):
+    # the observer is fed by 0 µs links: it runs in phase 1 of every window,
+    # after the ring nodes; main's forks onto every node are spawn records
+    scn = scenarios.token_ring(n_nodes=16, n_replicas=64, launch_duration=40_000_000, drop_log2=3)
+    st, ores, windows = _compare_lpb(scn, engine_mod, oracle_mod)
+    assert ores["dropped"].sum() > 0 and ores["delivered"].sum() > 0
+
+
+def test_lpb_token_ring_many_nodes(engine_mod, oracle_mod):
+    # C3's node count (spawns over several windows, the teardown burst at
+    # launchDuration), few replicas
+    scn = scenarios.token_ring(n_nodes=4096, n_replicas=4, launch_duration=20_000_000, drop_log2=10)
+    _compare_lpb(scn, engine_mod, oracle_mod)
+
+
+def test_lpb_rejects_short_link_out_of_phase1(engine_mod):
+    # a link shorter than the lookahead out of a node that itself is fed by one
+    # would need a third phase: tw_lpb_load refuses it
+    scn = scenarios.gossip(n_nodes=64, fanout=2)
+    lt = scn.link_table.copy()
+    a = 0
+    l_ab = int(scn.topo.out_off[a])
+    b = int(scn.topo.dst[l_ab])
+    l_bc = int(scn.topo.out_off[b])
+    lt[l_ab] = 0
+    lt[l_bc] = 0
+    scn.link_table = lt
     with engine_mod.Engine(0) as e:
         with pytest.raises(engine_mod.EngineError):
-            e.load(scn, geometry="lpb")
+            e.load_lpb(scn, lookahead_us=1000)

@@ -1418,7 +1418,10 @@ struct Lane {
                             // at now, wake pop at now+d, both at this node) and its delivery travels
                             // as a record: the receiver checks its binding at now+d
                             const int64_t dly = (int64_t)(e & 0x7FFFFFFFu) + tx_us(c, link, kind);
-                            if (dly < c.lookahead) {
+                            // shorter than the lookahead: only from a phase-0 node into a
+                            // phase-1 node (delivered in this window's phase 1)
+                            if (dly < c.lookahead &&
+                                !(c.phase && gp(c.phase)[th.w1] == 0 && gp(c.phase)[gp(c.link_dst)[link]] == 1)) {
                                 fail(TW_REP_ERR_INSN);
                                 tc = T_STOP;
                             } else {
@@ -1615,10 +1618,12 @@ struct Lane {
             if (LP && c.lpb && (cdel & 2u) && cg(CW_CNODE) != th.w1) {
                 // a fork onto another node (batched LP): a spawn record; the ref is
                 // opaque (-1: refs name engine slots, and a cross-node throwTo is
-                // outside LP mode anyway)
-                emit_spawn(now, cg(CW_CPC), lane_of(cg(CW_CNODE)), rf[0], rf[WG], rf[2 * WG], rf[3 * WG]);
+                // outside LP mode anyway).  Not from a phase-1 node: the window's
+                // phase 0 has finished by then.
+                ok = !(c.phase && gp(c.phase)[th.w1]);
+                if (ok) emit_spawn(now, cg(CW_CPC), lane_of(cg(CW_CNODE)), rf[0], rf[WG], rf[2 * WG], rf[3 * WG]);
+                else fail(TW_REP_ERR_INSN);
                 ref = -1;
-                ok = true;
             } else if (cdel & 2u)
                 ok = spawn(cg(CW_CPC), cg(CW_CNODE), rf[0], rf[WG], rf[2 * WG], rf[3 * WG], ref, ch, cslot);
             else
@@ -1721,6 +1726,7 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
     // device-driven windows: the window, its work list and whether this is the
     // window's first tick (the only one that drains inboxes) come from the device
     bool fresh = true;
+    uint32_t ph = 0;
     if (LP && c.win) {
         const int64_t GAS* w = gp(c.win);
         const int64_t fl = w[WN_FLAGS];
@@ -1728,7 +1734,8 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
         t_end = w[WN_T] + w[WN_L] - 1;
         c.act_cur = (uint32_t)w[WN_ACT];
         c.wid = (uint32_t)w[WN_WID];
-        fresh = (fl & WN_FRESH) != 0;
+        ph = (uint32_t)w[WN_PHASE];
+        fresh = (fl & (ph ? WN_PH1FRESH : WN_FRESH)) != 0;
     }
     // LP: workgroup -> (bucket, span) of the window's work list, the busiest
     // bucket first, each bucket padded to whole workgroups; workgroups past the
@@ -1776,6 +1783,7 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
         r = gp(c.act)[((size_t)c.act_cur * TW_LP_NB + lp_k) * c.R + i];
     }
     if (r >= c.R) return;
+    if (LP && c.phase && gp(c.phase)[(c.lp0 + r) >> c.rep_lg] != ph) return;  // the other phase's node
     uint64_t* sc = gp(c.scal) + r;
     const size_t R = c.R;
     if (sc[SC_STATUS * R] != TW_REP_RUNNING) return;
@@ -1918,6 +1926,10 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
             }
             used |= 1u << best;
             int64_t ta = ent_t(ba);
+            if (ta < L.now) {  // delivered after the node ran past it: not conservative
+                L.fail(TW_REP_ERR_INSN);
+                break;
+            }
             uint32_t s = L.alloc_slot();
             if (s == 0xFFFFFFFFu) break;
             Th ph;
@@ -2158,7 +2170,10 @@ __device__ __forceinline__ void lp_deliver(const Dev& c, uint4 a, uint4 b, uint6
     uint4 GAS* q = gp(c.inbox) + (ib_base(c, lp) + (size_t)k * ib_stride(c)) * 2;
     q[0] = a;
     q[1] = b;
-    __hip_atomic_fetch_min(tmin, (uint64_t)ent_t(a), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // (a record due in this window -- a short link into a phase-1 node -- is
+    // drained at phase 1's first tick: it does not bound the next window)
+    const bool intra = c.win && ent_t(a) < gp(c.win)[WN_T] + gp(c.win)[WN_L];
+    if (!intra) __hip_atomic_fetch_min(tmin, (uint64_t)ent_t(a), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     // a lane whose node may hold more than TW_LIGHT records is served by
     // tw_lp_due: its first pending record lists it for the next window's pass
     // (device loop; the list of window wid + 1)
@@ -2188,7 +2203,16 @@ __device__ __forceinline__ void lp_spawn(const Dev& c, const uint4 GAS* o, uint6
     q[1] = b;
     q[2] = d;
     q[3] = e;
-    __hip_atomic_fetch_min(tmin, (uint64_t)ent_t(a), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // this tick's earliest spawn: one in the current window reruns it (tw_lp_fill),
+    // with the target lane appended to the running window's work list (once)
+    (void)tmin;
+    __hip_atomic_fetch_min((uint64_t GAS*)(gp(c.win) + WN_SPN_MIN), (uint64_t)ent_t(a), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    if (__hip_atomic_exchange(gp(c.inlist) + lp, c.wid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != c.wid) {
+        const uint32_t i = __hip_atomic_fetch_add(gp(c.act_n) + c.act_cur * TW_LP_NB, 1u, __ATOMIC_RELAXED,
+                                                  __HIP_MEMORY_SCOPE_AGENT);
+        gp(c.act)[(size_t)c.act_cur * TW_LP_NB * c.R + i] = lp;
+    }
     lp_list_next(c, lp);
 }
 
@@ -2287,11 +2311,15 @@ __global__ void tw_lp_fill(Dev c, int64_t* red) {
         gp(red)[1] = 0;
         return;
     }
-    const uint64_t a = *gp(c.next_t), b = (uint64_t)w[WN_REC_MIN], p = *gp(c.pend_min);
+    const uint64_t a = *gp(c.next_t), b = (uint64_t)w[WN_REC_MIN], p = *gp(c.pend_min), sp = (uint64_t)w[WN_SPN_MIN];
     uint64_t m = a < b ? a : b;
     m = p < m ? p : m;
+    m = sp < m ? sp : m;
     gp(red)[0] = m >= (uint64_t)INT64_MAX ? INT64_MAX : (int64_t)m;
-    gp(red)[1] = -(int64_t)*gp(c.n_active);
+    // a child forked onto another node inside this window keeps the window
+    // (phase) running: its lane starts it at the next tick
+    const bool spawn_here = sp < (uint64_t)(w[WN_T] + w[WN_L]);
+    gp(red)[1] = -(int64_t)*gp(c.n_active) - (spawn_here ? 1 : 0);
 }
 // advance: every rank idle in this window -> T := the global next time (a
 // fresh window: flip the work lists), else rerun the window
@@ -2303,12 +2331,23 @@ __global__ void tw_lp_ctl(Dev c, const int64_t* red, uint4* send, uint32_t world
     for (uint32_t g = 0; send && g < world; ++g) gp(send)[(size_t)g * (cap + 1) * 2].x = 0;
     *gp(c.n_active) = 0;
     *gp(c.next_t) = ~0ull;
-    if (gp(red)[1] < 0) {
-        w[WN_FLAGS] &= ~WN_FRESH;
+    w[WN_SPN_MIN] = (int64_t)~0ull;
+    if (gp(red)[1] < 0) {  // rerun this phase of the window
+        w[WN_FLAGS] &= ~(WN_FRESH | WN_PH1FRESH);
+        return;
+    }
+    if (c.has_ph1 && w[WN_PHASE] == 0) {
+        // phase 0 is done with the window: phase 1 (the nodes fed by short
+        // links) runs it now; the phase-0 nodes' next time waits in WN_NT0
+        w[WN_PHASE] = 1;
+        w[WN_NT0] = gp(red)[0];
+        w[WN_FLAGS] = WN_PH1FRESH;
         return;
     }
     w[WN_WINDOWS] += 1;
-    const int64_t t = gp(red)[0];
+    int64_t t = gp(red)[0];
+    if (w[WN_PHASE]) t = w[WN_NT0] < t ? w[WN_NT0] : t;
+    w[WN_PHASE] = 0;
     if (t == INT64_MAX) {
         w[WN_T] = INT64_MAX;
         w[WN_FLAGS] = WN_DONE;
@@ -2382,6 +2421,7 @@ __global__ void __launch_bounds__(256) tw_lp_compact(Dev c, uint32_t mark, uint3
                     __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
                 gp(c.act)[((size_t)dst * TW_LP_NB + k) * c.R + base[k] + cnt[k][i * 4 + wv] + below] =
                     (uint32_t)(r0 + (size_t)i * 256);
+                if (c.inlist) gp(c.inlist)[r0 + (size_t)i * 256] = mark + 1u;
             }
         }
     }
@@ -2400,6 +2440,9 @@ __global__ void tw_lp_begin(Dev c, int64_t lookahead) {
     w[WN_FLAGS] = WN_FRESH;
     w[WN_ACT] = 1;
     w[WN_WID] = 1;
+    w[WN_PHASE] = 0;
+    w[WN_NT0] = INT64_MAX;
+    w[WN_SPN_MIN] = (int64_t)~0ull;
     for (int k = 0; k < TW_LP_NB; ++k) gp(c.act_n)[TW_LP_NB + k] = 0;
     *gp(c.out_n) = 0;
     *gp(c.n_active) = 0;
@@ -2573,6 +2616,7 @@ struct tw_ctx {
     uint32_t n_rep = 1;             // replicas batched per node
     bool heavy_ok = false;          // some node's inbox can exceed TW_LIGHT (tw_lp_due runs)
     uint64_t lpb_windows = 0, lpb_ticks = 0;  // of the last batched-LP tw_run
+    bool has_ph1 = false;           // two-phase windows (Dev::phase)
     uint4* foreign = nullptr;      // [out_cap][2]
     uint32_t* n_foreign = nullptr;
     uint4* staging = nullptr;      // inject staging [out_cap][2]
@@ -2830,6 +2874,7 @@ static int load_common(tw_ctx* c, const tw_scenario_desc* s, bool lp, uint32_t l
     c->lpb = lpb;
     c->n_rep = lpb ? s->n_replicas : 1u;
     c->heavy_ok = false;
+    c->has_ph1 = false;
     d.rep_lg = rep_lg;
     d.lpb = lpb ? 1u : 0u;
     d.R = lp ? lp_count : s->n_replicas;
@@ -2931,7 +2976,43 @@ static int load_common(tw_ctx* c, const tw_scenario_desc* s, bool lp, uint32_t l
 #endif
     uint32_t* iboff = nullptr;
     std::vector<uint32_t> h_iboff;
+    uint8_t* phd = nullptr;
+    std::vector<uint8_t> h_ph;
+    if (lpb) {
+        // two-phase windows: a link shorter than the lookahead (over every
+        // replica and ordinal) must run from a phase-0 node into a node that
+        // then runs in phase 1 (after phase 0 has finished the window), and such
+        // a node's inbox must be light (drained at phase 1's first tick)
+        h_ph.assign(s->n_nodes, 0);
+        std::vector<uint8_t> shortl(s->n_links, 0);
+        for (uint32_t l = 0; l < s->n_links; ++l) {
+            uint32_t dmin = 0;
+            if (s->link_table) {
+                dmin = 0x7FFFFFFFu;
+                const uint32_t* e = s->link_table + (size_t)l * s->link_depth * s->n_replicas;
+                for (size_t i = 0; i < (size_t)s->link_depth * s->n_replicas; ++i) {
+                    const uint32_t v = e[i] & 0x7FFFFFFFu;
+                    dmin = v < dmin ? v : dmin;
+                }
+            }
+            if ((int64_t)dmin < lookahead) {
+                shortl[l] = 1;
+                h_ph[s->link_dst[l]] = 1;
+            }
+        }
+        for (uint32_t n = 0; n < s->n_nodes; ++n)
+            for (uint32_t l = s->out_off[n]; l < s->out_off[n + 1]; ++l)
+                if (shortl[l] && h_ph[n]) { free_all(c); return TW_ERR_INVALID; }
+        for (uint32_t n = 0; n < s->n_nodes; ++n) {
+            if (!h_ph[n]) continue;
+            c->has_ph1 = true;
+            if ((node_caps ? node_caps[n] : inbox_cap) > TW_LIGHT) { free_all(c); return TW_ERR_INVALID; }
+        }
+    }
     if (lp) {
+        if (c->has_ph1) {
+            ALLOC(phd, h_ph.size());
+        }
         size_t ib_entries = (size_t)d.IB * R;
         if (lpb) {
             h_iboff.resize((size_t)s->n_nodes + 1);
@@ -2961,6 +3042,7 @@ static int load_common(tw_ctx* c, const tw_scenario_desc* s, bool lp, uint32_t l
         ALLOC(d.act, 2 * TW_LP_NB * R);
         ALLOC(d.act_n, 2 * TW_LP_NB);
         ALLOC(d.listed, R);
+        if (lpb) ALLOC(d.inlist, R);
         ALLOC(c->foreign, (size_t)d.out_cap * 2);
         ALLOC(c->n_foreign, 1);
         ALLOC(c->staging, (size_t)d.out_cap * 2);
@@ -2987,6 +3069,9 @@ static int load_common(tw_ctx* c, const tw_scenario_desc* s, bool lp, uint32_t l
     if (mregs) HIPCHK(hipMemcpyAsync(mregs, s->main_regs, 32ull * s->n_replicas, hipMemcpyHostToDevice, st));
     if (iboff) HIPCHK(hipMemcpy(iboff, h_iboff.data(), 4 * h_iboff.size(), hipMemcpyHostToDevice));
     d.ib_off = iboff;
+    if (phd) HIPCHK(hipMemcpy(phd, h_ph.data(), h_ph.size(), hipMemcpyHostToDevice));
+    d.phase = phd;
+    d.has_ph1 = c->has_ph1 ? 1u : 0u;
     if (nvi) HIPCHK(hipMemcpyAsync(nvi, s->node_vars, 32ull * d.Ntot, hipMemcpyHostToDevice, st));
     if (lsi) HIPCHK(hipMemcpyAsync(lsi, s->node_listen, 4ull * d.Ntot, hipMemcpyHostToDevice, st));
     if (mbytes) {
@@ -3044,6 +3129,7 @@ int tw_reset(tw_ctx* c) {
     if (c->lp) {
         HIPCHK(hipMemsetAsync(d.hash_g, 0, 8ull * ((size_t)d.Ntot << d.rep_lg), st));
         HIPCHK(hipMemsetAsync(d.heavy_n, 0, 8, st));
+        if (d.inlist) HIPCHK(hipMemsetAsync(d.inlist, 0, 4ull * R, st));
         HIPCHK(hipMemsetAsync(d.pend_min, 0xFF, 8, st));
         HIPCHK(hipMemsetAsync(d.out_n, 0, 4, st));
         HIPCHK(hipMemsetAsync(d.lp_err, 0, 4, st));

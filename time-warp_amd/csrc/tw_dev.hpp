@@ -128,6 +128,11 @@ struct Dev {
     uint32_t* heavy;     // [2][R] lanes with more than TW_LIGHT pending records
     uint32_t* heavy_n;   // [2]
     uint64_t* pend_min;  // [1] min time of records left pending by tw_lp_due
+    // two-phase windows (batched mode): nodes fed by links shorter than the
+    // lookahead (a token-ring observer: 0 µs) run in phase 1 of each window,
+    // after every phase-0 node has finished the window; null = one phase
+    const uint8_t* phase;  // [Ntot]
+    uint32_t has_ph1;
     uint4* outbox;       // [out_cap][2] records produced this window
     uint32_t* out_n;     // [1]
     uint64_t* next_t;    // [1] min next-event time (atomicMin)
@@ -139,6 +144,8 @@ struct Dev {
     uint32_t* act;       // [2][TW_LP_NB][R]
     uint32_t* act_n;     // [2][TW_LP_NB]
     uint32_t* listed;    // [R]
+    uint32_t* inlist;    // [R] window id whose work list holds the lane (batched mode: a
+                         // spawn target is appended to the running window's list once)
     uint32_t act_cur, wid;
     // device-driven windows (tw_lp_tick): the loop state, WN_* words; null
     // for the host-driven loop (tw_lp_window)
@@ -175,11 +182,13 @@ __device__ __forceinline__ int64_t tx_us(const Dev& c, uint64_t link, uint32_t k
 }
 
 // LP device-driven window words (Dev::win)
-enum { WN_T, WN_L, WN_REC_MIN, WN_WINDOWS, WN_TICKS, WN_FLAGS, WN_ACT, WN_WID, WN_COUNT };
+enum { WN_T, WN_L, WN_REC_MIN, WN_WINDOWS, WN_TICKS, WN_FLAGS, WN_ACT, WN_WID, WN_PHASE, WN_NT0, WN_SPN_MIN,
+       WN_COUNT };
 // spawn record markers in the kind field of an outbox entry pair (message kinds are < 256)
 #define TW_SPAWN_KIND 0xFFFFFFFFu
 #define TW_SPAWN_CONT 0xFFFFFFFEu
-enum : int64_t { WN_FRESH = 1, WN_DONE = 2 };
+// WN_FRESH: the window's first tick (phase 0); WN_PH1FRESH: phase 1's first tick
+enum : int64_t { WN_FRESH = 1, WN_DONE = 2, WN_PH1FRESH = 4 };
 
 // LP inbox addressing (see Dev::inbox)
 #define TW_LIGHT 32u   // a lane with at most this many pending records drains them in the event kernel

@@ -199,7 +199,14 @@ class Engine:
         if scn.link_table is None:
             raise EngineError("load_lpb: the scenario needs a link table (its smallest delay is the lookahead)")
         if lookahead_us is None:
-            lookahead_us = int((scn.link_table & np.uint32(0x7FFFFFFF)).min())
+            # the smallest positive link delay; links shorter than it (a 0 µs
+            # link into a sink, e.g. token ring's observer) make their
+            # destination a phase-1 node of every window (tw_lpb_load checks it)
+            dmin = (scn.link_table & np.uint32(0x7FFFFFFF)).min(axis=(1, 2))
+            pos = dmin[dmin > 0]
+            if pos.size == 0:
+                raise EngineError("load_lpb: no link with a positive delay (no lookahead)")
+            lookahead_us = int(pos.min())
         m = scn.meta
         s = copy.copy(scn)
         s.max_slots = int(m.get("lp_max_slots", 64))

@@ -167,7 +167,15 @@ def token_ring(n_nodes: int = 16, n_replicas: int = 1, launch_duration: int = se
         run_capacity=_capped(2 * N + 4 * hops + 256),
         near_horizon_us=near_horizon_us,
         meta=dict(config="token_ring", n_nodes=N, launch_duration=launch_duration,
-                  drop_log2=drop_log2, seed_base=seed_base),
+                  drop_log2=drop_log2, seed_base=seed_base,
+                  # batched node-partitioned mode (Engine.load_lpb): a ring node holds
+                  # launchNode's threads (worker, server, killer, the token's
+                  # deliverer and handler), the observer its server, checker, killer
+                  # and note deliveries; main's spawn pairs are a tick's records.
+                  # The observer's 0 µs links make it a phase-1 node.
+                  lp_inbox_cap=np.array([4] * N + [8, 1], np.uint32),
+                  lp_max_slots=12, lp_queue_capacity=16,
+                  lp_outbox_cap=min(1 << 27, (2 * (N + 2) + 64) * n_replicas)),
         live_kind=live_kind, live_lo=live_lo, live_hi=live_hi,
     )
 
