@@ -1696,6 +1696,7 @@ __global__ void __launch_bounds__(TW_WG) tw_init_kernel(Dev c, uint32_t main_pc,
         if (listen_init) gp(c.bind)[r] = listen_init[g];
         gp(c.inbox_n)[r] = 0;
         if (c.lpb) gp(c.spawn_n)[r] = 0;
+        gp(c.wake)[r] = INT64_MAX;
         gp(c.listed)[r] = 0;  // marked for the first window: it serves every node
         return;
     }
@@ -1720,69 +1721,12 @@ __host__ __device__ constexpr size_t fixed_lds_bytes() {
 
 // WG replicas per workgroup share its LDS; TPW of each wave's 64 lanes carry a
 // replica (64, or TW_HALF_LANES for the half geometry: twice the waves).
-template <bool LP, int WG, int NC, int TPW = 64>
-__global__ void __launch_bounds__(WG * 64 / TPW) __attribute__((amdgpu_waves_per_eu(LP ? 2 : (WG * 64 / TPW + 255) / 256, 2)))
-tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
-    // device-driven windows: the window, its work list and whether this is the
-    // window's first tick (the only one that drains inboxes) come from the device
-    bool fresh = true;
-    uint32_t ph = 0;
-    if (LP && c.win) {
-        const int64_t GAS* w = gp(c.win);
-        const int64_t fl = w[WN_FLAGS];
-        if (fl & WN_DONE) return;
-        t_end = w[WN_T] + w[WN_L] - 1;
-        c.act_cur = (uint32_t)w[WN_ACT];
-        c.wid = (uint32_t)w[WN_WID];
-        ph = (uint32_t)w[WN_PHASE];
-        fresh = (fl & (ph ? WN_PH1FRESH : WN_FRESH)) != 0;
-    }
-    // LP: workgroup -> (bucket, span) of the window's work list, the busiest
-    // bucket first, each bucket padded to whole workgroups; workgroups past the
-    // list leave before staging the program
-    uint32_t lp_k = 0, lp_i = 0, lp_n = 0;
-    if (LP) {
-        uint32_t blk = blockIdx.x;
-        int k = TW_LP_NB - 1;
-        for (; k >= 0; --k) {
-            lp_n = gp(c.act_n)[c.act_cur * TW_LP_NB + k];
-            const uint32_t nb = (lp_n + WG - 1) / WG;
-            if (blk < nb) break;
-            blk -= nb;
-        }
-        if (k < 0) return;
-        lp_k = (uint32_t)k;
-        lp_i = blk * WG;
-    }
-    extern __shared__ __attribute__((aligned(16))) uint64_t lds_raw[];
-    uint4 LAS* s_pf = (uint4 LAS*)lds_raw;
-    uint4 LAS* s_rq = s_pf + (LP ? 4 : 5) * WG;  // (staging quad 4 holds a far run's next entry: no runs in LP)
-    uint64_t LAS* s_k = (uint64_t LAS*)(s_rq + (LP ? 0 : RQ_COUNT) * WG);
-    int64_t LAS* s_rf = (int64_t LAS*)(s_k + NC * WG);
-    uint32_t LAS* s_s = (uint32_t LAS*)(s_rf + 4 * WG);
-    uint32_t LAS* s_cw = s_s + NC * WG;
-    uint2 LAS* s_p = (uint2 LAS*)(s_cw + (CW_COUNT + (LP ? DW_COUNT : 0)) * WG);
-    int64_t LAS* s_c = (int64_t LAS*)(s_p + c.n_insns + 1);
-    uint32_t LAS* s_u = (uint32_t LAS*)(s_c + c.n_consts);
-    {
-        for (uint32_t i = threadIdx.x; i <= c.n_insns; i += WG * 64 / TPW) {
-            const uint2 in = gp(c.insns)[i];
-            s_p[i] = in;
-            s_u[i] = uop_of(in.x & 0xFFu);
-        }
-        for (uint32_t i = threadIdx.x; i < c.n_consts; i += WG * 64 / TPW) s_c[i] = gp(c.consts)[i];
-        __syncthreads();
-    }
-    if (TPW < 64 && (threadIdx.x & 63u) >= TPW) return;
-    const uint32_t wbase = (threadIdx.x >> 6) * TPW;  // the wave's first lane in the LDS layout
-    const uint32_t li = wbase + (threadIdx.x & 63u);
-    uint32_t r = blockIdx.x * WG + li;
-    if (LP) {
-        const uint32_t i = lp_i + li;
-        if (i >= lp_n) return;
-        r = gp(c.act)[((size_t)c.act_cur * TW_LP_NB + lp_k) * c.R + i];
-    }
-    if (r >= c.R) return;
+// One lane's launch: a replica (replica geometries) or a logical process (LP).
+template <bool LP, int WG, int NC, int TPW>
+__device__ __forceinline__ void tw_lane(Dev& c, uint32_t r, uint32_t li, int64_t t_end, uint64_t max_events,
+                                        uint32_t budget, bool fresh, uint32_t ph, uint4 LAS* s_pf, uint4 LAS* s_rq,
+                                        uint64_t LAS* s_k, int64_t LAS* s_rf, uint32_t LAS* s_s, uint32_t LAS* s_cw,
+                                        uint2 LAS* s_p, int64_t LAS* s_c, uint32_t LAS* s_u, uint32_t wbase) {
     if (LP && c.phase && gp(c.phase)[(c.lp0 + r) >> c.rep_lg] != ph) return;  // the other phase's node
     uint64_t* sc = gp(c.scal) + r;
     const size_t R = c.R;
@@ -2152,7 +2096,94 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
     if (LP && L.status == TW_REP_RUNNING && tn != INT64_MAX)
         __hip_atomic_fetch_min(gp(c.next_t), (uint64_t)tn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (active) __hip_atomic_fetch_add(gp(c.n_active), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (LP && L.status == TW_REP_RUNNING && (L.live || pending_main)) lp_list_next(c, r);
+    if (LP) {
+        // device loop: the lane is listed again by the window its next event
+        // falls in (tw_lp_compact); host loop: for the next window
+        const bool more = L.status == TW_REP_RUNNING && (L.live || pending_main);
+        if (c.win) gp(c.wake)[r] = more ? (pending_main ? L.now : tn) : INT64_MAX;
+        else if (more) lp_list_next(c, r);
+    }
+}
+
+// PS (LP only): a persistent grid for huge lane counts (batched LP: tens of
+// millions of lanes, of which a window lists few), whose waves take 64-lane
+// chunks of the work list from a device counter (Dev::lp_ctr, reset before
+// every launch).  The loop costs registers (60-80 B of scratch per lane), so
+// the default LP kernel keeps one lane per thread over the whole list.
+template <bool LP, int WG, int NC, int TPW = 64, bool PS = false>
+__global__ void __launch_bounds__(WG * 64 / TPW) __attribute__((amdgpu_waves_per_eu(LP ? 2 : (WG * 64 / TPW + 255) / 256, 2)))
+tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
+    // device-driven windows: the window, its work list and whether this is the
+    // window's first tick (the only one that drains inboxes) come from the device
+    bool fresh = true;
+    uint32_t ph = 0;
+    if (LP && c.win) {
+        const int64_t GAS* w = gp(c.win);
+        const int64_t fl = w[WN_FLAGS];
+        if (fl & WN_DONE) return;
+        t_end = w[WN_T] + w[WN_L] - 1;
+        c.act_cur = (uint32_t)w[WN_ACT];
+        c.wid = (uint32_t)w[WN_WID];
+        ph = (uint32_t)w[WN_PHASE];
+        fresh = (fl & (ph ? WN_PH1FRESH : WN_FRESH)) != 0;
+    }
+    // LP: the window's work list (workgroups past it leave before staging the program)
+    static_assert(TW_LP_NB == 1, "the LP grid serves one work-list bucket");
+    uint32_t lp_n = 0;
+    if (LP) {
+        lp_n = gp(c.act_n)[c.act_cur * TW_LP_NB];
+        if (!PS && (size_t)blockIdx.x * WG >= lp_n) return;
+        if (lp_n == 0) return;
+    }
+    extern __shared__ __attribute__((aligned(16))) uint64_t lds_raw[];
+    uint4 LAS* s_pf = (uint4 LAS*)lds_raw;
+    uint4 LAS* s_rq = s_pf + (LP ? 4 : 5) * WG;  // (staging quad 4 holds a far run's next entry: no runs in LP)
+    uint64_t LAS* s_k = (uint64_t LAS*)(s_rq + (LP ? 0 : RQ_COUNT) * WG);
+    int64_t LAS* s_rf = (int64_t LAS*)(s_k + NC * WG);
+    uint32_t LAS* s_s = (uint32_t LAS*)(s_rf + 4 * WG);
+    uint32_t LAS* s_cw = s_s + NC * WG;
+    uint2 LAS* s_p = (uint2 LAS*)(s_cw + (CW_COUNT + (LP ? DW_COUNT : 0)) * WG);
+    int64_t LAS* s_c = (int64_t LAS*)(s_p + c.n_insns + 1);
+    uint32_t LAS* s_u = (uint32_t LAS*)(s_c + c.n_consts);
+    {
+        for (uint32_t i = threadIdx.x; i <= c.n_insns; i += WG * 64 / TPW) {
+            const uint2 in = gp(c.insns)[i];
+            s_p[i] = in;
+            s_u[i] = uop_of(in.x & 0xFFu);
+        }
+        for (uint32_t i = threadIdx.x; i < c.n_consts; i += WG * 64 / TPW) s_c[i] = gp(c.consts)[i];
+        __syncthreads();
+    }
+    if (TPW < 64 && (threadIdx.x & 63u) >= TPW) return;
+    const uint32_t wbase = (threadIdx.x >> 6) * TPW;  // the wave's first lane in the LDS layout
+    const uint32_t li = wbase + (threadIdx.x & 63u);
+    if constexpr (LP && !PS) {
+        const uint32_t i = blockIdx.x * WG + li;
+        if (i < lp_n)
+            tw_lane<LP, WG, NC, TPW>(c, gp(c.act)[(size_t)c.act_cur * TW_LP_NB * c.R + i], li, t_end, max_events, budget,
+                                     fresh, ph, s_pf, s_rq, s_k, s_rf, s_s, s_cw, s_p, s_c, s_u, wbase);
+    } else if constexpr (LP) {
+        for (;;) {
+            uint32_t ch = 0;
+            if ((threadIdx.x & 63u) == 0) ch = __hip_atomic_fetch_add(gp(c.lp_ctr), 1u, __ATOMIC_RELAXED,
+                                                                     __HIP_MEMORY_SCOPE_AGENT);
+            ch = __builtin_amdgcn_readfirstlane(ch);
+            if ((size_t)ch * 64 >= lp_n) break;
+            const uint32_t i = ch * 64 + (threadIdx.x & 63u);
+            // nothing derived from the lane's LDS slices may be hoisted out of
+            // the loop (it would stay live across it: spills at 256 registers)
+            uint32_t lj = li;
+            asm volatile("" : "+v"(lj));
+            if (i < lp_n)
+                tw_lane<LP, WG, NC, TPW>(c, gp(c.act)[(size_t)c.act_cur * TW_LP_NB * c.R + i], lj, t_end, max_events,
+                                         budget, fresh, ph, s_pf, s_rq, s_k, s_rf, s_s, s_cw, s_p, s_c, s_u, wbase);
+        }
+    } else {
+        const uint32_t r = blockIdx.x * WG + li;
+        if (r < c.R)
+            tw_lane<LP, WG, NC, TPW>(c, r, li, t_end, max_events, budget, fresh, ph, s_pf, s_rq, s_k, s_rf, s_s, s_cw,
+                                     s_p, s_c, s_u, wbase);
+    }
 }
 
 
@@ -2312,9 +2343,11 @@ __global__ void tw_lp_fill(Dev c, int64_t* red) {
         return;
     }
     const uint64_t a = *gp(c.next_t), b = (uint64_t)w[WN_REC_MIN], p = *gp(c.pend_min), sp = (uint64_t)w[WN_SPN_MIN];
+    const uint64_t sl = (uint64_t)w[WN_SLEEP_MIN];  // lanes not listed in this window
     uint64_t m = a < b ? a : b;
     m = p < m ? p : m;
     m = sp < m ? sp : m;
+    m = sl < m ? sl : m;
     gp(red)[0] = m >= (uint64_t)INT64_MAX ? INT64_MAX : (int64_t)m;
     // a child forked onto another node inside this window keeps the window
     // (phase) running: its lane starts it at the next tick
@@ -2331,6 +2364,7 @@ __global__ void tw_lp_ctl(Dev c, const int64_t* red, uint4* send, uint32_t world
     for (uint32_t g = 0; send && g < world; ++g) gp(send)[(size_t)g * (cap + 1) * 2].x = 0;
     *gp(c.n_active) = 0;
     *gp(c.next_t) = ~0ull;
+    *gp(c.lp_ctr) = 0;
     w[WN_SPN_MIN] = (int64_t)~0ull;
     if (gp(red)[1] < 0) {  // rerun this phase of the window
         w[WN_FLAGS] &= ~(WN_FRESH | WN_PH1FRESH);
@@ -2362,6 +2396,7 @@ __global__ void tw_lp_ctl(Dev c, const int64_t* red, uint4* send, uint32_t world
     gp(c.heavy_n)[(w[WN_WID] + 1) & 1] = 0;
     for (int k = 0; k < TW_LP_NB; ++k) gp(c.act_n)[act * TW_LP_NB + k] = 0;  // tw_lp_compact builds it next
     w[WN_REC_MIN] = (int64_t)~0ull;
+    w[WN_SLEEP_MIN] = INT64_MAX;  // tw_lp_compact recomputes it for the new window
     w[WN_FLAGS] = WN_FRESH;
 }
 // The window's work list: every node marked during the previous window
@@ -2373,13 +2408,19 @@ __global__ void tw_lp_ctl(Dev c, const int64_t* red, uint4* send, uint32_t world
 // (c.win): only at a window's first tick, with mark/list from the window words.
 #define TW_CPT 16
 __global__ void __launch_bounds__(256) tw_lp_compact(Dev c, uint32_t mark, uint32_t dst) {
+    int64_t tend = INT64_MIN;  // device loop: lanes whose next event is due in the window are listed too
     if (c.win) {
         const int64_t GAS* w = gp(c.win);
         const int64_t fl = w[WN_FLAGS];
         if (!(fl & WN_FRESH) || (fl & WN_DONE)) return;
         mark = (uint32_t)w[WN_WID] - 1u;
         dst = (uint32_t)w[WN_ACT];
+        tend = w[WN_T] + w[WN_L] - 1;
     }
+    __shared__ unsigned long long smin;
+    if (threadIdx.x == 0) smin = ~0ull;
+    __syncthreads();
+    unsigned long long mymin = ~0ull;
     __shared__ uint32_t cnt[TW_LP_NB][TW_CPT * 4];
     __shared__ uint32_t base[TW_LP_NB];
     const uint32_t wv = threadIdx.x >> 6;
@@ -2388,7 +2429,12 @@ __global__ void __launch_bounds__(256) tw_lp_compact(Dev c, uint32_t mark, uint3
 #pragma unroll
     for (int i = 0; i < TW_CPT; ++i) {
         const size_t r = r0 + (size_t)i * 256;
-        const bool b = r < c.R && gp(c.listed)[r] == mark;
+        bool b = r < c.R && gp(c.listed)[r] == mark;
+        if (c.win && r < c.R) {
+            const int64_t wk = gp(c.wake)[r];
+            b = b || wk <= tend;
+            if (!b && wk != INT64_MAX) mymin = (unsigned long long)wk < mymin ? (unsigned long long)wk : mymin;
+        }
         const uint32_t n_in = (TW_LP_NB > 1 && b) ? gp(c.inbox_n)[r] : 0u;
         key[i] = b ? (n_in < TW_LP_NB - 1 ? n_in : TW_LP_NB - 1) : 0xFFu;
 #pragma unroll
@@ -2397,7 +2443,11 @@ __global__ void __launch_bounds__(256) tw_lp_compact(Dev c, uint32_t mark, uint3
             if (__lane_id() == 0) cnt[k][i * 4 + wv] = (uint32_t)__builtin_popcountll(m);
         }
     }
+    if (mymin != ~0ull) atomicMin(&smin, mymin);
     __syncthreads();
+    if (threadIdx.x == 0 && smin != ~0ull)
+        __hip_atomic_fetch_min((unsigned long long GAS*)(gp(c.win) + WN_SLEEP_MIN), smin, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
     if (threadIdx.x < TW_LP_NB) {
         const uint32_t k = threadIdx.x;
         uint32_t run = 0;
@@ -2443,11 +2493,13 @@ __global__ void tw_lp_begin(Dev c, int64_t lookahead) {
     w[WN_PHASE] = 0;
     w[WN_NT0] = INT64_MAX;
     w[WN_SPN_MIN] = (int64_t)~0ull;
+    w[WN_SLEEP_MIN] = INT64_MAX;
     for (int k = 0; k < TW_LP_NB; ++k) gp(c.act_n)[TW_LP_NB + k] = 0;
     *gp(c.out_n) = 0;
     *gp(c.n_active) = 0;
     *gp(c.next_t) = ~0ull;
     *gp(c.pend_min) = ~0ull;
+    *gp(c.lp_ctr) = 0;
     gp(c.heavy_n)[0] = gp(c.heavy_n)[1] = 0;
 }
 
@@ -2581,6 +2633,34 @@ __global__ void __launch_bounds__(256) tw_lp_due(Dev c) {
     }
 }
 
+// Batched LP: a replica's results = its nodes' lanes (lane = node << rep_lg |
+// replica) reduced on the device: counts summed, final time the latest, status
+// the worst error (else done), the main exception whichever lane holds one.
+// out: [8][n_rep] words (final_t, events, delivered, dropped, undeliverable,
+// status, main_exc, threads).
+__global__ void __launch_bounds__(256) tw_lpb_reduce(Dev c, uint64_t* out) {
+    const uint32_t q = blockIdx.x * 256 + threadIdx.x;
+    const uint32_t nr = 1u << c.rep_lg;
+    if (q >= nr) return;
+    const size_t R = c.R;
+    int64_t ft = 0;
+    uint64_t ev = 0, dl = 0, dr = 0, ud = 0, th = 0, me = 0, st = TW_REP_DONE;
+    for (uint32_t n = 0; n < c.Ntot; ++n) {
+        const uint64_t GAS* sc = gp(c.scal) + ((size_t)n << c.rep_lg) + q;
+        const int64_t f = (int64_t)sc[SC_FINAL_T * R];
+        ft = f > ft ? f : ft;
+        ev += sc[SC_EVENTS * R]; dl += sc[SC_DELIVERED * R]; dr += sc[SC_DROPPED * R];
+        ud += sc[SC_UNDELIV * R]; th += sc[SC_THREADS * R];
+        const uint64_t x = sc[SC_MAIN_EXC * R], s2 = sc[SC_STATUS * R];
+        me = x ? x : me;
+        st = (s2 >= TW_REP_ABORTED && s2 > st) ? s2 : st;
+    }
+    uint64_t GAS* o = gp(out);
+    o[0 * (size_t)nr + q] = (uint64_t)ft; o[1 * (size_t)nr + q] = ev; o[2 * (size_t)nr + q] = dl;
+    o[3 * (size_t)nr + q] = dr; o[4 * (size_t)nr + q] = ud; o[5 * (size_t)nr + q] = st;
+    o[6 * (size_t)nr + q] = me; o[7 * (size_t)nr + q] = th;
+}
+
 // Per-replica digest of the results and node hashes (tw_tie_audit compares
 // runs under different tie orders without copying every hash to the host).
 __global__ void __launch_bounds__(256) tw_digest_kernel(Dev c, uint64_t* out) {
@@ -2691,11 +2771,17 @@ void free_all(tw_ctx* c) {
 
 }  // namespace
 
+#define TW_LP_GRID 2048      // persistent LP workgroups: 4 per CU are resident (LDS), the rest take over tails
+#define TW_LP_PERSIST (1u << 22)  // lanes from which the LP kernel runs persistent
 template <bool LP, int WG, int NC, int TPW = 64>
 static void launch_run(tw_ctx* c, hipStream_t st, int64_t t_end, uint64_t limit, uint32_t budget) {
-    const uint32_t blocks = (uint32_t)((c->d.R + WG - 1) / WG) + (LP ? TW_LP_NB : 0);  // LP: bucket padding
-    hipLaunchKernelGGL((tw_run_kernel<LP, WG, NC, TPW>), dim3(blocks), dim3(WG * 64 / TPW), c->lds_bytes, st, c->d, t_end, limit,
-                       budget);
+    const uint32_t blocks = (uint32_t)((c->d.R + WG - 1) / WG);
+    if (LP && c->d.R >= TW_LP_PERSIST)
+        hipLaunchKernelGGL((tw_run_kernel<LP, WG, NC, TPW, true>), dim3(blocks < TW_LP_GRID ? blocks : TW_LP_GRID),
+                           dim3(WG * 64 / TPW), c->lds_bytes, st, c->d, t_end, limit, budget);
+    else
+        hipLaunchKernelGGL((tw_run_kernel<LP, WG, NC, TPW>), dim3(blocks), dim3(WG * 64 / TPW), c->lds_bytes, st, c->d,
+                           t_end, limit, budget);
 }
 
 extern "C" {
@@ -2934,6 +3020,9 @@ static int load_common(tw_ctx* c, const tw_scenario_desc* s, bool lp, uint32_t l
     else if (lp)
         HIPCHK(hipFuncSetAttribute((const void*)tw_run_kernel<true, TW_WG_LP, TW_NEAR_LP>,
                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)c->lds_bytes));
+    if (lp)
+        HIPCHK(hipFuncSetAttribute((const void*)tw_run_kernel<true, TW_WG_LP, TW_NEAR_LP, 64, true>,
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)c->lds_bytes));
     else
         HIPCHK(hipFuncSetAttribute((const void*)tw_run_kernel<false, TW_WG, TW_NEAR_CAP>,
                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)c->lds_bytes));
@@ -3041,6 +3130,8 @@ static int load_common(tw_ctx* c, const tw_scenario_desc* s, bool lp, uint32_t l
         ALLOC(d.lp_err, 1);
         ALLOC(d.act, 2 * TW_LP_NB * R);
         ALLOC(d.act_n, 2 * TW_LP_NB);
+        ALLOC(d.lp_ctr, 1);
+        ALLOC(d.wake, R);
         ALLOC(d.listed, R);
         if (lpb) ALLOC(d.inlist, R);
         ALLOC(c->foreign, (size_t)d.out_cap * 2);
@@ -3197,6 +3288,7 @@ int tw_run(tw_ctx* c, int64_t t_end_us, uint64_t max_events, tw_stats* out) {
         for (int i = 0; i < per_check; ++i) {
             HIPCHK(hipMemsetAsync(d.n_active, 0, 4, st));
             if (c->lp) HIPCHK(hipMemsetAsync(d.next_t, 0xFF, 8, st));
+            if (c->lp) HIPCHK(hipMemsetAsync(d.lp_ctr, 0, 4, st));
             HIPCHK(hipEventRecord(c->ev_pool[2 * i], st));
             if (c->lp)
                 launch_run<true, TW_WG_LP, TW_NEAR_LP>(c, st, t_end_us, limit, budget);
@@ -3252,31 +3344,29 @@ int tw_read_results(tw_ctx* c, tw_replica_result* out, size_t n) {
     const Dev& d = c->d;
     if (n < (c->lpb ? c->n_rep : d.R)) return TW_ERR_INVALID;
     HIPCHK(hipSetDevice(c->device));
+    if (c->lpb) {
+        const uint32_t nr = c->n_rep;
+        uint64_t* dd = nullptr;
+        HIPCHK(hipMallocAsync((void**)&dd, 64ull * nr, c->stream));
+        hipLaunchKernelGGL(tw_lpb_reduce, dim3((nr + 255) / 256), dim3(256), 0, c->stream, d, dd);
+        HIPCHK(hipGetLastError());
+        std::vector<uint64_t> h(8ull * nr);
+        HIPCHK(hipMemcpyAsync(h.data(), dd, 64ull * nr, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipFreeAsync(dd, c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+        for (uint32_t q = 0; q < nr; ++q) {
+            tw_replica_result& o = out[q];
+            std::memset(&o, 0, sizeof(o));
+            o.final_t = (int64_t)h[q]; o.events = h[nr + q]; o.delivered = h[2ull * nr + q];
+            o.dropped = h[3ull * nr + q]; o.undeliverable = h[4ull * nr + q]; o.status = (uint32_t)h[5ull * nr + q];
+            o.main_exc = (uint32_t)h[6ull * nr + q]; o.threads = h[7ull * nr + q];
+        }
+        return TW_OK;
+    }
     std::vector<uint64_t> sc((size_t)SC_COUNT * d.R);
     HIPCHK(hipMemcpyAsync(sc.data(), d.scal, 8ull * SC_COUNT * d.R, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
     auto F = [&](int f, uint32_t i) { return sc[(size_t)f * d.R + i]; };
-    if (c->lpb) {
-        // per replica: the sum over its nodes' lanes (lane = node << rep_lg | replica);
-        // final time = the latest, status = the worst error, else done
-        const uint32_t nr = c->n_rep;
-        if (n < nr) return TW_ERR_INVALID;
-        for (uint32_t q = 0; q < nr; ++q) {
-            tw_replica_result& o = out[q];
-            std::memset(&o, 0, sizeof(o));
-            o.status = TW_REP_DONE;
-            for (uint32_t nd = 0; nd < d.Ntot; ++nd) {
-                const uint32_t i = (nd << d.rep_lg) | q;
-                if ((int64_t)F(SC_FINAL_T, i) > o.final_t) o.final_t = (int64_t)F(SC_FINAL_T, i);
-                o.events += F(SC_EVENTS, i); o.delivered += F(SC_DELIVERED, i); o.dropped += F(SC_DROPPED, i);
-                o.undeliverable += F(SC_UNDELIV, i); o.threads += F(SC_THREADS, i);
-                if (F(SC_MAIN_EXC, i)) o.main_exc = (uint32_t)F(SC_MAIN_EXC, i);
-                const uint32_t stt = (uint32_t)F(SC_STATUS, i);
-                if (stt >= TW_REP_ABORTED && stt > o.status) o.status = stt;
-            }
-        }
-        return TW_OK;
-    }
     for (uint32_t i = 0; i < d.R; ++i) {
         out[i].final_t = (int64_t)F(SC_FINAL_T, i); out[i].events = F(SC_EVENTS, i);
         out[i].delivered = F(SC_DELIVERED, i); out[i].dropped = F(SC_DROPPED, i);

@@ -143,6 +143,9 @@ struct Dev {
     // the marks (tw_lp_compact)
     uint32_t* act;       // [2][TW_LP_NB][R]
     uint32_t* act_n;     // [2][TW_LP_NB]
+    uint32_t* lp_ctr;    // [1] 64-lane chunks of the work list taken by the persistent LP grid
+    int64_t* wake;       // [R] device loop: the lane's next event time (INT64_MAX: none); a
+                         // window lists only lanes due in it, the others' minimum bounds the next
     uint32_t* listed;    // [R]
     uint32_t* inlist;    // [R] window id whose work list holds the lane (batched mode: a
                          // spawn target is appended to the running window's list once)
@@ -183,7 +186,7 @@ __device__ __forceinline__ int64_t tx_us(const Dev& c, uint64_t link, uint32_t k
 
 // LP device-driven window words (Dev::win)
 enum { WN_T, WN_L, WN_REC_MIN, WN_WINDOWS, WN_TICKS, WN_FLAGS, WN_ACT, WN_WID, WN_PHASE, WN_NT0, WN_SPN_MIN,
-       WN_COUNT };
+       WN_SLEEP_MIN, WN_COUNT };
 // spawn record markers in the kind field of an outbox entry pair (message kinds are < 256)
 #define TW_SPAWN_KIND 0xFFFFFFFFu
 #define TW_SPAWN_CONT 0xFFFFFFFEu
