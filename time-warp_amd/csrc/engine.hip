@@ -1721,12 +1721,59 @@ __host__ __device__ constexpr size_t fixed_lds_bytes() {
 
 // WG replicas per workgroup share its LDS; TPW of each wave's 64 lanes carry a
 // replica (64, or TW_HALF_LANES for the half geometry: twice the waves).
-// One lane's launch: a replica (replica geometries) or a logical process (LP).
-template <bool LP, int WG, int NC, int TPW>
-__device__ __forceinline__ void tw_lane(Dev& c, uint32_t r, uint32_t li, int64_t t_end, uint64_t max_events,
-                                        uint32_t budget, bool fresh, uint32_t ph, uint4 LAS* s_pf, uint4 LAS* s_rq,
-                                        uint64_t LAS* s_k, int64_t LAS* s_rf, uint32_t LAS* s_s, uint32_t LAS* s_cw,
-                                        uint2 LAS* s_p, int64_t LAS* s_c, uint32_t LAS* s_u, uint32_t wbase) {
+template <bool LP, int WG, int NC, int TPW = 64>
+__global__ void __launch_bounds__(WG * 64 / TPW) __attribute__((amdgpu_waves_per_eu(LP ? 2 : (WG * 64 / TPW + 255) / 256, 2)))
+tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
+    // device-driven windows: the window, its work list and whether this is the
+    // window's first tick (the only one that drains inboxes) come from the device
+    bool fresh = true;
+    uint32_t ph = 0;
+    if (LP && c.win) {
+        const int64_t GAS* w = gp(c.win);
+        const int64_t fl = w[WN_FLAGS];
+        if (fl & WN_DONE) return;
+        t_end = w[WN_T] + w[WN_L] - 1;
+        c.act_cur = (uint32_t)w[WN_ACT];
+        c.wid = (uint32_t)w[WN_WID];
+        ph = (uint32_t)w[WN_PHASE];
+        fresh = (fl & (ph ? WN_PH1FRESH : WN_FRESH)) != 0;
+    }
+    // LP: the window's work list (workgroups past it leave before staging the program)
+    static_assert(TW_LP_NB == 1, "the LP grid serves one work-list bucket");
+    uint32_t lp_n = 0;
+    if (LP) {
+        lp_n = gp(c.act_n)[c.act_cur * TW_LP_NB];
+        if ((size_t)blockIdx.x * WG >= lp_n) return;
+    }
+    extern __shared__ __attribute__((aligned(16))) uint64_t lds_raw[];
+    uint4 LAS* s_pf = (uint4 LAS*)lds_raw;
+    uint4 LAS* s_rq = s_pf + (LP ? 4 : 5) * WG;  // (staging quad 4 holds a far run's next entry: no runs in LP)
+    uint64_t LAS* s_k = (uint64_t LAS*)(s_rq + (LP ? 0 : RQ_COUNT) * WG);
+    int64_t LAS* s_rf = (int64_t LAS*)(s_k + NC * WG);
+    uint32_t LAS* s_s = (uint32_t LAS*)(s_rf + 4 * WG);
+    uint32_t LAS* s_cw = s_s + NC * WG;
+    uint2 LAS* s_p = (uint2 LAS*)(s_cw + (CW_COUNT + (LP ? DW_COUNT : 0)) * WG);
+    int64_t LAS* s_c = (int64_t LAS*)(s_p + c.n_insns + 1);
+    uint32_t LAS* s_u = (uint32_t LAS*)(s_c + c.n_consts);
+    {
+        for (uint32_t i = threadIdx.x; i <= c.n_insns; i += WG * 64 / TPW) {
+            const uint2 in = gp(c.insns)[i];
+            s_p[i] = in;
+            s_u[i] = uop_of(in.x & 0xFFu);
+        }
+        for (uint32_t i = threadIdx.x; i < c.n_consts; i += WG * 64 / TPW) s_c[i] = gp(c.consts)[i];
+        __syncthreads();
+    }
+    if (TPW < 64 && (threadIdx.x & 63u) >= TPW) return;
+    const uint32_t wbase = (threadIdx.x >> 6) * TPW;  // the wave's first lane in the LDS layout
+    const uint32_t li = wbase + (threadIdx.x & 63u);
+    uint32_t r = blockIdx.x * WG + li;
+    if (LP) {
+        const uint32_t i = blockIdx.x * WG + li;
+        if (i >= lp_n) return;
+        r = gp(c.act)[(size_t)c.act_cur * TW_LP_NB * c.R + i];
+    }
+    if (r >= c.R) return;
     if (LP && c.phase && gp(c.phase)[(c.lp0 + r) >> c.rep_lg] != ph) return;  // the other phase's node
     uint64_t* sc = gp(c.scal) + r;
     const size_t R = c.R;
@@ -2105,92 +2152,12 @@ __device__ __forceinline__ void tw_lane(Dev& c, uint32_t r, uint32_t li, int64_t
     }
 }
 
-// PS (LP only): a persistent grid for huge lane counts (batched LP: tens of
-// millions of lanes, of which a window lists few), whose waves take 64-lane
-// chunks of the work list from a device counter (Dev::lp_ctr, reset before
-// every launch).  The loop costs registers (60-80 B of scratch per lane), so
-// the default LP kernel keeps one lane per thread over the whole list.
-template <bool LP, int WG, int NC, int TPW = 64, bool PS = false>
-__global__ void __launch_bounds__(WG * 64 / TPW) __attribute__((amdgpu_waves_per_eu(LP ? 2 : (WG * 64 / TPW + 255) / 256, 2)))
-tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
-    // device-driven windows: the window, its work list and whether this is the
-    // window's first tick (the only one that drains inboxes) come from the device
-    bool fresh = true;
-    uint32_t ph = 0;
-    if (LP && c.win) {
-        const int64_t GAS* w = gp(c.win);
-        const int64_t fl = w[WN_FLAGS];
-        if (fl & WN_DONE) return;
-        t_end = w[WN_T] + w[WN_L] - 1;
-        c.act_cur = (uint32_t)w[WN_ACT];
-        c.wid = (uint32_t)w[WN_WID];
-        ph = (uint32_t)w[WN_PHASE];
-        fresh = (fl & (ph ? WN_PH1FRESH : WN_FRESH)) != 0;
-    }
-    // LP: the window's work list (workgroups past it leave before staging the program)
-    static_assert(TW_LP_NB == 1, "the LP grid serves one work-list bucket");
-    uint32_t lp_n = 0;
-    if (LP) {
-        lp_n = gp(c.act_n)[c.act_cur * TW_LP_NB];
-        if (!PS && (size_t)blockIdx.x * WG >= lp_n) return;
-        if (lp_n == 0) return;
-    }
-    extern __shared__ __attribute__((aligned(16))) uint64_t lds_raw[];
-    uint4 LAS* s_pf = (uint4 LAS*)lds_raw;
-    uint4 LAS* s_rq = s_pf + (LP ? 4 : 5) * WG;  // (staging quad 4 holds a far run's next entry: no runs in LP)
-    uint64_t LAS* s_k = (uint64_t LAS*)(s_rq + (LP ? 0 : RQ_COUNT) * WG);
-    int64_t LAS* s_rf = (int64_t LAS*)(s_k + NC * WG);
-    uint32_t LAS* s_s = (uint32_t LAS*)(s_rf + 4 * WG);
-    uint32_t LAS* s_cw = s_s + NC * WG;
-    uint2 LAS* s_p = (uint2 LAS*)(s_cw + (CW_COUNT + (LP ? DW_COUNT : 0)) * WG);
-    int64_t LAS* s_c = (int64_t LAS*)(s_p + c.n_insns + 1);
-    uint32_t LAS* s_u = (uint32_t LAS*)(s_c + c.n_consts);
-    {
-        for (uint32_t i = threadIdx.x; i <= c.n_insns; i += WG * 64 / TPW) {
-            const uint2 in = gp(c.insns)[i];
-            s_p[i] = in;
-            s_u[i] = uop_of(in.x & 0xFFu);
-        }
-        for (uint32_t i = threadIdx.x; i < c.n_consts; i += WG * 64 / TPW) s_c[i] = gp(c.consts)[i];
-        __syncthreads();
-    }
-    if (TPW < 64 && (threadIdx.x & 63u) >= TPW) return;
-    const uint32_t wbase = (threadIdx.x >> 6) * TPW;  // the wave's first lane in the LDS layout
-    const uint32_t li = wbase + (threadIdx.x & 63u);
-    if constexpr (LP && !PS) {
-        const uint32_t i = blockIdx.x * WG + li;
-        if (i < lp_n)
-            tw_lane<LP, WG, NC, TPW>(c, gp(c.act)[(size_t)c.act_cur * TW_LP_NB * c.R + i], li, t_end, max_events, budget,
-                                     fresh, ph, s_pf, s_rq, s_k, s_rf, s_s, s_cw, s_p, s_c, s_u, wbase);
-    } else if constexpr (LP) {
-        for (;;) {
-            uint32_t ch = 0;
-            if ((threadIdx.x & 63u) == 0) ch = __hip_atomic_fetch_add(gp(c.lp_ctr), 1u, __ATOMIC_RELAXED,
-                                                                     __HIP_MEMORY_SCOPE_AGENT);
-            ch = __builtin_amdgcn_readfirstlane(ch);
-            if ((size_t)ch * 64 >= lp_n) break;
-            const uint32_t i = ch * 64 + (threadIdx.x & 63u);
-            // nothing derived from the lane's LDS slices may be hoisted out of
-            // the loop (it would stay live across it: spills at 256 registers)
-            uint32_t lj = li;
-            asm volatile("" : "+v"(lj));
-            if (i < lp_n)
-                tw_lane<LP, WG, NC, TPW>(c, gp(c.act)[(size_t)c.act_cur * TW_LP_NB * c.R + i], lj, t_end, max_events,
-                                         budget, fresh, ph, s_pf, s_rq, s_k, s_rf, s_s, s_cw, s_p, s_c, s_u, wbase);
-        }
-    } else {
-        const uint32_t r = blockIdx.x * WG + li;
-        if (r < c.R)
-            tw_lane<LP, WG, NC, TPW>(c, r, li, t_end, max_events, budget, fresh, ph, s_pf, s_rq, s_k, s_rf, s_s, s_cw,
-                                     s_p, s_c, s_u, wbase);
-    }
-}
-
 
 // A delivery record for local node dst: claim an inbox slot (the drain at the
 // window's first tick sorts them), lower *tmin to its time, list the node for
 // the next window.
-__device__ __forceinline__ void lp_deliver(const Dev& c, uint4 a, uint4 b, uint64_t GAS* tmin) {
+__device__ __forceinline__ void lp_deliver(const Dev& c, uint4 a, uint4 b, uint64_t GAS* tmin,
+                                           int64_t wend = INT64_MIN) {
     const uint32_t lp = b.w - c.lp0;
     const uint32_t k = __hip_atomic_fetch_add(gp(c.inbox_n) + lp, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const uint32_t cap = ib_cap(c, lp);
@@ -2201,10 +2168,9 @@ __device__ __forceinline__ void lp_deliver(const Dev& c, uint4 a, uint4 b, uint6
     uint4 GAS* q = gp(c.inbox) + (ib_base(c, lp) + (size_t)k * ib_stride(c)) * 2;
     q[0] = a;
     q[1] = b;
-    // (a record due in this window -- a short link into a phase-1 node -- is
-    // drained at phase 1's first tick: it does not bound the next window)
-    const bool intra = c.win && ent_t(a) < gp(c.win)[WN_T] + gp(c.win)[WN_L];
-    if (!intra) __hip_atomic_fetch_min(tmin, (uint64_t)ent_t(a), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // (a record due in this window, t < wend -- a short link into a phase-1
+    // node -- is drained at phase 1's first tick: it does not bound the next window)
+    if (ent_t(a) >= wend) __hip_atomic_fetch_min(tmin, (uint64_t)ent_t(a), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     // a lane whose node may hold more than TW_LIGHT records is served by
     // tw_lp_due: its first pending record lists it for the next window's pass
     // (device loop; the list of window wid + 1)
@@ -2288,6 +2254,7 @@ __global__ void __launch_bounds__(256) tw_lp_pack(Dev c, uint4* send, const uint
     uint32_t n = *gp(c.out_n);
     n = n < c.out_cap ? n : c.out_cap;
     uint64_t GAS* tmin = (uint64_t GAS*)(gp(c.win) + WN_REC_MIN);
+    const int64_t wend = gp(c.win)[WN_T] + gp(c.win)[WN_L];
     for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
         const uint4 a = gp(c.outbox)[(size_t)i * 2], b = gp(c.outbox)[(size_t)i * 2 + 1];
         const uint32_t dst = b.w;
@@ -2297,7 +2264,7 @@ __global__ void __launch_bounds__(256) tw_lp_pack(Dev c, uint4* send, const uint
             continue;
         }
         if (dst >= c.lp0 && dst < c.lp0 + c.R) {
-            lp_deliver(c, a, b, tmin);
+            lp_deliver(c, a, b, tmin, wend);
         } else if (send && world > 1) {
             uint32_t lo = 0, hi = world;
             while (hi - lo > 1) {
@@ -2322,6 +2289,7 @@ __global__ void __launch_bounds__(256) tw_lp_pack(Dev c, uint4* send, const uint
 __global__ void __launch_bounds__(256) tw_lp_import(Dev c, const uint4* recv, uint32_t world, uint32_t cap) {
     if (!win_enter(c)) return;
     uint64_t GAS* tmin = (uint64_t GAS*)(gp(c.win) + WN_REC_MIN);
+    const int64_t wend = gp(c.win)[WN_T] + gp(c.win)[WN_L];
     const uint32_t total = world * cap;
     for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < total; i += gridDim.x * 256) {
         const uint32_t g = i / cap, k = i - g * cap;
@@ -2329,7 +2297,7 @@ __global__ void __launch_bounds__(256) tw_lp_import(Dev c, const uint4* recv, ui
         const uint32_t cnt = blk[0].x;
         if (k >= (cnt < cap ? cnt : cap)) continue;
         const uint4 a = blk[(size_t)(k + 1) * 2], b = blk[(size_t)(k + 1) * 2 + 1];
-        if (b.w >= c.lp0 && b.w < c.lp0 + c.R) lp_deliver(c, a, b, tmin);
+        if (b.w >= c.lp0 && b.w < c.lp0 + c.R) lp_deliver(c, a, b, tmin, wend);
         else __hip_atomic_fetch_or(gp(c.lp_err), 4u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
@@ -2364,7 +2332,6 @@ __global__ void tw_lp_ctl(Dev c, const int64_t* red, uint4* send, uint32_t world
     for (uint32_t g = 0; send && g < world; ++g) gp(send)[(size_t)g * (cap + 1) * 2].x = 0;
     *gp(c.n_active) = 0;
     *gp(c.next_t) = ~0ull;
-    *gp(c.lp_ctr) = 0;
     w[WN_SPN_MIN] = (int64_t)~0ull;
     if (gp(red)[1] < 0) {  // rerun this phase of the window
         w[WN_FLAGS] &= ~(WN_FRESH | WN_PH1FRESH);
@@ -2499,7 +2466,6 @@ __global__ void tw_lp_begin(Dev c, int64_t lookahead) {
     *gp(c.n_active) = 0;
     *gp(c.next_t) = ~0ull;
     *gp(c.pend_min) = ~0ull;
-    *gp(c.lp_ctr) = 0;
     gp(c.heavy_n)[0] = gp(c.heavy_n)[1] = 0;
 }
 
@@ -2771,17 +2737,11 @@ void free_all(tw_ctx* c) {
 
 }  // namespace
 
-#define TW_LP_GRID 2048      // persistent LP workgroups: 4 per CU are resident (LDS), the rest take over tails
-#define TW_LP_PERSIST (1u << 22)  // lanes from which the LP kernel runs persistent
 template <bool LP, int WG, int NC, int TPW = 64>
 static void launch_run(tw_ctx* c, hipStream_t st, int64_t t_end, uint64_t limit, uint32_t budget) {
     const uint32_t blocks = (uint32_t)((c->d.R + WG - 1) / WG);
-    if (LP && c->d.R >= TW_LP_PERSIST)
-        hipLaunchKernelGGL((tw_run_kernel<LP, WG, NC, TPW, true>), dim3(blocks < TW_LP_GRID ? blocks : TW_LP_GRID),
-                           dim3(WG * 64 / TPW), c->lds_bytes, st, c->d, t_end, limit, budget);
-    else
-        hipLaunchKernelGGL((tw_run_kernel<LP, WG, NC, TPW>), dim3(blocks), dim3(WG * 64 / TPW), c->lds_bytes, st, c->d,
-                           t_end, limit, budget);
+    hipLaunchKernelGGL((tw_run_kernel<LP, WG, NC, TPW>), dim3(blocks), dim3(WG * 64 / TPW), c->lds_bytes, st, c->d, t_end,
+                       limit, budget);
 }
 
 extern "C" {
@@ -3020,9 +2980,7 @@ static int load_common(tw_ctx* c, const tw_scenario_desc* s, bool lp, uint32_t l
     else if (lp)
         HIPCHK(hipFuncSetAttribute((const void*)tw_run_kernel<true, TW_WG_LP, TW_NEAR_LP>,
                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)c->lds_bytes));
-    if (lp)
-        HIPCHK(hipFuncSetAttribute((const void*)tw_run_kernel<true, TW_WG_LP, TW_NEAR_LP, 64, true>,
-                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)c->lds_bytes));
+
     else
         HIPCHK(hipFuncSetAttribute((const void*)tw_run_kernel<false, TW_WG, TW_NEAR_CAP>,
                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)c->lds_bytes));
@@ -3130,7 +3088,6 @@ static int load_common(tw_ctx* c, const tw_scenario_desc* s, bool lp, uint32_t l
         ALLOC(d.lp_err, 1);
         ALLOC(d.act, 2 * TW_LP_NB * R);
         ALLOC(d.act_n, 2 * TW_LP_NB);
-        ALLOC(d.lp_ctr, 1);
         ALLOC(d.wake, R);
         ALLOC(d.listed, R);
         if (lpb) ALLOC(d.inlist, R);
@@ -3288,7 +3245,6 @@ int tw_run(tw_ctx* c, int64_t t_end_us, uint64_t max_events, tw_stats* out) {
         for (int i = 0; i < per_check; ++i) {
             HIPCHK(hipMemsetAsync(d.n_active, 0, 4, st));
             if (c->lp) HIPCHK(hipMemsetAsync(d.next_t, 0xFF, 8, st));
-            if (c->lp) HIPCHK(hipMemsetAsync(d.lp_ctr, 0, 4, st));
             HIPCHK(hipEventRecord(c->ev_pool[2 * i], st));
             if (c->lp)
                 launch_run<true, TW_WG_LP, TW_NEAR_LP>(c, st, t_end_us, limit, budget);
@@ -3641,7 +3597,7 @@ int tw_lp_tick(tw_ctx* c) {
     launch_run<true, TW_WG_LP, TW_NEAR_LP>(c, st, 0, UINT64_MAX, c->lp_budget);
     c->d.win = nullptr;
     HIPCHK(hipGetLastError());
-    hipLaunchKernelGGL(tw_lp_pack, dim3(lp_grid(d.out_cap) < 512 ? lp_grid(d.out_cap) : 512), dim3(256), 0, st, d, c->ex_send,
+    hipLaunchKernelGGL(tw_lp_pack, dim3(lp_grid(d.out_cap)), dim3(256), 0, st, d, c->ex_send,
                        (const uint32_t*)c->ex_starts, c->ex_world, c->ex_cap);
     HIPCHK(hipGetLastError());
     return TW_OK;

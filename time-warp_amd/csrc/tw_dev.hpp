@@ -143,7 +143,6 @@ struct Dev {
     // the marks (tw_lp_compact)
     uint32_t* act;       // [2][TW_LP_NB][R]
     uint32_t* act_n;     // [2][TW_LP_NB]
-    uint32_t* lp_ctr;    // [1] 64-lane chunks of the work list taken by the persistent LP grid
     int64_t* wake;       // [R] device loop: the lane's next event time (INT64_MAX: none); a
                          // window lists only lanes due in it, the others' minimum bounds the next
     uint32_t* listed;    // [R]
