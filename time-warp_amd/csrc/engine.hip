@@ -3716,7 +3716,7 @@ static int lpb_run(tw_ctx* c, tw_stats* out) {
             if (rr[i].status >= TW_REP_ERR_SLOTS) ++out->replicas_error;
         }
         out->sends = out->delivered + out->dropped + out->undeliverable;
-        out->launches = (uint32_t)ls.ticks;
+        out->launches = 1;  // the window loop, timed as one (tw_last_launch_ms)
         out->kernel_ms = ms;
         out->wall_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - w0).count();
     }
