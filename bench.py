@@ -125,7 +125,7 @@ def engine_sha() -> str:
     return h.hexdigest()[:16]
 
 
-def measured_traffic(args, launches_per_step: float, events_per_step: float):
+def measured_traffic(args, launches_per_step: float, events_per_step: float, whole_loop: bool = False):
     """HBM traffic of this workload from the newest profiles/*/pmc_summary.json
     taken with tools/pmc.sh on THIS engine build (engine_sha) and the same
     workload (bench_workload); None otherwise.  rocprofv3 PMC counters cannot
@@ -147,11 +147,17 @@ def measured_traffic(args, launches_per_step: float, events_per_step: float):
     if best is None:
         return None
     f, pm = best
-    per_step = float(pm["hbm_bytes_total"]) / max(1, int(pm.get("steps", 1)))
+    key = "hbm_bytes_all_tw" if whole_loop else "hbm_bytes_total"
+    if key not in pm:
+        return None
+    per_step = float(pm[key]) / max(1, int(pm.get("steps", 1)))
     return {
         "traffic": per_step / max(1.0, launches_per_step),
         "traffic_per_event": per_step / max(1.0, events_per_step),
-        "fetch_size_kib": pm["fetch_size"], "write_size_kib": pm["write_size"],
+        "fetch_size_kib": pm["fetch_size_all_tw" if whole_loop else "fetch_size"],
+        "write_size_kib": pm["write_size_all_tw" if whole_loop else "write_size"],
+        "traffic_scope": "every kernel of the window loop (one launch = the loop)" if whole_loop else
+                         "the event kernel, per launch",
         "traffic_formula": pm.get("formula", "(2*FETCH_SIZE + WRITE_SIZE)*1024"),
         "traffic_source": os.path.relpath(f, ROOT) + f" (engine {pm['engine_sha']})",
     }
@@ -235,6 +241,9 @@ def bench_gossip(args, scn, workload, world, rank, local, dist_on, barrier):
                                            "advance kernels + collectives), up to its final stream sync"
                          if not args.host_windows else "summed event-kernel launches"},
         }
+        mt = measured_traffic(args, 1, ev, whole_loop=True) if world == 1 and not args.host_windows else None
+        if mt:
+            out["roofline"].update(mt)
         if not args.no_cpu_baseline:
             sys.path.insert(0, os.path.join(ROOT, "oracle"))
             import oracle
@@ -407,7 +416,8 @@ def main():
         # handler thread and wakes its receiver: DESIGN.md section 6)
         per["arrivals_frac"] = arrivals / max(1, per["events"])
         out["events_breakdown"] = per
-        mt = measured_traffic(args, launches / args.steps, events / args.steps) if world == 1 else None
+        mt = (measured_traffic(args, launches / args.steps, events / args.steps, eng.geometry() == "lpb")
+              if world == 1 else None)
         if mt:
             out["roofline"].update(mt)
         if not args.no_cpu_baseline:

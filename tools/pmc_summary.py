@@ -62,6 +62,13 @@ def main():
         summary["formula"] = "(2*FETCH_SIZE + WRITE_SIZE)*1024"
         summary["hbm_bytes_total"] = (2 * fetch + write) * 1024
         summary["hbm_bytes_per_dispatch"] = summary["hbm_bytes_total"] / max(1, run["FETCH_SIZE"]["dispatches"])
+    # window loops (LP / batched LP): every kernel of the loop moves bytes, the
+    # event kernel most; their sum is the loop's traffic
+    f_all = sum(v["FETCH_SIZE"]["sum"] for k, v in agg.items() if "FETCH_SIZE" in v and "tw_" in k)
+    w_all = sum(v["WRITE_SIZE"]["sum"] for k, v in agg.items() if "WRITE_SIZE" in v and "tw_" in k)
+    if f_all or w_all:
+        summary["hbm_bytes_all_tw"] = (2 * f_all + w_all) * 1024
+        summary["fetch_size_all_tw"], summary["write_size_all_tw"] = f_all, w_all
     json.dump(summary, open(out_path, "w"), indent=1)
     print(json.dumps({k: v for k, v in summary.items() if k != "counters"}, indent=1)[:3000])
 
