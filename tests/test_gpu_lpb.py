@@ -107,3 +107,25 @@ def test_lpb_rejects_short_link_out_of_phase1(engine_mod):
     with engine_mod.Engine(0) as e:
         with pytest.raises(engine_mod.EngineError):
             e.load_lpb(scn, lookahead_us=1000)
+
+
+def test_lpb_equals_replica_kernel_at_scale(engine_mod):
+    # GPU vs GPU at a size the oracle would take minutes for: the C5 shape with
+    # 64 replicas and 200 messages per sender, batched logical processes vs the
+    # wavefront-per-replica kernel (itself oracle-checked), every output field
+    # and node hash
+    scn = scenarios.hotspot(n_senders=256, n_replicas=64, msg_num=200)
+    with engine_mod.Engine(0) as e:
+        e.load(scn, geometry="lpb")
+        e.reset()
+        e.run()
+        r1, h1 = e.results(), e.hashes()
+    with engine_mod.Engine(0) as e:
+        e.load(scn, geometry="wave")
+        e.run()
+        r2, h2 = e.results(), e.hashes()
+    for f in RESULT_FIELDS:
+        if f != "tie_flags":
+            assert np.array_equal(r1[f], r2[f]), f
+    assert np.array_equal(h1, h2)
+    assert (r1["status"] == 1).all() and r1["delivered"].sum() == 2 * 256 * 200 * 64

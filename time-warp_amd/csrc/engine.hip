@@ -19,9 +19,9 @@
 //     working set on chip: TimedT's event queue (a pqueue MinQueue of
 //     continuations) becomes an LDS NEAR heap of 64-bit keys (events due within
 //     the scenario's horizon) with its root cached in registers, plus monotone
-//     FIFO runs and a 4-ary heap in HBM for far events; thread records of
-//     near-queued threads live in a write-back LDS cache (LRU), so the common
-//     pop -> run -> re-queue cycle never waits on HBM;
+//     FIFO runs and a 4-ary heap in HBM for far events; the record the next
+//     pop most likely needs is loaded into LDS staging by LDS-DMA one step
+//     ahead, so the common pop -> run -> re-queue cycle rarely waits on HBM;
 //   * every thread has at most one queued event, so throwTo's queue rebuild
 //     (TimedT.hs:361-368) becomes an O(1) re-stamp: a fresh (now, seq) entry is
 //     pushed (or the near entry re-keyed in place) and a superseded entry is
@@ -1655,6 +1655,23 @@ struct Lane {
         STIME(tt1);
         STADD(K_CYC_TERM, tt1 - tt0);
         store_tail(slot, th, fin == T_YIELD || fin == T_STOP, fin == T_EXIT, cslot, ch);
+        if constexpr (LP) {
+            // A child queued at now is usually the next pop (a deliverer's handler):
+            // its record goes to the staging quads right away instead of the
+            // prefetch's guess made before the step.  The store tail's 8 stores are
+            // younger than that prefetch, so vmcnt(8) proves it has landed and
+            // cannot overwrite these LDS writes.
+            if (cslot != 0xFFFFFFFFu && near_n != 0 && nrs == cslot) {
+                asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+                pfs[0] = make_uint4(ch.w0, ch.w1, ch.w2, ch.w3);
+                pfs[WG] = make_uint4(ch.f0, ch.f1, ch.xl, ch.xh);
+                pfs[2 * WG] = make_uint4((uint32_t)ch.r0, (uint32_t)((uint64_t)ch.r0 >> 32), (uint32_t)ch.r1,
+                                         (uint32_t)((uint64_t)ch.r1 >> 32));
+                pfs[3 * WG] = make_uint4((uint32_t)ch.r2, (uint32_t)((uint64_t)ch.r2 >> 32), (uint32_t)ch.r3,
+                                         (uint32_t)((uint64_t)ch.r3 >> 32));
+                pf_slot = cslot;
+            }
+        }
         STIME(tt2);
         STADD(K_CYC_STORE, tt2 - tt1);
     }
@@ -2303,7 +2320,7 @@ __global__ void __launch_bounds__(256) tw_lp_import(Dev c, const uint4* recv, ui
 }
 // red = {this rank's next event time (lanes' queues, records delivered this
 // window), -(lanes still active in the window)}, for an all-reduce(min)
-__global__ void tw_lp_fill(Dev c, int64_t* red) {
+__device__ __forceinline__ void lp_fill(const Dev& c, int64_t* red) {
     const int64_t GAS* w = gp(c.win);
     if (w[WN_FLAGS] & WN_DONE) {
         gp(red)[0] = INT64_MAX;
@@ -2322,9 +2339,13 @@ __global__ void tw_lp_fill(Dev c, int64_t* red) {
     const bool spawn_here = sp < (uint64_t)(w[WN_T] + w[WN_L]);
     gp(red)[1] = -(int64_t)*gp(c.n_active) - (spawn_here ? 1 : 0);
 }
+__global__ void tw_lp_fill(Dev c, int64_t* red) { lp_fill(c, red); }
 // advance: every rank idle in this window -> T := the global next time (a
 // fresh window: flip the work lists), else rerun the window
-__global__ void tw_lp_ctl(Dev c, const int64_t* red, uint4* send, uint32_t world, uint32_t cap) {
+// (one rank: the reduction words are this rank's own, filled here -- one
+// launch per tick fewer than tw_lp_fill + tw_lp_ctl)
+__global__ void tw_lp_ctl(Dev c, int64_t* red, uint4* send, uint32_t world, uint32_t cap) {
+    if (world == 1) lp_fill(c, red);
     int64_t GAS* w = gp(c.win);
     if (w[WN_FLAGS] & WN_DONE) return;
     w[WN_TICKS] += 1;
@@ -2747,8 +2768,8 @@ static void launch_run(tw_ctx* c, hipStream_t st, int64_t t_end, uint64_t limit,
 extern "C" {
 
 const char* tw_version(void) {
-    return "timewarp-mi355x 0.4 (gfx950; lane-per-replica dense/narrow/sparse kernels, wavefront-per-replica kernel, "
-           "node-partitioned LP kernel with device-driven windows; ABI 2)";
+    return "timewarp-mi355x 0.5 (gfx950; lane-per-replica dense/narrow/sparse kernels, wavefront-per-replica kernel, "
+           "node-partitioned LP kernel with device-driven windows, batched logical processes (tw_lpb_load); ABI 2)";
 }
 
 const char* tw_strerror(int code) {
@@ -3613,8 +3634,10 @@ int tw_lp_tick_import(tw_ctx* c) {
                            (const uint4*)c->ex_recv, c->ex_world, c->ex_cap);
         HIPCHK(hipGetLastError());
     }
-    hipLaunchKernelGGL(tw_lp_fill, dim3(1), dim3(1), 0, st, c->dwin(), c->ex_red);
-    HIPCHK(hipGetLastError());
+    if (c->ex_world > 1) {  // (one rank: tw_lp_ctl fills the words itself)
+        hipLaunchKernelGGL(tw_lp_fill, dim3(1), dim3(1), 0, st, c->dwin(), c->ex_red);
+        HIPCHK(hipGetLastError());
+    }
     return TW_OK;
 }
 
@@ -3622,8 +3645,8 @@ int tw_lp_tick_end(tw_ctx* c) {
     if (!c) return TW_ERR_INVALID;
     if (!c->loaded || !c->lp || !c->loop_ready) return TW_ERR_STATE;
     HIPCHK(hipSetDevice(c->device));
-    hipLaunchKernelGGL(tw_lp_ctl, dim3(1), dim3(1), 0, c->stream, c->dwin(), (const int64_t*)c->ex_red, c->ex_send,
-                       c->ex_world, c->ex_cap);
+    hipLaunchKernelGGL(tw_lp_ctl, dim3(1), dim3(1), 0, c->stream, c->dwin(), c->ex_red, c->ex_send, c->ex_world,
+                       c->ex_cap);
     HIPCHK(hipGetLastError());
     if (c->heavy_ok) {
         hipLaunchKernelGGL(tw_lp_due, dim3(TW_DUE_GRID), dim3(256), 0, c->stream, c->dwin());
