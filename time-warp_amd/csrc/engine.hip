@@ -776,6 +776,12 @@ struct Lane {
             fmsl = b ? hd[j].z : fmsl;
         }
     }
+    // every queued event (near heap, far sources, LP due run) is later than t
+    __device__ __forceinline__ bool queue_after(int64_t t) {
+        if (far_dirty) far_min();
+        const bool nl = near_n == 0 || nbase + (int64_t)(nrk >> 32) > t;
+        return nl && (fsrc < 0 || fmt > t);
+    }
     __device__ __forceinline__ void push_far(int64_t t, uint32_t sq, uint32_t slot) {
         if (!run_push(t, sq, slot)) far_push(t, sq, slot);
     }
@@ -1475,6 +1481,27 @@ struct Lane {
                         // later pops are ordinary (counted and hashed) pops
                         th_clr_flags(th, F_PHANTOM);
                         tgt = lpc & ~TW_LPC_INLINE;
+                    } else if (LP && d_ev + 2 < ev_room && tidc != 0xFFFFFFFFu && seq != 0xFFFFFFFFu &&
+                               queue_after(now)) {
+                        // LP, ForkStrategy fork_ (MonadDialog.hs:317) when every queued event
+                        // is later than now: the forked handler is the very next pop
+                        // (TimedT.hs:326-342, 242), so this lane runs it in place.  As in
+                        // the terminal's LP deliver fork, the deliverer's resume at now+1
+                        // is accounted at the sending node; the handler's creation (thread
+                        // id, insertion counter) and first pop (count, trace term) here.
+                        cinc(CW_DL);
+                        hash(dst, TW_KIND_RECV | kind, r0);
+                        hash_add((uint32_t)r2, term0(now + 1, TW_KIND_RESUME | (TW_PC_DELIVER_STUB + 2)));
+                        hash_add(dst, term0(now, TW_KIND_RESUME | (lpc & 0xFFFFu)));
+                        d_ev += 2;
+                        final_t = now + 1 > final_t ? now + 1 : final_t;
+                        th.w2 = tidc++;
+                        ++d_th;
+                        (void)next_seq();
+                        rf[0] = r0; rf[WG] = (int64_t)link; rf[2 * WG] = r2; rf[3 * WG] = (int64_t)kind;
+                        th_clr_flags(th, F_PHANTOM);
+                        n = 0;  // TW_STEP_CAP counts per pop
+                        tgt = lpc;
                     } else {
                         cinc(CW_DL);
                         hash(dst, TW_KIND_RECV | kind, r0);
