@@ -73,7 +73,10 @@ def test_gossip_device_windows_equal_oracle(engine_mod, oracle_mod, n, parts, dr
         assert int(agg[f]) == int(o.result[f]), (f, int(agg[f]), o.result[f])
     assert np.array_equal(hashes, o.hashes)
     _, _, host_windows = engine_mod.run_partitioned(scn, parts=parts)
-    assert windows == host_windows and ticks >= windows
+    # a window after one whose lanes delivered records straight into inboxes
+    # starts at that window's end (a bound below every such record) rather than
+    # at the earliest record: at most one extra, empty window per window
+    assert host_windows <= windows <= 2 * host_windows and ticks >= windows
 
 
 @pytest.mark.one_geometry

@@ -213,6 +213,9 @@ __device__ __forceinline__ uint32_t uop_of(uint32_t op) {
 // and the previous store tail.  Paths that load already waited for it.
 __device__ __forceinline__ void tw_vm_drain() { __builtin_amdgcn_s_waitcnt(0x0F70); }
 
+__device__ __forceinline__ void lp_deliver(const Dev& c, uint4 a, uint4 b, uint64_t GAS* tmin, int64_t wend,
+                                           bool upd_min = true);
+
 template <bool B>
 struct BoolC {
     static constexpr bool value = B;
@@ -995,7 +998,31 @@ struct Lane {
     }
     // LP mode: append a delivery record for another logical process
     __device__ __forceinline__ void emit(int64_t ta, int64_t payload, uint32_t link, uint32_t kind, uint32_t src,
-                                         uint32_t dst) {
+                                         uint32_t dst, uint4 dh = make_uint4(0x80000000u, 0, 0, 0)) {
+        if (c.dpar && c.win && !(dh.x >> 31) && dst - c.lp0 < c.R) {
+            // a light local lane: straight into its inbox (buffer of the next
+            // window), no tw_lp_pack pass.  The record is later than this window
+            // (t >= window end: a send is at least the lookahead): instead of a
+            // per-record atomic on the window's record minimum (one hot address)
+            // the lane notes that it sent (DW_IB bit 31) and its epilogue lowers
+            // the minimum to the window end once -- a bound below every such record
+            const uint32_t lp = dst - c.lp0;
+            const uint32_t par = (c.wid + 1u) & 1u;
+            const uint32_t k = __hip_atomic_fetch_add(gp(c.inbox_n) + (size_t)par * c.R + lp, 1u, __ATOMIC_RELAXED,
+                                                      __HIP_MEMORY_SCOPE_AGENT);
+            if (k >= dh.z) {
+                __hip_atomic_fetch_or(gp(c.lp_err), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                return;
+            }
+            const size_t base = c.ib_off ? ((size_t)dh.y << c.rep_lg) + (dst & ((1u << c.rep_lg) - 1u)) : (size_t)lp;
+            uint4 GAS* q = gp(c.inbox) + ((size_t)par * c.ib_total + base + (size_t)k * ib_stride(c)) * 2;
+            q[0] = make_uint4((uint32_t)ta, (uint32_t)((uint64_t)ta >> 32), (uint32_t)payload,
+                              (uint32_t)((uint64_t)payload >> 32));
+            q[1] = make_uint4(link, kind, src, dst);
+            lp_list_next(c, lp);
+            ds(DW_IB, dg(DW_IB) | 0x80000000u);
+            return;
+        }
         uint32_t i = __hip_atomic_fetch_add(gp(c.out_n), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (i >= c.out_cap) {
             __hip_atomic_fetch_or(gp(c.lp_err), 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1028,7 +1055,7 @@ struct Lane {
     // exactly as if it had been queued at the window's start.
     __device__ __forceinline__ void due_pop(Th& th, uint32_t& slot, uint32_t sq) {
         const uint32_t hn = dg(DW_HN), h = hn & 0xFFFFu, n = hn >> 16;
-        const size_t ib = dg(DW_IB), st = ib_stride(c);
+        const size_t ib = dg(DW_IB) & 0x7FFFFFFFu, st = ib_stride(c);
         const uint4 GAS* q = gp(c.due) + (ib + (size_t)h * st) * 2;
         const uint4 a = q[0], b = q[1];
         const uint4 nx = gp(c.due)[(ib + (size_t)(h + 1 < n ? h + 1 : h) * st) * 2];
@@ -1437,7 +1464,8 @@ struct Lane {
                                 d_ev += 2;
                                 ++d_th;
                                 final_t = ta > final_t ? ta : final_t;
-                                emit(ta, payload, (uint32_t)link, kind, th.w1, lane_of(gp(c.link_dst)[link]));
+                                const uint4 dh = gp(c.link_dsth)[link];  // destination | heavy, its inbox
+                                emit(ta, payload, (uint32_t)link, kind, th.w1, lane_of(dh.x & 0x7FFFFFFFu), dh);
                                 yt = now + 1;
                                 tc = T_YIELD;
                             }
@@ -1739,6 +1767,7 @@ __global__ void __launch_bounds__(TW_WG) tw_init_kernel(Dev c, uint32_t main_pc,
         gp(c.bind_rel)[r] = 0xFFFFFFFEu;
         if (listen_init) gp(c.bind)[r] = listen_init[g];
         gp(c.inbox_n)[r] = 0;
+        gp(c.inbox_n)[c.R + r] = 0;
         if (c.lpb) gp(c.spawn_n)[r] = 0;
         gp(c.wake)[r] = INT64_MAX;
         gp(c.listed)[r] = 0;  // marked for the first window: it serves every node
@@ -1828,10 +1857,13 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
     // whenever the node wakes again).  A light inbox (<= TW_LIGHT records) is
     // drained into the queue at the window's first tick; a heavy one was
     // sorted by tw_lp_due into this window's due run and the records due later.
-    uint32_t n_in = 0;
+    uint32_t n_in = 0, ipar = 0;
+    bool ilight = false;
     if (LP) {
-        n_in = gp(c.inbox_n)[r];
-        const bool drain = fresh && n_in != 0 && ib_cap(c, r) <= TW_LIGHT;
+        ilight = ib_cap(c, r) <= TW_LIGHT;
+        ipar = (c.dpar && c.win && ilight) ? (c.wid & 1u) : 0u;  // the buffer the last window filled
+        n_in = gp(c.inbox_n)[(size_t)ipar * R + r];
+        const bool drain = fresh && n_in != 0 && ilight;
         if (sc[SC_LIVE * R] == 0 && sc[SC_PENDING_MAIN * R] == 0 && !drain && sc[SC_DUE_H * R] >= sc[SC_DUE_N * R] &&
             !(c.lpb && gp(c.spawn_n)[r]))
             return;
@@ -1938,11 +1970,11 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
         }
     }
 
-    if (LP && fresh && n_in != 0 && ib_cap(c, r) <= TW_LIGHT) {
+    if (LP && fresh && n_in != 0 && ilight) {
         // delivery records addressed to this node become phantom deliverer
         // threads, inserted in (t, link, payload, src) order so queue seqs are
         // deterministic whatever order the records arrived in
-        const size_t ib = ib_base(c, r), ist = ib_stride(c);
+        const size_t ib = (size_t)ipar * c.ib_total + ib_base(c, r), ist = ib_stride(c);
         uint32_t used = 0;  // bitmask, n_in <= TW_LIGHT = 32
         for (uint32_t k = 0; k < n_in && L.status == TW_REP_RUNNING; ++k) {
             int best = -1;
@@ -1980,7 +2012,7 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
             L.enqueue(ph, s, ta);
             L.put_rec(s, ph);
         }
-        gp(c.inbox_n)[r] = 0;
+        gp(c.inbox_n)[(size_t)ipar * R + r] = 0;
     }
     if (LP && c.lpb) {
         // batched LP: children forked onto this node by another node of the
@@ -2162,7 +2194,12 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
     sc[SC_TMO_CTR * R] = L.cg(CW_TMO);
     sc[SC_TRACE_N * R] = L.cg(CW_TRN);
     sc[SC_EVENTS * R] = events0 + L.d_ev;
-    if (LP) sc[SC_DUE_H * R] = L.dg(DW_HN) & 0xFFFFu;
+    if (LP) {
+        sc[SC_DUE_H * R] = L.dg(DW_HN) & 0xFFFFu;
+        if (L.dg(DW_IB) >> 31)  // sent records straight into inboxes (Lane::emit)
+            __hip_atomic_fetch_min((uint64_t GAS*)(gp(c.win) + WN_REC_MIN), (uint64_t)(t_end + 1), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+    }
     sc[SC_DELIVERED * R] += L.cg(CW_DL); sc[SC_DROPPED * R] += L.cg(CW_DR);
     sc[SC_UNDELIV * R] += L.cg(CW_UD); sc[SC_THREADS * R] += L.d_th;
     if (!LP && c.Cr) {
@@ -2200,21 +2237,24 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
 // A delivery record for local node dst: claim an inbox slot (the drain at the
 // window's first tick sorts them), lower *tmin to its time, list the node for
 // the next window.
-__device__ __forceinline__ void lp_deliver(const Dev& c, uint4 a, uint4 b, uint64_t GAS* tmin,
-                                           int64_t wend = INT64_MIN) {
+__device__ __forceinline__ void lp_deliver(const Dev& c, uint4 a, uint4 b, uint64_t GAS* tmin, int64_t wend,
+                                           bool upd_min) {
     const uint32_t lp = b.w - c.lp0;
-    const uint32_t k = __hip_atomic_fetch_add(gp(c.inbox_n) + lp, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const uint32_t cap = ib_cap(c, lp);
+    const uint32_t par = ib_par_in(c, cap <= TW_LIGHT);
+    const uint32_t k =
+        __hip_atomic_fetch_add(gp(c.inbox_n) + (size_t)par * c.R + lp, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (k >= cap) {
         __hip_atomic_fetch_or(gp(c.lp_err), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         return;
     }
-    uint4 GAS* q = gp(c.inbox) + (ib_base(c, lp) + (size_t)k * ib_stride(c)) * 2;
+    uint4 GAS* q = gp(c.inbox) + ((size_t)par * c.ib_total + ib_base(c, lp) + (size_t)k * ib_stride(c)) * 2;
     q[0] = a;
     q[1] = b;
     // (a record due in this window, t < wend -- a short link into a phase-1
     // node -- is drained at phase 1's first tick: it does not bound the next window)
-    if (ent_t(a) >= wend) __hip_atomic_fetch_min(tmin, (uint64_t)ent_t(a), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (upd_min && ent_t(a) >= wend)
+        __hip_atomic_fetch_min(tmin, (uint64_t)ent_t(a), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     // a lane whose node may hold more than TW_LIGHT records is served by
     // tw_lp_due: its first pending record lists it for the next window's pass
     // (device loop; the list of window wid + 1)
@@ -2266,7 +2306,7 @@ __global__ void __launch_bounds__(256) tw_lp_scatter(Dev c, const uint4* recs, u
     uint4 a = gp(recs)[(size_t)i * 2], b = gp(recs)[(size_t)i * 2 + 1];
     uint32_t dst = b.w;
     if (dst >= c.lp0 && dst < c.lp0 + c.R) {
-        lp_deliver(c, a, b, gp(c.next_t));
+        lp_deliver(c, a, b, gp(c.next_t), INT64_MIN);
     } else if (foreign) {
         uint32_t k = __hip_atomic_fetch_add(gp(n_foreign), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (k >= foreign_cap) {
@@ -2341,7 +2381,7 @@ __global__ void __launch_bounds__(256) tw_lp_import(Dev c, const uint4* recv, ui
         const uint32_t cnt = blk[0].x;
         if (k >= (cnt < cap ? cnt : cap)) continue;
         const uint4 a = blk[(size_t)(k + 1) * 2], b = blk[(size_t)(k + 1) * 2 + 1];
-        if (b.w >= c.lp0 && b.w < c.lp0 + c.R) lp_deliver(c, a, b, tmin, wend);
+        if (b.w >= c.lp0 && b.w < c.lp0 + c.R) lp_deliver(c, a, b, tmin, wend);  // (import)
         else __hip_atomic_fetch_or(gp(c.lp_err), 4u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
@@ -2952,7 +2992,7 @@ static int load_common(tw_ctx* c, const tw_scenario_desc* s, bool lp, uint32_t l
             if (k == 0 || k > TW_HEAVY_CAP) return TW_ERR_INVALID;
             tot += k;
         }
-        if ((tot << rep_lg) > 0xFFFFFFFFull) return TW_ERR_INVALID;
+        if ((tot << rep_lg) > 0x7FFFFFFFull) return TW_ERR_INVALID;  // (a lane's inbox base: 31 bits, DW_IB)
         lp_begin = 0;
         lp_count = s->n_nodes << rep_lg;
     } else if (lp && (s->n_replicas != 1 || lp_count == 0 || (uint64_t)lp_begin + lp_count > s->n_nodes ||
@@ -3124,12 +3164,13 @@ static int load_common(tw_ctx* c, const tw_scenario_desc* s, bool lp, uint32_t l
             ALLOC(d.spawn_n, R);
         }
         ALLOC(d.hash_g, (size_t)d.Ntot << rep_lg);
-        ALLOC(d.inbox, ib_entries * 2);
+        ALLOC(d.inbox, ib_entries * 2 * 2);  // two buffers (Dev::dpar)
+        d.ib_total = ib_entries;
         ALLOC(d.due, c->heavy_ok ? ib_entries * 2 : 2);
         ALLOC(d.heavy, c->heavy_ok ? 2 * R : 2);
         ALLOC(d.heavy_n, 2);
         ALLOC(d.pend_min, 1);
-        ALLOC(d.inbox_n, R);
+        ALLOC(d.inbox_n, 2 * R);
         ALLOC(d.outbox, (size_t)d.out_cap * 2);
         ALLOC(d.out_n, 1);
         ALLOC(d.next_t, 1);
@@ -3166,6 +3207,22 @@ static int load_common(tw_ctx* c, const tw_scenario_desc* s, bool lp, uint32_t l
     if (iboff) HIPCHK(hipMemcpy(iboff, h_iboff.data(), 4 * h_iboff.size(), hipMemcpyHostToDevice));
     d.ib_off = iboff;
     if (phd) HIPCHK(hipMemcpy(phd, h_ph.data(), h_ph.size(), hipMemcpyHostToDevice));
+    if (lp) {
+        // destination of every link with the heavy bit of its node (a send to a
+        // heavy node goes through tw_lp_pack, to a light one straight in)
+        std::vector<uint4> h_dh(d.L ? d.L : 1, make_uint4(0, 0, 0, 0));
+        for (uint32_t l = 0; l < d.L; ++l) {
+            const uint32_t n = s->link_dst[l];
+            const uint32_t cap = lpb ? (node_caps ? node_caps[n] : inbox_cap) : d.IB;
+            const bool heavy = lpb && cap > TW_LIGHT;
+            h_dh[l] = make_uint4(n | (heavy ? 0x80000000u : 0u), lpb ? h_iboff[n] : 0u, cap, 0u);
+        }
+        uint4* ldh = nullptr;
+        if ((e = dalloc(c, &ldh, h_dh.size())) != TW_OK) { free_all(c); return e; }
+        HIPCHK(hipMemcpy(ldh, h_dh.data(), 16 * h_dh.size(), hipMemcpyHostToDevice));
+        d.link_dsth = ldh;
+        d.dpar = c->has_ph1 ? 0u : 1u;  // (phase-1 lanes drain inside the window: one buffer)
+    }
     d.phase = phd;
     d.has_ph1 = c->has_ph1 ? 1u : 0u;
     if (nvi) HIPCHK(hipMemcpyAsync(nvi, s->node_vars, 32ull * d.Ntot, hipMemcpyHostToDevice, st));

@@ -120,7 +120,15 @@ struct Dev {
     uint64_t* hash_g;    // [Ntot << rep_lg] this context's additions to every node's hash
     uint4* inbox;        // delivery records addressed to local lanes: entry k of lane r at
                          // ib_base(r) + k * ib_stride (x2 quads); [IB][R] without ib_off
-    uint32_t* inbox_n;   // [R]
+    uint32_t* inbox_n;   // [2][R]
+    // device loop without phases (dpar): a record for a light lane (<= TW_LIGHT
+    // pending) is delivered by the sending lane itself, into inbox buffer
+    // (wid + 1) & 1, and drained from buffer wid & 1 at the window's first tick
+    // (no tw_lp_pack pass for it); heavy lanes and the host loop use buffer 0
+    uint32_t dpar;
+    size_t ib_total;     // inbox entries per buffer
+    const uint4* link_dsth;  // [L] LP: {link_dst | heavy << 31, its inbox offset (ib_off), its inbox
+                             // capacity, 0}: a send delivers without looking the node up
     const uint32_t* ib_off;  // batched mode: [Nloc + 1] per-node capacity prefix (records), or null
     uint4* due;          // same layout: a heavy lane's records due in this window, sorted
     uint4* spawn;        // [TW_SPN][R][4] spawn records (batched mode)
@@ -202,6 +210,10 @@ __device__ __forceinline__ size_t ib_base(const Dev& c, uint32_t r) {
     return ((size_t)gp(c.ib_off)[n] << c.rep_lg) + (g & ((1u << c.rep_lg) - 1u));
 }
 __device__ __forceinline__ size_t ib_stride(const Dev& c) { return c.ib_off ? (size_t)1 << c.rep_lg : (size_t)c.R; }
+// the inbox buffer a delivery to a light lane goes to during window wid
+__device__ __forceinline__ uint32_t ib_par_in(const Dev& c, bool light) {
+    return (c.dpar && c.win && light) ? ((c.wid + 1u) & 1u) : 0u;
+}
 __device__ __forceinline__ uint32_t ib_cap(const Dev& c, uint32_t r) {
     if (!c.ib_off) return c.IB;
     const uint32_t n = ((c.lp0 + r) >> c.rep_lg) - (c.lp0 >> c.rep_lg);
