@@ -129,3 +129,21 @@ def test_lpb_equals_replica_kernel_at_scale(engine_mod):
             assert np.array_equal(r1[f], r2[f]), f
     assert np.array_equal(h1, h2)
     assert (r1["status"] == 1).all() and r1["delivered"].sum() == 2 * 256 * 200 * 64
+
+
+def test_lpb_hotspot_bandwidth(engine_mod, oracle_mod):
+    # BinaryP wire sizes -> transmission time added to each link delay
+    # (Message.hs:155-202): the lookahead is the smallest delay including it
+    scn = scenarios.hotspot(n_senders=32, n_replicas=16, msg_num=40, payload_bytes=512,
+                            bandwidth_bytes_per_s=2_000_000)
+    _compare_lpb(scn, engine_mod, oracle_mod)
+
+
+def test_lpb_token_ring_laps(engine_mod, oracle_mod):
+    # the token goes round the ring twice (every ring node's worker woken by a
+    # throwTo from its server's handler, notes to the phase-1 observer each hop)
+    N = 12
+    scn = scenarios.token_ring(n_nodes=N, n_replicas=32, launch_duration=(2 * N + 2) * 3_000_000 + 5_000_000,
+                               drop_log2=6)
+    st, ores, windows = _compare_lpb(scn, engine_mod, oracle_mod)
+    assert ores["delivered"].sum() > 2 * 2 * N * 32 * 0.5
