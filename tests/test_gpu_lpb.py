@@ -147,3 +147,18 @@ def test_lpb_token_ring_laps(engine_mod, oracle_mod):
                                drop_log2=6)
     st, ores, windows = _compare_lpb(scn, engine_mod, oracle_mod)
     assert ores["delivered"].sum() > 2 * 2 * N * 32 * 0.5
+
+
+@pytest.mark.parametrize("bad", ["replicas", "inbox"])
+def test_lpb_load_validation(engine_mod, bad):
+    # the replica count must be a power of two (lanes are node << log2 R |
+    # replica) and a node's inbox at most 2048 records (tw_lp_due stages it in LDS)
+    if bad == "replicas":
+        scn = scenarios.hotspot(n_senders=4, n_replicas=12, msg_num=4)
+        cap = None
+    else:
+        scn = scenarios.hotspot(n_senders=4, n_replicas=8, msg_num=4)
+        cap = np.full(scn.n_nodes, 4096, np.uint32)
+    with engine_mod.Engine(0) as e:
+        with pytest.raises(engine_mod.EngineError):
+            e.load_lpb(scn, node_inbox_cap=cap)
