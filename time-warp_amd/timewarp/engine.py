@@ -199,14 +199,7 @@ class Engine:
         if scn.link_table is None:
             raise EngineError("load_lpb: the scenario needs a link table (its smallest delay is the lookahead)")
         if lookahead_us is None:
-            # the smallest positive link delay; links shorter than it (a 0 µs
-            # link into a sink, e.g. token ring's observer) make their
-            # destination a phase-1 node of every window (tw_lpb_load checks it)
-            dmin = (scn.link_table & np.uint32(0x7FFFFFFF)).min(axis=(1, 2))
-            pos = dmin[dmin > 0]
-            if pos.size == 0:
-                raise EngineError("load_lpb: no link with a positive delay (no lookahead)")
-            lookahead_us = int(pos.min())
+            lookahead_us = lpb_lookahead(scn)
         m = scn.meta
         s = copy.copy(scn)
         s.max_slots = int(m.get("lp_max_slots", 64))
@@ -291,6 +284,27 @@ class Engine:
         n = self.lib.tw_last_launch_ms(self.ctx, buf.ctypes.data, buf.shape[0])
         _check(n, "tw_last_launch_ms")
         return buf[:n].copy()
+
+
+def lpb_lookahead(scn: Scenario) -> int:
+    """The batched mode's window length: the smallest positive link delay over
+    every replica and ordinal.  Links shorter than it (a 0 µs link into a sink,
+    e.g. token ring's observer) make their destination a phase-1 node of every
+    window; tw_lpb_load refuses a short link out of such a node."""
+    if scn.link_table is None:
+        raise EngineError("load_lpb: the scenario needs a link table (its smallest delay is the lookahead)")
+    dmin = (scn.link_table & np.uint32(0x7FFFFFFF)).min(axis=(1, 2))
+    pos = dmin[dmin > 0]
+    if pos.size == 0:
+        raise EngineError("load_lpb: no link with a positive delay (no lookahead)")
+    return int(pos.min())
+
+
+def lpb_short_link_destinations(scn: Scenario, lookahead_us: int) -> np.ndarray:
+    """Nodes fed by a link shorter than the lookahead (the phase-1 nodes
+    tw_lpb_load derives on the device side), for inspection and tests."""
+    dmin = (scn.link_table & np.uint32(0x7FFFFFFF)).min(axis=(1, 2))
+    return np.unique(scn.topo.dst[dmin < lookahead_us]).astype(np.int64)
 
 
 def run_scenario(scn: Scenario, device: int = 0, t_end: int = T_INF, max_events: int = UNLIMITED,
