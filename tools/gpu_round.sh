@@ -55,6 +55,7 @@ for s in "$@"; do
     prof_c3_8k_lpb) step prof_c3_8k_lpb 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_c3_8k_lpb -o run -- python3 bench.py --replicas 8192 --geometry lpb --steps 1 --warmup 0 --no-cpu-baseline ;;
     benchq_c3_8k_lpb) step benchq_c3_8k_lpb 300 python bench.py --replicas 8192 --geometry lpb --steps 2 --warmup 1 --no-cpu-baseline ;;
     pmct_c5) bash tools/pmc_traffic.sh gpurun_out/pmct_c5$SFX --config hotspot > gpurun_out/pmct_c5$SFX.log 2>&1; rc=$?; echo "pmct_c5=$rc"; [ $rc -eq 0 ] || exit $rc ;;
+    pmct_c2) bash tools/pmc_traffic.sh gpurun_out/pmct_c2$SFX --config ping_pong > gpurun_out/pmct_c2$SFX.log 2>&1; rc=$?; echo "pmct_c2=$rc"; [ $rc -eq 0 ] || exit $rc ;;
     pmct_c4) bash tools/pmc_traffic.sh gpurun_out/pmct_c4$SFX --config gossip > gpurun_out/pmct_c4$SFX.log 2>&1; rc=$?; echo "pmct_c4=$rc"; [ $rc -eq 0 ] || exit $rc ;;
     # A/B of an alternative build (lib=NAME -> time-warp_amd/lib/libtimewarp_NAME.so) is
     # a sequence like: lib=old benchq_c5 benchq_c4 lib=default benchq_c5 benchq_c4
