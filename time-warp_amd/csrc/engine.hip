@@ -1975,6 +1975,11 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
         // threads, inserted in (t, link, payload, src) order so queue seqs are
         // deterministic whatever order the records arrived in
         const size_t ib = (size_t)ipar * c.ib_total + ib_base(c, r), ist = ib_stride(c);
+        const uint32_t cap = ib_cap(c, r);  // (an overflowed inbox -- lp_err set -- keeps its first cap)
+        if (n_in > cap) {
+            L.fail(TW_REP_ERR_QUEUE);
+            n_in = cap;
+        }
         uint32_t used = 0;  // bitmask, n_in <= TW_LIGHT = 32
         for (uint32_t k = 0; k < n_in && L.status == TW_REP_RUNNING; ++k) {
             int best = -1;
