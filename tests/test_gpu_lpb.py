@@ -162,3 +162,23 @@ def test_lpb_load_validation(engine_mod, bad):
     with engine_mod.Engine(0) as e:
         with pytest.raises(engine_mod.EngineError):
             e.load_lpb(scn, node_inbox_cap=cap)
+
+
+@pytest.mark.parametrize("recv_cap", [2, 48])
+def test_lpb_inbox_overflow_is_an_error(engine_mod, oracle_mod, recv_cap):
+    # an undersized receiver inbox: 2 records (light path: the drain clamps the
+    # overflowed count to the capacity) or 48 of the ~300 pending (heavy path:
+    # tw_lp_due); the run must stop with TW_ERR_REPLICA, not read past the
+    # lane's records, and the device stays usable for a correct run after it
+    S = 64
+    scn = scenarios.hotspot(n_senders=S, n_replicas=16, msg_num=40)
+    caps = np.array(scn.meta["lp_inbox_cap"], np.uint32)
+    assert caps[S] > recv_cap
+    bad = caps.copy()
+    bad[S] = recv_cap
+    with engine_mod.Engine(0) as e:
+        e.load_lpb(scn, node_inbox_cap=bad)
+        e.reset()
+        with pytest.raises(engine_mod.EngineError, match=r"failed: -6 "):
+            e.run()
+    _compare_lpb(scn, engine_mod, oracle_mod)
