@@ -2266,7 +2266,8 @@ __device__ __forceinline__ void lp_deliver(const Dev& c, uint4 a, uint4 b, uint6
     if (k == 0 && cap > TW_LIGHT && c.win) {
         const uint32_t l = (c.wid + 1u) & 1u;
         const uint32_t i = __hip_atomic_fetch_add(gp(c.heavy_n) + l, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        gp(c.heavy)[(size_t)l * c.R + i] = lp;
+        if (i < c.R) gp(c.heavy)[(size_t)l * c.R + i] = lp;  // (once per lane and list: a guard, not a limit)
+        else __hip_atomic_fetch_or(gp(c.lp_err), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     lp_list_next(c, lp);
 }
@@ -2297,7 +2298,8 @@ __device__ __forceinline__ void lp_spawn(const Dev& c, const uint4 GAS* o, uint6
     if (__hip_atomic_exchange(gp(c.inlist) + lp, c.wid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != c.wid) {
         const uint32_t i = __hip_atomic_fetch_add(gp(c.act_n) + c.act_cur * TW_LP_NB, 1u, __ATOMIC_RELAXED,
                                                   __HIP_MEMORY_SCOPE_AGENT);
-        gp(c.act)[(size_t)c.act_cur * TW_LP_NB * c.R + i] = lp;
+        if (i < c.R) gp(c.act)[(size_t)c.act_cur * TW_LP_NB * c.R + i] = lp;  // (inlist: once per window)
+        else __hip_atomic_fetch_or(gp(c.lp_err), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     lp_list_next(c, lp);
 }
@@ -2589,7 +2591,8 @@ __global__ void __launch_bounds__(256) tw_lp_due(Dev c) {
     const uint32_t wid = (uint32_t)w[WN_WID];
     const int64_t tend = w[WN_T] + w[WN_L] - 1;
     const uint32_t lst = wid & 1u;
-    const uint32_t nh = gp(c.heavy_n)[lst];
+    uint32_t nh = gp(c.heavy_n)[lst];
+    nh = nh < c.R ? nh : c.R;  // (an over-full list has set lp_err)
     __shared__ uint4 ea[TW_HEAVY_CAP], eb[TW_HEAVY_CAP];
     __shared__ uint16_t dix[TW_HEAVY_CAP];  // entry index of the i-th due record (arrival order)
     __shared__ uint32_t cnt[257];           // exclusive scan of the due counts per thread; [256] = total
@@ -2685,7 +2688,8 @@ __global__ void __launch_bounds__(256) tw_lp_due(Dev c) {
                 const uint32_t l = lst ^ 1u;
                 const uint32_t i = __hip_atomic_fetch_add(gp(c.heavy_n) + l, 1u, __ATOMIC_RELAXED,
                                                           __HIP_MEMORY_SCOPE_AGENT);
-                gp(c.heavy)[(size_t)l * c.R + i] = r;
+                if (i < c.R) gp(c.heavy)[(size_t)l * c.R + i] = r;
+                else __hip_atomic_fetch_or(gp(c.lp_err), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
         }
         __syncthreads();
