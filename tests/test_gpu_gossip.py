@@ -93,3 +93,25 @@ def test_gossip_device_windows_rerun_ticks(engine_mod, oracle_mod, monkeypatch, 
         assert int(agg[f]) == int(o.result[f]), (f, int(agg[f]), o.result[f])
     assert np.array_equal(hashes, o.hashes)
     assert ticks > windows
+
+
+@pytest.mark.one_geometry
+def test_gossip_device_windows_inbox_overflow_is_an_error(engine_mod, oracle_mod):
+    """An inbox of one record per node: a node sent more than that in a window
+    ends the device loop with TW_ERR_REPLICA (the drain keeps to the capacity,
+    never reading another node's records), and the device stays usable."""
+    scn = scenarios.gossip(2000, seed=3)
+    s = engine_mod.lp_scenario(scn)
+    e = engine_mod.LPEngine(s, 0, scn.n_nodes, int(scn.meta["lookahead_us"]), 0, inbox_cap=1)
+    try:
+        e.reset()
+        e.loop_begin()
+        with pytest.raises(engine_mod.EngineError, match=r"failed: -6 "):
+            e.run_windows(1 << 20)
+    finally:
+        e.close()
+    agg, hashes, windows, ticks = engine_mod.run_partitioned_device(scn, parts=1)
+    o = oracle_mod.run(scn, trace_cap=0)
+    for f in FIELDS:
+        assert int(agg[f]) == int(o.result[f]), (f, int(agg[f]), o.result[f])
+    assert np.array_equal(hashes, o.hashes)
