@@ -181,9 +181,12 @@ def bench_gossip(args, scn, workload, world, rank, local, dist_on, barrier):
     b0, b1 = twd.strong_block(N, world, rank)
     starts = np.array([twd.strong_block(N, world, r)[0] for r in range(world)])
     dev = f"cuda:{local}" if dist_on else None
-    eng = LPEngine(lp_scenario(scn), b0, b1 - b0, L, local)
-    cuda = torch.device("cuda", local)
-    bounds = np.append(starts, N).astype(np.uint32)
+    # one rank of the job: the library owns the RCCL communicator over the
+    # ranks (tw_create_rank); its window loop (tw_lp_run) exchanges record
+    # blocks and reduces the window words itself, and tw_lp_results is the
+    # whole job's.  The host-driven loop keeps per-rank contexts.
+    comm = twd.library_comm(world, rank) if dist_on and not args.host_windows else None
+    eng = LPEngine(lp_scenario(scn), b0, b1 - b0, L, local, comm=comm)
 
     def one_run():
         """(windows, ticks, device ms) of one whole-scenario run"""
@@ -191,9 +194,10 @@ def bench_gossip(args, scn, workload, world, rank, local, dist_on, barrier):
             w, k = twd.lp_loop(eng, starts, L, dev, dist_on)
             return w, w, k
         # the device loop synchronises its stream before returning, so the
-        # wall time of the call is the loop's device time (+ one sync)
+        # wall time of the call is the loop's device time (+ one sync); its
+        # exchange buffers are made by the first (warm-up) run
         t0 = time.perf_counter()
-        st = twd.lp_loop_device(eng, world, rank, bounds, cuda)
+        st = eng.run_lp()
         return int(st.windows), int(st.ticks), (time.perf_counter() - t0) * 1e3
 
     for _ in range(args.warmup):
@@ -212,13 +216,13 @@ def bench_gossip(args, scn, workload, world, rank, local, dist_on, barrier):
         kms += k
         windows, ticks = w, tk
     agg, h = eng.lp_results()
-    if int(agg["status"]) >= 2:  # TW_REP_ABORTED or an error status on a local node
-        raise SystemExit(f"gossip: local nodes ended in status {int(agg['status'])}")
-    if dist_on:
+    if int(agg["status"]) >= 2:  # TW_REP_ABORTED or an error status on some node
+        raise SystemExit(f"gossip: nodes ended in status {int(agg['status'])}")
+    if dist_on and args.host_windows:
         tot, hashes = twd.reduce_lp(agg, h, dev)
-        (max_elapsed,) = [twd.reduce_stats({"elapsed_s": elapsed}, device=dev)["elapsed_s"]]
-    else:
-        tot, hashes, max_elapsed = {f: int(agg[f]) for f in agg.dtype.names}, h, elapsed
+    else:  # one context, or the library's job-wide reduction (tw_lp_results)
+        tot, hashes = {f: int(agg[f]) for f in agg.dtype.names}, h
+    max_elapsed = twd.reduce_stats({"elapsed_s": elapsed}, device=dev)["elapsed_s"] if dist_on else elapsed
     if rank == 0:
         ev = int(tot["events"])
         sends = int(tot["delivered"]) + int(tot["dropped"]) + int(tot["undeliverable"])
@@ -232,8 +236,9 @@ def bench_gossip(args, scn, workload, world, rank, local, dist_on, barrier):
             "config": {"workload": workload, "nodes": N, "events_per_step": ev, "windows": windows,
                        "ticks": ticks,
                        "window_loop": "host (tw_lp_window per window)" if args.host_windows else
-                       "device (tw_lp_tick: window advance, exchange and GVT on the GPU; one host sync per 16 ticks)",
-                       "parallelism": f"node-partitioned x{world}, RCCL all-to-all of fixed record blocks per tick"},
+                       "device (tw_lp_run: window advance, exchange and GVT on the GPU; one host sync per 16 ticks)",
+                       "parallelism": f"node-partitioned x{world}, library-owned RCCL: send/recv of record blocks "
+                                      "sized by the ranks' demand + all-reduce(min) of the window words per tick"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": None, "kernel": "tw_run_kernel<LP>",
                          "kernel_ms_per_step": kms / args.steps,
@@ -279,7 +284,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--geometry", default=None, choices=["dense", "sparse", "half", "wave", "narrow", "lpb"],
                     help="replica configs: kernel geometry (default: the library's choice by replica count); "
-                         "lpb = every (node, replica) a logical process in one window loop")
+                         "lpb = every (node, replica) a logical process in one window loop (the replicas per "
+                         "GPU must be a power of two: lanes are node << log2(R) | replica)")
     ap.add_argument("--host-windows", action="store_true",
                     help="gossip: the host-driven window loop (round-1 path) instead of the device loop")
     ap.add_argument("--workload-key", action="store_true",
@@ -316,10 +322,18 @@ def main():
     from timewarp import dist as twd
     from timewarp.engine import Engine
 
+    if args.geometry == "lpb" and args.config != "gossip":
+        _, r_rank = replica_block(args, rank, world)
+        if r_rank & (r_rank - 1):
+            raise SystemExit(f"--geometry lpb needs a power-of-two replica count per GPU (lanes are node << log2(R) "
+                             f"| replica); rank {rank} of {world} would get {r_rank} of {args.replicas} replicas")
     scn, workload = build_scenario(args, rank, world)
     if args.config == "gossip":
         return bench_gossip(args, scn, workload, world, rank, local, dist_on, barrier)
-    eng = Engine(local).load(scn, geometry=args.geometry)
+    # one rank of the job: the library's RCCL communicator over the ranks
+    # (tw_create_rank) all-reduces every tw_run's statistics
+    comm = twd.library_comm(world, rank) if dist_on else None
+    eng = Engine(local, comm=comm).load(scn, geometry=args.geometry)
 
     for _ in range(args.warmup):
         eng.reset()
@@ -354,13 +368,17 @@ def main():
 
     res = eng.results()
     hashes = eng.hashes()
-    tot = twd.reduce_stats({"events": events, "sends": sends, "elapsed_s": elapsed},
-                           device=f"cuda:{local}" if dist_on else None)
-    tot_events, max_elapsed = tot["events"], tot["elapsed_s"]
+    # st.* are the job's (tw_run's statistics, all-reduced by the library over
+    # the ranks); this rank's own share is in its replicas' results
+    loc_events = int(res["events"].sum()) * args.steps
+    loc_sends = int((res["delivered"] + res["dropped"] + res["undeliverable"]).sum()) * args.steps
+    tot_events = events
+    max_elapsed = (twd.reduce_stats({"elapsed_s": elapsed}, device=f"cuda:{local}")["elapsed_s"]
+                   if dist_on else elapsed)
 
     if rank == 0:
         value = tot_events / max_elapsed
-        alg_bytes = BYTES_PER_EVENT * events + BYTES_PER_SEND * sends   # this rank, K steps
+        alg_bytes = BYTES_PER_EVENT * loc_events + BYTES_PER_SEND * loc_sends   # this rank, K steps
         achieved = alg_bytes / (kernel_ms / 1e3) / 1e9 if kernel_ms > 0 else 0.0
         out = {
             "metric": "committed events/sec (whole node) + % HBM roofline, token-ring 64k replicas"
@@ -397,14 +415,14 @@ def main():
                 "algorithmic_bytes": "64 B/event + 8 B/send (SURVEY.md 8d)",
             },
         }
-        out["roofline"]["algorithmic_per_event"] = alg_bytes / max(1, events)
+        out["roofline"]["algorithmic_per_event"] = alg_bytes / max(1, loc_events)
         if eng.geometry() == "lpb":
             out["config"]["parallelism"] = (f"replica-sharded x{world}; inside a GPU every (node, replica) pair is a "
                                             "logical process: one device window loop, lookahead = min link delay")
             out["config"]["windows"], out["config"]["ticks"] = lpb_wt
             out["roofline"]["kernel_ms_note"] = ("one launch = the whole device window loop (event kernels + "
                                                  "due/pack/compact/advance kernels), HIP events")
-        # what the timed events are (rank 0, per step): message sends, arrivals
+        # what the timed events are (the job, per step): message sends, arrivals
         # (delivered / dropped / no listener), threads forked, and the rest
         # (waits, wake-ups, kills, timeouts)
         per = {k: v // args.steps for k, v in msg.items()}
@@ -416,7 +434,7 @@ def main():
         # handler thread and wakes its receiver: DESIGN.md section 6)
         per["arrivals_frac"] = arrivals / max(1, per["events"])
         out["events_breakdown"] = per
-        mt = (measured_traffic(args, launches / args.steps, events / args.steps, eng.geometry() == "lpb")
+        mt = (measured_traffic(args, launches / args.steps, loc_events / args.steps, eng.geometry() == "lpb")
               if world == 1 else None)
         if mt:
             out["roofline"].update(mt)

@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define TW_ABI_VERSION 2u
+#define TW_ABI_VERSION 2u  /* scenario descriptor layout (unchanged since ABI 2) */
 /* Async exception payloads (throwTo's value, `SomeException` in the
  * reference's asyncExceptions map, TimedT.hs:113,359) are carried as int64. */
 
@@ -41,8 +41,9 @@ typedef enum tw_status {
     TW_ERR_OOM = -4,          /* device allocation failed                   */
     TW_ERR_STATE = -5,        /* call out of order (run before load, ...)   */
     TW_ERR_REPLICA = -6,      /* one or more replicas ended in error status */
-    TW_ERR_INCOMPLETE = -7    /* tw_run's relaunch cap was reached before every
+    TW_ERR_INCOMPLETE = -7,   /* tw_run's relaunch cap was reached before every
                                  replica stopped (quiescence / t_end / cap)  */
+    TW_ERR_COMM = -8          /* RCCL error (communicator setup or a collective) */
 } tw_status;
 
 /* per-replica status (tw_replica_result.status) */
@@ -250,8 +251,35 @@ typedef struct tw_stats {
 
 typedef struct tw_ctx tw_ctx;
 
-/* Create a context on HIP device `device` (no CPU fallback). */
-int tw_create(int device, tw_ctx** out);
+/* Create a context over `ndev` HIP devices of this process, devices[0..ndev)
+ * (no CPU fallback; each must be a gfx950).  SURVEY.md 8(b)'s runner over a
+ * node's GPUs: with ndev > 1 the library owns one RCCL communicator per
+ * device (ncclCommInitAll) --
+ *   tw_load / tw_lpb_load split the replicas into contiguous blocks
+ *     [g*R/G, (g+1)*R/G); tw_run runs every block at once
+ *     and all-reduces the statistics over RCCL; results and hashes read back
+ *     in replica order;
+ *   tw_lp_load splits the node range; tw_lp_run runs the window loop with the
+ *     record blocks moved by RCCL send/recv and the window words by RCCL
+ *     all-reduce(min).
+ * A device listed more than once (or TW_TRANSPORT=copy) moves the blocks and
+ * words by device copies ordered with HIP events instead (same results).
+ * Replaces runTimedT (TimedT.hs:293-304) for a batch spread over GPUs. */
+int tw_create(const int* devices, int ndev, tw_ctx** out);
+
+/* One process per GPU (e.g. torchrun): rank 0 makes a job id with
+ * tw_comm_id, the caller hands it to every rank (any side channel), and each
+ * rank calls tw_create_rank; the library then owns an RCCL communicator over
+ * the ranks (ncclCommInitRank).  tw_load takes this rank's block of replicas;
+ * tw_run's stats and tw_lp_results are the whole job's; tw_lp_run exchanges
+ * with the other ranks itself.  nranks == 1 is a one-rank job (its
+ * collectives still go through RCCL). */
+#define TW_COMM_ID_BYTES 128
+int tw_comm_id(uint8_t id[TW_COMM_ID_BYTES]);
+int tw_create_rank(int device, int nranks, int rank, const uint8_t id[TW_COMM_ID_BYTES], tw_ctx** out);
+/* Shape of a context: devices of this process, ranks of the job, the global
+ * rank of its first device, transport (0 none, 1 RCCL, 2 device copies). */
+int tw_ctx_info(tw_ctx* ctx, int* ndev, int* world, int* rank0, int* transport);
 
 /* Copy a lowered scenario into HBM and reset every replica to t=0, queue empty,
  * main thread about to run (TimedT.hs:120-127, 234-237).  Replaces the
@@ -266,7 +294,8 @@ int tw_reset(tw_ctx* ctx);
 /* Run every replica's event loop (launchTimedT, TimedT.hs:234-286) until its
  * queue is empty, the next event is later than t_end_us, or its committed-event
  * total (since tw_load) reached max_events (UINT64_MAX = no cap).  May be called
- * repeatedly to advance in pieces.  Blocking.  Replaces runTimedT. */
+ * repeatedly to advance in pieces.  Blocking.  Replaces runTimedT.  `out` is
+ * the whole job's (every device, every rank: counts summed, times the max). */
 int tw_run(tw_ctx* ctx, int64_t t_end_us, uint64_t max_events, tw_stats* out);
 
 /* Per-replica results (final virtual time, counters, status, main exception). */
@@ -322,8 +351,8 @@ int tw_set_counter_base(tw_ctx* ctx, uint32_t seq0, uint32_t tid0);
  *   SPARSE one lane per replica, 16 per workgroup, large on-chip queue;
  *   HALF   the dense layout as two 32-lane waves per SIMD (an experiment);
  *   WAVE   one wavefront per replica: lane-parallel queue (few replicas);
- *   NARROW the dense layout with 8 replicas per wave (few replicas: one
- *          wave per SIMD);
+ *   NARROW the dense layout with one 64-replica wave per workgroup (fewer
+ *          replicas than fill the GPU: the waves spread over every CU);
  *   LP     node-partitioned mode (tw_lp_load);
  *   LPB    batched node-partitioned mode (tw_lpb_load). */
 enum { TW_GEO_DENSE = 0, TW_GEO_SPARSE = 1, TW_GEO_HALF = 2, TW_GEO_WAVE = 3, TW_GEO_LP = 4, TW_GEO_NARROW = 5,
@@ -372,9 +401,11 @@ int tw_lp_window(tw_ctx* ctx, int64_t t_end_excl, int64_t* next_t, uint64_t* n_f
 int tw_lp_take_outbox(tw_ctx* ctx, tw_lp_record* out, size_t cap, size_t* n);
 /* Hand records addressed to local nodes in; updates *next_t. */
 int tw_lp_inject(tw_ctx* ctx, const tw_lp_record* recs, size_t n, int64_t* next_t);
-/* Aggregate counters of the local nodes (final_t = max, counts = sums, status =
- * worst) and this context's additions to every node's hash (length n_nodes;
- * the scenario's hashes are the sum over contexts mod 2^64). */
+/* Aggregate counters (final_t = max, counts = sums, status = worst) and node
+ * hash additions (length n_nodes; a scenario's hashes are the sum over
+ * contexts mod 2^64).  A one-device context without a communicator reports
+ * its own nodes; a multi-device or RCCL context the whole job's (reduced
+ * over its devices and ranks). */
 int tw_lp_results(tw_ctx* ctx, tw_replica_result* agg, uint64_t* node_hashes, size_t n_nodes);
 
 /* ---- batched node-partitioned mode (intra-replica parallelism)
@@ -405,7 +436,7 @@ int tw_lpb_windows(tw_ctx* ctx, uint64_t* windows, uint64_t* ticks);
  * and advances T itself.  One "tick" is: the event kernel over window
  * [T, T + lookahead), the local delivery of this context's records, and the
  * packing of foreign records into fixed per-rank blocks; then, between
- * ranks, an all-to-all of those blocks and an all-reduce(min) of two int64
+ * ranks, an all-to-all of those blocks and an all-reduce(min) of four int64
  * words; then the advance: when no rank has work left in the window, T := the
  * global next-event time (INT64_MAX: done), else the same window runs again.
  * Records are drained into node queues only at a window's first tick, so the
@@ -417,14 +448,20 @@ int tw_lpb_windows(tw_ctx* ctx, uint64_t* windows, uint64_t* ticks);
  *
  * Block layout (send and recv, world blocks of (cap + 1) tw_lp_records):
  * record 0 of block g is a header whose first uint32 is the record count, then
- * up to cap records.  red: 2 device int64 {next event time, -(lanes active)},
- * all-reduced with MIN between tw_lp_tick_import and tw_lp_tick_end. */
+ * up to cap records (the header counts every record meant for that rank: the
+ * ones beyond cap wait in a carry buffer for the next tick, whose window then
+ * reruns -- never an overflow).  red: 4 device int64 {next event time,
+ * -(lanes active), -(overflow bits), -(largest per-rank record count)},
+ * all-reduced with MIN between tw_lp_tick_import and tw_lp_tick_end: an
+ * overflow on any rank (tw_lp_state.err) ends every rank's loop at the same
+ * tick, with bit 16 set. */
 typedef struct tw_lp_state {
     uint64_t windows;   /* windows completed                                 */
     uint64_t ticks;     /* ticks run (>= windows)                            */
     int64_t  t;         /* current window start (INT64_MAX when done)        */
     uint32_t done;      /* 1: every queue is empty everywhere                */
-    uint32_t err;       /* inbox / outbox / exchange-block overflow bits     */
+    uint32_t err;       /* inbox / outbox / exchange-block overflow bits; bit
+                           16: the loop stopped because some rank overflowed */
 } tw_lp_state;
 /* Use the caller's HIP stream (hipStream_t) for every later call; NULL = the
  * context's own stream. */
@@ -432,7 +469,7 @@ int tw_set_stream(tw_ctx* ctx, void* hip_stream);
 /* world == 1: send/recv/red may be NULL (the context keeps its own red).
  * starts: host array of world + 1 node boundaries (rank g owns nodes
  * [starts[g], starts[g+1])).  send/recv: device buffers of
- * world * (cap + 1) * 32 bytes; red: device int64[2]. */
+ * world * (cap + 1) * 32 bytes; red: device int64[4]. */
 int tw_lp_exchange_setup(tw_ctx* ctx, uint32_t world, uint32_t rank, const uint32_t* starts, void* send,
                          void* recv, uint32_t cap, int64_t* red);
 /* Start the device loop at T = 0 (after tw_reset). */
@@ -448,6 +485,19 @@ int tw_lp_progress(tw_ctx* ctx, tw_lp_state* out);
 /* Single context (world 1): enqueue ticks in batches of 16 with one host
  * synchronisation per batch until done or max_ticks. */
 int tw_lp_run_windows(tw_ctx* ctx, uint64_t max_ticks, tw_lp_state* out);
+/* The whole device window loop from t = 0 (after tw_reset) over every device
+ * and rank of the context, the exchange owned by the library: per tick the
+ * event kernels and packing, the record blocks between ranks (RCCL
+ * send/recv), the import, an RCCL all-reduce(min) of the window words, the
+ * advance; one host synchronisation per 16 ticks.  Blocks travel at the size
+ * the ranks last agreed on -- the largest per-rank demand of a tick, rounded
+ * up, re-chosen every 16 ticks from the reduced words (TW_LP_XCAP caps it,
+ * default 16384 records); records beyond it wait a tick in a carry buffer
+ * (the window reruns), so an exchange never overflows.  The multi-GPU
+ * replacement of MonadDialog's cross-node send path (MonadDialog.hs:149-166)
+ * with runTimedT's loop around it.  The caller-driven primitives
+ * (tw_lp_exchange_setup / tw_lp_tick ...) remain for one-device contexts. */
+int tw_lp_run(tw_ctx* ctx, uint64_t max_ticks, tw_lp_state* out);
 
 /* ---------------------------------------------------------------- hashing
  * Per-node trace hash (made fully commutative): every

@@ -29,8 +29,11 @@ def mix(n, t, p):
 
 
 class StandinLP:
-    def __init__(self, n_nodes, lp_begin, lp_count, lookahead, budget=1 << 30, seeds=None):
+    def __init__(self, n_nodes, lp_begin, lp_count, lookahead, budget=1 << 30, seeds=None, overflow_tick=None):
         self.N, self.b0, self.n, self.L, self.budget = n_nodes, lp_begin, lp_count, lookahead, budget
+        # overflow_tick: at that tick this rank reports an inbox overflow (bit 1),
+        # as tw_lp_tick does when a node's inbox is full
+        self.overflow_tick = overflow_tick
         self.seeds = seeds if seeds is not None else [(i, (i % 7) * 100, 8) for i in range(0, n_nodes, 3)]
         self.reset()
 
@@ -120,7 +123,7 @@ class StandinLP:
 
     def loop_begin(self):
         self.T, self.windows, self.ticks, self.fresh, self.done, self.rec_min = 0, 0, 0, True, False, T_INF
-        self.active = False
+        self.active, self.err = False, 0
         return self
 
     def tick(self):
@@ -131,6 +134,8 @@ class StandinLP:
                 self._push(r)
             self.inbox = []
         self.active = self._run(self.T + self.L, self.budget)
+        if self.overflow_tick is not None and self.ticks == self.overflow_tick:
+            self.err |= 1
         for r in self.out:
             if self._local(r[2]):
                 self.inbox.append(r)
@@ -147,9 +152,10 @@ class StandinLP:
 
     def tick_import(self):
         if self.bufs is None:
-            red = self._red = np.zeros(2, np.int64)
+            red = self._red = np.zeros(4, np.int64)
         else:
             red = self.bufs[2]
+        red[2] = -self.err  # the overflow bits, reduced with MIN like the other words
         if self.done:
             red[0], red[1] = T_INF, 0
             return
@@ -172,6 +178,10 @@ class StandinLP:
         if self.bufs is not None and self.world > 1:
             for g in range(self.world):
                 self.bufs[0][g * (self.cap + 1)]["t_arr"] = 0
+        if red[2] < 0:  # some rank overflowed: every rank stops at this tick
+            self.err |= int(-red[2]) | 16
+            self.done = True
+            return
         if red[1] < 0:
             self.fresh = False
             return
@@ -186,7 +196,7 @@ class StandinLP:
             pass
 
         s = S()
-        s.windows, s.ticks, s.t, s.done, s.err = self.windows, self.ticks, self.T, int(self.done), 0
+        s.windows, s.ticks, s.t, s.done, s.err = self.windows, self.ticks, self.T, int(self.done), self.err
         return s
 
     def run_windows(self, max_ticks):

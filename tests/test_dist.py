@@ -1,16 +1,18 @@
 """Multi-rank replica sharding with world_size 2 over gloo (CPU).
 
-Each rank owns a weak-scaling block of replicas; the per-rank run (here the
-oracle, standing in for the per-GPU engine which needs a device) is reduced
-with timewarp.dist exactly as bench.py does over RCCL.  The union must equal a
-single-process run of all replicas, replica for replica."""
+Each rank owns a contiguous block of one global batch (strong scaling,
+bench.py's default: dist.strong_block, uneven here so the remainder rule is
+exercised); the per-rank run (here the oracle, standing in for the per-GPU
+engine which needs a device) is reduced with timewarp.dist exactly as bench.py
+does over RCCL.  The union must equal a single-process run of all replicas,
+replica for replica."""
 import os
 import socket
 
 import numpy as np
 import torch.multiprocessing as mp
 
-R_PER_RANK = 12
+R_TOTAL = 25  # split 13 + 12 over two ranks
 
 
 def _free_port():
@@ -34,7 +36,8 @@ def _worker(rank, world, port, out_path):
 
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    seed_base, n = twd.weak_block(rank, R_PER_RANK)
+    r0, r1 = twd.strong_block(R_TOTAL, world, rank)
+    seed_base, n = r0, r1 - r0
     scn = scenarios.token_ring(n_nodes=9, n_replicas=n, launch_duration=30_000_000, drop_log2=3,
                                link_depth=4, seed_base=seed_base)
     res, hashes = oracle.run_batch(scn, threads=2)
@@ -55,7 +58,7 @@ def test_two_rank_sharding_equals_single_process(tmp_path, oracle_mod):
     out = str(tmp_path / "r.npz")
     mp.spawn(_worker, args=(2, _free_port(), out), nprocs=2, join=True)
     got = np.load(out)
-    scn = scenarios.token_ring(n_nodes=9, n_replicas=2 * R_PER_RANK, launch_duration=30_000_000, drop_log2=3,
+    scn = scenarios.token_ring(n_nodes=9, n_replicas=R_TOTAL, launch_duration=30_000_000, drop_log2=3,
                                link_depth=4, seed_base=0)
     res, hashes = oracle_mod.run_batch(scn, threads=4)
     for f in res.dtype.names:
@@ -65,6 +68,7 @@ def test_two_rank_sharding_equals_single_process(tmp_path, oracle_mod):
     assert got["max_final_t"] == res["final_t"].max()
     assert abs(float(got["elapsed"]) - 0.2) < 1e-12  # max over ranks
     assert twd.strong_block(10, 3, 0) == (0, 4) and twd.strong_block(10, 3, 2) == (7, 10)
+    assert twd.strong_block(R_TOTAL, 2, 0) == (0, 13) and twd.weak_block(1, 12) == (12, 12)
 
 
 def _xchg_worker(rank, world, port, out_path):

@@ -39,7 +39,7 @@ def _single(budget):
     return ev, h, st.windows
 
 
-def _worker(rank, world, port, out_path, mode, budget):
+def _worker(rank, world, port, out_path, mode, budget, overflow_rank=None):
     import sys
 
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -53,7 +53,19 @@ def _worker(rank, world, port, out_path, mode, budget):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     b0, b1 = twd.strong_block(N, world, rank)
     starts = np.array([twd.strong_block(N, world, r)[0] for r in range(world)] + [N])
-    e = StandinLP(N, b0, b1 - b0, L, budget=budget)
+    e = StandinLP(N, b0, b1 - b0, L, budget=budget, overflow_tick=4 if rank == overflow_rank else None)
+    if overflow_rank is not None:
+        # one rank overflows: both ranks must stop at the same check and raise
+        # (the overflow bits are the third reduction word), none left waiting
+        # in a collective
+        try:
+            twd.lp_loop_device(e, world, rank, starts, None, cap=256, check_every=3)
+            err = 0
+        except RuntimeError as x:
+            err = int(str(x).split("overflow bits ")[1].split()[0])
+        np.save(f"{out_path}.{rank}.npy", np.array([err, e.ticks]))
+        dist.destroy_process_group()
+        return
     if mode == "host":
         windows, _ = twd.lp_loop(e, starts[:-1], L, None, distributed=True)
     else:
@@ -81,3 +93,16 @@ def test_two_rank_window_loop_equals_single_process(tmp_path, mode, budget):
     assert int(got["events"]) == ev
     assert np.array_equal(got["hashes"], h)
     assert int(got["windows"]) == windows
+
+
+def test_overflow_on_one_rank_stops_both(tmp_path):
+    """An inbox overflow on rank 1 only: both ranks' device loops
+    stop at the same tick and raise with the overflowing rank's bits (the
+    all-reduce(min) of -bits) plus bit 16 (stopped by the shared error word);
+    the processes exit."""
+    out = str(tmp_path / "o")
+    mp.spawn(_worker, args=(2, _free_port(), out, "device", 1 << 30, 1), nprocs=2, join=True)
+    e0, t0 = np.load(out + ".0.npy")
+    e1, t1 = np.load(out + ".1.npy")
+    assert e0 == e1 == 1 | 16
+    assert t0 == t1 == 5  # stopped at the tick after the overflow's

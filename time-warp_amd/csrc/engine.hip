@@ -39,6 +39,7 @@
 
 #include "../../include/timewarp.h"
 #include "tw_dev.hpp"
+#include "shard.hpp"
 
 #define TW_NEAR_CAP 16          // on-chip queue entries per replica (LDS)
 #define TW_WG 256               // lanes per workgroup (4 waves share one program image)
@@ -215,6 +216,20 @@ __device__ __forceinline__ void tw_vm_drain() { __builtin_amdgcn_s_waitcnt(0x0F7
 
 __device__ __forceinline__ void lp_deliver(const Dev& c, uint4 a, uint4 b, uint64_t GAS* tmin, int64_t wend,
                                            bool upd_min = true);
+
+// The order delivery records enter a logical process's queue (light drain and
+// tw_lp_due alike): (t, link, payload, src, kind), so queue seqs do not depend
+// on the order the records arrived in.  a/c: {t lo, t hi, payload lo, payload
+// hi}; b/d: {link, kind, src, dst}.
+__device__ __forceinline__ bool rec_less(uint4 a, uint4 b, uint4 c, uint4 d) {
+    const int64_t t1 = ent_t(a), t2 = ent_t(c);
+    if (t1 != t2) return t1 < t2;
+    if (b.x != d.x) return b.x < d.x;
+    const uint64_t p1 = ((uint64_t)a.w << 32) | a.z, p2 = ((uint64_t)c.w << 32) | c.z;
+    if (p1 != p2) return p1 < p2;
+    if (b.z != d.z) return b.z < d.z;
+    return b.y < d.y;
+}
 
 template <bool B>
 struct BoolC {
@@ -1972,7 +1987,8 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
 
     if (LP && fresh && n_in != 0 && ilight) {
         // delivery records addressed to this node become phantom deliverer
-        // threads, inserted in (t, link, payload, src) order so queue seqs are
+        // threads, inserted in (t, link, payload, src, kind) order (rec_less, the
+        // order tw_lp_due gives a heavy lane's due run) so queue seqs are
         // deterministic whatever order the records arrived in
         const size_t ib = (size_t)ipar * c.ib_total + ib_base(c, r), ist = ib_stride(c);
         const uint32_t cap = ib_cap(c, r);  // (an overflowed inbox -- lp_err set -- keeps its first cap)
@@ -1988,13 +2004,7 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
                 if (used & (1u << j)) continue;
                 const uint4 GAS* q = gp(c.inbox) + (ib + (size_t)j * ist) * 2;
                 uint4 ea = q[0], eb = q[1];
-                bool less = best < 0;
-                if (!less) {
-                    int64_t t1 = ent_t(ea), t2 = ent_t(ba);
-                    uint64_t p1 = ((uint64_t)ea.w << 32) | ea.z, p2 = ((uint64_t)ba.w << 32) | ba.z;
-                    less = t1 < t2 || (t1 == t2 && (eb.x < bb.x || (eb.x == bb.x && (p1 < p2 || (p1 == p2 && eb.z < bb.z)))));
-                }
-                if (less) { best = (int)j; ba = ea; bb = eb; }
+                if (best < 0 || rec_less(ea, eb, ba, bb)) { best = (int)j; ba = ea; bb = eb; }
             }
             used |= 1u << best;
             int64_t ta = ent_t(ba);
@@ -2338,15 +2348,57 @@ __device__ __forceinline__ bool win_enter(Dev& c) {
     return true;
 }
 // this tick's records: local ones into inboxes, foreign ones into the send
-// block of their owner rank (starts[g] <= dst < starts[g + 1])
+// block of their owner rank (starts[g] <= dst < starts[g + 1]).  Blocks are
+// `stride` records apart; this tick sends the first `cap` of each (the size
+// the ranks agreed on, <= stride).  A block's header counts every record
+// meant for that rank (the demand, reduced as RD_DEMAND); records beyond cap
+// -- and the carry of the previous tick, sent first -- wait in the carry
+// buffer for the next tick, which keeps the window running (lp_fill), so an
+// exchange never overflows and never loses a record.
+__device__ __forceinline__ void lp_foreign(const Dev& c, uint4 a, uint4 b, uint4* send, const uint32_t* starts,
+                                           uint32_t world, uint32_t stride, uint32_t cap, uint32_t cout) {
+    const uint32_t dst = b.w;
+    uint32_t lo = 0, hi = world;
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (gp(starts)[mid] <= dst) lo = mid; else hi = mid;
+    }
+    uint4 GAS* blk = gp(send) + (size_t)lo * (stride + 1) * 2;
+    const uint32_t k = __hip_atomic_fetch_add((uint32_t GAS*)blk, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (k < cap) {
+        blk[(size_t)(k + 1) * 2] = a;
+        blk[(size_t)(k + 1) * 2 + 1] = b;
+        return;
+    }
+    const uint32_t j = __hip_atomic_fetch_add(gp(c.carry_n) + cout, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (j >= c.carry_cap) {
+        __hip_atomic_fetch_or(gp(c.lp_err), 8u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return;
+    }
+    uint4 GAS* q = gp(c.carry) + ((size_t)cout * c.carry_cap + j) * 2;
+    q[0] = a;
+    q[1] = b;
+}
 __global__ void __launch_bounds__(256) tw_lp_pack(Dev c, uint4* send, const uint32_t* starts, uint32_t world,
-                                                  uint32_t cap) {
+                                                  uint32_t stride, uint32_t cap) {
     if (!win_enter(c)) return;
     uint32_t n = *gp(c.out_n);
     n = n < c.out_cap ? n : c.out_cap;
     uint64_t GAS* tmin = (uint64_t GAS*)(gp(c.win) + WN_REC_MIN);
     const int64_t wend = gp(c.win)[WN_T] + gp(c.win)[WN_L];
-    for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
+    // carry buffers by tick parity: read the previous tick's, write this one's
+    const uint32_t tk = (uint32_t)gp(c.win)[WN_TICKS], cout = tk & 1u, cin = cout ^ 1u;
+    uint32_t nc = 0;
+    if (c.carry && send && world > 1) {
+        nc = *gp(c.carry_n + cin);
+        nc = nc < c.carry_cap ? nc : c.carry_cap;
+    }
+    for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n + nc; i += gridDim.x * 256) {
+        if (i >= n) {  // a record the previous tick's blocks had no room for
+            const uint4 GAS* q = gp(c.carry) + ((size_t)cin * c.carry_cap + (i - n)) * 2;
+            lp_foreign(c, q[0], q[1], send, starts, world, stride, cap, cout);
+            continue;
+        }
         const uint4 a = gp(c.outbox)[(size_t)i * 2], b = gp(c.outbox)[(size_t)i * 2 + 1];
         const uint32_t dst = b.w;
         if (b.y == TW_SPAWN_CONT) continue;  // second half of a spawn pair
@@ -2356,35 +2408,23 @@ __global__ void __launch_bounds__(256) tw_lp_pack(Dev c, uint4* send, const uint
         }
         if (dst >= c.lp0 && dst < c.lp0 + c.R) {
             lp_deliver(c, a, b, tmin, wend);
-        } else if (send && world > 1) {
-            uint32_t lo = 0, hi = world;
-            while (hi - lo > 1) {
-                const uint32_t mid = (lo + hi) >> 1;
-                if (gp(starts)[mid] <= dst) lo = mid; else hi = mid;
-            }
-            uint4 GAS* blk = gp(send) + (size_t)lo * (cap + 1) * 2;
-            const uint32_t k = __hip_atomic_fetch_add((uint32_t GAS*)blk, 1u, __ATOMIC_RELAXED,
-                                                      __HIP_MEMORY_SCOPE_AGENT);
-            if (k >= cap) {
-                __hip_atomic_fetch_or(gp(c.lp_err), 8u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                continue;
-            }
-            blk[(size_t)(k + 1) * 2] = a;
-            blk[(size_t)(k + 1) * 2 + 1] = b;
+        } else if (send && world > 1 && c.carry) {
+            lp_foreign(c, a, b, send, starts, world, stride, cap, cout);
         } else {
             __hip_atomic_fetch_or(gp(c.lp_err), 4u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
 }
-// the records other ranks sent this tick
-__global__ void __launch_bounds__(256) tw_lp_import(Dev c, const uint4* recv, uint32_t world, uint32_t cap) {
+// the records other ranks sent this tick (the first min(count, cap) of each block)
+__global__ void __launch_bounds__(256) tw_lp_import(Dev c, const uint4* recv, uint32_t world, uint32_t stride,
+                                                    uint32_t cap) {
     if (!win_enter(c)) return;
     uint64_t GAS* tmin = (uint64_t GAS*)(gp(c.win) + WN_REC_MIN);
     const int64_t wend = gp(c.win)[WN_T] + gp(c.win)[WN_L];
     const uint32_t total = world * cap;
     for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < total; i += gridDim.x * 256) {
         const uint32_t g = i / cap, k = i - g * cap;
-        const uint4 GAS* blk = gp(recv) + (size_t)g * (cap + 1) * 2;
+        const uint4 GAS* blk = gp(recv) + (size_t)g * (stride + 1) * 2;
         const uint32_t cnt = blk[0].x;
         if (k >= (cnt < cap ? cnt : cap)) continue;
         const uint4 a = blk[(size_t)(k + 1) * 2], b = blk[(size_t)(k + 1) * 2 + 1];
@@ -2393,12 +2433,23 @@ __global__ void __launch_bounds__(256) tw_lp_import(Dev c, const uint4* recv, ui
     }
 }
 // red = {this rank's next event time (lanes' queues, records delivered this
-// window), -(lanes still active in the window)}, for an all-reduce(min)
-__device__ __forceinline__ void lp_fill(const Dev& c, int64_t* red) {
+// window), -(lanes still active in the window), -(this rank's overflow bits),
+// -(its largest per-rank record demand this tick)}, for an all-reduce(min):
+// an overflow on any rank ends every rank's loop at the same tick
+// (tw_lp_ctl), so no rank is left waiting in a collective
+__device__ __forceinline__ void lp_fill(const Dev& c, int64_t* red, const uint4* send, uint32_t world,
+                                        uint32_t stride) {
     const int64_t GAS* w = gp(c.win);
+    gp(red)[RD_ERR] = -(int64_t)*gp(c.lp_err);
+    uint32_t dem = 0;
+    for (uint32_t g = 0; send && g < world; ++g) {
+        const uint32_t k = gp(send)[(size_t)g * (stride + 1) * 2].x;
+        dem = k > dem ? k : dem;
+    }
+    gp(red)[RD_DEMAND] = -(int64_t)dem;
     if (w[WN_FLAGS] & WN_DONE) {
-        gp(red)[0] = INT64_MAX;
-        gp(red)[1] = 0;
+        gp(red)[RD_NEXT] = INT64_MAX;
+        gp(red)[RD_ACTIVE] = 0;
         return;
     }
     const uint64_t a = *gp(c.next_t), b = (uint64_t)w[WN_REC_MIN], p = *gp(c.pend_min), sp = (uint64_t)w[WN_SPN_MIN];
@@ -2407,28 +2458,41 @@ __device__ __forceinline__ void lp_fill(const Dev& c, int64_t* red) {
     m = p < m ? p : m;
     m = sp < m ? sp : m;
     m = sl < m ? sl : m;
-    gp(red)[0] = m >= (uint64_t)INT64_MAX ? INT64_MAX : (int64_t)m;
+    gp(red)[RD_NEXT] = m >= (uint64_t)INT64_MAX ? INT64_MAX : (int64_t)m;
     // a child forked onto another node inside this window keeps the window
-    // (phase) running: its lane starts it at the next tick
+    // (phase) running: its lane starts it at the next tick; so do records
+    // still waiting in the exchange carry
     const bool spawn_here = sp < (uint64_t)(w[WN_T] + w[WN_L]);
-    gp(red)[1] = -(int64_t)*gp(c.n_active) - (spawn_here ? 1 : 0);
+    const bool carried = c.carry && *gp(c.carry_n + ((uint32_t)w[WN_TICKS] & 1u)) != 0;
+    gp(red)[RD_ACTIVE] = -(int64_t)*gp(c.n_active) - (spawn_here ? 1 : 0) - (carried ? 1 : 0);
 }
-__global__ void tw_lp_fill(Dev c, int64_t* red) { lp_fill(c, red); }
+__global__ void tw_lp_fill(Dev c, int64_t* red, const uint4* send, uint32_t world, uint32_t stride) {
+    lp_fill(c, red, send, world, stride);
+}
 // advance: every rank idle in this window -> T := the global next time (a
 // fresh window: flip the work lists), else rerun the window
 // (one rank: the reduction words are this rank's own, filled here -- one
 // launch per tick fewer than tw_lp_fill + tw_lp_ctl)
-__global__ void tw_lp_ctl(Dev c, int64_t* red, uint4* send, uint32_t world, uint32_t cap) {
-    if (world == 1) lp_fill(c, red);
+__global__ void tw_lp_ctl(Dev c, int64_t* red, uint4* send, uint32_t world, uint32_t stride, uint32_t filled) {
+    if (!filled) lp_fill(c, red, nullptr, 1, 0);
     int64_t GAS* w = gp(c.win);
     if (w[WN_FLAGS] & WN_DONE) return;
     w[WN_TICKS] += 1;
+    // the carry buffer the next tick writes (this tick's pack read it)
+    if (c.carry) gp(c.carry_n)[(uint32_t)w[WN_TICKS] & 1u] = 0;
+    const int64_t dem = -gp(red)[RD_DEMAND];
+    w[WN_XMAX] = dem > w[WN_XMAX] ? dem : w[WN_XMAX];
     *gp(c.out_n) = 0;
-    for (uint32_t g = 0; send && g < world; ++g) gp(send)[(size_t)g * (cap + 1) * 2].x = 0;
+    for (uint32_t g = 0; send && g < world; ++g) gp(send)[(size_t)g * (stride + 1) * 2].x = 0;
     *gp(c.n_active) = 0;
     *gp(c.next_t) = ~0ull;
     w[WN_SPN_MIN] = (int64_t)~0ull;
-    if (gp(red)[1] < 0) {  // rerun this phase of the window
+    if (gp(red)[RD_ERR] < 0) {  // some rank overflowed: every rank stops here (tw_lp_progress reports it)
+        *gp(c.lp_err) |= (uint32_t)(-gp(red)[RD_ERR]) | 16u;
+        w[WN_FLAGS] = WN_DONE;
+        return;
+    }
+    if (gp(red)[RD_ACTIVE] < 0) {  // rerun this phase of the window
         w[WN_FLAGS] &= ~(WN_FRESH | WN_PH1FRESH);
         return;
     }
@@ -2436,12 +2500,12 @@ __global__ void tw_lp_ctl(Dev c, int64_t* red, uint4* send, uint32_t world, uint
         // phase 0 is done with the window: phase 1 (the nodes fed by short
         // links) runs it now; the phase-0 nodes' next time waits in WN_NT0
         w[WN_PHASE] = 1;
-        w[WN_NT0] = gp(red)[0];
+        w[WN_NT0] = gp(red)[RD_NEXT];
         w[WN_FLAGS] = WN_PH1FRESH;
         return;
     }
     w[WN_WINDOWS] += 1;
-    int64_t t = gp(red)[0];
+    int64_t t = gp(red)[RD_NEXT];
     if (w[WN_PHASE]) t = w[WN_NT0] < t ? w[WN_NT0] : t;
     w[WN_PHASE] = 0;
     if (t == INT64_MAX) {
@@ -2556,6 +2620,8 @@ __global__ void tw_lp_begin(Dev c, int64_t lookahead) {
     w[WN_NT0] = INT64_MAX;
     w[WN_SPN_MIN] = (int64_t)~0ull;
     w[WN_SLEEP_MIN] = INT64_MAX;
+    w[WN_XMAX] = 0;
+    if (c.carry) gp(c.carry_n)[0] = gp(c.carry_n)[1] = 0;
     for (int k = 0; k < TW_LP_NB; ++k) gp(c.act_n)[TW_LP_NB + k] = 0;
     *gp(c.out_n) = 0;
     *gp(c.n_active) = 0;
@@ -2575,15 +2641,6 @@ __global__ void tw_lp_begin(Dev c, int64_t lookahead) {
 // (their earliest time bounds the next window) and the lane is listed for the
 // next window's pass.
 #define TW_DUE_GRID 1024  // tw_lp_due workgroups (each serves heavy lanes in turn)
-__device__ __forceinline__ bool rec_less(uint4 a, uint4 b, uint4 c, uint4 d) {
-    const int64_t t1 = ent_t(a), t2 = ent_t(c);
-    if (t1 != t2) return t1 < t2;
-    if (b.x != d.x) return b.x < d.x;
-    const uint64_t p1 = ((uint64_t)a.w << 32) | a.z, p2 = ((uint64_t)c.w << 32) | c.z;
-    if (p1 != p2) return p1 < p2;
-    if (b.z != d.z) return b.z < d.z;
-    return b.y < d.y;
-}
 __global__ void __launch_bounds__(256) tw_lp_due(Dev c) {
     const int64_t GAS* w = gp(c.win);
     const int64_t fl = w[WN_FLAGS];
@@ -2740,7 +2797,7 @@ __global__ void __launch_bounds__(256) tw_digest_kernel(Dev c, uint64_t* out) {
 }  // namespace
 
 // ======================================================================= C ABI
-struct tw_ctx {
+struct tw_shard {
     int device = 0;
     hipStream_t stream = nullptr;
     Dev d{};
@@ -2769,13 +2826,17 @@ struct tw_ctx {
     Dev* d_dev = nullptr;             // device copy of d (the wave kernel reads it through the scalar cache)
     uint32_t seq0 = 0, tid0 = 1;      // tw_set_counter_base
     hipStream_t own_stream = nullptr; // the context's stream (tw_set_stream may replace `stream`)
-    // device-driven windows (tw_lp_exchange_setup)
-    uint32_t ex_world = 1, ex_rank = 0, ex_cap = 0;
+    // device-driven windows (tw_lp_exchange_setup / sh_lp_exchange_own):
+    // blocks of ex_cap records (the stride) of which the first ex_cap_eff go
+    // over the wire this tick (<= ex_cap; the library loop adapts it)
+    uint32_t ex_world = 1, ex_rank = 0, ex_cap = 0, ex_cap_eff = 0;
     uint32_t* ex_starts = nullptr;    // device, world + 1
-    uint4* ex_send = nullptr;         // caller's device buffers
+    uint4* ex_send = nullptr;         // caller's device buffers (or ex_own's)
     uint4* ex_recv = nullptr;
-    int64_t* ex_red = nullptr;        // caller's (or red_own)
+    int64_t* ex_red = nullptr;        // caller's (or red_own, or ex_own's)
     int64_t* red_own = nullptr;
+    void* ex_own = nullptr;           // library-owned send | recv | red (sh_lp_exchange_own)
+    void* ex_carry = nullptr;         // Dev::carry + carry_n
     int64_t* win_buf = nullptr;       // the device loop's WN_* words
     int64_t* h_win = nullptr;         // pinned host copy of them + lp_err (tw_lp_progress)
     bool loop_ready = false;
@@ -2806,7 +2867,7 @@ int hip_fail(hipError_t e) {
     } while (0)
 
 template <class T>
-int dalloc(tw_ctx* c, T** p, size_t n) {
+int dalloc(tw_shard* c, T** p, size_t n) {
     void* q = nullptr;
     if (n == 0) n = 1;
     HIPCHK(hipMalloc(&q, n * sizeof(T)));
@@ -2815,19 +2876,25 @@ int dalloc(tw_ctx* c, T** p, size_t n) {
     return TW_OK;
 }
 
-void free_all(tw_ctx* c) {
+void free_all(tw_shard* c) {
     for (void* p : c->allocs) (void)hipFree(p);
     c->allocs.clear();
     if (c->d.trace) (void)hipFree(c->d.trace);
     c->d.trace = nullptr;
     c->d.trace_cap = 0;
     if (c->ex_starts) (void)hipFree(c->ex_starts);
+    if (c->ex_own) (void)hipFree(c->ex_own);
+    if (c->ex_carry) (void)hipFree(c->ex_carry);
     c->ex_starts = nullptr;
+    c->ex_own = c->ex_carry = nullptr;
+    c->d.carry = nullptr;
+    c->d.carry_n = nullptr;
+    c->d.carry_cap = 0;
     c->ex_send = c->ex_recv = nullptr;
     c->ex_red = c->red_own = nullptr;
     c->win_buf = nullptr;
     c->ex_world = 1;
-    c->ex_rank = c->ex_cap = 0;
+    c->ex_rank = c->ex_cap = c->ex_cap_eff = 0;
     c->loop_ready = false;
     c->loaded = false;
 }
@@ -2835,34 +2902,15 @@ void free_all(tw_ctx* c) {
 }  // namespace
 
 template <bool LP, int WG, int NC, int TPW = 64>
-static void launch_run(tw_ctx* c, hipStream_t st, int64_t t_end, uint64_t limit, uint32_t budget) {
+static void launch_run(tw_shard* c, hipStream_t st, int64_t t_end, uint64_t limit, uint32_t budget) {
     const uint32_t blocks = (uint32_t)((c->d.R + WG - 1) / WG);
     hipLaunchKernelGGL((tw_run_kernel<LP, WG, NC, TPW>), dim3(blocks), dim3(WG * 64 / TPW), c->lds_bytes, st, c->d, t_end,
                        limit, budget);
 }
 
-extern "C" {
+namespace tw {
 
-const char* tw_version(void) {
-    return "timewarp-mi355x 0.5 (gfx950; lane-per-replica dense/narrow/sparse kernels, wavefront-per-replica kernel, "
-           "node-partitioned LP kernel with device-driven windows, batched logical processes (tw_lpb_load); ABI 2)";
-}
-
-const char* tw_strerror(int code) {
-    switch (code) {
-    case TW_OK: return "ok";
-    case TW_ERR_INVALID: return "invalid argument or scenario descriptor";
-    case TW_ERR_NO_DEVICE: return "no HIP device";
-    case TW_ERR_HIP: return "HIP runtime error";
-    case TW_ERR_OOM: return "device out of memory";
-    case TW_ERR_STATE: return "call out of order";
-    case TW_ERR_REPLICA: return "replica error";
-    case TW_ERR_INCOMPLETE: return "relaunch cap reached before every replica stopped";
-    default: return "unknown error";
-    }
-}
-
-int tw_create(int device, tw_ctx** out) {
+int sh_create(int device, tw_shard** out) {
     if (!out) return TW_ERR_INVALID;
     *out = nullptr;
     int n = 0;
@@ -2873,7 +2921,7 @@ int tw_create(int device, tw_ctx** out) {
         if (hipGetDeviceProperties(&prop, device) != hipSuccess || strncmp(prop.gcnArchName, "gfx950", 6) != 0)
             return TW_ERR_NO_DEVICE;
     }
-    tw_ctx* c = new (std::nothrow) tw_ctx;
+    tw_shard* c = new (std::nothrow) tw_shard;
     if (!c) return TW_ERR_OOM;
     c->device = device;
     if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
@@ -2886,7 +2934,7 @@ int tw_create(int device, tw_ctx** out) {
     return TW_OK;
 }
 
-void tw_destroy(tw_ctx* c) {
+void sh_destroy(tw_shard* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
@@ -2917,7 +2965,7 @@ static int validate(const tw_scenario_desc* s) {
     return TW_OK;
 }
 
-int tw_reset(tw_ctx* c);
+int sh_reset(tw_shard* c);
 
 // Batch class of every resume pc for the wave kernel (wave.hip PC_*): what the
 // code a thread runs from that pc until its next yield may touch.
@@ -2982,7 +3030,7 @@ static void classify_pcs(const tw_scenario_desc* s, std::vector<uint8_t>& cls) {
     }
 }
 
-static int load_common(tw_ctx* c, const tw_scenario_desc* s, bool lp, uint32_t lp_begin, uint32_t lp_count,
+static int load_common(tw_shard* c, const tw_scenario_desc* s, bool lp, uint32_t lp_begin, uint32_t lp_count,
                        int64_t lookahead, uint32_t inbox_cap, uint32_t outbox_cap, bool lpb = false,
                        const uint32_t* node_caps = nullptr) {
     if (!c) return TW_ERR_INVALID;
@@ -3096,7 +3144,8 @@ static int load_common(tw_ctx* c, const tw_scenario_desc* s, bool lp, uint32_t l
     ALLOC(d.free_stk, (size_t)d.S * R);
     ALLOC(d.far, (size_t)d.Q * R);
     ALLOC(d.runs, (size_t)(d.Cr ? TW_RUNS * (size_t)d.Cr : 1) * R);
-    ALLOC(d.near_spill, (size_t)(c->geo == 1 ? TW_NEAR_SPARSE : c->geo == 3 ? wave_spill_entries(d.R) : TW_NEAR_CAP) * R);
+    if (c->geo == 3) d.wave_k = (uint32_t)wave_near_k(d.R);
+    ALLOC(d.near_spill, (size_t)(c->geo == 1 ? TW_NEAR_SPARSE : c->geo == 3 ? wave_spill_entries(d.wave_k) : TW_NEAR_CAP) * R);
     ALLOC(d.dummy, (size_t)TW_DUMMY_REC + R);
     ALLOC(d.nvars, (size_t)d.N * 4 * R);
     ALLOC(d.hash, (size_t)d.N * R);
@@ -3193,7 +3242,7 @@ static int load_common(tw_ctx* c, const tw_scenario_desc* s, bool lp, uint32_t l
         ALLOC(c->n_foreign, 1);
         ALLOC(c->staging, (size_t)d.out_cap * 2);
         ALLOC(c->win_buf, WN_COUNT);  // d.win stays null: the host-driven loop
-        ALLOC(c->red_own, 2);
+        ALLOC(c->red_own, RD_COUNT);
     }
     int64_t *mregs = nullptr, *nvi = nullptr;
     if (s->main_regs && (!lp || lpb)) ALLOC(mregs, (size_t)s->n_replicas * 4);
@@ -3258,25 +3307,25 @@ static int load_common(tw_ctx* c, const tw_scenario_desc* s, bool lp, uint32_t l
     c->nv_init = nvi;
     c->listen_init = lsi;
     c->loaded = true;
-    int rc = tw_reset(c);
+    int rc = sh_reset(c);
     if (rc) return rc;
     HIPCHK(hipStreamSynchronize(st));
     return TW_OK;
 }
 
-int tw_load(tw_ctx* c, const tw_scenario_desc* s) { return load_common(c, s, false, 0, 0, 0, 0, 0); }
+int sh_load(tw_shard* c, const tw_scenario_desc* s) { return load_common(c, s, false, 0, 0, 0, 0, 0); }
 
-int tw_lp_load(tw_ctx* c, const tw_scenario_desc* s, uint32_t lp_begin, uint32_t lp_count, int64_t lookahead_us,
+int sh_lp_load(tw_shard* c, const tw_scenario_desc* s, uint32_t lp_begin, uint32_t lp_count, int64_t lookahead_us,
                uint32_t inbox_cap, uint32_t outbox_cap) {
     return load_common(c, s, true, lp_begin, lp_count, lookahead_us, inbox_cap, outbox_cap);
 }
 
-int tw_lpb_load(tw_ctx* c, const tw_scenario_desc* s, int64_t lookahead_us, const uint32_t* node_inbox_cap,
+int sh_lpb_load(tw_shard* c, const tw_scenario_desc* s, int64_t lookahead_us, const uint32_t* node_inbox_cap,
                 uint32_t inbox_cap, uint32_t outbox_cap) {
     return load_common(c, s, true, 0, 0, lookahead_us, inbox_cap, outbox_cap, true, node_inbox_cap);
 }
 
-int tw_reset(tw_ctx* c) {
+int sh_reset(tw_shard* c) {
     if (!c) return TW_ERR_INVALID;
     if (!c->loaded) return TW_ERR_STATE;
     HIPCHK(hipSetDevice(c->device));
@@ -3309,9 +3358,9 @@ int tw_reset(tw_ctx* c) {
 }
 
 
-static int lpb_run(tw_ctx* c, tw_stats* out);
+static int lpb_run(tw_shard* c, tw_stats* out);
 
-int tw_run(tw_ctx* c, int64_t t_end_us, uint64_t max_events, tw_stats* out) {
+int sh_run(tw_shard* c, int64_t t_end_us, uint64_t max_events, tw_stats* out) {
     if (!c) return TW_ERR_INVALID;
     if (!c->loaded) return TW_ERR_STATE;
     if (c->lpb) {
@@ -3389,7 +3438,7 @@ int tw_run(tw_ctx* c, int64_t t_end_us, uint64_t max_events, tw_stats* out) {
     if (out) {
         std::memset(out, 0, sizeof(*out));
         std::vector<tw_replica_result> rr(d.R);
-        int rc = tw_read_results(c, rr.data(), d.R);
+        int rc = sh_read_results(c, rr.data(), d.R);
         if (rc) return rc;
         for (uint32_t i = 0; i < d.R; ++i) {
             out->events += rr[i].events - ev0[i];
@@ -3408,7 +3457,7 @@ int tw_run(tw_ctx* c, int64_t t_end_us, uint64_t max_events, tw_stats* out) {
     return quiet ? TW_OK : TW_ERR_INCOMPLETE;
 }
 
-int tw_read_results(tw_ctx* c, tw_replica_result* out, size_t n) {
+int sh_read_results(tw_shard* c, tw_replica_result* out, size_t n) {
     if (!c || !out) return TW_ERR_INVALID;
     if (!c->loaded) return TW_ERR_STATE;
     const Dev& d = c->d;
@@ -3448,7 +3497,7 @@ int tw_read_results(tw_ctx* c, tw_replica_result* out, size_t n) {
     return TW_OK;
 }
 
-static int digest(tw_ctx* c, std::vector<uint64_t>& h) {
+static int digest(tw_shard* c, std::vector<uint64_t>& h) {
     const Dev& d = c->d;
     uint64_t* dd = nullptr;
     HIPCHK(hipMallocAsync((void**)&dd, 8ull * d.R, c->stream));
@@ -3461,7 +3510,7 @@ static int digest(tw_ctx* c, std::vector<uint64_t>& h) {
     return TW_OK;
 }
 
-int tw_tie_audit(tw_ctx* c, int64_t t_end_us, uint64_t max_events, uint32_t probes, tw_stats* out) {
+int sh_tie_audit(tw_shard* c, int64_t t_end_us, uint64_t max_events, uint32_t probes, tw_stats* out) {
     if (!c) return TW_ERR_INVALID;
     if (!c->loaded) return TW_ERR_STATE;
     if (c->lp || probes < 1 || probes > 2) return TW_ERR_INVALID;
@@ -3470,8 +3519,8 @@ int tw_tie_audit(tw_ctx* c, int64_t t_end_us, uint64_t max_events, uint32_t prob
     int rc = TW_OK;
     for (uint32_t p = probes; p + 1 > 0 && rc == TW_OK; --p) {  // probes first, the canonical run last
         c->d.tie_mode = p;
-        rc = tw_reset(c);
-        if (rc == TW_OK) rc = tw_run(c, t_end_us, max_events, p == 0 ? out : nullptr);
+        rc = sh_reset(c);
+        if (rc == TW_OK) rc = sh_run(c, t_end_us, max_events, p == 0 ? out : nullptr);
         if (rc == TW_OK) rc = digest(c, dg[p]);
         if (p == 0) break;
     }
@@ -3484,20 +3533,20 @@ int tw_tie_audit(tw_ctx* c, int64_t t_end_us, uint64_t max_events, uint32_t prob
     return TW_OK;
 }
 
-int tw_geometry(tw_ctx* c) {
+int sh_geometry(tw_shard* c) {
     if (!c) return TW_ERR_INVALID;
     if (!c->loaded) return TW_ERR_STATE;
     return c->lpb ? TW_GEO_LPB : c->lp ? TW_GEO_LP : c->geo;
 }
 
-int tw_set_counter_base(tw_ctx* c, uint32_t seq0, uint32_t tid0) {
+int sh_set_counter_base(tw_shard* c, uint32_t seq0, uint32_t tid0) {
     if (!c || tid0 == 0) return TW_ERR_INVALID;
     c->seq0 = seq0;
     c->tid0 = tid0;
     return TW_OK;
 }
 
-int tw_read_hashes(tw_ctx* c, uint64_t* out, size_t n) {
+int sh_read_hashes(tw_shard* c, uint64_t* out, size_t n) {
     if (!c || !out) return TW_ERR_INVALID;
     if (!c->loaded) return TW_ERR_STATE;
     const Dev& d = c->d;
@@ -3519,26 +3568,7 @@ int tw_read_hashes(tw_ctx* c, uint64_t* out, size_t n) {
     return TW_OK;
 }
 
-int tw_read_final(tw_ctx* c, int64_t* max_final_t, uint64_t* delivered, uint64_t* dropped, uint64_t* events) {
-    if (!c) return TW_ERR_INVALID;
-    if (!c->loaded) return TW_ERR_STATE;
-    std::vector<tw_replica_result> rr(c->d.R);
-    int rc = tw_read_results(c, rr.data(), rr.size());
-    if (rc) return rc;
-    int64_t ft = 0;
-    uint64_t dl = 0, dr = 0, ev = 0;
-    for (auto& x : rr) {
-        ft = x.final_t > ft ? x.final_t : ft;
-        dl += x.delivered; dr += x.dropped; ev += x.events;
-    }
-    if (max_final_t) *max_final_t = ft;
-    if (delivered) *delivered = dl;
-    if (dropped) *dropped = dr;
-    if (events) *events = ev;
-    return TW_OK;
-}
-
-static int lp_scatter(tw_ctx* c, const uint4* recs, uint32_t n, bool to_foreign) {
+static int lp_scatter(tw_shard* c, const uint4* recs, uint32_t n, bool to_foreign) {
     const Dev& d = c->d;
     if (n == 0) return TW_OK;
     uint32_t blocks = (n + 255) / 256;
@@ -3548,11 +3578,11 @@ static int lp_scatter(tw_ctx* c, const uint4* recs, uint32_t n, bool to_foreign)
     return TW_OK;
 }
 
-int tw_lp_window(tw_ctx* c, int64_t t_end_excl, int64_t* next_t, uint64_t* n_foreign) {
+int sh_lp_window(tw_shard* c, int64_t t_end_excl, int64_t* next_t, uint64_t* n_foreign) {
     if (!c || !next_t) return TW_ERR_INVALID;
     if (!c->loaded || !c->lp) return TW_ERR_STATE;
     tw_stats st{};
-    int rc = tw_run(c, t_end_excl - 1, UINT64_MAX, nullptr);
+    int rc = sh_run(c, t_end_excl - 1, UINT64_MAX, nullptr);
     if (rc) return rc;
     (void)st;
     const Dev& d = c->d;
@@ -3576,7 +3606,7 @@ int tw_lp_window(tw_ctx* c, int64_t t_end_excl, int64_t* next_t, uint64_t* n_for
     return TW_OK;
 }
 
-int tw_lp_take_outbox(tw_ctx* c, tw_lp_record* out, size_t cap, size_t* n) {
+int sh_lp_take_outbox(tw_shard* c, tw_lp_record* out, size_t cap, size_t* n) {
     if (!c || !n) return TW_ERR_INVALID;
     if (!c->loaded || !c->lp) return TW_ERR_STATE;
     hipStream_t s = c->stream;
@@ -3591,7 +3621,7 @@ int tw_lp_take_outbox(tw_ctx* c, tw_lp_record* out, size_t cap, size_t* n) {
     return TW_OK;
 }
 
-int tw_lp_inject(tw_ctx* c, const tw_lp_record* recs, size_t n, int64_t* next_t) {
+int sh_lp_inject(tw_shard* c, const tw_lp_record* recs, size_t n, int64_t* next_t) {
     if (!c || (n && !recs)) return TW_ERR_INVALID;
     if (!c->loaded || !c->lp) return TW_ERR_STATE;
     const Dev& d = c->d;
@@ -3612,12 +3642,12 @@ int tw_lp_inject(tw_ctx* c, const tw_lp_record* recs, size_t n, int64_t* next_t)
     return TW_OK;
 }
 
-int tw_lp_results(tw_ctx* c, tw_replica_result* agg, uint64_t* node_hashes, size_t n_nodes) {
+int sh_lp_results(tw_shard* c, tw_replica_result* agg, uint64_t* node_hashes, size_t n_nodes) {
     if (!c || !agg) return TW_ERR_INVALID;
     if (!c->loaded || !c->lp) return TW_ERR_STATE;
     const Dev& d = c->d;
     std::vector<tw_replica_result> rr(d.R);
-    int rc = tw_read_results(c, rr.data(), rr.size());
+    int rc = sh_read_results(c, rr.data(), rr.size());
     if (rc) return rc;
     std::memset(agg, 0, sizeof(*agg));
     agg->status = TW_REP_DONE;
@@ -3636,7 +3666,7 @@ int tw_lp_results(tw_ctx* c, tw_replica_result* agg, uint64_t* node_hashes, size
     return TW_OK;
 }
 
-int tw_set_stream(tw_ctx* c, void* hs) {
+int sh_set_stream(tw_shard* c, void* hs) {
     if (!c) return TW_ERR_INVALID;
     HIPCHK(hipSetDevice(c->device));
     HIPCHK(hipStreamSynchronize(c->stream));  // finish what was queued on the old one
@@ -3644,25 +3674,52 @@ int tw_set_stream(tw_ctx* c, void* hs) {
     return TW_OK;
 }
 
-int tw_lp_exchange_setup(tw_ctx* c, uint32_t world, uint32_t rank, const uint32_t* starts, void* send, void* recv,
-                         uint32_t cap, int64_t* red) {
+// The exchange of the device loop over `world` ranks; this shard is `rank`,
+// owning nodes [starts[rank], starts[rank + 1]).  send/recv: world blocks of
+// (cap + 1) records (header + records); red: RD_COUNT int64.  Also sizes the
+// carry buffer (records beyond a tick's block size wait there).
+static int exchange_common(tw_shard* c, uint32_t world, uint32_t rank, const uint32_t* starts, uint32_t cap) {
     if (!c || world == 0 || rank >= world || !starts) return TW_ERR_INVALID;
     if (!c->loaded || !c->lp) return TW_ERR_STATE;
-    if (world > 1 && (!send || !recv || !red || cap == 0)) return TW_ERR_INVALID;
+    if (world > 1 && cap == 0) return TW_ERR_INVALID;
     for (uint32_t g = 0; g < world; ++g)
         if (starts[g] > starts[g + 1]) return TW_ERR_INVALID;
     if (starts[rank] != c->d.lp0 || starts[rank + 1] != c->d.lp0 + c->d.R) return TW_ERR_INVALID;
     HIPCHK(hipSetDevice(c->device));
-    if (c->ex_starts) {
-        HIPCHK(hipStreamSynchronize(c->stream));
-        HIPCHK(hipFree(c->ex_starts));
-        c->ex_starts = nullptr;
-    }
+    HIPCHK(hipStreamSynchronize(c->stream));
+    if (c->ex_starts) HIPCHK(hipFree(c->ex_starts));
+    if (c->ex_carry) HIPCHK(hipFree(c->ex_carry));
+    c->ex_starts = nullptr;
+    c->ex_carry = nullptr;
+    c->d.carry = nullptr;
+    c->d.carry_n = nullptr;
+    c->d.carry_cap = 0;
     HIPCHK(hipMalloc((void**)&c->ex_starts, 4ull * (world + 1)));
     HIPCHK(hipMemcpy(c->ex_starts, starts, 4ull * (world + 1), hipMemcpyHostToDevice));
+    if (world > 1) {
+        // a tick's foreign records beyond the block size: at most a tick's outbox
+        const uint32_t cc = c->d.out_cap < (1u << 20) ? c->d.out_cap : (1u << 20);
+        const size_t bytes = 2ull * cc * 32 + 256;
+        HIPCHK(hipMalloc(&c->ex_carry, bytes));
+        HIPCHK(hipMemsetAsync(c->ex_carry, 0, bytes, c->stream));
+        c->d.carry_n = (uint32_t*)c->ex_carry;
+        c->d.carry = (uint4*)((char*)c->ex_carry + 256);
+        c->d.carry_cap = cc;
+    }
     c->ex_world = world;
     c->ex_rank = rank;
-    c->ex_cap = world > 1 ? cap : 0;
+    c->ex_cap = cap;
+    c->ex_cap_eff = c->ex_cap;
+    return TW_OK;
+}
+
+int sh_lp_exchange_setup(tw_shard* c, uint32_t world, uint32_t rank, const uint32_t* starts, void* send, void* recv,
+                         uint32_t cap, int64_t* red) {
+    if (c && world > 1 && (!send || !recv || !red)) return TW_ERR_INVALID;
+    int rc = exchange_common(c, world, rank, starts, cap);
+    if (rc) return rc;
+    if (c->ex_own) HIPCHK(hipFree(c->ex_own));
+    c->ex_own = nullptr;
     c->ex_send = world > 1 ? (uint4*)send : nullptr;
     c->ex_recv = world > 1 ? (uint4*)recv : nullptr;
     c->ex_red = world > 1 ? red : c->red_own;
@@ -3670,7 +3727,49 @@ int tw_lp_exchange_setup(tw_ctx* c, uint32_t world, uint32_t rank, const uint32_
     return TW_OK;
 }
 
-int tw_lp_loop_begin(tw_ctx* c) {
+// The same with library-owned buffers (the library-driven loop of abi.hip:
+// RCCL send/recv or device copies between shards move the blocks).
+int sh_lp_exchange_own(tw_shard* c, uint32_t world, uint32_t rank, const uint32_t* starts, uint32_t cap) {
+    int rc = exchange_common(c, world, rank, starts, world > 1 ? cap : 1u);
+    if (rc) return rc;
+    if (c->ex_own) HIPCHK(hipFree(c->ex_own));
+    c->ex_own = nullptr;
+    const size_t blk = 32ull * world * ((size_t)c->ex_cap + 1);
+    HIPCHK(hipMalloc(&c->ex_own, 2 * blk + 8ull * RD_COUNT));
+    HIPCHK(hipMemsetAsync(c->ex_own, 0, 2 * blk + 8ull * RD_COUNT, c->stream));
+    // (one rank too: its import, fill and the all-reduce of the words then go
+    // through the transport -- a one-rank RCCL communicator -- like any rank's)
+    c->ex_send = (uint4*)c->ex_own;
+    c->ex_recv = (uint4*)((char*)c->ex_own + blk);
+    c->ex_red = (int64_t*)((char*)c->ex_own + 2 * blk);
+    return TW_OK;
+}
+
+void sh_lp_exchange_info(tw_shard* c, ShardXchg* x) {
+    x->device = c->device;
+    x->stream = c->stream;
+    x->send = c->ex_send;
+    x->recv = c->ex_recv;
+    x->red = c->ex_red;
+    x->world = c->ex_world;
+    x->stride = c->ex_cap;
+    x->cap_eff = c->ex_cap_eff;
+}
+int sh_lp_set_block(tw_shard* c, uint32_t cap_eff) {
+    if (!c || cap_eff == 0 || cap_eff > c->ex_cap) return TW_ERR_INVALID;
+    c->ex_cap_eff = cap_eff;
+    return TW_OK;
+}
+// WN_XMAX after a tw_lp_progress (the largest per-rank demand of one tick since
+// the last clear); clear it on the device (stream-ordered)
+int64_t sh_lp_xmax(tw_shard* c) { return c->h_win ? c->h_win[WN_XMAX] : 0; }
+int sh_lp_clear_xmax(tw_shard* c) {
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipMemsetAsync(c->win_buf + WN_XMAX, 0, 8, c->stream));
+    return TW_OK;
+}
+
+int sh_lp_loop_begin(tw_shard* c) {
     if (!c) return TW_ERR_INVALID;
     if (!c->loaded || !c->lp) return TW_ERR_STATE;
     if (const char* b = getenv("TW_LP_TICK_BUDGET")) {
@@ -3699,7 +3798,7 @@ static uint32_t lp_grid(uint32_t n) {
     return b < 1 ? 1 : b > 2048 ? 2048 : b;
 }
 
-int tw_lp_tick(tw_ctx* c) {
+int sh_lp_tick(tw_shard* c) {
     if (!c) return TW_ERR_INVALID;
     if (!c->loaded || !c->lp || !c->loop_ready) return TW_ERR_STATE;
     HIPCHK(hipSetDevice(c->device));
@@ -3712,34 +3811,35 @@ int tw_lp_tick(tw_ctx* c) {
     c->d.win = nullptr;
     HIPCHK(hipGetLastError());
     hipLaunchKernelGGL(tw_lp_pack, dim3(lp_grid(d.out_cap)), dim3(256), 0, st, d, c->ex_send,
-                       (const uint32_t*)c->ex_starts, c->ex_world, c->ex_cap);
+                       (const uint32_t*)c->ex_starts, c->ex_world, c->ex_cap, c->ex_cap_eff);
     HIPCHK(hipGetLastError());
     return TW_OK;
 }
 
-int tw_lp_tick_import(tw_ctx* c) {
+int sh_lp_tick_import(tw_shard* c) {
     if (!c) return TW_ERR_INVALID;
     if (!c->loaded || !c->lp || !c->loop_ready) return TW_ERR_STATE;
     HIPCHK(hipSetDevice(c->device));
     hipStream_t st = c->stream;
-    if (c->ex_world > 1) {
-        hipLaunchKernelGGL(tw_lp_import, dim3(lp_grid(c->ex_world * c->ex_cap)), dim3(256), 0, st, c->dwin(),
-                           (const uint4*)c->ex_recv, c->ex_world, c->ex_cap);
+    // (no exchange buffers -- one rank of a caller-driven loop: tw_lp_ctl
+    // fills the words itself)
+    if (c->ex_send) {
+        hipLaunchKernelGGL(tw_lp_import, dim3(lp_grid(c->ex_world * c->ex_cap_eff)), dim3(256), 0, st, c->dwin(),
+                           (const uint4*)c->ex_recv, c->ex_world, c->ex_cap, c->ex_cap_eff);
         HIPCHK(hipGetLastError());
-    }
-    if (c->ex_world > 1) {  // (one rank: tw_lp_ctl fills the words itself)
-        hipLaunchKernelGGL(tw_lp_fill, dim3(1), dim3(1), 0, st, c->dwin(), c->ex_red);
+        hipLaunchKernelGGL(tw_lp_fill, dim3(1), dim3(1), 0, st, c->dwin(), c->ex_red, (const uint4*)c->ex_send,
+                           c->ex_world, c->ex_cap);
         HIPCHK(hipGetLastError());
     }
     return TW_OK;
 }
 
-int tw_lp_tick_end(tw_ctx* c) {
+int sh_lp_tick_end(tw_shard* c) {
     if (!c) return TW_ERR_INVALID;
     if (!c->loaded || !c->lp || !c->loop_ready) return TW_ERR_STATE;
     HIPCHK(hipSetDevice(c->device));
     hipLaunchKernelGGL(tw_lp_ctl, dim3(1), dim3(1), 0, c->stream, c->dwin(), c->ex_red, c->ex_send, c->ex_world,
-                       c->ex_cap);
+                       c->ex_cap, c->ex_send ? 1u : 0u);
     HIPCHK(hipGetLastError());
     if (c->heavy_ok) {
         hipLaunchKernelGGL(tw_lp_due, dim3(TW_DUE_GRID), dim3(256), 0, c->stream, c->dwin());
@@ -3750,7 +3850,7 @@ int tw_lp_tick_end(tw_ctx* c) {
     return TW_OK;
 }
 
-int tw_lp_progress(tw_ctx* c, tw_lp_state* out) {
+int sh_lp_progress(tw_shard* c, tw_lp_state* out) {
     if (!c || !out) return TW_ERR_INVALID;
     if (!c->loaded || !c->lp || !c->loop_ready) return TW_ERR_STATE;
     HIPCHK(hipSetDevice(c->device));
@@ -3769,20 +3869,20 @@ int tw_lp_progress(tw_ctx* c, tw_lp_state* out) {
     return TW_OK;
 }
 
-int tw_lp_run_windows(tw_ctx* c, uint64_t max_ticks, tw_lp_state* out) {
+int sh_lp_run_windows(tw_shard* c, uint64_t max_ticks, tw_lp_state* out) {
     if (!c || !out) return TW_ERR_INVALID;
     if (!c->loaded || !c->lp || !c->loop_ready) return TW_ERR_STATE;
     if (c->ex_world != 1) return TW_ERR_STATE;
     for (uint64_t done_ticks = 0; done_ticks < max_ticks;) {
         const uint64_t batch = max_ticks - done_ticks < 16 ? max_ticks - done_ticks : 16;
         for (uint64_t i = 0; i < batch; ++i) {
-            int rc = tw_lp_tick(c);
-            if (!rc) rc = tw_lp_tick_import(c);
-            if (!rc) rc = tw_lp_tick_end(c);
+            int rc = sh_lp_tick(c);
+            if (!rc) rc = sh_lp_tick_import(c);
+            if (!rc) rc = sh_lp_tick_end(c);
             if (rc) return rc;
         }
         done_ticks += batch;
-        int rc = tw_lp_progress(c, out);
+        int rc = sh_lp_progress(c, out);
         if (rc) return rc;
         if (out->err) return TW_ERR_REPLICA;
         if (out->done) return TW_OK;
@@ -3791,12 +3891,12 @@ int tw_lp_run_windows(tw_ctx* c, uint64_t max_ticks, tw_lp_state* out) {
 }
 
 // Batched LP: tw_run = the whole device window loop (one host sync per 16 ticks)
-static int lpb_run(tw_ctx* c, tw_stats* out) {
+static int lpb_run(tw_shard* c, tw_stats* out) {
     auto w0 = std::chrono::steady_clock::now();
     std::vector<tw_replica_result> before;
     if (out) {
         before.resize(c->n_rep);
-        int rc = tw_read_results(c, before.data(), before.size());
+        int rc = sh_read_results(c, before.data(), before.size());
         if (rc) return rc;
     }
     while (c->ev_pool.size() < 2) {
@@ -3804,11 +3904,11 @@ static int lpb_run(tw_ctx* c, tw_stats* out) {
         HIPCHK(hipEventCreate(&e));
         c->ev_pool.push_back(e);
     }
-    int rc = tw_lp_loop_begin(c);
+    int rc = sh_lp_loop_begin(c);
     if (rc) return rc;
     HIPCHK(hipEventRecord(c->ev_pool[0], c->stream));
     tw_lp_state ls{};
-    rc = tw_lp_run_windows(c, 1ull << 40, &ls);
+    rc = sh_lp_run_windows(c, 1ull << 40, &ls);
     HIPCHK(hipEventRecord(c->ev_pool[1], c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
     float ms = 0.f;
@@ -3820,7 +3920,7 @@ static int lpb_run(tw_ctx* c, tw_stats* out) {
     if (out) {
         std::memset(out, 0, sizeof(*out));
         std::vector<tw_replica_result> rr(c->n_rep);
-        rc = tw_read_results(c, rr.data(), rr.size());
+        rc = sh_read_results(c, rr.data(), rr.size());
         if (rc) return rc;
         for (uint32_t i = 0; i < c->n_rep; ++i) {
             out->events += rr[i].events - before[i].events;
@@ -3839,7 +3939,7 @@ static int lpb_run(tw_ctx* c, tw_stats* out) {
     return TW_OK;
 }
 
-int tw_lpb_windows(tw_ctx* c, uint64_t* windows, uint64_t* ticks) {
+int sh_lpb_windows(tw_shard* c, uint64_t* windows, uint64_t* ticks) {
     if (!c) return TW_ERR_INVALID;
     if (!c->loaded || !c->lpb) return TW_ERR_STATE;
     if (windows) *windows = c->lpb_windows;
@@ -3847,18 +3947,28 @@ int tw_lpb_windows(tw_ctx* c, uint64_t* windows, uint64_t* ticks) {
     return TW_OK;
 }
 
+// Diagnostic build only (-DTW_STATS): copy the P_COUNT counters out,
+// optionally zeroing them; the product build has none (TW_ERR_STATE).
+int sh_prof_read(tw_shard* c, unsigned long long* out, size_t cap, int reset) {
 #ifdef TW_STATS
-// Diagnostic build only: copy the P_COUNT counters out, optionally zeroing them.
-int tw_prof_read(tw_ctx* c, unsigned long long* out, size_t cap, int reset) {
     if (!c || !out || !c->loaded || !c->d.prof) return TW_ERR_STATE;
     size_t n = cap < (size_t)P_COUNT ? cap : (size_t)P_COUNT;
+    HIPCHK(hipSetDevice(c->device));
     HIPCHK(hipMemcpy(out, c->d.prof, 8 * n, hipMemcpyDeviceToHost));
     if (reset) HIPCHK(hipMemset(c->d.prof, 0, 8 * P_COUNT));
     return (int)n;
-}
+#else
+    (void)c; (void)out; (void)cap; (void)reset;
+    return TW_ERR_STATE;
 #endif
+}
 
-int tw_set_trace(tw_ctx* c, uint32_t cap) {
+uint32_t sh_replicas(tw_shard* c) { return c->lpb ? c->n_rep : c->d.R; }
+uint32_t sh_nodes(tw_shard* c) { return c->lpb ? c->d.Ntot : c->d.N; }
+bool sh_is_lp(tw_shard* c) { return c->lp; }
+int sh_device(tw_shard* c) { return c->device; }
+
+int sh_set_trace(tw_shard* c, uint32_t cap) {
     if (!c) return TW_ERR_INVALID;
     if (!c->loaded) return TW_ERR_STATE;
     if (c->lp) return TW_ERR_INVALID;  // LP lanes are nodes: no replica execution order to record
@@ -3876,7 +3986,7 @@ int tw_set_trace(tw_ctx* c, uint32_t cap) {
     return TW_OK;
 }
 
-int tw_read_trace(tw_ctx* c, uint32_t replica, tw_trace_rec* out, size_t cap, uint64_t* n_emitted) {
+int sh_read_trace(tw_shard* c, uint32_t replica, tw_trace_rec* out, size_t cap, uint64_t* n_emitted) {
     if (!c || (cap && !out)) return TW_ERR_INVALID;
     if (!c->loaded) return TW_ERR_STATE;
     const Dev& d = c->d;
@@ -3905,11 +4015,11 @@ int tw_read_trace(tw_ctx* c, uint32_t replica, tw_trace_rec* out, size_t cap, ui
     return TW_OK;
 }
 
-int tw_last_launch_ms(tw_ctx* c, double* out, size_t cap) {
+int sh_last_launch_ms(tw_shard* c, double* out, size_t cap) {
     if (!c || !out) return TW_ERR_INVALID;
     size_t n = c->launch_ms.size() < cap ? c->launch_ms.size() : cap;
     for (size_t i = 0; i < n; ++i) out[i] = c->launch_ms[i];
     return (int)n;
 }
 
-}  // extern "C"
+}  // namespace tw

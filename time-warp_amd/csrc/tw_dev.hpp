@@ -141,6 +141,12 @@ struct Dev {
     // after every phase-0 node has finished the window; null = one phase
     const uint8_t* phase;  // [Ntot]
     uint32_t has_ph1;
+    // exchange carry (device loop): foreign records beyond this tick's block
+    // size wait here for the next tick (the window reruns until none is left):
+    // [2][carry_cap][2], buffer (ticks & 1) written, the other one read
+    uint4* carry;
+    uint32_t* carry_n;   // [2]
+    uint32_t carry_cap;
     uint4* outbox;       // [out_cap][2] records produced this window
     uint32_t* out_n;     // [1]
     uint64_t* next_t;    // [1] min next-event time (atomicMin)
@@ -171,6 +177,7 @@ struct Dev {
     const uint64_t* link_bw;    // [L] or null
     uint32_t tie_mode;          // TW_TIE_*: order of equal-timestamp events
     const uint8_t* pc_cls;      // [n_insns + 1] wave kernel: batch class of each resume pc (classify_pcs)
+    uint32_t wave_k;            // wave kernel: near-queue entries per lane (4, 24 or 32), fixed by tw_load
 };
 
 // The key an insertion counter value takes in the queues (equal timestamps pop
@@ -192,8 +199,13 @@ __device__ __forceinline__ int64_t tx_us(const Dev& c, uint64_t link, uint32_t k
 }
 
 // LP device-driven window words (Dev::win)
+// WN_XMAX: the largest per-rank record demand of one tick since the host last
+// cleared it (from the all-reduced words, so identical on every rank: the
+// ranks agree on the next exchange block size without talking)
 enum { WN_T, WN_L, WN_REC_MIN, WN_WINDOWS, WN_TICKS, WN_FLAGS, WN_ACT, WN_WID, WN_PHASE, WN_NT0, WN_SPN_MIN,
-       WN_SLEEP_MIN, WN_COUNT };
+       WN_SLEEP_MIN, WN_XMAX, WN_COUNT };
+// reduction words of the device loop (all-reduced with MIN between ranks)
+enum { RD_NEXT, RD_ACTIVE, RD_ERR, RD_DEMAND, RD_COUNT };
 // spawn record markers in the kind field of an outbox entry pair (message kinds are < 256)
 #define TW_SPAWN_KIND 0xFFFFFFFFu
 #define TW_SPAWN_CONT 0xFFFFFFFEu
@@ -277,8 +289,8 @@ __device__ __forceinline__ void atom_add64(unsigned long long GAS* p, uint64_t v
 }
 
 // wave.hip: the wave-per-replica kernel (geometry TW_GEO_WAVE)
-int wave_near_k(uint32_t R);                // near-queue entries per lane it uses for R replicas
-size_t wave_spill_entries(uint32_t R);      // near-queue spill entries per replica
+int wave_near_k(uint32_t R);                // near-queue entries per lane (K) for R replicas (tw_load)
+size_t wave_spill_entries(uint32_t K);      // near-queue spill entries per replica
 hipError_t wave_launch(const Dev& d, const Dev* d_dev, hipStream_t st, int64_t t_end, uint64_t limit,
                        uint32_t budget);
 

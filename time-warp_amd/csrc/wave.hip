@@ -26,6 +26,8 @@
 //     heap in HBM, laid out per replica (one replica's far queue is contiguous);
 //   * many replicas per SIMD (up to 8 waves) hide the remaining HBM latency of
 //     thread records and node state.
+#include <cstdlib>
+
 #include "tw_dev.hpp"
 
 #define TW_STEP_CAP (1u << 22)  // instructions per thread step (== oracle kStepCap, engine.hip)
@@ -220,6 +222,13 @@ struct Wave {
     __device__ __forceinline__ void near_push(int64_t t, uint32_t sq, uint32_t slot) {
         const uint64_t key = ((uint64_t)(t - nbase) << 32) | sq;
         uint64_t room = __builtin_amdgcn_ballot_w64(lcnt < (uint32_t)K);
+        if (room == 0) {
+            // the lanes' counts disagree with near_n (near_fits let the push
+            // through): a broken invariant, reported as a queue error status
+            // instead of an entry silently dropped (ctz of an empty ballot)
+            fail(TW_REP_ERR_QUEUE);
+            return;
+        }
         room = (room >> rot) | (rot ? room << (64 - rot) : 0ull);  // rotate right by rot
         const uint32_t tl = (rfl((uint32_t)__builtin_ctzll(room)) + rot) & 63u;
         rot = (tl + 1) & 63u;
@@ -240,7 +249,12 @@ struct Wave {
     }
     // remove the minimum (key gmin); returns its slot
     __device__ __forceinline__ uint32_t near_pop() {
-        const uint32_t wl = rfl((uint32_t)__builtin_ctzll(__builtin_amdgcn_ballot_w64(lmk == gmin)));
+        const uint64_t hold = __builtin_amdgcn_ballot_w64(lmk == gmin);
+        if (hold == 0) {  // no lane holds the minimum: a broken invariant, a status (the caller stops)
+            fail(TW_REP_ERR_QUEUE);
+            return 0;
+        }
+        const uint32_t wl = rfl((uint32_t)__builtin_ctzll(hold));
         uint32_t s = 0;
         const bool me = lane == wl;
 #pragma unroll
@@ -875,6 +889,7 @@ __global__ void __launch_bounds__(64) tw_wave_kernel(const Dev* dptr, int64_t t_
                 else W.run_pop(src);
             } else {
                 slot = W.near_pop();
+                if (W.status != TW_REP_RUNNING) break;
             }
             urec_load(W.hrec(slot), dv->RQ, th);
             if (th.w3 != sq) continue;  // superseded by a throwTo re-stamp
@@ -950,28 +965,34 @@ __global__ void __launch_bounds__(64) tw_wave_kernel(const Dev* dptr, int64_t t_
 
 }  // namespace
 
-// near-queue entries per lane for few replicas (<= 4096)
-#ifndef TW_WAVE_K_FEW
-#define TW_WAVE_K_FEW 32
-#endif
-// Host launcher (engine.hip's tw_run): one 64-lane workgroup per replica.
+// near-queue entries per lane (K): 32 for few replicas (<= 4096: C5's
+// hotspot receiver keeps 1-2k events on chip), else 4; TW_WAVE_K=4|24|32
+// overrides (tests run the tie-audit and random-program cases under each)
 int wave_near_k(uint32_t R) {
-    // registers per lane hold K queue entries: few replicas per SIMD leave
-    // room for a deep on-chip queue (C5's hotspot receiver keeps 1-2k events)
-    return R <= 4096 ? TW_WAVE_K_FEW : 4;
+    if (const char* k = getenv("TW_WAVE_K")) {
+        const int v = atoi(k);
+        if (v == 4 || v == 24 || v == 32) return v;
+    }
+    return R <= 4096 ? 32 : 4;
 }
-size_t wave_spill_entries(uint32_t R) { return 64u * (size_t)wave_near_k(R); }
+size_t wave_spill_entries(uint32_t K) { return 64u * (size_t)K; }
 
+// Host launcher (engine.hip's tw_run): one 64-lane workgroup per replica;
+// K is the one tw_load chose (Dev::wave_k: the spill area is sized for it).
 hipError_t wave_launch(const Dev& d, const Dev* d_dev, hipStream_t st, int64_t t_end, uint64_t limit,
                        uint32_t budget) {
     // the kernel reads the context from device memory (scalar loads on use),
     // not from kernel arguments held in scalar registers for the whole launch
     hipError_t e = hipMemcpyAsync((void*)d_dev, &d, sizeof(Dev), hipMemcpyHostToDevice, st);
     if (e != hipSuccess) return e;
-    if (wave_near_k(d.R) == TW_WAVE_K_FEW)
-        hipLaunchKernelGGL((tw_wave_kernel<TW_WAVE_K_FEW>), dim3(d.R), dim3(64), 0, st, d_dev, t_end, limit, budget);
-    else
+    if (d.wave_k == 32)
+        hipLaunchKernelGGL((tw_wave_kernel<32>), dim3(d.R), dim3(64), 0, st, d_dev, t_end, limit, budget);
+    else if (d.wave_k == 24)
+        hipLaunchKernelGGL((tw_wave_kernel<24>), dim3(d.R), dim3(64), 0, st, d_dev, t_end, limit, budget);
+    else if (d.wave_k == 4)
         hipLaunchKernelGGL((tw_wave_kernel<4>), dim3(d.R), dim3(64), 0, st, d_dev, t_end, limit, budget);
+    else
+        return hipErrorInvalidValue;
     return hipGetLastError();
 }
 

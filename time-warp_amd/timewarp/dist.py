@@ -1,12 +1,20 @@
 """Replica sharding across GPUs (one process per GPU, torch.distributed).
 
 Replicas are independent runTimedT calls, so the only cross-GPU traffic is the
-statistics reduction (RCCL all-reduce over xGMI with the "nccl" backend, or
-gloo on CPU): there is no data-path collective.
+statistics reduction: there is no data-path collective.  The collectives of
+the product path belong to the library (include/timewarp.h tw_create_rank):
+`library_comm` only hands rank 0's RCCL job id to every rank; tw_run then
+all-reduces its statistics and tw_lp_run exchanges a node-partitioned
+scenario's records over the library's own RCCL communicator.  The
+torch.distributed helpers below remain the thin caller-side pieces (the
+barrier and elapsed-time max of bench.py) and the caller-driven window loops,
+which the gloo tests exercise on CPU.
 
-Weak scaling (the default of bench.py): rank g owns the global replicas
-[g*R, (g+1)*R) and draws their link tables from mkStdGen(g*R + i), so the
-union over ranks is bit-identical to one process running all world*R replicas.
+Strong scaling (the default of bench.py, BASELINE config 3): one batch of R
+replicas is split into contiguous blocks, rank g owning [g*R/G, (g+1)*R/G)
+(strong_block) and drawing their link tables from mkStdGen(global replica
+id), so the union over ranks is bit-identical to one process running all R
+replicas.  `bench.py --weak` keeps R replicas per rank instead (weak_block).
 """
 from __future__ import annotations
 
@@ -28,6 +36,19 @@ def strong_block(total: int, world: int, rank: int) -> Tuple[int, int]:
     base, rem = divmod(total, world)
     r0 = rank * base + min(rank, rem)
     return r0, r0 + base + (1 if rank < rem else 0)
+
+
+def library_comm(world: int, rank: int):
+    """(nranks, rank, job id) for Engine(comm=...): rank 0 makes the RCCL job
+    id (tw_comm_id) and torch.distributed broadcasts it; the library then
+    creates and owns the communicator (ncclCommInitRank)."""
+    import torch.distributed as dist
+
+    from .engine import comm_id
+
+    box = [comm_id() if rank == 0 else None]
+    dist.broadcast_object_list(box, src=0)
+    return world, rank, box[0]
 
 
 def reduce_stats(local: Dict[str, float], device=None) -> Dict[str, float]:
@@ -148,7 +169,9 @@ def lp_loop_device(eng, world: int, rank: int, starts: np.ndarray, device=None, 
     """The device-driven window loop of one rank (tw_lp_tick ...): per tick the
     event kernel + local delivery + packing, an all-to-all of fixed-size record
     blocks, the import, an all-reduce(min) of {next time, -active lanes}, and
-    the device-side advance.  The host enqueues `check_every` ticks between
+    the device-side advance.  The reduction words are {next time, -active
+    lanes, -overflow bits}, so an overflow on one rank stops every rank at the
+    same tick.  The host enqueues `check_every` ticks between
     synchronisations (tw_lp_progress); no record ever goes through host memory.
     `starts` has world + 1 entries.  Over the "nccl" backend the collectives
     are RCCL on xGMI on the same stream as the engine's kernels.  `cap`
@@ -157,22 +180,44 @@ def lp_loop_device(eng, world: int, rank: int, starts: np.ndarray, device=None, 
     sends ~1.5k per pair per window); an overflow is an error, never a loss.
     Returns the final tw_lp_state."""
     import torch
-    import torch.distributed as dist
 
     starts = np.asarray(starts, dtype=np.uint32)
     if world == 1:
         eng.exchange_setup(1, 0, starts)  # the context's own stream; run_windows synchronises it
         eng.loop_begin()
         return eng.run_windows(max_ticks)
-    if device is not None and torch.cuda.current_stream(device).cuda_stream == 0:
-        # the engine and the collectives need one ordered, non-default stream
-        with torch.cuda.stream(torch.cuda.Stream(device)):
-            return lp_loop_device(eng, world, rank, starts, device, cap, check_every, max_ticks)
-    blk = (cap + 1) * 32
-    send = torch.zeros(world * blk, dtype=torch.uint8, device=device)
-    recv = torch.zeros_like(send)
-    red = torch.zeros(2, dtype=torch.int64, device=device)
-    eng.exchange_tensors(world, rank, starts, send, recv, cap, red)
+    bufs = lp_loop_device_setup(eng, world, rank, starts, device, cap)
+    with torch.cuda.stream(bufs["stream"]):
+        return _lp_ticks(eng, rank, bufs["send"], bufs["recv"], bufs["red"], check_every, max_ticks)
+
+
+def lp_loop_device_setup(eng, world: int, rank: int, starts: np.ndarray, device=None, cap: int = 1 << 14):
+    """The exchange buffers, the boundary table and the stream the engine and
+    the collectives share (one ordered, non-default stream) for
+    lp_loop_device: made once per engine and kept on it, so later runs (and
+    bench.py's timed steps) are the window loop only."""
+    import torch
+
+    starts = np.asarray(starts, dtype=np.uint32)
+    key = (world, rank, cap, tuple(starts.tolist()))
+    bufs = getattr(eng, "_loop_bufs", None)
+    if bufs is None or bufs["key"] != key:
+        stream = torch.cuda.Stream(device) if device is not None else None
+        blk = (cap + 1) * 32
+        with torch.cuda.stream(stream):
+            send = torch.zeros(world * blk, dtype=torch.uint8, device=device)
+            recv = torch.zeros_like(send)
+            red = torch.zeros(4, dtype=torch.int64, device=device)
+            eng.exchange_tensors(world, rank, starts, send, recv, cap, red)
+        if stream is not None:
+            stream.synchronize()
+        bufs = eng._loop_bufs = dict(key=key, stream=stream, send=send, recv=recv, red=red)
+    return bufs
+
+
+def _lp_ticks(eng, rank, send, recv, red, check_every, max_ticks):
+    import torch.distributed as dist
+
     eng.loop_begin()
     ticks, st = 0, None
     while ticks < max_ticks:
@@ -185,6 +230,9 @@ def lp_loop_device(eng, world: int, rank: int, starts: np.ndarray, device=None, 
         ticks += check_every
         st = eng.progress()
         if st.err:
+            # the overflow bits travel in the third reduction word, so every
+            # rank stops at the same tick and raises here together (bit 16:
+            # stopped because another rank overflowed)
             raise RuntimeError(f"device window loop: overflow bits {st.err} on rank {rank}")
         if st.done:
             break

@@ -24,7 +24,7 @@ LIB_PATH = os.path.join(_PKG_ROOT, "lib", "libtimewarp.so")
 UNLIMITED = (1 << 64) - 1
 T_INF = (1 << 63) - 1
 
-EXPORTS = ["tw_create", "tw_load", "tw_reset", "tw_run", "tw_read_results", "tw_read_hashes", "tw_read_final",
+EXPORTS = ["tw_create", "tw_comm_id", "tw_create_rank", "tw_ctx_info", "tw_lp_run", "tw_load", "tw_reset", "tw_run", "tw_read_results", "tw_read_hashes", "tw_read_final",
            "tw_last_launch_ms", "tw_destroy", "tw_strerror", "tw_version",
            "tw_lp_load", "tw_lp_window", "tw_lp_take_outbox", "tw_lp_inject", "tw_lp_results",
            "tw_set_trace", "tw_read_trace", "tw_tie_audit", "tw_set_counter_base", "tw_geometry",
@@ -67,7 +67,11 @@ def load_library(path: Optional[str] = None):
     except ImportError:
         pass
     lib = C.CDLL(p)
-    lib.tw_create.argtypes = [C.c_int, C.POINTER(C.c_void_p)]
+    lib.tw_create.argtypes = [C.POINTER(C.c_int), C.c_int, C.POINTER(C.c_void_p)]
+    lib.tw_comm_id.argtypes = [C.c_void_p]
+    lib.tw_create_rank.argtypes = [C.c_int, C.c_int, C.c_int, C.c_void_p, C.POINTER(C.c_void_p)]
+    lib.tw_ctx_info.argtypes = [C.c_void_p] + [C.POINTER(C.c_int)] * 4
+    lib.tw_lp_run.argtypes = [C.c_void_p, C.c_uint64, C.POINTER(TwLpState)]
     lib.tw_load.argtypes = [C.c_void_p, C.c_void_p]
     lib.tw_reset.argtypes = [C.c_void_p]
     lib.tw_run.argtypes = [C.c_void_p, C.c_int64, C.c_uint64, C.POINTER(TwStats)]
@@ -98,7 +102,7 @@ def load_library(path: Optional[str] = None):
     lib.tw_lp_run_windows.argtypes = [C.c_void_p, C.c_uint64, C.POINTER(TwLpState)]
     lib.tw_lpb_load.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p, C.c_uint32, C.c_uint32]
     lib.tw_lpb_windows.argtypes = [C.c_void_p, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
-    for name in ("tw_create", "tw_load", "tw_reset", "tw_run", "tw_read_results", "tw_read_hashes", "tw_read_final",
+    for name in ("tw_create", "tw_comm_id", "tw_create_rank", "tw_ctx_info", "tw_lp_run", "tw_load", "tw_reset", "tw_run", "tw_read_results", "tw_read_hashes", "tw_read_final",
                  "tw_last_launch_ms", "tw_lp_load", "tw_lp_window", "tw_lp_take_outbox", "tw_lp_inject",
                  "tw_lp_results", "tw_set_trace", "tw_read_trace", "tw_tie_audit", "tw_set_counter_base",
                  "tw_geometry", "tw_set_stream", "tw_lp_exchange_setup", "tw_lp_loop_begin", "tw_lp_tick",
@@ -131,15 +135,44 @@ class RunStats:
     wall_ms: float
 
 
-class Engine:
-    """A tw_ctx on one GPU holding one loaded scenario."""
+COMM_ID_BYTES = 128  # TW_COMM_ID_BYTES
 
-    def __init__(self, device: int = 0):
+
+def comm_id() -> bytes:
+    """A fresh RCCL job id (tw_comm_id): made by rank 0, handed to every rank
+    (e.g. torch.distributed.broadcast_object_list) for Engine(comm=...)."""
+    buf = (C.c_uint8 * COMM_ID_BYTES)()
+    _check(load_library().tw_comm_id(buf), "tw_comm_id")
+    return bytes(buf)
+
+
+class Engine:
+    """A tw_ctx holding one loaded scenario: on one GPU (`device`), on several
+    GPUs of this process (`devices`: replicas split into contiguous blocks,
+    statistics all-reduced over the library's RCCL communicators), or as one
+    rank of a multi-process job (`comm=(nranks, rank, job_id)` from comm_id():
+    the library's RCCL communicator over the ranks)."""
+
+    def __init__(self, device: int = 0, devices=None, comm=None):
         self.lib = load_library()
         ctx = C.c_void_p()
-        _check(self.lib.tw_create(device, C.byref(ctx)), "tw_create")
+        if comm is not None:
+            nranks, rank, jid = comm
+            idb = (C.c_uint8 * COMM_ID_BYTES).from_buffer_copy(jid)
+            _check(self.lib.tw_create_rank(int(device), int(nranks), int(rank), idb, C.byref(ctx)), "tw_create_rank")
+        else:
+            devs = list(devices) if devices is not None else [int(device)]
+            arr = (C.c_int * len(devs))(*devs)
+            _check(self.lib.tw_create(arr, len(devs), C.byref(ctx)), "tw_create")
         self.ctx = ctx
         self.scn: Optional[Scenario] = None
+
+    def info(self):
+        """(devices of this process, ranks of the job, global rank of the
+        first device, transport: 0 none, 1 RCCL, 2 device copies)."""
+        v = [C.c_int() for _ in range(4)]
+        _check(self.lib.tw_ctx_info(self.ctx, *[C.byref(x) for x in v]), "tw_ctx_info")
+        return tuple(x.value for x in v)
 
     def close(self):
         if self.ctx:
@@ -318,11 +351,12 @@ def run_scenario(scn: Scenario, device: int = 0, t_end: int = T_INF, max_events:
 
 class LPEngine(Engine):
     """One context of a node-partitioned run (config 4): owns nodes
-    [lp_begin, lp_begin + lp_count) of a single scenario."""
+    [lp_begin, lp_begin + lp_count) of a single scenario (split over
+    `devices` when given; a rank's share of a job with `comm`)."""
 
     def __init__(self, scn: Scenario, lp_begin: int, lp_count: int, lookahead_us: int, device: int = 0,
-                 inbox_cap: int = 16, outbox_cap: int = 1 << 22):
-        super().__init__(device)
+                 inbox_cap: int = 16, outbox_cap: int = 1 << 22, devices=None, comm=None):
+        super().__init__(device, devices=devices, comm=comm)
         d = scn.desc()
         _check(self.lib.tw_lp_load(self.ctx, C.addressof(d), lp_begin, lp_count, lookahead_us, inbox_cap,
                                    outbox_cap), "tw_lp_load")
@@ -356,7 +390,7 @@ class LPEngine(Engine):
     def exchange_setup(self, world: int, rank: int, starts, send_ptr: int = 0, recv_ptr: int = 0, cap: int = 0,
                        red_ptr: int = 0):
         """starts: world + 1 node boundaries; buffers are device pointers
-        (world * (cap + 1) * 32 bytes each; red: 2 int64)."""
+        (world * (cap + 1) * 32 bytes each; red: 4 int64)."""
         st = np.ascontiguousarray(starts, dtype=np.uint32)
         _check(self.lib.tw_lp_exchange_setup(self.ctx, world, rank, st.ctypes.data, C.c_void_p(send_ptr or None),
                                              C.c_void_p(recv_ptr or None), cap, C.c_void_p(red_ptr or None)),
@@ -393,6 +427,15 @@ class LPEngine(Engine):
     def progress(self) -> TwLpState:
         st = TwLpState()
         _check(self.lib.tw_lp_progress(self.ctx, C.byref(st)), "tw_lp_progress")
+        return st
+
+    def run_lp(self, max_ticks: int = 1 << 22) -> TwLpState:
+        """The whole window loop from t = 0 (after reset) over every device
+        and rank of the context, the exchange owned by the library
+        (tw_lp_run: RCCL send/recv of record blocks, all-reduce(min) of the
+        window words)."""
+        st = TwLpState()
+        _check(self.lib.tw_lp_run(self.ctx, int(max_ticks), C.byref(st)), "tw_lp_run")
         return st
 
     def run_windows(self, max_ticks: int = 1 << 20) -> TwLpState:
@@ -504,7 +547,7 @@ def run_partitioned_device(scn: Scenario, parts: int = 1, lookahead_us: Optional
         blk = (cap + 1) * 32
         send = [torch.zeros(parts * blk, dtype=torch.uint8, device=dev) for _ in range(parts)]
         recv = [torch.zeros(parts * blk, dtype=torch.uint8, device=dev) for _ in range(parts)]
-        red = [torch.zeros(2, dtype=torch.int64, device=dev) for _ in range(parts)]
+        red = [torch.zeros(4, dtype=torch.int64, device=dev) for _ in range(parts)]
         for g, e in enumerate(engines):
             e.set_stream(stream.cuda_stream)
             e.exchange_setup(parts, g, starts, send[g].data_ptr(), recv[g].data_ptr(), cap, red[g].data_ptr())
