@@ -282,7 +282,7 @@ def main():
     ap.add_argument("--msg-num", type=int, default=1000)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--geometry", default=None, choices=["dense", "sparse", "half", "wave", "narrow", "lpb"],
+    ap.add_argument("--geometry", default=None, choices=["dense", "sparse", "half", "wave", "narrow", "compact", "lpb"],
                     help="replica configs: kernel geometry (default: the library's choice by replica count); "
                          "lpb = every (node, replica) a logical process in one window loop (the replicas per "
                          "GPU must be a power of two: lanes are node << log2(R) | replica)")

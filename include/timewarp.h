@@ -69,7 +69,12 @@ enum {
 enum {
     TW_TIE_FIFO = 0,
     TW_TIE_LIFO = 1,
-    TW_TIE_SCRAMBLE = 2
+    TW_TIE_SCRAMBLE = 2,
+    TW_TIE_PQUEUE = 3   /* TimedT's own order: the queue is pqueue-1.3.1.1's
+                           binomial MinQueue ordered by timestamp only
+                           (TimedT.hs:100-104, 242), throwTo rebuilds it with
+                           fromList . map . toList (TimedT.hs:361-368); the
+                           wave geometry only (tw_set_tie_mode) */
 };
 
 /* ------------------------------------------------------------- exceptions */
@@ -340,13 +345,23 @@ int tw_read_trace(tw_ctx* ctx, uint32_t replica, tw_trace_rec* out, size_t cap, 
  * 242) could give a different trace than this engine. */
 int tw_tie_audit(tw_ctx* ctx, int64_t t_end_us, uint64_t max_events, uint32_t probes, tw_stats* out);
 
+/* The equal-timestamp order of later tw_reset / tw_run calls: TW_TIE_FIFO
+ * (the default, the engine's (t, seq) order), TW_TIE_LIFO / TW_TIE_SCRAMBLE
+ * (the audit probes), or TW_TIE_PQUEUE: TimedT's structural order, so a replica
+ * tw_tie_audit flagged can be re-run exactly as TimedT orders it (pqueue's
+ * MinQueue, PARITY UNPINNED against pqueue itself: its sources are not in the
+ * reference; equal to the oracle's pqueue transcription).  PQUEUE needs the
+ * wave geometry (TW_ERR_INVALID otherwise) and a queue_capacity covering the
+ * replica's pending events. */
+int tw_set_tie_mode(tw_ctx* ctx, uint32_t mode);
+
 /* Testing hook: from the next tw_reset on, start every replica's insertion
  * counter at seq0 and its thread counter at tid0 (>= 1; main is tid 0), so the
  * TW_REP_ERR_COUNTER guard can be reached in a short run. */
 int tw_set_counter_base(tw_ctx* ctx, uint32_t seq0, uint32_t tid0);
 
 /* Kernel geometry of the loaded scenario, chosen by tw_load from the replica
- * count (environment TW_GEOMETRY=dense|sparse|half|wave|narrow overrides):
+ * count (environment TW_GEOMETRY=dense|sparse|half|wave|narrow|compact overrides):
  *   DENSE  one lane per replica, 256 replicas per workgroup (many replicas);
  *   SPARSE one lane per replica, 16 per workgroup, large on-chip queue;
  *   HALF   the dense layout as two 32-lane waves per SIMD (an experiment);
@@ -354,9 +369,12 @@ int tw_set_counter_base(tw_ctx* ctx, uint32_t seq0, uint32_t tid0);
  *   NARROW the dense layout with one 64-replica wave per workgroup (fewer
  *          replicas than fill the GPU: the waves spread over every CU);
  *   LP     node-partitioned mode (tw_lp_load);
- *   LPB    batched node-partitioned mode (tw_lpb_load). */
+ *   LPB    batched node-partitioned mode (tw_lpb_load);
+ *   COMPACT the dense layout without far runs (far events in the HBM heap
+ *          only) and an 8-entry on-chip queue, two waves per SIMD: dense
+ *          batches of scenarios with run_capacity 0 (TW_GEOMETRY=compact). */
 enum { TW_GEO_DENSE = 0, TW_GEO_SPARSE = 1, TW_GEO_HALF = 2, TW_GEO_WAVE = 3, TW_GEO_LP = 4, TW_GEO_NARROW = 5,
-       TW_GEO_LPB = 6 };
+       TW_GEO_LPB = 6, TW_GEO_COMPACT = 7 };
 int tw_geometry(tw_ctx* ctx);
 
 /* Duration (ms) of every event-kernel launch of the last tw_run, measured with

@@ -10,7 +10,7 @@ for p in (os.path.join(ROOT, "time-warp_amd"), os.path.join(ROOT, "oracle"), ROO
 
 
 # every replica-mode GPU test runs under each kernel geometry (TW_GEOMETRY)
-GEOMETRIES = ["dense", "sparse", "half", "wave", "narrow"]
+GEOMETRIES = ["dense", "sparse", "half", "wave", "narrow", "compact"]
 
 
 def pytest_configure(config):

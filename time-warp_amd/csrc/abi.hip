@@ -517,6 +517,15 @@ int tw_set_counter_base(tw_ctx* c, uint32_t seq0, uint32_t tid0) {
     return TW_OK;
 }
 
+int tw_set_tie_mode(tw_ctx* c, uint32_t mode) {
+    if (!c) return TW_ERR_INVALID;
+    for (tw_shard* s : c->sh) {
+        int rc = sh_set_tie_mode(s, mode);
+        if (rc) return rc;
+    }
+    return TW_OK;
+}
+
 int tw_geometry(tw_ctx* c) {
     if (!c) return TW_ERR_INVALID;
     return sh_geometry(c->sh[0]);

@@ -61,6 +61,7 @@
 // (LP nodes queue few events), so three workgroups share a CU's LDS
 #define TW_WG_LP 128
 #define TW_NEAR_LP 8      // an LP node queues few events: 8 on chip (4 workgroups per CU)
+#define TW_NEAR_COMPACT 8 // compact geometry: 8 on-chip entries per replica, no far runs
 // work-list buckets by pending delivery records (tw_lp_compact).  Measured
 // with 4 buckets: C4 1.45 vs 1.58 G events/s -- pending records do not predict
 // a node's events in the window (most arrive for later windows) -- so 1.
@@ -236,8 +237,12 @@ struct BoolC {
     static constexpr bool value = B;
 };
 
-template <bool LP, int WG, int NC>
+template <bool LP, int WG, int NC, bool RUNS = true>
 struct Lane {
+    // the replica kernels keep monotone far runs (LDS bookkeeping + HBM FIFOs)
+    // unless built without them (the compact geometry: far events go to the
+    // HBM heap only, and the LDS a lane needs halves)
+    static constexpr bool HR = !LP && RUNS;
     // per-lane hot passes (lanes at different hot ops share a pass) pay off where
     // lanes diverge -- logical processes and the few-replica sparse geometry; the
     // dense replica geometry runs lock-step programs and keeps the cheaper
@@ -282,6 +287,10 @@ struct Lane {
     // this iteration's hash terms for the popped thread's node, one atomic at the end
     uint64_t hacc;
     uint32_t hnode;
+    // LP: the lane's node's first out-link (LINK never loads it), and the
+    // reverse of the link the lane's last delivery came in on (DELIVER loads
+    // it with the listener binding, so a handler's reply RLINK never waits)
+    uint32_t oo, rlc_link, rlc_rev;
     // free slots: bump pointer + stack with its top in a register
     uint32_t free_n, ftop, bump;
     // replica scalars
@@ -698,6 +707,7 @@ struct Lane {
     // Called after prefetch_all (4 younger vector-memory ops) and before the
     // store tail: vmcnt(4) proves the entry landed without waiting for them.
     __device__ __forceinline__ void run_commit() {
+        if constexpr (!HR) return;
         if (prun >= 0) {
             asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
             *rqp(RQ_SEC + prun) = pfs[4 * WG];
@@ -705,7 +715,7 @@ struct Lane {
         }
     }
     __device__ __forceinline__ bool run_push(int64_t t, uint32_t sq, uint32_t slot) {
-        if constexpr (LP) return false;  // LP nodes have no far runs (no LDS for them either)
+        if constexpr (!HR) return false;  // LP nodes / the compact geometry: no far runs (no LDS for them either)
         if (c.Cr == 0) return false;
         uint4 tl[TW_RUNS];
 #pragma unroll
@@ -744,7 +754,7 @@ struct Lane {
     // The head moves to the second entry; the entry after it is loaded now, by
     // LDS-DMA into staging quad 4, and committed before the store tail.
     __device__ __forceinline__ void run_pop(int sel) {
-        if constexpr (LP) return;  // unreachable: fsrc is never a run in LP mode
+        if constexpr (!HR) return;  // unreachable: fsrc is never a run without runs
         run_commit();
         far_dirty = true;
         uint4 ix4 = *rqp(RQ_IDX);
@@ -781,6 +791,7 @@ struct Lane {
             }
             return;
         }
+        if constexpr (!HR) return;
         uint4 hd[TW_RUNS], tl[TW_RUNS];
 #pragma unroll
         for (int j = 0; j < TW_RUNS; ++j) { hd[j] = *rqp(RQ_HEAD + j); tl[j] = *rqp(RQ_TAIL + j); }
@@ -1329,12 +1340,22 @@ struct Lane {
                         const int64_t x = gp(c.nvars)[nix(nv ? th.w1 : 0u, b & 3)];
                         v = nv ? x : v;
                     }
-                    if (need(ld == LD_OUT || ld == LD_RL)) {
+                    bool cached = false;
+                    if constexpr (LP) {
+                        // every lane's LINK / RLINK answered from the lane's cache: no load, no wait
+                        const bool miss = rl && (uint32_t)rb != rlc_link;
+                        if (need(ld == LD_OUT || ld == LD_RL) && !__builtin_amdgcn_ballot_w64(miss) &&
+                            !__builtin_amdgcn_ballot_w64(me && ld == LD_NV)) {
+                            v = ol ? (int64_t)oo + imm : (rl ? (int64_t)rlc_rev : v);
+                            cached = true;
+                        }
+                    }
+                    if (!cached && need(ld == LD_OUT || ld == LD_RL)) {
                         const uint32_t GAS* tb = ol ? gp(c.out_off) : gp(c.link_rev);
                         const uint32_t x = tb[ol ? (size_t)th.w1 : (rl && !bad ? (size_t)rb : 0)];
                         v = ol ? (int64_t)x + imm : (rl ? (int64_t)x : v);
                     }
-                    tw_vm_drain();
+                    if (!cached) tw_vm_drain();
                     wr = true;
                     lw = lw || ((nv || ol || rl) && !bad);
                     wv = v;
@@ -1455,7 +1476,11 @@ struct Lane {
                     } else {
                         const uint32_t kind = b & 0xFFu;
                         const int64_t payload = rf[((b >> 8) & 3u) * WG];
+                        // the link's ordinal and (LP) its destination entry: independent
+                        // loads in flight together, one wait
                         const uint32_t ord = gp(c.link_ord)[lix(link)];
+                        uint4 dh = make_uint4(0x80000000u, 0, 0, 0);
+                        if (LP) dh = gp(c.link_dsth)[link];  // destination | heavy, its inbox
                         gp(c.link_ord)[lix(link)] = ord + 1;
                         const uint32_t e = c.link_table ? gp(c.link_table)[tix(link, ord)] : 0u;
                         if (e & TW_LINK_DROP) {
@@ -1479,7 +1504,6 @@ struct Lane {
                                 d_ev += 2;
                                 ++d_th;
                                 final_t = ta > final_t ? ta : final_t;
-                                const uint4 dh = gp(c.link_dsth)[link];  // destination | heavy, its inbox
                                 emit(ta, payload, (uint32_t)link, kind, th.w1, lane_of(dh.x & 0x7FFFFFFFu), dh);
                                 yt = now + 1;
                                 tc = T_YIELD;
@@ -1503,6 +1527,10 @@ struct Lane {
                     const uint32_t dst = gp(c.link_dst)[link];
                     const uint32_t set0 = gp(c.bind)[bix(dst)];
                     const uint32_t own = gp(c.bind_own)[bix(dst)], rel = gp(c.bind_rel)[bix(dst)];
+                    if (LP) {  // the reply link a handler's RLINK asks for, loaded with the binding
+                        rlc_rev = gp(c.link_rev)[link];
+                        rlc_link = (uint32_t)link;
+                    }
                     const uint32_t set = own == rel ? 0u : set0;  // owner died: released
                     uint32_t lpc = TW_PC_NONE;
                     if (set && kind < c.n_kinds) lpc = gp(c.lpc)[(size_t)(set - 1) * c.n_kinds + kind];
@@ -1801,17 +1829,22 @@ __global__ void __launch_bounds__(TW_WG) tw_init_kernel(Dev c, uint32_t main_pc,
 // LDS per workgroup: near heap keys + slots, the running threads' register
 // files, the cold words, then the program image and constant pool, so
 // instruction fetch and time constants never leave the CU.
-template <int WG, int NC, bool LP = false>
+template <int WG, int NC, bool LP = false, bool RUNS = true>
 __host__ __device__ constexpr size_t fixed_lds_bytes() {
-    return (size_t)(LP ? 4 : 5) * WG * 16 + (size_t)(LP ? 0 : RQ_COUNT) * WG * 16 + (size_t)NC * WG * 12 +
+    return (size_t)(LP || !RUNS ? 4 : 5) * WG * 16 + (size_t)(LP || !RUNS ? 0 : RQ_COUNT) * WG * 16 + (size_t)NC * WG * 12 +
            (size_t)4 * WG * 8 + (size_t)(CW_COUNT + (LP ? DW_COUNT : 0)) * WG * 4;
 }
 
 // WG replicas per workgroup share its LDS; TPW of each wave's 64 lanes carry a
 // replica (64, or TW_HALF_LANES for the half geometry: twice the waves).
-template <bool LP, int WG, int NC, int TPW = 64>
-__global__ void __launch_bounds__(WG * 64 / TPW) __attribute__((amdgpu_waves_per_eu(LP ? 2 : (WG * 64 / TPW + 255) / 256, 2)))
+// RUNS = false (the compact geometry): no far runs, and built for two waves
+// per SIMD (<= 256 registers, half the LDS of a dense lane), so 1M-replica
+// batches keep two workgroups per CU
+template <bool LP, int WG, int NC, int TPW = 64, bool RUNS = true>
+__global__ void __launch_bounds__(WG * 64 / TPW)
+    __attribute__((amdgpu_waves_per_eu((LP || !RUNS) ? 2 : (WG * 64 / TPW + 255) / 256, 2)))
 tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
+    constexpr bool HR = !LP && RUNS;
     // device-driven windows: the window, its work list and whether this is the
     // window's first tick (the only one that drains inboxes) come from the device
     bool fresh = true;
@@ -1835,8 +1868,8 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
     }
     extern __shared__ __attribute__((aligned(16))) uint64_t lds_raw[];
     uint4 LAS* s_pf = (uint4 LAS*)lds_raw;
-    uint4 LAS* s_rq = s_pf + (LP ? 4 : 5) * WG;  // (staging quad 4 holds a far run's next entry: no runs in LP)
-    uint64_t LAS* s_k = (uint64_t LAS*)(s_rq + (LP ? 0 : RQ_COUNT) * WG);
+    uint4 LAS* s_rq = s_pf + (HR ? 5 : 4) * WG;  // (staging quad 4 holds a far run's next entry: runs only)
+    uint64_t LAS* s_k = (uint64_t LAS*)(s_rq + (HR ? RQ_COUNT : 0) * WG);
     int64_t LAS* s_rf = (int64_t LAS*)(s_k + NC * WG);
     uint32_t LAS* s_s = (uint32_t LAS*)(s_rf + 4 * WG);
     uint32_t LAS* s_cw = s_s + NC * WG;
@@ -1884,7 +1917,7 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
             return;
     }
 
-    Lane<LP, WG, NC> L;
+    Lane<LP, WG, NC, RUNS> L;
     L.c = c;
     L.r = r;
     L.nk = s_k + li;
@@ -1920,7 +1953,11 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
     L.d_ev = 0;
     L.d_th = 0;
     if (L.far_n) L.set_ftop(L.far_ld(0));
+    L.rlc_link = 0xFFFFFFFFu;
+    L.rlc_rev = 0;
+    L.oo = 0;
     if constexpr (LP) {
+        L.oo = gp(c.out_off)[(c.lp0 + r) >> c.rep_lg];  // (the lane's node: every thread of an LP lane runs on it)
         const uint32_t dn = (uint32_t)sc[SC_DUE_N * R], dh = (uint32_t)sc[SC_DUE_H * R];
         const size_t ib = ib_base(c, r);
         L.ds(DW_IB, (uint32_t)ib);
@@ -1931,7 +1968,7 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
         L.ds(DW_TL, h.x);
         L.ds(DW_TH, h.y);
     }
-    if constexpr (!LP) {
+    if constexpr (HR) {
         uint32_t rh4[TW_RUNS];
 #pragma unroll
         for (int j = 0; j < TW_RUNS; ++j) {
@@ -2217,11 +2254,11 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
     }
     sc[SC_DELIVERED * R] += L.cg(CW_DL); sc[SC_DROPPED * R] += L.cg(CW_DR);
     sc[SC_UNDELIV * R] += L.cg(CW_UD); sc[SC_THREADS * R] += L.d_th;
-    if (!LP && c.Cr) {
+    if (HR && c.Cr) {
         const uint4 ix4 = *L.rqp(RQ_IDX);
 #pragma unroll
         for (int j = 0; j < TW_RUNS; ++j) {
-            sc[(SC_RH0 + j) * R] = Lane<LP, WG, NC>::q_at(ix4, j);
+            sc[(SC_RH0 + j) * R] = Lane<LP, WG, NC, RUNS>::q_at(ix4, j);
             sc[(SC_RC0 + j) * R] = L.rqp(RQ_TAIL + j)->w;
         }
     }
@@ -2901,11 +2938,11 @@ void free_all(tw_shard* c) {
 
 }  // namespace
 
-template <bool LP, int WG, int NC, int TPW = 64>
+template <bool LP, int WG, int NC, int TPW = 64, bool RUNS = true>
 static void launch_run(tw_shard* c, hipStream_t st, int64_t t_end, uint64_t limit, uint32_t budget) {
     const uint32_t blocks = (uint32_t)((c->d.R + WG - 1) / WG);
-    hipLaunchKernelGGL((tw_run_kernel<LP, WG, NC, TPW>), dim3(blocks), dim3(WG * 64 / TPW), c->lds_bytes, st, c->d, t_end,
-                       limit, budget);
+    hipLaunchKernelGGL((tw_run_kernel<LP, WG, NC, TPW, RUNS>), dim3(blocks), dim3(WG * 64 / TPW), c->lds_bytes, st, c->d,
+                       t_end, limit, budget);
 }
 
 namespace tw {
@@ -3095,8 +3132,12 @@ static int load_common(tw_shard* c, const tw_scenario_desc* s, bool lp, uint32_t
     // wave); else dense (one workgroup of 256 per CU)
     {
         const char* g = getenv("TW_GEOMETRY");
-        int geo = lp ? 0 : R <= 4096 ? 3 : R < 65536 ? 5 : 0;
+        // dense batches of a scenario without far runs (run_capacity 0, e.g.
+        // C2's ping-pong: every event within the near horizon) take the
+        // compact geometry: two waves per SIMD
+        int geo = lp ? 0 : R <= 4096 ? 3 : R < 65536 ? 5 : (s->run_capacity == 0 ? 7 : 0);
         if (g && !strcmp(g, "dense")) geo = 0;
+        if (g && !strcmp(g, "compact")) geo = 7;
         if (g && !strcmp(g, "sparse")) geo = 1;
         if (g && !strcmp(g, "half")) geo = 2;
         if (g && !strcmp(g, "wave")) geo = 3;
@@ -3105,7 +3146,9 @@ static int load_common(tw_shard* c, const tw_scenario_desc* s, bool lp, uint32_t
         if (geo == 1 && fixed_lds_bytes<TW_WG_SPARSE, TW_NEAR_SPARSE>() + prog_lds > 160 * 1024) geo = 0;
         c->geo = geo;
     }
+    if (c->geo == 7) d.Cr = 0;  // far events: the HBM heap only
     c->lds_bytes = (lp            ? fixed_lds_bytes<TW_WG_LP, TW_NEAR_LP, true>()
+                    : c->geo == 7 ? fixed_lds_bytes<TW_WG, TW_NEAR_COMPACT, false, false>()
                     : c->geo == 1 ? fixed_lds_bytes<TW_WG_SPARSE, TW_NEAR_SPARSE>()
                     : c->geo == 5 ? fixed_lds_bytes<TW_NARROW, TW_NEAR_CAP>()
                                   : fixed_lds_bytes<TW_WG, TW_NEAR_CAP>()) +
@@ -3121,6 +3164,9 @@ static int load_common(tw_shard* c, const tw_scenario_desc* s, bool lp, uint32_t
                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)c->lds_bytes));
     else if (c->geo == 5)
         HIPCHK(hipFuncSetAttribute((const void*)tw_run_kernel<false, TW_NARROW, TW_NEAR_CAP, TW_NARROW>,
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)c->lds_bytes));
+    else if (c->geo == 7)
+        HIPCHK(hipFuncSetAttribute((const void*)tw_run_kernel<false, TW_WG, TW_NEAR_COMPACT, 64, false>,
                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)c->lds_bytes));
     else if (lp)
         HIPCHK(hipFuncSetAttribute((const void*)tw_run_kernel<true, TW_WG_LP, TW_NEAR_LP>,
@@ -3349,6 +3395,14 @@ int sh_reset(tw_shard* c) {
         c->d.wid = 0;
         HIPCHK(hipMemsetAsync(d.act_n, 0, 8 * TW_LP_NB, st));
     }
+    if (d.pq_hdr) {
+        // empty MinQueues: no element, no node used, every rank a Skip
+        std::vector<uint32_t> h((size_t)R * PQ_WORDS, 0u);
+        for (size_t r = 0; r < R; ++r)
+            for (int k = 0; k < 32; ++k) h[r * PQ_WORDS + PQ_FOREST + k] = 0xFFFFFFFFu;
+        HIPCHK(hipMemcpyAsync(d.pq_hdr, h.data(), 4 * h.size(), hipMemcpyHostToDevice, st));
+        HIPCHK(hipStreamSynchronize(st));
+    }
     uint32_t blocks = (uint32_t)((R + TW_WG - 1) / TW_WG);
     hipLaunchKernelGGL(tw_init_kernel, dim3(blocks), dim3(TW_WG), 0, st, d, c->main_pc, c->main_node,
                        (const int64_t*)c->main_regs, (const int64_t*)c->nv_init, (const uint32_t*)c->listen_init,
@@ -3419,6 +3473,8 @@ int sh_run(tw_shard* c, int64_t t_end_us, uint64_t max_events, tw_stats* out) {
                 launch_run<false, TW_WG, TW_NEAR_CAP, TW_HALF_LANES>(c, st, t_end_us, limit, budget);
             else if (c->geo == 5)
                 launch_run<false, TW_NARROW, TW_NEAR_CAP, TW_NARROW>(c, st, t_end_us, limit, budget);
+            else if (c->geo == 7)
+                launch_run<false, TW_WG, TW_NEAR_COMPACT, 64, false>(c, st, t_end_us, limit, budget);
             else
                 launch_run<false, TW_WG, TW_NEAR_CAP>(c, st, t_end_us, limit, budget);
             HIPCHK(hipGetLastError());
@@ -3537,6 +3593,32 @@ int sh_geometry(tw_shard* c) {
     if (!c) return TW_ERR_INVALID;
     if (!c->loaded) return TW_ERR_STATE;
     return c->lpb ? TW_GEO_LPB : c->lp ? TW_GEO_LP : c->geo;
+}
+
+// The equal-timestamp order of later runs (include/timewarp.h tw_set_tie_mode).
+// TW_TIE_PQUEUE runs the wave kernel with each replica's queue as pqueue's
+// binomial MinQueue (wave.hip); its node links, free stack, rebuild scratch
+// and header are allocated here on first use.
+int sh_set_tie_mode(tw_shard* c, uint32_t mode) {
+    if (!c) return TW_ERR_INVALID;
+    if (!c->loaded) return TW_ERR_STATE;
+    if (mode > TW_TIE_PQUEUE) return TW_ERR_INVALID;
+    if (mode == TW_TIE_PQUEUE) {
+        if (c->lp || c->geo != 3) return TW_ERR_INVALID;  // the wave kernel only
+        HIPCHK(hipSetDevice(c->device));
+        HIPCHK(hipStreamSynchronize(c->stream));
+        Dev& d = c->d;
+        const size_t n = (size_t)d.Q * d.R;
+        int e;
+        if (!d.pq_link) {
+            if ((e = dalloc(c, &d.pq_link, n)) != TW_OK) return e;
+            if ((e = dalloc(c, &d.pq_free, n)) != TW_OK) return e;
+            if ((e = dalloc(c, &d.pq_scr, n)) != TW_OK) return e;
+            if ((e = dalloc(c, &d.pq_hdr, (size_t)d.R * PQ_WORDS)) != TW_OK) return e;
+        }
+    }
+    c->d.tie_mode = mode;
+    return TW_OK;
 }
 
 int sh_set_counter_base(tw_shard* c, uint32_t seq0, uint32_t tid0) {

@@ -178,13 +178,24 @@ struct Dev {
     uint32_t tie_mode;          // TW_TIE_*: order of equal-timestamp events
     const uint8_t* pc_cls;      // [n_insns + 1] wave kernel: batch class of each resume pc (classify_pcs)
     uint32_t wave_k;            // wave kernel: near-queue entries per lane (4, 24 or 32), fixed by tw_load
+    // wave kernel, tie mode TW_TIE_PQUEUE: each replica's queue is a binomial
+    // MinQueue whose nodes are far[r * Q + i] (entries) + pq_link[r * Q + i]
+    // {highest-rank child, next lower-rank sibling}; pq_free its free-node
+    // stack, pq_scr the toList scratch of a throwTo rebuild, pq_hdr the queue
+    // header between launches (PQ_* words)
+    uint2* pq_link;
+    uint32_t* pq_free;
+    uint4* pq_scr;
+    uint32_t* pq_hdr;
 };
+// pqueue header words (per replica, [r * PQ_WORDS + w])
+enum { PQ_N, PQ_NFREE, PQ_BUMP, PQ_FLEN, PQ_MIN, PQ_FOREST = PQ_MIN + 4, PQ_WORDS = PQ_FOREST + 32 };
 
 // The key an insertion counter value takes in the queues (equal timestamps pop
 // in key order): FIFO (canonical), reverse (LIFO) or a scrambled bijection.
 // Every mode maps 0 to 0 and nothing else to 0 (wake_seq 0 = not queued).
 __device__ __forceinline__ uint32_t seq_key(uint32_t mode, uint32_t s) {
-    if (mode == TW_TIE_FIFO) return s;
+    if (mode == TW_TIE_FIFO || mode == TW_TIE_PQUEUE) return s;  // (pqueue: seq only names the entry)
     if (mode == TW_TIE_LIFO) return 0u - s;
     uint32_t x = s;  // xorshift-multiply: a bijection of u32 with x(0) = 0
     x ^= x >> 16; x *= 0x7feb352du; x ^= x >> 15; x *= 0x846ca68bu; x ^= x >> 16;

@@ -147,6 +147,15 @@ struct WCold {
     uint32_t dl, dr, ud, d_th, main_exc, tmo, trn;   // delivered/dropped/undeliverable, threads, ...
 };
 
+// pqueue mode (TW_TIE_PQUEUE): the queue header in LDS while the replica runs
+// (loaded from / stored to Dev::pq_hdr around each launch, PQ_* words)
+struct PQCold {
+    uint32_t n, nfree, bump, flen;  // size, free-node stack depth, nodes ever used, forest length
+    uint4 min;                      // MinQueue's held minimum {t lo, t hi, slot, seq}
+    uint32_t forest[32];            // root node of rank k, or PQ_NONE (a Skip)
+};
+#define PQ_NONE 0xFFFFFFFFu
+
 // BinaryP transmission time (== tx_us of tw_dev.hpp, context in constant memory)
 __device__ __forceinline__ int64_t tx_us_w(const Dev CAS* dv, uint64_t link, uint32_t kind) {
     if (!dv->msg_bytes || !dv->link_bw || kind >= dv->n_kinds) return 0;
@@ -418,10 +427,169 @@ struct Wave {
         fm_src = src; fm_t = t; fm_s = sq; fm_sl = sl;
     }
 
+    // ---------------------------------------- pqueue mode (TW_TIE_PQUEUE)
+    // TimedT's queue itself: pqueue-1.3.1.1 `Data.PQueue.Min.MinQueue` of
+    // events ordered by timestamp only (TimedT.hs:100-104), restated node by
+    // node from the oracle's transcription (oracle/pqueue_min.hpp, SURVEY.md
+    // Appendix B; PARITY UNPINNED against pqueue itself): a held minimum plus
+    // a binomial forest, joinBin putting t1 on top iff root t1 <= root t2.
+    // Wave-uniform scalar code; nodes in HBM (entries in the replica's far
+    // area, links {highest-rank child, next lower-rank sibling}).
+    bool pqm;        // the tie mode is TW_TIE_PQUEUE
+    PQCold LAS* pc;  // queue header (LDS)
+    __device__ __forceinline__ uint4 GAS* pqe(uint32_t i) const { return gp(dv->far) + (size_t)r * dv->Q + i; }
+    __device__ __forceinline__ uint2 GAS* pql(uint32_t i) const { return gp(dv->pq_link) + (size_t)r * dv->Q + i; }
+    __device__ __forceinline__ uint4 pq_ld(uint32_t i) const {
+        const uint4 e = *pqe(i);
+        return make_uint4(rfl(e.x), rfl(e.y), rfl(e.z), rfl(e.w));
+    }
+    __device__ __forceinline__ uint2 pq_lk(uint32_t i) const {
+        const uint2 l = *pql(i);
+        return make_uint2(rfl(l.x), rfl(l.y));
+    }
+    __device__ __forceinline__ void pq_setlk(uint32_t i, uint32_t child, uint32_t sib) const {
+        st64((uint64_t GAS*)pql(i), ((uint64_t)sib << 32) | child);
+    }
+    __device__ __forceinline__ uint4 pq_min() const {
+        return make_uint4(rfl(pc->min.x), rfl(pc->min.y), rfl(pc->min.z), rfl(pc->min.w));
+    }
+    __device__ uint32_t pq_new(uint4 e) {
+        const uint32_t nf = rfl(pc->nfree);
+        uint32_t i;
+        if (nf) {
+            i = rfl(gp(dv->pq_free)[(size_t)r * dv->Q + nf - 1]);
+            pc->nfree = nf - 1;
+        } else {
+            const uint32_t b = rfl(pc->bump);
+            if (b >= dv->Q) { fail(TW_REP_ERR_QUEUE); return PQ_NONE; }
+            i = b;
+            pc->bump = b + 1;
+        }
+        st128(pqe(i), e);
+        pq_setlk(i, PQ_NONE, PQ_NONE);
+        return i;
+    }
+    __device__ void pq_del(uint32_t i) {
+        const uint32_t nf = rfl(pc->nfree);
+        st32(gp(dv->pq_free) + (size_t)r * dv->Q + nf, i);
+        pc->nfree = nf + 1;
+    }
+    // joinBin: t1 on top iff root t1 <= root t2; the other becomes its
+    // highest-rank child
+    __device__ uint32_t pq_join(uint32_t t1, uint32_t t2) {
+        const bool top1 = ent_t(pq_ld(t1)) <= ent_t(pq_ld(t2));
+        const uint32_t top = top1 ? t1 : t2, sub = top1 ? t2 : t1;
+        const uint2 lt = pq_lk(top), ls = pq_lk(sub);
+        pq_setlk(sub, ls.x, lt.x);
+        pq_setlk(top, sub, lt.y);
+        return top;
+    }
+    // incr: binary-counter carry from rank k up
+    __device__ void pq_incr(uint32_t t, uint32_t k) {
+        for (;;) {
+            const uint32_t fl = rfl(pc->flen);
+            if (k >= fl) {  // Nil -> Cons t Nil
+                pc->forest[fl] = t;
+                pc->flen = fl + 1;
+                return;
+            }
+            const uint32_t u = rfl(pc->forest[k]);
+            if (u == PQ_NONE) {  // Skip f -> Cons t f
+                pc->forest[k] = t;
+                return;
+            }
+            pc->forest[k] = PQ_NONE;  // Cons t' f -> Skip (incr (joinBin t t') f)
+            t = pq_join(t, u);
+            ++k;
+        }
+    }
+    // insert' le x (MinQueue n x' ts)
+    __device__ void pq_insert(uint4 e) {
+        const uint32_t n = rfl(pc->n);
+        if (n == 0) {
+            pc->min = e;
+            pc->n = 1;
+            return;
+        }
+        const uint4 m = pq_min();
+        uint32_t t;
+        if (ent_t(e) <= ent_t(m)) {
+            t = pq_new(m);
+            pc->min = e;
+        } else {
+            t = pq_new(e);
+        }
+        if (t == PQ_NONE) return;
+        pq_incr(t, 0);
+        pc->n = n + 1;
+    }
+    // extractHeap: the root a lower rank wins ties with, its children merged
+    // back rank by rank (incrExtract / incrExtract')
+    __device__ void pq_extract() {
+        const uint32_t fl = rfl(pc->flen);
+        int m = -1;
+        int64_t mt = 0;
+        for (int k = (int)fl - 1; k >= 0; --k) {
+            const uint32_t t = rfl(pc->forest[k]);
+            if (t == PQ_NONE) continue;
+            const int64_t tt = ent_t(pq_ld(t));
+            if (m < 0 || tt <= mt) { m = k; mt = tt; }
+        }
+        if (m < 0) { fail(TW_REP_ERR_QUEUE); return; }  // (n > 0 with an empty forest: a broken invariant)
+        const uint32_t w = rfl(pc->forest[m]);
+        pc->forest[m] = PQ_NONE;
+        uint32_t ch = pq_lk(w).x;  // the rank m-1 child, then its lower-rank siblings
+        for (int k = m - 1; k >= 0; --k) {
+            const uint32_t kc = ch;
+            ch = pq_lk(kc).y;
+            const uint32_t u = rfl(pc->forest[k]);
+            if (u == PQ_NONE) {
+                pc->forest[k] = kc;
+            } else {
+                pc->forest[k] = PQ_NONE;
+                pq_incr(pq_join(u, kc), (uint32_t)k + 1);
+            }
+        }
+        uint32_t f2 = rfl(pc->flen);
+        while (f2 && rfl(pc->forest[f2 - 1]) == PQ_NONE) --f2;
+        pc->flen = f2;
+        pc->min = pq_ld(w);
+        pq_del(w);
+    }
+    // minView
+    __device__ uint4 pq_pop() {
+        const uint4 out = pq_min();
+        const uint32_t n = rfl(pc->n) - 1;
+        pc->n = n;
+        if (n > 0) pq_extract();
+        return out;
+    }
+    // throwTo's rebuild (TimedT.hs:361-368): fromList . map re-stamp . toList,
+    // the entry of thread slot `rs` (if any) moved to tnow
+    __device__ void pq_rebuild(uint32_t rs, int64_t tnow) {
+        uint4 GAS* scr = gp(dv->pq_scr) + (size_t)r * dv->Q;
+        uint32_t cnt = 0;
+        while (rfl(pc->n) > 0 && status == TW_REP_RUNNING) {  // toList = toAscList
+            uint4 e = pq_pop();
+            if (e.z == rs) { e.x = (uint32_t)tnow; e.y = (uint32_t)((uint64_t)tnow >> 32); }
+            st128(scr + cnt, e);
+            ++cnt;
+        }
+        for (uint32_t i = cnt; i-- > 0;) {  // fromList = foldr insert empty
+            const uint4 e = scr[i];
+            pq_insert(make_uint4(rfl(e.x), rfl(e.y), rfl(e.z), rfl(e.w)));
+        }
+    }
+
     __device__ __forceinline__ bool enqueue(URec& th, uint32_t slot, int64_t t) {
         const uint32_t s = next_seq();
         if (th.w3 == 0) ++live;
         th.w3 = s;
+        if (pqm) {
+            pq_insert(ent(t, slot, s));
+            th.w0 &= ~(F_NEARQ << FL_SHIFT);
+            return false;
+        }
         if (near_fits(t)) {
             near_push(t, s, slot);
             th.w0 |= F_NEARQ << FL_SHIFT;
@@ -514,6 +682,17 @@ struct Wave {
     // now with a fresh seq; the first pending exception wins; no yield.
     __device__ void throw_to(URec& self, uint32_t self_slot, int64_t ref, uint32_t code, int64_t val) {
         const uint32_t ts = (uint32_t)ref, tid = (uint32_t)((uint64_t)ref >> 32);
+        if (pqm) {
+            // TimedT rebuilds its queue on every throwTo, whether or not the
+            // target has an event queued (or is alive at all)
+            uint32_t rs = PQ_NONE;
+            if (ts < dv->S && ts != self_slot) {
+                URec t;
+                urec_load(hrec(ts), dv->RQ, t);
+                if (t.w2 == tid && t.w3 != 0) rs = ts;
+            }
+            pq_rebuild(rs, now);
+        }
         if (ts >= dv->S) return;
         if (ts == self_slot) {
             if (self.w2 != tid) return;
@@ -523,7 +702,7 @@ struct Wave {
         URec t;
         urec_load(hrec(ts), dv->RQ, t);
         if (t.w2 != tid) return;  // dead: the map entry is unobservable
-        if (t.w3 != 0) {
+        if (t.w3 != 0 && !pqm) {  // (pqueue mode: re-stamped in place by the rebuild, same seq)
             bool on_chip = (u_flags(t) & F_NEARQ) != 0;
             const uint32_t s = next_seq();
             if (!(on_chip && near_rekey(t.w3, now, s, ts))) {
@@ -807,6 +986,16 @@ __global__ void __launch_bounds__(64) tw_wave_kernel(const Dev* dptr, int64_t t_
     W.bump = rfl((uint32_t)sc[SC_BUMP * R]);
     __shared__ WCold cold;
     W.cw = (WCold LAS*)&cold;
+    __shared__ PQCold pqc;
+    W.pc = (PQCold LAS*)&pqc;
+    W.pqm = dv->tie_mode == TW_TIE_PQUEUE;
+    if (W.pqm) {
+        const uint32_t GAS* h = gp(dv->pq_hdr) + (size_t)r * PQ_WORDS;
+        pqc.n = rfl(h[PQ_N]); pqc.nfree = rfl(h[PQ_NFREE]); pqc.bump = rfl(h[PQ_BUMP]); pqc.flen = rfl(h[PQ_FLEN]);
+        pqc.min = make_uint4(rfl(h[PQ_MIN]), rfl(h[PQ_MIN + 1]), rfl(h[PQ_MIN + 2]), rfl(h[PQ_MIN + 3]));
+#pragma unroll
+        for (int k = 0; k < 32; ++k) pqc.forest[k] = rfl(h[PQ_FOREST + k]);
+    }
     cold.main_exc = rfl((uint32_t)sc[SC_MAIN_EXC * R]);
     cold.tmo = rfl((uint32_t)sc[SC_TMO_CTR * R]);
     cold.trn = rfl((uint32_t)sc[SC_TRACE_N * R]);
@@ -871,6 +1060,44 @@ __global__ void __launch_bounds__(64) tw_wave_kernel(const Dev* dptr, int64_t t_
         } else {
             if (W.live == 0) { W.status = TW_REP_DONE; break; }  // whileM_ notDone
             if (W.d_ev >= ev_room) break;                        // this call's event cap
+            if (W.pqm) {  // PQ.minView (TimedT.hs:242)
+                if (rfl(pqc.n) == 0) break;
+                const uint4 m = W.pq_min();
+                const int64_t t = ent_t(m);
+                if (t > t_end) break;  // parked beyond t_end
+                W.pq_pop();
+                if (W.status != TW_REP_RUNNING) break;
+                slot = m.z;
+                urec_load(W.hrec(slot), dv->RQ, th);
+                // (no superseded entries: a throwTo re-stamps the event in place)
+                th.w3 = 0;
+                --W.live;
+                W.now = t;
+                W.hnode = th.w1;
+                W.final_t = t;
+                ++W.d_ev;
+                const uint32_t exc = u_exc(th);
+                if (exc) {
+                    const int64_t val = (int64_t)(((uint64_t)th.xh << 32) | th.xl);
+                    u_set_exc(th, 0);
+                    th.xl = th.xh = 0;
+                    W.hacc += term0(t, TW_KIND_EXC | exc);
+                    if (!(u_flags(th) & (F_STARTED | F_MAIN))) {
+                        W.status = TW_REP_ABORTED;
+                        cold.main_exc = exc;
+                        urec_store(W.hrec(slot), dv->RQ, th, 0, 4);
+                    } else {
+                        run = W.unwind(th, slot, exc, val);
+                    }
+                } else {
+                    W.hacc += term0(t, TW_KIND_RESUME | u_pc(th));
+                    run = true;
+                }
+                if (run) W.step(th, slot);
+                W.hash_flush();
+                alive = W.status == TW_REP_RUNNING;
+                continue;
+            }
             // PQ.minView: the near minimum or the far minimum
             if (W.far_dirty) W.far_min();
             const int src = W.fm_src;
@@ -953,7 +1180,15 @@ __global__ void __launch_bounds__(64) tw_wave_kernel(const Dev* dptr, int64_t t_
     }
     bool active = W.status == TW_REP_RUNNING && W.d_ev < ev_room;
     int64_t tn = INT64_MAX;
-    {
+    if (W.pqm) {
+        if (rfl(pqc.n)) tn = ent_t(W.pq_min());
+        if (W.lane == 0) {
+            uint32_t* h = gp(dv->pq_hdr) + (size_t)r * PQ_WORDS;
+            h[PQ_N] = pqc.n; h[PQ_NFREE] = pqc.nfree; h[PQ_BUMP] = pqc.bump; h[PQ_FLEN] = pqc.flen;
+            h[PQ_MIN] = pqc.min.x; h[PQ_MIN + 1] = pqc.min.y; h[PQ_MIN + 2] = pqc.min.z; h[PQ_MIN + 3] = pqc.min.w;
+            for (int k = 0; k < 32; ++k) h[PQ_FOREST + k] = pqc.forest[k];
+        }
+    } else {
         if (W.near_n) tn = W.nbase + (int64_t)(W.gmin >> 32);
         W.far_min();
         if (W.fm_src >= 0 && W.fm_t < tn) tn = W.fm_t;

@@ -24,13 +24,13 @@ LIB_PATH = os.path.join(_PKG_ROOT, "lib", "libtimewarp.so")
 UNLIMITED = (1 << 64) - 1
 T_INF = (1 << 63) - 1
 
-EXPORTS = ["tw_create", "tw_comm_id", "tw_create_rank", "tw_ctx_info", "tw_lp_run", "tw_load", "tw_reset", "tw_run", "tw_read_results", "tw_read_hashes", "tw_read_final",
+EXPORTS = ["tw_create", "tw_comm_id", "tw_create_rank", "tw_ctx_info", "tw_lp_run", "tw_set_tie_mode", "tw_load", "tw_reset", "tw_run", "tw_read_results", "tw_read_hashes", "tw_read_final",
            "tw_last_launch_ms", "tw_destroy", "tw_strerror", "tw_version",
            "tw_lp_load", "tw_lp_window", "tw_lp_take_outbox", "tw_lp_inject", "tw_lp_results",
            "tw_set_trace", "tw_read_trace", "tw_tie_audit", "tw_set_counter_base", "tw_geometry",
            "tw_set_stream", "tw_lp_exchange_setup", "tw_lp_loop_begin", "tw_lp_tick", "tw_lp_tick_import",
            "tw_lp_tick_end", "tw_lp_progress", "tw_lp_run_windows", "tw_lpb_load", "tw_lpb_windows"]
-GEOMETRIES = ("dense", "sparse", "half", "wave", "lp", "narrow", "lpb")  # TW_GEO_* order
+GEOMETRIES = ("dense", "sparse", "half", "wave", "lp", "narrow", "lpb", "compact")  # TW_GEO_* order
 
 # tw_trace_rec (include/timewarp.h)
 TRACE_DTYPE = np.dtype([("t", np.int64), ("val", np.int64), ("node", np.uint32), ("tag", np.uint32)])
@@ -72,6 +72,7 @@ def load_library(path: Optional[str] = None):
     lib.tw_create_rank.argtypes = [C.c_int, C.c_int, C.c_int, C.c_void_p, C.POINTER(C.c_void_p)]
     lib.tw_ctx_info.argtypes = [C.c_void_p] + [C.POINTER(C.c_int)] * 4
     lib.tw_lp_run.argtypes = [C.c_void_p, C.c_uint64, C.POINTER(TwLpState)]
+    lib.tw_set_tie_mode.argtypes = [C.c_void_p, C.c_uint32]
     lib.tw_load.argtypes = [C.c_void_p, C.c_void_p]
     lib.tw_reset.argtypes = [C.c_void_p]
     lib.tw_run.argtypes = [C.c_void_p, C.c_int64, C.c_uint64, C.POINTER(TwStats)]
@@ -102,7 +103,7 @@ def load_library(path: Optional[str] = None):
     lib.tw_lp_run_windows.argtypes = [C.c_void_p, C.c_uint64, C.POINTER(TwLpState)]
     lib.tw_lpb_load.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p, C.c_uint32, C.c_uint32]
     lib.tw_lpb_windows.argtypes = [C.c_void_p, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
-    for name in ("tw_create", "tw_comm_id", "tw_create_rank", "tw_ctx_info", "tw_lp_run", "tw_load", "tw_reset", "tw_run", "tw_read_results", "tw_read_hashes", "tw_read_final",
+    for name in ("tw_create", "tw_comm_id", "tw_create_rank", "tw_ctx_info", "tw_lp_run", "tw_set_tie_mode", "tw_load", "tw_reset", "tw_run", "tw_read_results", "tw_read_hashes", "tw_read_final",
                  "tw_last_launch_ms", "tw_lp_load", "tw_lp_window", "tw_lp_take_outbox", "tw_lp_inject",
                  "tw_lp_results", "tw_set_trace", "tw_read_trace", "tw_tie_audit", "tw_set_counter_base",
                  "tw_geometry", "tw_set_stream", "tw_lp_exchange_setup", "tw_lp_loop_begin", "tw_lp_tick",
@@ -205,8 +206,9 @@ class Engine:
         d = scn.desc()
         old = os.environ.get("TW_GEOMETRY")
         if geometry is not None:
-            if geometry not in ("dense", "sparse", "half", "wave", "narrow"):
-                raise ValueError(f"geometry must be 'dense', 'sparse', 'half', 'wave' or 'narrow', not {geometry!r}")
+            if geometry not in ("dense", "sparse", "half", "wave", "narrow", "compact"):
+                raise ValueError(f"geometry must be 'dense', 'sparse', 'half', 'wave', 'narrow' or 'compact', "
+                                 f"not {geometry!r}")
             os.environ["TW_GEOMETRY"] = geometry
         try:
             _check(self.lib.tw_load(self.ctx, C.addressof(d)), "tw_load")
@@ -281,6 +283,16 @@ class Engine:
         _check(self.lib.tw_tie_audit(self.ctx, int(t_end), int(max_events), int(probes), C.byref(st)),
                "tw_tie_audit")
         return RunStats(**{f: getattr(st, f) for f, _ in TwStats._fields_ if f != "reserved"})
+
+    TIE_MODES = {"fifo": 0, "lifo": 1, "scramble": 2, "pqueue": 3}  # TW_TIE_*
+
+    def set_tie_mode(self, mode: str) -> "Engine":
+        """Equal-timestamp order of later runs: "fifo" (the engine's (t, seq)),
+        the audit probes "lifo" / "scramble", or "pqueue": TimedT's own order
+        (pqueue's MinQueue by timestamp only, TimedT.hs:100-104, with the
+        throwTo rebuild of TimedT.hs:361-368), wave geometry only."""
+        _check(self.lib.tw_set_tie_mode(self.ctx, self.TIE_MODES[mode]), "tw_set_tie_mode")
+        return self
 
     def set_counter_base(self, seq0: int, tid0: int = 1) -> "Engine":
         """Testing hook: start the 32-bit insertion / thread counters at these
