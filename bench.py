@@ -256,8 +256,12 @@ def bench_gossip(args, scn, workload, world, rank, local, dist_on, barrier):
             t0 = time.perf_counter()
             o = oracle.run(scn, trace_cap=0)
             dt = time.perf_counter() - t0
+            threads, cpu_desc = host_cpu()
             out["cpu_baseline"] = {"value": o.result["events"] / dt, "unit": "events/s", "cores": 1, "kind": "port",
-                                   "sample": f"the whole scenario, sequential oracle (canonical), {dt:.1f} s"}
+                                   "cpu": cpu_desc,
+                                   "sample": f"the whole scenario, sequential oracle (canonical), {dt:.1f} s; one "
+                                             f"thread by design, not the {threads} of nproc: C4 is ONE scenario, and "
+                                             f"TimedT runs a scenario as one sequential loop (TimedT.hs:239-263)"}
             out["parity_sample"] = {"scenario": "whole", "bit_exact": bool(
                 all(int(tot[f]) == int(o.result[f]) for f in ("final_t", "events", "delivered", "dropped", "undeliverable", "threads"))
                 and np.array_equal(hashes, o.hashes))}

@@ -215,6 +215,32 @@ __device__ __forceinline__ uint32_t uop_of(uint32_t op) {
 // and the previous store tail.  Paths that load already waited for it.
 __device__ __forceinline__ void tw_vm_drain() { __builtin_amdgcn_s_waitcnt(0x0F70); }
 
+// atomic min on a word every lane of a window bounds (the window's record
+// minimum, the next event time): a plain read first skips the atomic unless
+// it can lower the value, so the L2 does not serialise a million same-address
+// atomics per window
+__device__ __forceinline__ void min_hot(uint64_t GAS* p, uint64_t v) {
+    if (v < __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+        __hip_atomic_fetch_min(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Claim k consecutive entries of a shared append counter for every lane
+// running this code (the active lanes of a divergent region): one atomic per
+// wave by its first active lane (ballot-aggregated), each lane's share placed
+// by its rank among the active lanes.  Every sender of a hotspot appends to the
+// one outbox counter; per-lane atomics on it serialise in the L2.
+__device__ __forceinline__ uint32_t wave_append(uint32_t GAS* ctr, uint32_t k) {
+    const uint64_t m = __builtin_amdgcn_ballot_w64(true);
+    const uint32_t lead = (uint32_t)__builtin_ctzll(m);
+    const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+    uint32_t base = 0;
+    if (below == 0)
+        base = __hip_atomic_fetch_add(ctr, k * (uint32_t)__builtin_popcountll(m), __ATOMIC_RELAXED,
+                                      __HIP_MEMORY_SCOPE_AGENT);
+    base = (uint32_t)__builtin_amdgcn_readlane((int)base, (int)lead);
+    return base + k * below;
+}
+
 __device__ __forceinline__ void lp_deliver(const Dev& c, uint4 a, uint4 b, uint64_t GAS* tmin, int64_t wend,
                                            bool upd_min = true);
 
@@ -1049,7 +1075,7 @@ struct Lane {
             ds(DW_IB, dg(DW_IB) | 0x80000000u);
             return;
         }
-        uint32_t i = __hip_atomic_fetch_add(gp(c.out_n), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t i = wave_append(gp(c.out_n), 1u);
         if (i >= c.out_cap) {
             __hip_atomic_fetch_or(gp(c.lp_err), 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             return;
@@ -1065,7 +1091,7 @@ struct Lane {
     // at its next tick, before running anything later than t).
     __device__ __forceinline__ void emit_spawn(int64_t t, uint32_t pc, uint32_t dst, int64_t q0, int64_t q1,
                                                int64_t q2, int64_t q3) {
-        uint32_t i = __hip_atomic_fetch_add(gp(c.out_n), 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t i = wave_append(gp(c.out_n), 2u);
         if (i + 1 >= c.out_cap) {
             __hip_atomic_fetch_or(gp(c.lp_err), 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             return;
@@ -2249,8 +2275,7 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
     if (LP) {
         sc[SC_DUE_H * R] = L.dg(DW_HN) & 0xFFFFu;
         if (L.dg(DW_IB) >> 31)  // sent records straight into inboxes (Lane::emit)
-            __hip_atomic_fetch_min((uint64_t GAS*)(gp(c.win) + WN_REC_MIN), (uint64_t)(t_end + 1), __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
+            min_hot((uint64_t GAS*)(gp(c.win) + WN_REC_MIN), (uint64_t)(t_end + 1));
     }
     sc[SC_DELIVERED * R] += L.cg(CW_DL); sc[SC_DROPPED * R] += L.cg(CW_DR);
     sc[SC_UNDELIV * R] += L.cg(CW_UD); sc[SC_THREADS * R] += L.d_th;
@@ -2273,9 +2298,14 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
     if (L.near_n) tn = L.nbase + (int64_t)(L.nrk >> 32);
     if (L.fsrc >= 0 && L.fmt < tn) tn = L.fmt;
     if (active && (tn == INT64_MAX || tn > t_end) && !pending_main) active = false;  // parked beyond t_end
-    if (LP && L.status == TW_REP_RUNNING && tn != INT64_MAX)
-        __hip_atomic_fetch_min(gp(c.next_t), (uint64_t)tn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (active) __hip_atomic_fetch_add(gp(c.n_active), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (LP && L.status == TW_REP_RUNNING && tn != INT64_MAX) min_hot(gp(c.next_t), (uint64_t)tn);
+    {   // lanes still active: one atomic per wave
+        const uint64_t am = __builtin_amdgcn_ballot_w64(active);
+        const uint64_t ex = __builtin_amdgcn_ballot_w64(true);
+        if (am && __builtin_amdgcn_mbcnt_hi((uint32_t)(ex >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)ex, 0u)) == 0)
+            __hip_atomic_fetch_add(gp(c.n_active), (uint32_t)__builtin_popcountll(am), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+    }
     if (LP) {
         // device loop: the lane is listed again by the window its next event
         // falls in (tw_lp_compact); host loop: for the next window
@@ -2305,8 +2335,7 @@ __device__ __forceinline__ void lp_deliver(const Dev& c, uint4 a, uint4 b, uint6
     q[1] = b;
     // (a record due in this window, t < wend -- a short link into a phase-1
     // node -- is drained at phase 1's first tick: it does not bound the next window)
-    if (upd_min && ent_t(a) >= wend)
-        __hip_atomic_fetch_min(tmin, (uint64_t)ent_t(a), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (upd_min && ent_t(a) >= wend) min_hot(tmin, (uint64_t)ent_t(a));
     // a lane whose node may hold more than TW_LIGHT records is served by
     // tw_lp_due: its first pending record lists it for the next window's pass
     // (device loop; the list of window wid + 1)
@@ -2340,8 +2369,7 @@ __device__ __forceinline__ void lp_spawn(const Dev& c, const uint4 GAS* o, uint6
     // this tick's earliest spawn: one in the current window reruns it (tw_lp_fill),
     // with the target lane appended to the running window's work list (once)
     (void)tmin;
-    __hip_atomic_fetch_min((uint64_t GAS*)(gp(c.win) + WN_SPN_MIN), (uint64_t)ent_t(a), __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
+    min_hot((uint64_t GAS*)(gp(c.win) + WN_SPN_MIN), (uint64_t)ent_t(a));
     if (__hip_atomic_exchange(gp(c.inlist) + lp, c.wid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != c.wid) {
         const uint32_t i = __hip_atomic_fetch_add(gp(c.act_n) + c.act_cur * TW_LP_NB, 1u, __ATOMIC_RELAXED,
                                                   __HIP_MEMORY_SCOPE_AGENT);
@@ -2672,26 +2700,58 @@ __global__ void tw_lp_begin(Dev c, int64_t lookahead) {
 // messages in flight) would otherwise hold every one of them as a phantom
 // thread, with a slot, in its queue.  Here one workgroup per such lane with
 // records stages them in LDS, keeps the ones due in this window [T, T + L) as
-// the lane's due run, sorted by (t, link, payload, src, kind) -- the order the
-// light drain inserts them in -- with their queue seqs reserved now, as if
-// they had been queued at the window's start; the rest stay in the inbox
+// the lane's due run, sorted by (t, link, payload, src, kind) -- rec_less, the
+// order the light drain inserts them in -- with their queue seqs reserved now,
+// as if they had been queued at the window's start; the rest stay in the inbox
 // (their earliest time bounds the next window) and the lane is listed for the
 // next window's pass.
+//
+// The sort is an LDS segmented radix (counting) sort by timestamp: a due
+// record's key is its offset t - T < L inside the window, so one counting pass
+// over L bins (histogram by LDS atomics, a workgroup scan of the bins, a
+// scatter) orders the run by timestamp; each segment of equal timestamps
+// (mostly 0-2 records) is then put in rec_less order by one thread.  Windows
+// longer than TW_DUE_BINS use a rank-by-comparison fallback.
 #define TW_DUE_GRID 1024  // tw_lp_due workgroups (each serves heavy lanes in turn)
+#define TW_DUE_BINS 2048  // counting-sort bins: windows up to 2048 µs
+// exclusive prefix sum of one value per thread over the 256-thread workgroup
+// (a shuffle scan in each wave, then the four wave totals); *total = the sum
+__device__ __forceinline__ uint32_t wg_excl_scan(uint32_t v, uint32_t* wsum, uint32_t* total) {
+    const uint32_t lane = __lane_id(), wv = threadIdx.x >> 6;
+    uint32_t x = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(x, d, 64);
+        x += lane >= (uint32_t)d ? y : 0u;
+    }
+    if (lane == 63) wsum[wv] = x;
+    __syncthreads();
+    uint32_t base = 0;
+    for (uint32_t k = 0; k < wv; ++k) base += wsum[k];
+    *total = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+    __syncthreads();
+    return base + x - v;
+}
 __global__ void __launch_bounds__(256) tw_lp_due(Dev c) {
     const int64_t GAS* w = gp(c.win);
     const int64_t fl = w[WN_FLAGS];
     if (!(fl & WN_FRESH) || (fl & WN_DONE)) return;
     const uint32_t wid = (uint32_t)w[WN_WID];
-    const int64_t tend = w[WN_T] + w[WN_L] - 1;
+    const int64_t T = w[WN_T], L = w[WN_L];
+    const int64_t tend = T + L - 1;
+    const bool radix = L <= TW_DUE_BINS;
+    const uint32_t nb = radix ? (uint32_t)L : 0u;
     const uint32_t lst = wid & 1u;
     uint32_t nh = gp(c.heavy_n)[lst];
     nh = nh < c.R ? nh : c.R;  // (an over-full list has set lp_err)
     __shared__ uint4 ea[TW_HEAVY_CAP], eb[TW_HEAVY_CAP];
     __shared__ uint16_t dix[TW_HEAVY_CAP];  // entry index of the i-th due record (arrival order)
-    __shared__ uint32_t cnt[257];           // exclusive scan of the due counts per thread; [256] = total
+    __shared__ uint16_t srt[TW_HEAVY_CAP];  // ... of the i-th due record in due-run order
+    __shared__ uint32_t bins[TW_DUE_BINS];  // counts -> segment offsets -> segment ends
+    __shared__ uint32_t wsum[4];
     __shared__ unsigned long long smin;
     static_assert(TW_HEAVY_CAP == 256 * 8, "eight entries per thread");
+    static_assert(TW_DUE_BINS == 256 * 8, "eight bins per thread");
     const uint32_t tid = threadIdx.x;
     const size_t st = ib_stride(c);
     for (uint32_t hi = blockIdx.x; hi < nh; hi += gridDim.x) {
@@ -2706,6 +2766,7 @@ __global__ void __launch_bounds__(256) tw_lp_due(Dev c) {
             eb[k] = q[1];
         }
         if (tid == 0) smin = ~0ull;
+        for (uint32_t i = tid; i < nb; i += 256) bins[i] = 0;
         __syncthreads();
         // thread tid owns entries [8 tid, 8 tid + 8): due flags, then a scan
         uint32_t my = 0;
@@ -2713,22 +2774,11 @@ __global__ void __launch_bounds__(256) tw_lp_due(Dev c) {
             const uint32_t k = tid * 8 + j;
             my += (k < n && ent_t(ea[k]) <= tend) ? 1u : 0u;
         }
-        cnt[tid] = my;
-        __syncthreads();
-        if (tid == 0) {
-            uint32_t run = 0;
-            for (int i = 0; i < 256; ++i) {
-                const uint32_t v = cnt[i];
-                cnt[i] = run;
-                run += v;
-            }
-            cnt[256] = run;
-        }
-        __syncthreads();
-        const uint32_t nd = cnt[256];
-        // due records -> dix (arrival order); the rest compacted back into the
-        // inbox in arrival order (every record is staged in LDS already)
-        uint32_t before = cnt[tid];
+        uint32_t nd = 0;
+        uint32_t before = wg_excl_scan(my, wsum, &nd);
+        // due records -> dix (arrival order) and their timestamp bins; the rest
+        // compacted back into the inbox in arrival order (every record is
+        // staged in LDS already)
         unsigned long long mn = ~0ull;
         for (uint32_t j = 0; j < 8; ++j) {
             const uint32_t k = tid * 8 + j;
@@ -2736,6 +2786,7 @@ __global__ void __launch_bounds__(256) tw_lp_due(Dev c) {
             const int64_t t = ent_t(ea[k]);
             if (t <= tend) {
                 dix[before++] = (uint16_t)k;
+                if (radix) atomicAdd(&bins[t > T ? (uint32_t)(t - T) : 0u], 1u);
             } else {
                 uint4 GAS* q = gp(c.inbox) + (ib + (size_t)(k - before) * st) * 2;
                 q[0] = ea[k];
@@ -2745,19 +2796,66 @@ __global__ void __launch_bounds__(256) tw_lp_due(Dev c) {
         }
         if (mn != ~0ull) atomicMin(&smin, mn);
         __syncthreads();
-        // rank of every due record among the due ones (ties by arrival) = its
-        // position in the due run
-        for (uint32_t i = tid; i < nd; i += 256) {
-            const uint32_t k = dix[i];
-            const uint4 a = ea[k], b = eb[k];
-            uint32_t rank = 0;
-            for (uint32_t j = 0; j < nd; ++j) {
-                const uint32_t m = dix[j];
-                rank += (rec_less(ea[m], eb[m], a, b) || (j < i && !rec_less(a, b, ea[m], eb[m]))) ? 1u : 0u;
+        if (radix) {
+            // bin counts -> each bin's first position (thread tid owns bins [8 tid, 8 tid + 8))
+            uint32_t cnt8[8], sum = 0;
+            for (uint32_t j = 0; j < 8; ++j) {
+                const uint32_t bi = tid * 8 + j;
+                cnt8[j] = bi < nb ? bins[bi] : 0u;
+                sum += cnt8[j];
             }
-            uint4 GAS* q = gp(c.due) + (ib + (size_t)rank * st) * 2;
-            q[0] = a;
-            q[1] = b;
+            uint32_t tot = 0;
+            uint32_t off = wg_excl_scan(sum, wsum, &tot);
+            for (uint32_t j = 0; j < 8; ++j) {
+                const uint32_t bi = tid * 8 + j;
+                if (bi < nb) bins[bi] = off;
+                off += cnt8[j];
+            }
+            __syncthreads();
+            // scatter by timestamp (positions inside a segment in any order);
+            // afterwards bins[b] = the end of segment b
+            for (uint32_t i = tid; i < nd; i += 256) {
+                const uint32_t k = dix[i];
+                const int64_t t = ent_t(ea[k]);
+                const uint32_t pos = atomicAdd(&bins[t > T ? (uint32_t)(t - T) : 0u], 1u);
+                srt[pos] = (uint16_t)k;
+            }
+            __syncthreads();
+            // each segment of equal timestamps into rec_less order
+            for (uint32_t bi = tid; bi < nb; bi += 256) {
+                const uint32_t s0 = bi ? bins[bi - 1] : 0u, s1 = bins[bi];
+                for (uint32_t x = s0 + 1; x < s1; ++x) {
+                    const uint16_t k = srt[x];
+                    uint32_t y = x;
+                    while (y > s0 && rec_less(ea[k], eb[k], ea[srt[y - 1]], eb[srt[y - 1]])) {
+                        srt[y] = srt[y - 1];
+                        --y;
+                    }
+                    srt[y] = k;
+                }
+            }
+            __syncthreads();
+            for (uint32_t i = tid; i < nd; i += 256) {
+                const uint32_t k = srt[i];
+                uint4 GAS* q = gp(c.due) + (ib + (size_t)i * st) * 2;
+                q[0] = ea[k];
+                q[1] = eb[k];
+            }
+        } else {
+            // long windows: rank of every due record among the due ones (ties by
+            // arrival) = its position in the due run
+            for (uint32_t i = tid; i < nd; i += 256) {
+                const uint32_t k = dix[i];
+                const uint4 a = ea[k], b = eb[k];
+                uint32_t rank = 0;
+                for (uint32_t j = 0; j < nd; ++j) {
+                    const uint32_t m = dix[j];
+                    rank += (rec_less(ea[m], eb[m], a, b) || (j < i && !rec_less(a, b, ea[m], eb[m]))) ? 1u : 0u;
+                }
+                uint4 GAS* q = gp(c.due) + (ib + (size_t)rank * st) * 2;
+                q[0] = a;
+                q[1] = b;
+            }
         }
         if (tid == 0) {
             const uint32_t left = n - nd;

@@ -280,23 +280,23 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ void st32(uint32_t GAS* p, uint32_t v, uint64_t mask = 1) {
     uint64_t sv;
     asm volatile("s_mov_b64 %0, exec\n\ts_and_b64 exec, exec, %3\n\tglobal_store_dword %1, %2, off\n\t"
-                 "s_mov_b64 exec, %0" : "=&s"(sv) : "v"(p), "v"(v), "s"(mask) : "memory");
+                 "s_mov_b64 exec, %0" : "=&s"(sv) : "v"(p), "v"(v), "s"(mask) : "memory", "scc");
 }
 __device__ __forceinline__ void st128(uint4 GAS* p, uint4 v, uint64_t mask = 1) {
     uint64_t sv;
     const u32x4 d = {v.x, v.y, v.z, v.w};
     asm volatile("s_mov_b64 %0, exec\n\ts_and_b64 exec, exec, %3\n\tglobal_store_dwordx4 %1, %2, off\n\t"
-                 "s_mov_b64 exec, %0" : "=&s"(sv) : "v"(p), "v"(d), "s"(mask) : "memory");
+                 "s_mov_b64 exec, %0" : "=&s"(sv) : "v"(p), "v"(d), "s"(mask) : "memory", "scc");
 }
 __device__ __forceinline__ void st8(uint8_t GAS* p, uint32_t v, uint64_t mask = 1) {
     uint64_t sv;
     asm volatile("s_mov_b64 %0, exec\n\ts_and_b64 exec, exec, %3\n\tglobal_store_byte %1, %2, off\n\t"
-                 "s_mov_b64 exec, %0" : "=&s"(sv) : "v"(p), "v"(v), "s"(mask) : "memory");
+                 "s_mov_b64 exec, %0" : "=&s"(sv) : "v"(p), "v"(v), "s"(mask) : "memory", "scc");
 }
 __device__ __forceinline__ void atom_add64(unsigned long long GAS* p, uint64_t v, uint64_t mask = 1) {
     uint64_t sv;
     asm volatile("s_mov_b64 %0, exec\n\ts_and_b64 exec, exec, %3\n\tglobal_atomic_add_x2 %1, %2, off\n\t"
-                 "s_mov_b64 exec, %0" : "=&s"(sv) : "v"(p), "v"(v), "s"(mask) : "memory");
+                 "s_mov_b64 exec, %0" : "=&s"(sv) : "v"(p), "v"(v), "s"(mask) : "memory", "scc");
 }
 
 // wave.hip: the wave-per-replica kernel (geometry TW_GEO_WAVE)

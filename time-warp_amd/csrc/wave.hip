@@ -74,7 +74,7 @@ __device__ __forceinline__ uint64_t wave_min64(uint64_t v) {
 __device__ __forceinline__ void st64(uint64_t GAS* p, uint64_t v, uint64_t mask = 1) {
     uint64_t sv;
     asm volatile("s_mov_b64 %0, exec\n\ts_and_b64 exec, exec, %3\n\tglobal_store_dwordx2 %1, %2, off\n\t"
-                 "s_mov_b64 exec, %0" : "=&s"(sv) : "v"(p), "v"(v), "s"(mask) : "memory");
+                 "s_mov_b64 exec, %0" : "=&s"(sv) : "v"(p), "v"(v), "s"(mask) : "memory", "scc");
 }
 __device__ __forceinline__ void st_i64(int64_t GAS* p, int64_t v) { st64((uint64_t GAS*)p, (uint64_t)v); }
 
