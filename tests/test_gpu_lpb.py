@@ -182,3 +182,45 @@ def test_lpb_inbox_overflow_is_an_error(engine_mod, oracle_mod, recv_cap):
         with pytest.raises(engine_mod.EngineError, match=r"failed: -6 "):
             e.run()
     _compare_lpb(scn, engine_mod, oracle_mod)
+
+
+@pytest.mark.parametrize("windows", ["per_replica", "global"])
+@pytest.mark.parametrize("case", ["token_ring_two_phase", "token_ring_many_nodes", "hotspot_heavy", "gossip"])
+def test_lpb_grid_stride_work_list(engine_mod, oracle_mod, monkeypatch, case, windows):
+    """Contexts of more than TW_LP_GRID workgroups of lanes (C3's 33.6M lanes
+    at 8,192 replicas) launch TW_LP_GRID workgroups that walk the window's
+    work list grid-stride; a grid of 3 workgroups makes every list take many
+    passes.  Both window modes: every replica in its own window (the default)
+    and one window for the whole batch (TW_LPB_GLOBAL=1, where the work-list
+    scan skips idle 256-lane blocks)."""
+    monkeypatch.setenv("TW_LP_GRID", "3")
+    if windows == "global":
+        monkeypatch.setenv("TW_LPB_GLOBAL", "1")
+    scn = {
+        "token_ring_two_phase": lambda: scenarios.token_ring(n_nodes=16, n_replicas=64, launch_duration=40_000_000,
+                                                             drop_log2=3),
+        "token_ring_many_nodes": lambda: scenarios.token_ring(n_nodes=4096, n_replicas=4, launch_duration=20_000_000,
+                                                              drop_log2=10),
+        "hotspot_heavy": lambda: scenarios.hotspot(n_senders=64, n_replicas=32, msg_num=60),
+        "gossip": lambda: scenarios.gossip(n_nodes=4096, fanout=4),
+    }[case]()
+    _compare_lpb(scn, engine_mod, oracle_mod, threads=1 if case == "gossip" else 8)
+
+
+@pytest.mark.parametrize("case", ["token_ring_drift", "hotspot"])
+def test_lpb_per_replica_windows_fewer(engine_mod, oracle_mod, monkeypatch, case):
+    """Per-replica windows: the replicas' token hops drift apart, so one
+    window for the whole batch has to cover the union of their event times;
+    every replica in its own window takes fewer windows for the same,
+    bit-exact outputs."""
+    scn = {
+        "token_ring_drift": lambda: scenarios.token_ring(n_nodes=32, n_replicas=64, launch_duration=30_000_000,
+                                                         drop_log2=6),
+        "hotspot": lambda: scenarios.hotspot(n_senders=16, n_replicas=32, msg_num=40),
+    }[case]()
+    _, _, w_rep = _compare_lpb(scn, engine_mod, oracle_mod)
+    monkeypatch.setenv("TW_LPB_GLOBAL", "1")
+    _, _, w_glob = _compare_lpb(scn, engine_mod, oracle_mod)
+    assert w_rep <= w_glob, (w_rep, w_glob)
+    if case == "token_ring_drift":
+        assert w_rep < w_glob, (w_rep, w_glob)

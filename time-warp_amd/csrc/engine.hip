@@ -65,6 +65,9 @@
 // work-list buckets by pending delivery records (tw_lp_compact).  Measured
 // with 4 buckets: C4 1.45 vs 1.58 G events/s -- pending records do not predict
 // a node's events in the window (most arrive for later windows) -- so 1.
+// LP event kernel: a context of more lanes than this many workgroups hold
+// (16384 x 128 = 2M) launches this many, walking the work list grid-stride
+#define TW_LP_GRID 16384u
 #ifndef TW_LP_NB
 #define TW_LP_NB 1
 #endif
@@ -1839,7 +1842,11 @@ __global__ void __launch_bounds__(TW_WG) tw_init_kernel(Dev c, uint32_t main_pc,
         gp(c.inbox_n)[c.R + r] = 0;
         if (c.lpb) gp(c.spawn_n)[r] = 0;
         gp(c.wake)[r] = INT64_MAX;
-        gp(c.listed)[r] = 0;  // marked for the first window: it serves every node
+        lp_mark(c, r, 0);  // marked for the first window: it serves every node
+        if ((r & ((1u << TW_SUB_LG) - 1u)) == 0) {
+            gp(c.sb_scan)[r >> TW_SUB_LG] = 0xFFFFFFFFu;
+            gp(c.sb_min)[r >> TW_SUB_LG] = INT64_MAX;
+        }
         return;
     }
     if (nv_init)
@@ -1866,7 +1873,7 @@ __host__ __device__ constexpr size_t fixed_lds_bytes() {
 // RUNS = false (the compact geometry): no far runs, and built for two waves
 // per SIMD (<= 256 registers, half the LDS of a dense lane), so 1M-replica
 // batches keep two workgroups per CU
-template <bool LP, int WG, int NC, int TPW = 64, bool RUNS = true>
+template <bool LP, int WG, int NC, int TPW = 64, bool RUNS = true, bool GS = false>
 __global__ void __launch_bounds__(WG * 64 / TPW)
     __attribute__((amdgpu_waves_per_eu((LP || !RUNS) ? 2 : (WG * 64 / TPW + 255) / 256, 2)))
 tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
@@ -1875,10 +1882,12 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
     // window's first tick (the only one that drains inboxes) come from the device
     bool fresh = true;
     uint32_t ph = 0;
+    int64_t lwin = 0;  // the lookahead (per-replica windows: t_end is the lane's replica's)
     if (LP && c.win) {
         const int64_t GAS* w = gp(c.win);
         const int64_t fl = w[WN_FLAGS];
         if (fl & WN_DONE) return;
+        lwin = w[WN_L];
         t_end = w[WN_T] + w[WN_L] - 1;
         c.act_cur = (uint32_t)w[WN_ACT];
         c.wid = (uint32_t)w[WN_WID];
@@ -1914,404 +1923,415 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
     if (TPW < 64 && (threadIdx.x & 63u) >= TPW) return;
     const uint32_t wbase = (threadIdx.x >> 6) * TPW;  // the wave's first lane in the LDS layout
     const uint32_t li = wbase + (threadIdx.x & 63u);
-    uint32_t r = blockIdx.x * WG + li;
-    if (LP) {
-        const uint32_t i = blockIdx.x * WG + li;
-        if (i >= lp_n) return;
-        r = gp(c.act)[(size_t)c.act_cur * TW_LP_NB * c.R + i];
-    }
-    if (r >= c.R) return;
-    if (LP && c.phase && gp(c.phase)[(c.lp0 + r) >> c.rep_lg] != ph) return;  // the other phase's node
-    uint64_t* sc = gp(c.scal) + r;
-    const size_t R = c.R;
-    if (sc[SC_STATUS * R] != TW_REP_RUNNING) return;
-    // LP: a node with no live thread, nothing to drain, no due run and no
-    // spawn record has nothing to do in this window (every live thread holds
-    // its one queued event; a superseded entry left behind pops without effect
-    // whenever the node wakes again).  A light inbox (<= TW_LIGHT records) is
-    // drained into the queue at the window's first tick; a heavy one was
-    // sorted by tw_lp_due into this window's due run and the records due later.
-    uint32_t n_in = 0, ipar = 0;
-    bool ilight = false;
-    if (LP) {
-        ilight = ib_cap(c, r) <= TW_LIGHT;
-        ipar = (c.dpar && c.win && ilight) ? (c.wid & 1u) : 0u;  // the buffer the last window filled
-        n_in = gp(c.inbox_n)[(size_t)ipar * R + r];
-        const bool drain = fresh && n_in != 0 && ilight;
-        if (sc[SC_LIVE * R] == 0 && sc[SC_PENDING_MAIN * R] == 0 && !drain && sc[SC_DUE_H * R] >= sc[SC_DUE_N * R] &&
-            !(c.lpb && gp(c.spawn_n)[r]))
-            return;
-    }
+    // GS (LP contexts of more than TW_LP_GRID workgroups of lanes): the
+    // workgroups walk the window's work list grid-stride, so a list of a few
+    // thousand lanes out of millions dispatches no empty workgroups (the loop
+    // costs registers: the smaller LP contexts launch one workgroup per WG lanes)
+    for (uint32_t blk = blockIdx.x;; blk += gridDim.x) {
+        do {
+            uint32_t r = blk * WG + li;
+            if (LP) {
+                const uint32_t i = blk * WG + li;
+                if (i >= lp_n) break;  // (the next block of the work list)
+                r = gp(c.act)[(size_t)c.act_cur * TW_LP_NB * c.R + i];
+            }
+            if (r >= c.R) break;  // (the next block of the work list)
+            if (LP && c.phase && gp(c.phase)[(c.lp0 + r) >> c.rep_lg] != ph) break;  // the other phase's node
+            uint64_t* sc = gp(c.scal) + r;
+            const size_t R = c.R;
+            if (sc[SC_STATUS * R] != TW_REP_RUNNING) break;  // (the next block of the work list)
+            const int64_t te = (LP && c.rw && c.win) ? rw_tend(c, r, lwin) : t_end;  // this lane's window end
+            // LP: a node with no live thread, nothing to drain, no due run and no
+            // spawn record has nothing to do in this window (every live thread holds
+            // its one queued event; a superseded entry left behind pops without effect
+            // whenever the node wakes again).  A light inbox (<= TW_LIGHT records) is
+            // drained into the queue at the window's first tick; a heavy one was
+            // sorted by tw_lp_due into this window's due run and the records due later.
+            uint32_t n_in = 0, ipar = 0;
+            bool ilight = false;
+            if (LP) {
+                ilight = ib_cap(c, r) <= TW_LIGHT;
+                ipar = (c.dpar && c.win && ilight) ? (c.wid & 1u) : 0u;  // the buffer the last window filled
+                n_in = gp(c.inbox_n)[(size_t)ipar * R + r];
+                const bool drain = fresh && n_in != 0 && ilight;
+                if (sc[SC_LIVE * R] == 0 && sc[SC_PENDING_MAIN * R] == 0 && !drain && sc[SC_DUE_H * R] >= sc[SC_DUE_N * R] &&
+                    !(c.lpb && gp(c.spawn_n)[r]))
+                    break;  // (the next block of the work list)
+            }
 
-    Lane<LP, WG, NC, RUNS> L;
-    L.c = c;
-    L.r = r;
-    L.nk = s_k + li;
-    L.ns = s_s + li;
-    L.rf = s_rf + li;
-    L.cw = s_cw + li;
-    L.pfs = s_pf + li;
-    L.rq = s_rq + li;
-    L.pfs_wave = __builtin_amdgcn_readfirstlane((uint32_t)(size_t)(s_pf + wbase));
-    L.P = s_p;
-    L.PU = s_u;
-    L.K = s_c;
-    L.pf_slot = 0xFFFFFFFFu;
-    L.prun = -1;
-    L.hacc = 0;
-    L.hnode = 0xFFFFFFFFu;
-    L.now = (int64_t)sc[SC_NOW * R]; L.final_t = (int64_t)sc[SC_FINAL_T * R];
-    L.seq = (uint32_t)sc[SC_SEQ * R]; L.tidc = (uint32_t)sc[SC_TIDC * R]; L.live = (uint32_t)sc[SC_LIVE * R];
-    const uint32_t near_n0 = (uint32_t)sc[SC_NEAR_N * R];
-    L.far_n = (uint32_t)sc[SC_FAR_N * R];
-    L.status = (uint32_t)sc[SC_STATUS * R];
-    L.free_n = (uint32_t)sc[SC_FREE_N * R]; L.ftop = (uint32_t)sc[SC_FTOP * R]; L.bump = (uint32_t)sc[SC_BUMP * R];
-#pragma unroll
-    for (int w = 0; w < CW_COUNT; ++w) L.cs(w, 0);
-    L.cs(CW_MAINEXC, (uint32_t)sc[SC_MAIN_EXC * R]);
-    L.cs(CW_TMO, (uint32_t)sc[SC_TMO_CTR * R]);
-    L.cs(CW_TRN, (uint32_t)sc[SC_TRACE_N * R]);
-    const uint64_t events0 = sc[SC_EVENTS * R];
-    const uint64_t ev_room64 = max_events > events0 ? max_events - events0 : 0;
-    const uint32_t ev_room = ev_room64 > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)ev_room64;
-    L.t_end = t_end;
-    L.ev_room = ev_room;
-    L.d_ev = 0;
-    L.d_th = 0;
-    if (L.far_n) L.set_ftop(L.far_ld(0));
-    L.rlc_link = 0xFFFFFFFFu;
-    L.rlc_rev = 0;
-    L.oo = 0;
-    if constexpr (LP) {
-        L.oo = gp(c.out_off)[(c.lp0 + r) >> c.rep_lg];  // (the lane's node: every thread of an LP lane runs on it)
-        const uint32_t dn = (uint32_t)sc[SC_DUE_N * R], dh = (uint32_t)sc[SC_DUE_H * R];
-        const size_t ib = ib_base(c, r);
-        L.ds(DW_IB, (uint32_t)ib);
-        L.ds(DW_HN, dh | (dn << 16));
-        L.ds(DW_SQ0, (uint32_t)sc[SC_DUE_SEQ * R]);
-        uint4 h = make_uint4(0, 0, 0, 0);
-        if (dh < dn) h = gp(c.due)[(ib + (size_t)dh * ib_stride(c)) * 2];
-        L.ds(DW_TL, h.x);
-        L.ds(DW_TH, h.y);
-    }
-    if constexpr (HR) {
-        uint32_t rh4[TW_RUNS];
-#pragma unroll
-        for (int j = 0; j < TW_RUNS; ++j) {
-            // (no far runs configured, e.g. LP nodes: nothing to load)
-            const uint32_t rh = c.Cr ? (uint32_t)sc[(SC_RH0 + j) * R] : 0u;
-            const uint32_t rn = c.Cr ? (uint32_t)sc[(SC_RC0 + j) * R] : 0u;
-            rh4[j] = rh;
-            uint4 h = make_uint4(0, 0, 0, 0), s2 = h, u = h;
-            if (rn) {
-                h = *L.run_at(j, rh);
-                uint32_t tp = rh + rn - 1;
-                if (tp >= c.Cr) tp -= c.Cr;
-                u = *L.run_at(j, tp);
-                if (rn >= 2) s2 = *L.run_at(j, rh + 1 == c.Cr ? 0 : rh + 1);
+            Lane<LP, WG, NC, RUNS> L;
+            L.c = c;
+            L.r = r;
+            L.nk = s_k + li;
+            L.ns = s_s + li;
+            L.rf = s_rf + li;
+            L.cw = s_cw + li;
+            L.pfs = s_pf + li;
+            L.rq = s_rq + li;
+            L.pfs_wave = __builtin_amdgcn_readfirstlane((uint32_t)(size_t)(s_pf + wbase));
+            L.P = s_p;
+            L.PU = s_u;
+            L.K = s_c;
+            L.pf_slot = 0xFFFFFFFFu;
+            L.prun = -1;
+            L.hacc = 0;
+            L.hnode = 0xFFFFFFFFu;
+            L.now = (int64_t)sc[SC_NOW * R]; L.final_t = (int64_t)sc[SC_FINAL_T * R];
+            L.seq = (uint32_t)sc[SC_SEQ * R]; L.tidc = (uint32_t)sc[SC_TIDC * R]; L.live = (uint32_t)sc[SC_LIVE * R];
+            const uint32_t near_n0 = (uint32_t)sc[SC_NEAR_N * R];
+            L.far_n = (uint32_t)sc[SC_FAR_N * R];
+            L.status = (uint32_t)sc[SC_STATUS * R];
+            L.free_n = (uint32_t)sc[SC_FREE_N * R]; L.ftop = (uint32_t)sc[SC_FTOP * R]; L.bump = (uint32_t)sc[SC_BUMP * R];
+        #pragma unroll
+            for (int w = 0; w < CW_COUNT; ++w) L.cs(w, 0);
+            L.cs(CW_MAINEXC, (uint32_t)sc[SC_MAIN_EXC * R]);
+            L.cs(CW_TMO, (uint32_t)sc[SC_TMO_CTR * R]);
+            L.cs(CW_TRN, (uint32_t)sc[SC_TRACE_N * R]);
+            const uint64_t events0 = sc[SC_EVENTS * R];
+            const uint64_t ev_room64 = max_events > events0 ? max_events - events0 : 0;
+            const uint32_t ev_room = ev_room64 > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)ev_room64;
+            L.t_end = te;
+            L.ev_room = ev_room;
+            L.d_ev = 0;
+            L.d_th = 0;
+            if (L.far_n) L.set_ftop(L.far_ld(0));
+            L.rlc_link = 0xFFFFFFFFu;
+            L.rlc_rev = 0;
+            L.oo = 0;
+            if constexpr (LP) {
+                L.oo = gp(c.out_off)[(c.lp0 + r) >> c.rep_lg];  // (the lane's node: every thread of an LP lane runs on it)
+                const uint32_t dn = (uint32_t)sc[SC_DUE_N * R], dh = (uint32_t)sc[SC_DUE_H * R];
+                const size_t ib = ib_base(c, r);
+                L.ds(DW_IB, (uint32_t)ib);
+                L.ds(DW_HN, dh | (dn << 16));
+                L.ds(DW_SQ0, (uint32_t)sc[SC_DUE_SEQ * R]);
+                uint4 h = make_uint4(0, 0, 0, 0);
+                if (dh < dn) h = gp(c.due)[(ib + (size_t)dh * ib_stride(c)) * 2];
+                L.ds(DW_TL, h.x);
+                L.ds(DW_TH, h.y);
             }
-            *L.rqp(RQ_HEAD + j) = h;
-            *L.rqp(RQ_SEC + j) = s2;
-            *L.rqp(RQ_TAIL + j) = make_uint4(u.x, u.y, u.w, rn);
-        }
-        *L.rqp(RQ_IDX) = make_uint4(rh4[0], rh4[1], rh4[2], rh4[3]);
-    }
-    L.far_min();
-    // near heap: the spill area holds heap positions [0, near_n) verbatim with
-    // absolute times; re-keyed to this launch's base (a common shift keeps the
-    // heap order) they go back in place, without sifting.  An entry too far
-    // ahead for a 32-bit key (or an oversized spill) takes the pushing path.
-    L.nbase = L.now;
-    L.near_init();
-    {
-        bool fits = near_n0 <= (uint32_t)NC;
-        for (uint32_t j = 0; j < near_n0 && fits; ++j)
-            fits = (uint64_t)(ent_t(gp(c.near_spill)[(size_t)j * R + r]) - L.nbase) < 0xFFFFFFFFull;
-        if (fits) {
-            for (uint32_t j = 0; j < near_n0; ++j) {
-                const uint4 e = gp(c.near_spill)[(size_t)j * R + r];
-                L.nk[j * WG] = L.nkey(ent_t(e), e.w);
-                L.ns[j * WG] = e.z;
-            }
-            L.near_n = near_n0;
-            L.nrk = L.nk[0];
-            L.nrs = L.ns[0];
-        } else {
-            for (uint32_t j = 0; j < near_n0; ++j) {
-                uint4 e = gp(c.near_spill)[(size_t)j * R + r];
-                if (L.near_n < NC && (uint64_t)(ent_t(e) - L.nbase) < 0xFFFFFFFFull) {
-                    L.near_push(ent_t(e), e.w, e.z);
-                    continue;
+            if constexpr (HR) {
+                uint32_t rh4[TW_RUNS];
+        #pragma unroll
+                for (int j = 0; j < TW_RUNS; ++j) {
+                    // (no far runs configured, e.g. LP nodes: nothing to load)
+                    const uint32_t rh = c.Cr ? (uint32_t)sc[(SC_RH0 + j) * R] : 0u;
+                    const uint32_t rn = c.Cr ? (uint32_t)sc[(SC_RC0 + j) * R] : 0u;
+                    rh4[j] = rh;
+                    uint4 h = make_uint4(0, 0, 0, 0), s2 = h, u = h;
+                    if (rn) {
+                        h = *L.run_at(j, rh);
+                        uint32_t tp = rh + rn - 1;
+                        if (tp >= c.Cr) tp -= c.Cr;
+                        u = *L.run_at(j, tp);
+                        if (rn >= 2) s2 = *L.run_at(j, rh + 1 == c.Cr ? 0 : rh + 1);
+                    }
+                    *L.rqp(RQ_HEAD + j) = h;
+                    *L.rqp(RQ_SEC + j) = s2;
+                    *L.rqp(RQ_TAIL + j) = make_uint4(u.x, u.y, u.w, rn);
                 }
-                L.push_far(ent_t(e), e.w, e.z);  // the thread's F_NEARQ hint only speeds up throwTo
+                *L.rqp(RQ_IDX) = make_uint4(rh4[0], rh4[1], rh4[2], rh4[3]);
             }
-        }
-    }
-
-    if (LP && fresh && n_in != 0 && ilight) {
-        // delivery records addressed to this node become phantom deliverer
-        // threads, inserted in (t, link, payload, src, kind) order (rec_less, the
-        // order tw_lp_due gives a heavy lane's due run) so queue seqs are
-        // deterministic whatever order the records arrived in
-        const size_t ib = (size_t)ipar * c.ib_total + ib_base(c, r), ist = ib_stride(c);
-        const uint32_t cap = ib_cap(c, r);  // (an overflowed inbox -- lp_err set -- keeps its first cap)
-        if (n_in > cap) {
-            L.fail(TW_REP_ERR_QUEUE);
-            n_in = cap;
-        }
-        uint32_t used = 0;  // bitmask, n_in <= TW_LIGHT = 32
-        for (uint32_t k = 0; k < n_in && L.status == TW_REP_RUNNING; ++k) {
-            int best = -1;
-            uint4 ba = make_uint4(0, 0, 0, 0), bb = ba;
-            for (uint32_t j = 0; j < n_in; ++j) {
-                if (used & (1u << j)) continue;
-                const uint4 GAS* q = gp(c.inbox) + (ib + (size_t)j * ist) * 2;
-                uint4 ea = q[0], eb = q[1];
-                if (best < 0 || rec_less(ea, eb, ba, bb)) { best = (int)j; ba = ea; bb = eb; }
-            }
-            used |= 1u << best;
-            int64_t ta = ent_t(ba);
-            if (ta < L.now) {  // delivered after the node ran past it: not conservative
-                L.fail(TW_REP_ERR_INSN);
-                break;
-            }
-            uint32_t s = L.alloc_slot();
-            if (s == 0xFFFFFFFFu) break;
-            Th ph;
-            ph.w0 = ((TW_PC_DELIVER_STUB + 1) & 0xFFFFu) | ((F_STARTED | F_PHANTOM) << FL_SHIFT);
-            ph.w1 = (c.lp0 + r) >> c.rep_lg;
-            ph.w2 = 0xFFFFFFFEu;  // never a throwTo target
-            ph.w3 = 0;
-            ph.f0 = ph.f1 = ph.xl = ph.xh = 0;
-            ph.r0 = (int64_t)(((uint64_t)ba.w << 32) | ba.z);  // payload
-            ph.r1 = bb.x;                                     // link
-            ph.r2 = bb.z;                                     // sending node
-            ph.r3 = bb.y;                                     // kind
-            L.enqueue(ph, s, ta);
-            L.put_rec(s, ph);
-        }
-        gp(c.inbox_n)[(size_t)ipar * R + r] = 0;
-    }
-    if (LP && c.lpb) {
-        // batched LP: children forked onto this node by another node of the
-        // replica (emit_spawn), queued at their fork time
-        uint32_t nsp = gp(c.spawn_n)[r];
-        if (nsp) {
-            if (nsp > TW_SPN) {
-                L.fail(TW_REP_ERR_QUEUE);
-                nsp = TW_SPN;
-            }
-            for (uint32_t k = 0; k < nsp && L.status == TW_REP_RUNNING; ++k) {
-                const uint4 GAS* q = gp(c.spawn) + ((size_t)k * R + r) * 4;
-                const uint4 a = q[0], b = q[1], d = q[2], e = q[3];
-                const int64_t t = ent_t(a);
-                if (t < L.now) {  // the lane already ran past the fork time: not conservative
-                    L.fail(TW_REP_ERR_INSN);
-                    break;
-                }
-                const uint32_t s = L.alloc_slot();
-                if (s == 0xFFFFFFFFu) break;
-                if (L.tidc == 0xFFFFFFFFu) {
-                    L.fail(TW_REP_ERR_COUNTER);
-                    break;
-                }
-                Th ch;
-                ch.w0 = b.x & 0xFFFFu;
-                ch.w1 = (c.lp0 + r) >> c.rep_lg;
-                ch.w2 = L.tidc++;
-                ch.w3 = 0;
-                ch.f0 = ch.f1 = ch.xl = ch.xh = 0;
-                ch.r0 = (int64_t)(((uint64_t)a.w << 32) | a.z);
-                ch.r1 = (int64_t)(((uint64_t)d.y << 32) | d.x);
-                ch.r2 = (int64_t)(((uint64_t)d.w << 32) | d.z);
-                ch.r3 = (int64_t)(((uint64_t)e.z << 32) | e.x);
-                ++L.d_th;
-                L.enqueue(ch, s, t);
-                L.put_rec(s, ch);
-            }
-            gp(c.spawn_n)[r] = 0;
-        }
-    }
-
-#ifdef TW_STATS
-    for (int i = 0; i < P_COUNT; ++i) L.st[i] = 0;
-#endif
-    uint32_t pending_main = (uint32_t)sc[SC_PENDING_MAIN * R];
-    // nothing loaded before the loop may stay pending into it (a loop-header
-    // wait would otherwise drain the counter on every iteration)
-    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
-    // The loop is wave-uniform: a lane that stops (quiescence, t_end, event
-    // cap, error) just idles through the remaining iterations, so no per-lane
-    // break/continue splits the wave's control flow.
-    bool alive = L.status == TW_REP_RUNNING;
-    for (uint32_t it = 0; it < budget; ++it) {
-        if (!__builtin_amdgcn_ballot_w64(alive)) break;
-        STIME(tl0);
-        STATL(K_ITER);  // lane-iterations, idle lanes included (pops / this = lane efficiency)
-        Th th;
-        uint32_t slot = 0;
-        bool run = false;
-        // the rare cases (main's first run, quiescence, the event cap) behind one
-        // wave-uniform branch; the common path is a single divergent region
-        const bool rare = alive && (pending_main || L.live == 0 || L.d_ev >= ev_room);
-        if (__builtin_amdgcn_ballot_w64(rare)) {
-            if (rare && pending_main) {  // runInSandbox main (TimedT.hs:237): runs at t=0, not a pop
-                pending_main = 0;
-                L.pf_slot = 0xFFFFFFFFu;
-                L.fetch_rec(0, th);
-                L.rf[0] = th.r0; L.rf[WG] = th.r1; L.rf[2 * WG] = th.r2; L.rf[3 * WG] = th.r3;
-                L.hnode = th.w1;
-                run = true;
-            } else if (rare) {  // whileM_ notDone, or this launch's event cap
-                if (!LP && L.live == 0) L.status = TW_REP_DONE;  // an LP may still receive records
-                alive = false;
-            }
-        }
-        bool popping = alive && !rare;
-        L.q1d = false;
-        {
-            // PQ.minView: the min of the near root and the far sources
-            if (L.far_dirty) L.far_min();
-            const bool use_near = L.near_n != 0;
-            const int64_t tn = L.nbase + (int64_t)(L.nrk >> 32);
-            const bool use_far = L.fsrc >= 0 && (!use_near || tless(L.fmt, L.fms, tn, (uint32_t)L.nrk));
-            const int64_t t = use_far ? L.fmt : tn;
-            const uint32_t sq = use_far ? L.fms : (uint32_t)L.nrk;
-            slot = use_far ? L.fmsl : (use_near ? L.nrs : 0u);
-            STIME(ts1);
-            STADDL(K_CYC_SEL, ts1 - tl0);
-            // parked beyond t_end (an empty queue cannot happen while live > 0)
-            const bool parked = popping && ((!use_near && !use_far) || t > t_end);
-            alive = parked ? false : alive;
-            popping = popping && !parked;
-            if (popping) {
-                {
-                    const bool due = LP && use_far && L.fsrc == 0;
-                    if (due) L.due_pop(th, slot, sq);
-                    else L.fetch_rec(slot, th);  // prefetched copy or HBM
-                    STIME(ts2);
-                    STADDL(K_CYC_FETCH, ts2 - ts1);
-                    if (due) {
-                    } else if (!use_far) L.near_pop();
-                    else if (L.fsrc == TW_RUNS) L.far_pop();
-                    else L.run_pop(L.fsrc);
-                    STIME(ts3);
-                    STADDL(K_CYC_QPOP, ts3 - ts2);
-                    if (slot == L.pf_slot) L.pf_slot = 0xFFFFFFFFu;
-                    if (th.w3 != sq) {
-                        STATL(K_SUPERSEDED);  // superseded by a throwTo re-stamp
-                    } else {
-                        STATL(K_POP);
-                        // curTime .= timestamp (TimedT.hs:241-247)
-                        th.w3 = 0;
-                        --L.live;
-                        L.now = t;
-                        if (t - L.nbase > (int64_t)0x7FFFFFFF) L.near_rebase(t);
-                        L.hnode = th.w1;
-                        L.rf[0] = th.r0; L.rf[WG] = th.r1; L.rf[2 * WG] = th.r2; L.rf[3 * WG] = th.r3;
-                        // LP phantom = the deliverer's wake, already counted and hashed by the sender
-                        const bool phantom = LP && (th_flags(th) & F_PHANTOM);
-                        if (!phantom) {
-                            L.final_t = LP ? (t > L.final_t ? t : L.final_t) : t;
-                            ++L.d_ev;
+            L.far_min();
+            // near heap: the spill area holds heap positions [0, near_n) verbatim with
+            // absolute times; re-keyed to this launch's base (a common shift keeps the
+            // heap order) they go back in place, without sifting.  An entry too far
+            // ahead for a 32-bit key (or an oversized spill) takes the pushing path.
+            L.nbase = L.now;
+            L.near_init();
+            {
+                bool fits = near_n0 <= (uint32_t)NC;
+                for (uint32_t j = 0; j < near_n0 && fits; ++j)
+                    fits = (uint64_t)(ent_t(gp(c.near_spill)[(size_t)j * R + r]) - L.nbase) < 0xFFFFFFFFull;
+                if (fits) {
+                    for (uint32_t j = 0; j < near_n0; ++j) {
+                        const uint4 e = gp(c.near_spill)[(size_t)j * R + r];
+                        L.nk[j * WG] = L.nkey(ent_t(e), e.w);
+                        L.ns[j * WG] = e.z;
+                    }
+                    L.near_n = near_n0;
+                    L.nrk = L.nk[0];
+                    L.nrs = L.ns[0];
+                } else {
+                    for (uint32_t j = 0; j < near_n0; ++j) {
+                        uint4 e = gp(c.near_spill)[(size_t)j * R + r];
+                        if (L.near_n < NC && (uint64_t)(ent_t(e) - L.nbase) < 0xFFFFFFFFull) {
+                            L.near_push(ent_t(e), e.w, e.z);
+                            continue;
                         }
-                        const uint32_t exc = th_exc(th);  // asyncExceptions . at tid <<.= Nothing (:252)
-                        if (exc) {
-                            const int64_t val = th_xval(th);
-                            th_set_exc(th, 0);
-                            th.xl = th.xh = 0;
-                            L.q1d = true;
-                            L.hacc += term0(t, TW_KIND_EXC | exc);
-                            if (!(th_flags(th) & (F_STARTED | F_MAIN))) {  // escapes launchTimedT (:252-263)
-                                L.status = TW_REP_ABORTED;
-                                L.cs(CW_MAINEXC, exc);
-                                L.put_rec(slot, th);
-                            } else {
-                                run = L.unwind(th, slot, exc, val);
-                            }
-                        } else {
-                            if (!phantom) L.hacc += term0(t, TW_KIND_RESUME | th_pc(th));
-                            run = true;
-                        }
+                        L.push_far(ent_t(e), e.w, e.z);  // the thread's F_NEARQ hint only speeds up throwTo
                     }
                 }
             }
-        }
-        if (!popping) slot = 0u;  // main's first run is slot 0; idle lanes do not use it
-        STIME(tp0);
-        L.prefetch_all(run ? slot : 0xFFFFFFFFu);
-        STIME(tl1);
-        STADDL(K_CYC_PF, tl1 - tp0);
-        STADDL(K_CYC_POP, tl1 - tl0);
-        L.step(th, slot, run);
-        STIME(th0);
-        L.hash_flush_all();
-        STIME(th1);
-        STADDL(K_CYC_HASH, th1 - th0);
-        alive = alive && L.status == TW_REP_RUNNING;
-        STIME(tl2);
-        STADDL(K_CYC_TAIL, tl2 - tl1);
-    }
-    L.hash_flush();
-    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
-    L.run_commit();
-#ifdef TW_STATS
-    if (c.prof)
-        for (int i = 0; i < P_COUNT; ++i)
-            __hip_atomic_fetch_add(gp(c.prof) + i, (unsigned long long)L.st[i], __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
-#endif
-    sc[SC_PENDING_MAIN * R] = pending_main;
-    if (!LP && L.status == TW_REP_RUNNING && L.live == 0) L.status = TW_REP_DONE;
 
-    sc[SC_NOW * R] = (uint64_t)L.now; sc[SC_FINAL_T * R] = (uint64_t)L.final_t;
-    sc[SC_SEQ * R] = L.seq; sc[SC_TIDC * R] = L.tidc; sc[SC_LIVE * R] = L.live;
-    sc[SC_NEAR_N * R] = L.near_n; sc[SC_FAR_N * R] = L.far_n;
-    sc[SC_STATUS * R] = L.status; sc[SC_MAIN_EXC * R] = L.cg(CW_MAINEXC);
-    sc[SC_FREE_N * R] = L.free_n; sc[SC_FTOP * R] = L.ftop; sc[SC_BUMP * R] = L.bump;
-    sc[SC_TMO_CTR * R] = L.cg(CW_TMO);
-    sc[SC_TRACE_N * R] = L.cg(CW_TRN);
-    sc[SC_EVENTS * R] = events0 + L.d_ev;
-    if (LP) {
-        sc[SC_DUE_H * R] = L.dg(DW_HN) & 0xFFFFu;
-        if (L.dg(DW_IB) >> 31)  // sent records straight into inboxes (Lane::emit)
-            min_hot((uint64_t GAS*)(gp(c.win) + WN_REC_MIN), (uint64_t)(t_end + 1));
-    }
-    sc[SC_DELIVERED * R] += L.cg(CW_DL); sc[SC_DROPPED * R] += L.cg(CW_DR);
-    sc[SC_UNDELIV * R] += L.cg(CW_UD); sc[SC_THREADS * R] += L.d_th;
-    if (HR && c.Cr) {
-        const uint4 ix4 = *L.rqp(RQ_IDX);
-#pragma unroll
-        for (int j = 0; j < TW_RUNS; ++j) {
-            sc[(SC_RH0 + j) * R] = Lane<LP, WG, NC, RUNS>::q_at(ix4, j);
-            sc[(SC_RC0 + j) * R] = L.rqp(RQ_TAIL + j)->w;
-        }
-    }
-    for (uint32_t i = 0, j = 0; i < NC; ++i) {
-        const uint64_t k = L.nk[i * WG];
-        if (k != ~0ull)
-            gp(c.near_spill)[(size_t)(j++) * R + r] = ent(L.nbase + (int64_t)(k >> 32), L.ns[i * WG], (uint32_t)k);
-    }
-    bool active = L.status == TW_REP_RUNNING && L.d_ev < ev_room;
-    int64_t tn = INT64_MAX;
-    if (L.far_dirty) L.far_min();
-    if (L.near_n) tn = L.nbase + (int64_t)(L.nrk >> 32);
-    if (L.fsrc >= 0 && L.fmt < tn) tn = L.fmt;
-    if (active && (tn == INT64_MAX || tn > t_end) && !pending_main) active = false;  // parked beyond t_end
-    if (LP && L.status == TW_REP_RUNNING && tn != INT64_MAX) min_hot(gp(c.next_t), (uint64_t)tn);
-    {   // lanes still active: one atomic per wave
-        const uint64_t am = __builtin_amdgcn_ballot_w64(active);
-        const uint64_t ex = __builtin_amdgcn_ballot_w64(true);
-        if (am && __builtin_amdgcn_mbcnt_hi((uint32_t)(ex >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)ex, 0u)) == 0)
-            __hip_atomic_fetch_add(gp(c.n_active), (uint32_t)__builtin_popcountll(am), __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
-    }
-    if (LP) {
-        // device loop: the lane is listed again by the window its next event
-        // falls in (tw_lp_compact); host loop: for the next window
-        const bool more = L.status == TW_REP_RUNNING && (L.live || pending_main);
-        if (c.win) gp(c.wake)[r] = more ? (pending_main ? L.now : tn) : INT64_MAX;
-        else if (more) lp_list_next(c, r);
+            if (LP && fresh && n_in != 0 && ilight) {
+                // delivery records addressed to this node become phantom deliverer
+                // threads, inserted in (t, link, payload, src, kind) order (rec_less, the
+                // order tw_lp_due gives a heavy lane's due run) so queue seqs are
+                // deterministic whatever order the records arrived in
+                const size_t ib = (size_t)ipar * c.ib_total + ib_base(c, r), ist = ib_stride(c);
+                const uint32_t cap = ib_cap(c, r);  // (an overflowed inbox -- lp_err set -- keeps its first cap)
+                if (n_in > cap) {
+                    L.fail(TW_REP_ERR_QUEUE);
+                    n_in = cap;
+                }
+                uint32_t used = 0;  // bitmask, n_in <= TW_LIGHT = 32
+                for (uint32_t k = 0; k < n_in && L.status == TW_REP_RUNNING; ++k) {
+                    int best = -1;
+                    uint4 ba = make_uint4(0, 0, 0, 0), bb = ba;
+                    for (uint32_t j = 0; j < n_in; ++j) {
+                        if (used & (1u << j)) continue;
+                        const uint4 GAS* q = gp(c.inbox) + (ib + (size_t)j * ist) * 2;
+                        uint4 ea = q[0], eb = q[1];
+                        if (best < 0 || rec_less(ea, eb, ba, bb)) { best = (int)j; ba = ea; bb = eb; }
+                    }
+                    used |= 1u << best;
+                    int64_t ta = ent_t(ba);
+                    if (ta < L.now) {  // delivered after the node ran past it: not conservative
+                        L.fail(TW_REP_ERR_INSN);
+                        break;
+                    }
+                    uint32_t s = L.alloc_slot();
+                    if (s == 0xFFFFFFFFu) break;
+                    Th ph;
+                    ph.w0 = ((TW_PC_DELIVER_STUB + 1) & 0xFFFFu) | ((F_STARTED | F_PHANTOM) << FL_SHIFT);
+                    ph.w1 = (c.lp0 + r) >> c.rep_lg;
+                    ph.w2 = 0xFFFFFFFEu;  // never a throwTo target
+                    ph.w3 = 0;
+                    ph.f0 = ph.f1 = ph.xl = ph.xh = 0;
+                    ph.r0 = (int64_t)(((uint64_t)ba.w << 32) | ba.z);  // payload
+                    ph.r1 = bb.x;                                     // link
+                    ph.r2 = bb.z;                                     // sending node
+                    ph.r3 = bb.y;                                     // kind
+                    L.enqueue(ph, s, ta);
+                    L.put_rec(s, ph);
+                }
+                gp(c.inbox_n)[(size_t)ipar * R + r] = 0;
+            }
+            if (LP && c.lpb) {
+                // batched LP: children forked onto this node by another node of the
+                // replica (emit_spawn), queued at their fork time
+                uint32_t nsp = gp(c.spawn_n)[r];
+                if (nsp) {
+                    if (nsp > TW_SPN) {
+                        L.fail(TW_REP_ERR_QUEUE);
+                        nsp = TW_SPN;
+                    }
+                    for (uint32_t k = 0; k < nsp && L.status == TW_REP_RUNNING; ++k) {
+                        const uint4 GAS* q = gp(c.spawn) + ((size_t)k * R + r) * 4;
+                        const uint4 a = q[0], b = q[1], d = q[2], e = q[3];
+                        const int64_t t = ent_t(a);
+                        if (t < L.now) {  // the lane already ran past the fork time: not conservative
+                            L.fail(TW_REP_ERR_INSN);
+                            break;
+                        }
+                        const uint32_t s = L.alloc_slot();
+                        if (s == 0xFFFFFFFFu) break;
+                        if (L.tidc == 0xFFFFFFFFu) {
+                            L.fail(TW_REP_ERR_COUNTER);
+                            break;
+                        }
+                        Th ch;
+                        ch.w0 = b.x & 0xFFFFu;
+                        ch.w1 = (c.lp0 + r) >> c.rep_lg;
+                        ch.w2 = L.tidc++;
+                        ch.w3 = 0;
+                        ch.f0 = ch.f1 = ch.xl = ch.xh = 0;
+                        ch.r0 = (int64_t)(((uint64_t)a.w << 32) | a.z);
+                        ch.r1 = (int64_t)(((uint64_t)d.y << 32) | d.x);
+                        ch.r2 = (int64_t)(((uint64_t)d.w << 32) | d.z);
+                        ch.r3 = (int64_t)(((uint64_t)e.z << 32) | e.x);
+                        ++L.d_th;
+                        L.enqueue(ch, s, t);
+                        L.put_rec(s, ch);
+                    }
+                    gp(c.spawn_n)[r] = 0;
+                }
+            }
+
+        #ifdef TW_STATS
+            for (int i = 0; i < P_COUNT; ++i) L.st[i] = 0;
+        #endif
+            uint32_t pending_main = (uint32_t)sc[SC_PENDING_MAIN * R];
+            // nothing loaded before the loop may stay pending into it (a loop-header
+            // wait would otherwise drain the counter on every iteration)
+            __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+            // The loop is wave-uniform: a lane that stops (quiescence, t_end, event
+            // cap, error) just idles through the remaining iterations, so no per-lane
+            // break/continue splits the wave's control flow.
+            bool alive = L.status == TW_REP_RUNNING;
+            for (uint32_t it = 0; it < budget; ++it) {
+                if (!__builtin_amdgcn_ballot_w64(alive)) break;
+                STIME(tl0);
+                STATL(K_ITER);  // lane-iterations, idle lanes included (pops / this = lane efficiency)
+                Th th;
+                uint32_t slot = 0;
+                bool run = false;
+                // the rare cases (main's first run, quiescence, the event cap) behind one
+                // wave-uniform branch; the common path is a single divergent region
+                const bool rare = alive && (pending_main || L.live == 0 || L.d_ev >= ev_room);
+                if (__builtin_amdgcn_ballot_w64(rare)) {
+                    if (rare && pending_main) {  // runInSandbox main (TimedT.hs:237): runs at t=0, not a pop
+                        pending_main = 0;
+                        L.pf_slot = 0xFFFFFFFFu;
+                        L.fetch_rec(0, th);
+                        L.rf[0] = th.r0; L.rf[WG] = th.r1; L.rf[2 * WG] = th.r2; L.rf[3 * WG] = th.r3;
+                        L.hnode = th.w1;
+                        run = true;
+                    } else if (rare) {  // whileM_ notDone, or this launch's event cap
+                        if (!LP && L.live == 0) L.status = TW_REP_DONE;  // an LP may still receive records
+                        alive = false;
+                    }
+                }
+                bool popping = alive && !rare;
+                L.q1d = false;
+                {
+                    // PQ.minView: the min of the near root and the far sources
+                    if (L.far_dirty) L.far_min();
+                    const bool use_near = L.near_n != 0;
+                    const int64_t tn = L.nbase + (int64_t)(L.nrk >> 32);
+                    const bool use_far = L.fsrc >= 0 && (!use_near || tless(L.fmt, L.fms, tn, (uint32_t)L.nrk));
+                    const int64_t t = use_far ? L.fmt : tn;
+                    const uint32_t sq = use_far ? L.fms : (uint32_t)L.nrk;
+                    slot = use_far ? L.fmsl : (use_near ? L.nrs : 0u);
+                    STIME(ts1);
+                    STADDL(K_CYC_SEL, ts1 - tl0);
+                    // parked beyond t_end (an empty queue cannot happen while live > 0)
+                    const bool parked = popping && ((!use_near && !use_far) || t > te);
+                    alive = parked ? false : alive;
+                    popping = popping && !parked;
+                    if (popping) {
+                        {
+                            const bool due = LP && use_far && L.fsrc == 0;
+                            if (due) L.due_pop(th, slot, sq);
+                            else L.fetch_rec(slot, th);  // prefetched copy or HBM
+                            STIME(ts2);
+                            STADDL(K_CYC_FETCH, ts2 - ts1);
+                            if (due) {
+                            } else if (!use_far) L.near_pop();
+                            else if (L.fsrc == TW_RUNS) L.far_pop();
+                            else L.run_pop(L.fsrc);
+                            STIME(ts3);
+                            STADDL(K_CYC_QPOP, ts3 - ts2);
+                            if (slot == L.pf_slot) L.pf_slot = 0xFFFFFFFFu;
+                            if (th.w3 != sq) {
+                                STATL(K_SUPERSEDED);  // superseded by a throwTo re-stamp
+                            } else {
+                                STATL(K_POP);
+                                // curTime .= timestamp (TimedT.hs:241-247)
+                                th.w3 = 0;
+                                --L.live;
+                                L.now = t;
+                                if (t - L.nbase > (int64_t)0x7FFFFFFF) L.near_rebase(t);
+                                L.hnode = th.w1;
+                                L.rf[0] = th.r0; L.rf[WG] = th.r1; L.rf[2 * WG] = th.r2; L.rf[3 * WG] = th.r3;
+                                // LP phantom = the deliverer's wake, already counted and hashed by the sender
+                                const bool phantom = LP && (th_flags(th) & F_PHANTOM);
+                                if (!phantom) {
+                                    L.final_t = LP ? (t > L.final_t ? t : L.final_t) : t;
+                                    ++L.d_ev;
+                                }
+                                const uint32_t exc = th_exc(th);  // asyncExceptions . at tid <<.= Nothing (:252)
+                                if (exc) {
+                                    const int64_t val = th_xval(th);
+                                    th_set_exc(th, 0);
+                                    th.xl = th.xh = 0;
+                                    L.q1d = true;
+                                    L.hacc += term0(t, TW_KIND_EXC | exc);
+                                    if (!(th_flags(th) & (F_STARTED | F_MAIN))) {  // escapes launchTimedT (:252-263)
+                                        L.status = TW_REP_ABORTED;
+                                        L.cs(CW_MAINEXC, exc);
+                                        L.put_rec(slot, th);
+                                    } else {
+                                        run = L.unwind(th, slot, exc, val);
+                                    }
+                                } else {
+                                    if (!phantom) L.hacc += term0(t, TW_KIND_RESUME | th_pc(th));
+                                    run = true;
+                                }
+                            }
+                        }
+                    }
+                }
+                if (!popping) slot = 0u;  // main's first run is slot 0; idle lanes do not use it
+                STIME(tp0);
+                L.prefetch_all(run ? slot : 0xFFFFFFFFu);
+                STIME(tl1);
+                STADDL(K_CYC_PF, tl1 - tp0);
+                STADDL(K_CYC_POP, tl1 - tl0);
+                L.step(th, slot, run);
+                STIME(th0);
+                L.hash_flush_all();
+                STIME(th1);
+                STADDL(K_CYC_HASH, th1 - th0);
+                alive = alive && L.status == TW_REP_RUNNING;
+                STIME(tl2);
+                STADDL(K_CYC_TAIL, tl2 - tl1);
+            }
+            L.hash_flush();
+            __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+            L.run_commit();
+        #ifdef TW_STATS
+            if (c.prof)
+                for (int i = 0; i < P_COUNT; ++i)
+                    __hip_atomic_fetch_add(gp(c.prof) + i, (unsigned long long)L.st[i], __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+        #endif
+            sc[SC_PENDING_MAIN * R] = pending_main;
+            if (!LP && L.status == TW_REP_RUNNING && L.live == 0) L.status = TW_REP_DONE;
+
+            sc[SC_NOW * R] = (uint64_t)L.now; sc[SC_FINAL_T * R] = (uint64_t)L.final_t;
+            sc[SC_SEQ * R] = L.seq; sc[SC_TIDC * R] = L.tidc; sc[SC_LIVE * R] = L.live;
+            sc[SC_NEAR_N * R] = L.near_n; sc[SC_FAR_N * R] = L.far_n;
+            sc[SC_STATUS * R] = L.status; sc[SC_MAIN_EXC * R] = L.cg(CW_MAINEXC);
+            sc[SC_FREE_N * R] = L.free_n; sc[SC_FTOP * R] = L.ftop; sc[SC_BUMP * R] = L.bump;
+            sc[SC_TMO_CTR * R] = L.cg(CW_TMO);
+            sc[SC_TRACE_N * R] = L.cg(CW_TRN);
+            sc[SC_EVENTS * R] = events0 + L.d_ev;
+            if (LP) {
+                sc[SC_DUE_H * R] = L.dg(DW_HN) & 0xFFFFu;
+                if (L.dg(DW_IB) >> 31)  // sent records straight into inboxes (Lane::emit)
+                    min_hot((uint64_t GAS*)(c.rw ? rw_at(c, RW_WIN, r) : gp(c.win) + WN_REC_MIN), (uint64_t)(te + 1));
+            }
+            sc[SC_DELIVERED * R] += L.cg(CW_DL); sc[SC_DROPPED * R] += L.cg(CW_DR);
+            sc[SC_UNDELIV * R] += L.cg(CW_UD); sc[SC_THREADS * R] += L.d_th;
+            if (HR && c.Cr) {
+                const uint4 ix4 = *L.rqp(RQ_IDX);
+        #pragma unroll
+                for (int j = 0; j < TW_RUNS; ++j) {
+                    sc[(SC_RH0 + j) * R] = Lane<LP, WG, NC, RUNS>::q_at(ix4, j);
+                    sc[(SC_RC0 + j) * R] = L.rqp(RQ_TAIL + j)->w;
+                }
+            }
+            for (uint32_t i = 0, j = 0; i < NC; ++i) {
+                const uint64_t k = L.nk[i * WG];
+                if (k != ~0ull)
+                    gp(c.near_spill)[(size_t)(j++) * R + r] = ent(L.nbase + (int64_t)(k >> 32), L.ns[i * WG], (uint32_t)k);
+            }
+            bool active = L.status == TW_REP_RUNNING && L.d_ev < ev_room;
+            int64_t tn = INT64_MAX;
+            if (L.far_dirty) L.far_min();
+            if (L.near_n) tn = L.nbase + (int64_t)(L.nrk >> 32);
+            if (L.fsrc >= 0 && L.fmt < tn) tn = L.fmt;
+            if (active && (tn == INT64_MAX || tn > te) && !pending_main) active = false;  // parked beyond t_end
+            if (LP && L.status == TW_REP_RUNNING && tn != INT64_MAX)
+                min_hot((c.rw && c.win) ? (uint64_t GAS*)rw_at(c, RW_TICK, r) : gp(c.next_t), (uint64_t)tn);
+            {   // lanes still active: one atomic per wave
+                const uint64_t am = __builtin_amdgcn_ballot_w64(active);
+                const uint64_t ex = __builtin_amdgcn_ballot_w64(true);
+                if (am && __builtin_amdgcn_mbcnt_hi((uint32_t)(ex >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)ex, 0u)) == 0)
+                    __hip_atomic_fetch_add(gp(c.n_active), (uint32_t)__builtin_popcountll(am), __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+            }
+            if (LP) {
+                // device loop: the lane is listed again by the window its next event
+                // falls in (tw_lp_compact); host loop: for the next window
+                const bool more = L.status == TW_REP_RUNNING && (L.live || pending_main);
+                if (c.win) gp(c.wake)[r] = more ? (pending_main ? L.now : tn) : INT64_MAX;
+                else if (more) lp_list_next(c, r);
+            }
+        } while (0);
+        if (!(LP && GS) || (size_t)(blk + gridDim.x) * WG >= lp_n) break;
     }
 }
 
@@ -2335,7 +2355,12 @@ __device__ __forceinline__ void lp_deliver(const Dev& c, uint4 a, uint4 b, uint6
     q[1] = b;
     // (a record due in this window, t < wend -- a short link into a phase-1
     // node -- is drained at phase 1's first tick: it does not bound the next window)
-    if (upd_min && ent_t(a) >= wend) min_hot(tmin, (uint64_t)ent_t(a));
+    if (upd_min && c.rw && c.win) {  // per-replica windows: the record's replica's window and minimum
+        const int64_t te = rw_tend(c, lp, gp(c.win)[WN_L]);
+        if (ent_t(a) > te) min_hot((uint64_t GAS*)rw_at(c, RW_WIN, lp), (uint64_t)ent_t(a));
+    } else if (upd_min && ent_t(a) >= wend) {
+        min_hot(tmin, (uint64_t)ent_t(a));
+    }
     // a lane whose node may hold more than TW_LIGHT records is served by
     // tw_lp_due: its first pending record lists it for the next window's pass
     // (device loop; the list of window wid + 1)
@@ -2369,7 +2394,12 @@ __device__ __forceinline__ void lp_spawn(const Dev& c, const uint4 GAS* o, uint6
     // this tick's earliest spawn: one in the current window reruns it (tw_lp_fill),
     // with the target lane appended to the running window's work list (once)
     (void)tmin;
-    min_hot((uint64_t GAS*)(gp(c.win) + WN_SPN_MIN), (uint64_t)ent_t(a));
+    if (c.rw && c.win) {  // per-replica windows: the spawn bounds its replica's next window, or reruns this one
+        min_hot((uint64_t GAS*)rw_at(c, RW_TICK, lp), (uint64_t)ent_t(a));
+        if (ent_t(a) <= rw_tend(c, lp, gp(c.win)[WN_L])) gp(c.win)[WN_SPN_HERE] = 1;
+    } else {
+        min_hot((uint64_t GAS*)(gp(c.win) + WN_SPN_MIN), (uint64_t)ent_t(a));
+    }
     if (__hip_atomic_exchange(gp(c.inlist) + lp, c.wid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != c.wid) {
         const uint32_t i = __hip_atomic_fetch_add(gp(c.act_n) + c.act_cur * TW_LP_NB, 1u, __ATOMIC_RELAXED,
                                                   __HIP_MEMORY_SCOPE_AGENT);
@@ -2527,7 +2557,11 @@ __device__ __forceinline__ void lp_fill(const Dev& c, int64_t* red, const uint4*
     // a child forked onto another node inside this window keeps the window
     // (phase) running: its lane starts it at the next tick; so do records
     // still waiting in the exchange carry
-    const bool spawn_here = sp < (uint64_t)(w[WN_T] + w[WN_L]);
+    bool spawn_here = sp < (uint64_t)(w[WN_T] + w[WN_L]);
+    if (c.rw) {  // per-replica windows: the replicas' own minima decide (tw_lpb_rctl)
+        gp(red)[RD_NEXT] = 0;
+        spawn_here = w[WN_SPN_HERE] != 0;
+    }
     const bool carried = c.carry && *gp(c.carry_n + ((uint32_t)w[WN_TICKS] & 1u)) != 0;
     gp(red)[RD_ACTIVE] = -(int64_t)*gp(c.n_active) - (spawn_here ? 1 : 0) - (carried ? 1 : 0);
 }
@@ -2552,13 +2586,16 @@ __global__ void tw_lp_ctl(Dev c, int64_t* red, uint4* send, uint32_t world, uint
     *gp(c.n_active) = 0;
     *gp(c.next_t) = ~0ull;
     w[WN_SPN_MIN] = (int64_t)~0ull;
+    w[WN_SPN_HERE] = 0;
     if (gp(red)[RD_ERR] < 0) {  // some rank overflowed: every rank stops here (tw_lp_progress reports it)
         *gp(c.lp_err) |= (uint32_t)(-gp(red)[RD_ERR]) | 16u;
         w[WN_FLAGS] = WN_DONE;
+        w[WN_STEP] = RS_STOP;
         return;
     }
     if (gp(red)[RD_ACTIVE] < 0) {  // rerun this phase of the window
         w[WN_FLAGS] &= ~(WN_FRESH | WN_PH1FRESH);
+        w[WN_STEP] = RS_RERUN;
         return;
     }
     if (c.has_ph1 && w[WN_PHASE] == 0) {
@@ -2567,12 +2604,15 @@ __global__ void tw_lp_ctl(Dev c, int64_t* red, uint4* send, uint32_t world, uint
         w[WN_PHASE] = 1;
         w[WN_NT0] = gp(red)[RD_NEXT];
         w[WN_FLAGS] = WN_PH1FRESH;
+        w[WN_STEP] = RS_PHASE1;
         return;
     }
     w[WN_WINDOWS] += 1;
     int64_t t = gp(red)[RD_NEXT];
     if (w[WN_PHASE]) t = w[WN_NT0] < t ? w[WN_NT0] : t;
     w[WN_PHASE] = 0;
+    w[WN_STEP] = RS_ADVANCE;
+    w[WN_REPS] = 0;  // (per-replica windows: tw_lpb_rctl counts the replicas still running)
     if (t == INT64_MAX) {
         w[WN_T] = INT64_MAX;
         w[WN_FLAGS] = WN_DONE;
@@ -2590,6 +2630,50 @@ __global__ void tw_lp_ctl(Dev c, int64_t* red, uint4* send, uint32_t world, uint
     w[WN_SLEEP_MIN] = INT64_MAX;  // tw_lp_compact recomputes it for the new window
     w[WN_FLAGS] = WN_FRESH;
 }
+// Per-replica windows (batched LP, Dev::rw): this tick's decision of
+// tw_lp_ctl applied to every replica's own window -- a rerun keeps it, phase 1
+// keeps phase 0's next time, an advance moves the replica's window to its own
+// next event (the minimum of its lanes' next events, records, pending records
+// and sleeping lanes) and counts the replicas that still have one.
+__global__ void __launch_bounds__(256) tw_lpb_rctl(Dev c) {
+    int64_t GAS* w = gp(c.win);
+    if (w[WN_FLAGS] & WN_DONE) return;
+    const uint32_t q = blockIdx.x * 256 + threadIdx.x;
+    const size_t nrep = (size_t)1 << c.rep_lg;
+    const int64_t step = w[WN_STEP];
+    bool live = false;
+    if (q < nrep) {
+        uint64_t GAS* rw = (uint64_t GAS*)gp(c.rw);
+        const uint64_t tk = rw[RW_TICK * nrep + q];
+        rw[RW_TICK * nrep + q] = ~0ull;
+        if (step == RS_PHASE1) {
+            const uint64_t wn = rw[RW_WIN * nrep + q];
+            rw[RW_NT0 * nrep + q] = tk < wn ? tk : wn;
+        } else if (step == RS_ADVANCE && (int64_t)rw[RW_T * nrep + q] != INT64_MAX) {
+            uint64_t t = rw[RW_WIN * nrep + q];
+            t = tk < t ? tk : t;
+            if (c.has_ph1) {  // the window ran phase 1 last: phase 0's next time joins
+                const uint64_t n0 = rw[RW_NT0 * nrep + q];
+                t = n0 < t ? n0 : t;
+            }
+            rw[RW_NT0 * nrep + q] = ~0ull;
+            rw[RW_WIN * nrep + q] = ~0ull;
+            live = t < (uint64_t)INT64_MAX;
+            rw[RW_T * nrep + q] = live ? t : (uint64_t)INT64_MAX;
+        }
+    }
+    const uint64_t m = __builtin_amdgcn_ballot_w64(live);
+    if (m && __lane_id() == (uint32_t)__builtin_ctzll(m))
+        __hip_atomic_fetch_add((unsigned long long GAS*)(w + WN_REPS), (unsigned long long)__builtin_popcountll(m),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// ... and the loop ends once an advance leaves no replica running
+__global__ void tw_lpb_fin(Dev c) {
+    int64_t GAS* w = gp(c.win);
+    if ((w[WN_FLAGS] & WN_DONE) || w[WN_STEP] != RS_ADVANCE || w[WN_REPS] != 0) return;
+    w[WN_T] = INT64_MAX;
+    w[WN_FLAGS] = WN_DONE;
+}
 // The window's work list: every node marked during the previous window
 // (listed[r] == mark), split into TW_LP_NB buckets by the node's pending
 // delivery records (min(inbox_n, NB-1): a wave runs until its busiest lane is
@@ -2600,15 +2684,24 @@ __global__ void tw_lp_ctl(Dev c, int64_t* red, uint4* send, uint32_t world, uint
 #define TW_CPT 16
 __global__ void __launch_bounds__(256) tw_lp_compact(Dev c, uint32_t mark, uint32_t dst) {
     int64_t tend = INT64_MIN;  // device loop: lanes whose next event is due in the window are listed too
+    int64_t L = 0;
     if (c.win) {
         const int64_t GAS* w = gp(c.win);
         const int64_t fl = w[WN_FLAGS];
         if (!(fl & WN_FRESH) || (fl & WN_DONE)) return;
         mark = (uint32_t)w[WN_WID] - 1u;
         dst = (uint32_t)w[WN_ACT];
-        tend = w[WN_T] + w[WN_L] - 1;
+        L = w[WN_L];
+        tend = w[WN_T] + L - 1;
     }
+    // per-replica windows: each lane's own replica window, and the sleeping
+    // lanes' minimum per replica (every block is scanned: a block's summary
+    // mixes 256 replicas)
+    const bool prw = c.win && c.rw;
+    static_assert(1 << TW_SUB_LG == 256, "a scan block is one pass of the workgroup");
     __shared__ unsigned long long smin;
+    __shared__ unsigned long long sbm[TW_CPT][4];  // per scan block and wave: min unlisted wake
+    __shared__ uint32_t sbl[TW_CPT][4];            // per scan block and wave: lanes listed
     if (threadIdx.x == 0) smin = ~0ull;
     __syncthreads();
     unsigned long long mymin = ~0ull;
@@ -2616,15 +2709,53 @@ __global__ void __launch_bounds__(256) tw_lp_compact(Dev c, uint32_t mark, uint3
     __shared__ uint32_t base[TW_LP_NB];
     const uint32_t wv = threadIdx.x >> 6;
     const size_t r0 = (size_t)blockIdx.x * TW_CPT * 256 + threadIdx.x;
+    const uint32_t sb0 = blockIdx.x * TW_CPT;
+    __shared__ uint32_t sbs[TW_CPT];  // the block was scanned
     uint32_t key[TW_CPT];
 #pragma unroll
     for (int i = 0; i < TW_CPT; ++i) {
         const size_t r = r0 + (size_t)i * 256;
-        bool b = r < c.R && gp(c.listed)[r] == mark;
-        if (c.win && r < c.R) {
-            const int64_t wk = gp(c.wake)[r];
-            b = b || wk <= tend;
-            if (!b && wk != INT64_MAX) mymin = (unsigned long long)wk < mymin ? (unsigned long long)wk : mymin;
+        // device loop: a 256-lane block none of whose lanes was marked, listed
+        // last window or due now is skipped; its unlisted minimum still counts
+        bool scan = true;
+        const size_t rb = (size_t)(sb0 + i) << TW_SUB_LG;  // the block's first lane
+        if (c.win) {
+            scan = rb < c.R;
+            if (scan && !prw) {
+                const uint32_t sb = sb0 + (uint32_t)i;
+                const int64_t bm = gp(c.sb_min)[sb];
+                scan = gp(c.sb_mark)[sb] == mark || gp(c.sb_scan)[sb] == mark || bm <= tend;
+                if (!scan && bm != INT64_MAX) mymin = (unsigned long long)bm < mymin ? (unsigned long long)bm : mymin;
+            }
+        }
+        if (threadIdx.x == 0) sbs[i] = scan;
+        bool b = false;
+        unsigned long long um = ~0ull;
+        if (scan) {
+            b = r < c.R && gp(c.listed)[r] == mark;
+            if (c.win && r < c.R) {
+                const int64_t wk = gp(c.wake)[r];
+                b = b || wk <= (prw ? rw_tend(c, (uint32_t)r, L) : tend);
+                if (!b && wk != INT64_MAX) {
+                    if (prw) min_hot((uint64_t GAS*)rw_at(c, RW_WIN, (uint32_t)r), (uint64_t)wk);
+                    else um = (unsigned long long)wk;
+                }
+            }
+        }
+        if (c.win && scan) {
+            mymin = um < mymin ? um : mymin;
+            // the block's summary for the next window: its unlisted minimum, and
+            // whether it lists lanes (they run now and move their wakes)
+#pragma unroll
+            for (int d = 32; d >= 1; d >>= 1) {
+                const unsigned long long o = __shfl_xor(um, d, 64);
+                um = o < um ? o : um;
+            }
+            const uint64_t lb = __builtin_amdgcn_ballot_w64(b);
+            if (__lane_id() == 0) {
+                sbm[i][wv] = um;
+                sbl[i][wv] = lb != 0;
+            }
         }
         const uint32_t n_in = (TW_LP_NB > 1 && b) ? gp(c.inbox_n)[r] : 0u;
         key[i] = b ? (n_in < TW_LP_NB - 1 ? n_in : TW_LP_NB - 1) : 0xFFu;
@@ -2636,6 +2767,13 @@ __global__ void __launch_bounds__(256) tw_lp_compact(Dev c, uint32_t mark, uint3
     }
     if (mymin != ~0ull) atomicMin(&smin, mymin);
     __syncthreads();
+    if (c.win && threadIdx.x < TW_CPT && sbs[threadIdx.x]) {
+        const uint32_t i = threadIdx.x;
+        unsigned long long m = sbm[i][0];
+        for (int k = 1; k < 4; ++k) m = sbm[i][k] < m ? sbm[i][k] : m;
+        gp(c.sb_min)[sb0 + i] = m == ~0ull ? INT64_MAX : (int64_t)m;
+        if (sbl[i][0] | sbl[i][1] | sbl[i][2] | sbl[i][3]) gp(c.sb_scan)[sb0 + i] = mark + 1u;
+    }
     if (threadIdx.x == 0 && smin != ~0ull)
         __hip_atomic_fetch_min((unsigned long long GAS*)(gp(c.win) + WN_SLEEP_MIN), smin, __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);
@@ -2686,6 +2824,9 @@ __global__ void tw_lp_begin(Dev c, int64_t lookahead) {
     w[WN_SPN_MIN] = (int64_t)~0ull;
     w[WN_SLEEP_MIN] = INT64_MAX;
     w[WN_XMAX] = 0;
+    w[WN_SPN_HERE] = 0;
+    w[WN_REPS] = 0;
+    w[WN_STEP] = RS_RERUN;
     if (c.carry) gp(c.carry_n)[0] = gp(c.carry_n)[1] = 0;
     for (int k = 0; k < TW_LP_NB; ++k) gp(c.act_n)[TW_LP_NB + k] = 0;
     *gp(c.out_n) = 0;
@@ -2737,8 +2878,7 @@ __global__ void __launch_bounds__(256) tw_lp_due(Dev c) {
     const int64_t fl = w[WN_FLAGS];
     if (!(fl & WN_FRESH) || (fl & WN_DONE)) return;
     const uint32_t wid = (uint32_t)w[WN_WID];
-    const int64_t T = w[WN_T], L = w[WN_L];
-    const int64_t tend = T + L - 1;
+    const int64_t T0 = w[WN_T], L = w[WN_L];
     const bool radix = L <= TW_DUE_BINS;
     const uint32_t nb = radix ? (uint32_t)L : 0u;
     const uint32_t lst = wid & 1u;
@@ -2756,6 +2896,10 @@ __global__ void __launch_bounds__(256) tw_lp_due(Dev c) {
     const size_t st = ib_stride(c);
     for (uint32_t hi = blockIdx.x; hi < nh; hi += gridDim.x) {
         const uint32_t r = gp(c.heavy)[(size_t)lst * c.R + hi];
+        // the lane's window: the batch's, or its replica's own (per-replica windows)
+        const int64_t T = c.rw ? *rw_at(c, RW_T, r) : T0;
+        if (T == INT64_MAX) continue;  // (a finished replica has no records)
+        const int64_t tend = T + L - 1;
         uint32_t n = gp(c.inbox_n)[r];
         const uint32_t cap = ib_cap(c, r);
         n = n < cap ? n : cap;
@@ -2872,10 +3016,11 @@ __global__ void __launch_bounds__(256) tw_lp_due(Dev c) {
             sc[SC_DUE_N * R] = nd;
             sc[SC_DUE_H * R] = 0;
             if (smin != ~0ull)
-                __hip_atomic_fetch_min(gp(c.pend_min), (uint64_t)smin, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_fetch_min(c.rw ? (uint64_t GAS*)rw_at(c, RW_WIN, r) : gp(c.pend_min), (uint64_t)smin,
+                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             // due now: this window's list (compacted next, from mark wid - 1);
             // records left for later windows: the next window's pass
-            if (nd) gp(c.listed)[r] = wid - 1u;
+            if (nd) lp_mark(c, r, wid - 1u);
             if (left) {
                 const uint32_t l = lst ^ 1u;
                 const uint32_t i = __hip_atomic_fetch_add(gp(c.heavy_n) + l, 1u, __ATOMIC_RELAXED,
@@ -2978,6 +3123,7 @@ struct tw_shard {
     // pops per lane per tick of the device loop (TW_LP_TICK_BUDGET overrides it,
     // for tests: a small budget makes windows take several ticks)
     uint32_t lp_budget = 1u << 14;
+    uint32_t lp_grid = TW_LP_GRID;  // LP launches above this many workgroups walk the list (TW_LP_GRID env)
     Dev dwin() const {                // the descriptor the device loop's kernels get
         Dev x = d;
         x.win = win_buf;
@@ -3039,8 +3185,15 @@ void free_all(tw_shard* c) {
 template <bool LP, int WG, int NC, int TPW = 64, bool RUNS = true>
 static void launch_run(tw_shard* c, hipStream_t st, int64_t t_end, uint64_t limit, uint32_t budget) {
     const uint32_t blocks = (uint32_t)((c->d.R + WG - 1) / WG);
-    hipLaunchKernelGGL((tw_run_kernel<LP, WG, NC, TPW, RUNS>), dim3(blocks), dim3(WG * 64 / TPW), c->lds_bytes, st, c->d,
-                       t_end, limit, budget);
+    if constexpr (LP) {
+        if (blocks > c->lp_grid) {  // many lanes, few listed: the work list walked grid-stride
+            hipLaunchKernelGGL((tw_run_kernel<LP, WG, NC, TPW, RUNS, true>), dim3(c->lp_grid), dim3(WG * 64 / TPW),
+                               c->lds_bytes, st, c->d, t_end, limit, budget);
+            return;
+        }
+    }
+    hipLaunchKernelGGL((tw_run_kernel<LP, WG, NC, TPW, RUNS>), dim3(blocks), dim3(WG * 64 / TPW), c->lds_bytes, st,
+                       c->d, t_end, limit, budget);
 }
 
 namespace tw {
@@ -3381,7 +3534,16 @@ static int load_common(tw_shard* c, const tw_scenario_desc* s, bool lp, uint32_t
         ALLOC(d.act_n, 2 * TW_LP_NB);
         ALLOC(d.wake, R);
         ALLOC(d.listed, R);
+        {
+            const size_t nsb = (R + (1u << TW_SUB_LG) - 1) >> TW_SUB_LG;
+            ALLOC(d.sb_mark, nsb);
+            ALLOC(d.sb_scan, nsb);
+            ALLOC(d.sb_min, nsb);
+        }
         if (lpb) ALLOC(d.inlist, R);
+        // per-replica windows (TW_LPB_GLOBAL=1: one window for the whole batch)
+        d.rw = nullptr;
+        if (lpb && !getenv("TW_LPB_GLOBAL")) ALLOC(d.rw, (size_t)RW_COUNT << rep_lg);
         ALLOC(c->foreign, (size_t)d.out_cap * 2);
         ALLOC(c->n_foreign, 1);
         ALLOC(c->staging, (size_t)d.out_cap * 2);
@@ -3956,12 +4118,21 @@ int sh_lp_loop_begin(tw_shard* c) {
         const long v = strtol(b, nullptr, 10);
         c->lp_budget = v >= 1 && v <= (1 << 20) ? (uint32_t)v : (1u << 14);
     }
+    if (const char* b = getenv("TW_LP_GRID")) {  // (tests: the grid-stride walk on small contexts)
+        const long v = strtol(b, nullptr, 10);
+        c->lp_grid = v >= 1 && v <= (1 << 20) ? (uint32_t)v : TW_LP_GRID;
+    }
     HIPCHK(hipSetDevice(c->device));
     if (!c->ex_red) c->ex_red = c->red_own;  // world 1 without an explicit setup
     c->d.act_cur = 0;
     c->d.wid = 0;
     hipLaunchKernelGGL(tw_lp_begin, dim3(1), dim3(1), 0, c->stream, c->dwin(), c->d.lookahead);
     HIPCHK(hipGetLastError());
+    if (c->d.rw) {  // every replica's first window starts at 0; minima empty
+        const size_t nrep = (size_t)1 << c->d.rep_lg;
+        HIPCHK(hipMemsetAsync(c->d.rw + RW_T * nrep, 0, 8 * nrep, c->stream));
+        HIPCHK(hipMemsetAsync(c->d.rw + RW_TICK * nrep, 0xFF, 8 * nrep * (RW_COUNT - RW_TICK), c->stream));
+    }
     if (c->heavy_ok) {
         hipLaunchKernelGGL(tw_lp_due, dim3(TW_DUE_GRID), dim3(256), 0, c->stream, c->dwin());
         HIPCHK(hipGetLastError());
@@ -4021,6 +4192,13 @@ int sh_lp_tick_end(tw_shard* c) {
     hipLaunchKernelGGL(tw_lp_ctl, dim3(1), dim3(1), 0, c->stream, c->dwin(), c->ex_red, c->ex_send, c->ex_world,
                        c->ex_cap, c->ex_send ? 1u : 0u);
     HIPCHK(hipGetLastError());
+    if (c->d.rw) {
+        const uint32_t nrep = 1u << c->d.rep_lg;
+        hipLaunchKernelGGL(tw_lpb_rctl, dim3((nrep + 255) / 256), dim3(256), 0, c->stream, c->dwin());
+        HIPCHK(hipGetLastError());
+        hipLaunchKernelGGL(tw_lpb_fin, dim3(1), dim3(1), 0, c->stream, c->dwin());
+        HIPCHK(hipGetLastError());
+    }
     if (c->heavy_ok) {
         hipLaunchKernelGGL(tw_lp_due, dim3(TW_DUE_GRID), dim3(256), 0, c->stream, c->dwin());
         HIPCHK(hipGetLastError());

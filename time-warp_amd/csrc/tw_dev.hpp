@@ -116,6 +116,7 @@ struct Dev {
     // travel as spawn records)
     uint32_t lp0, Ntot, IB, out_cap;
     uint32_t rep_lg, lpb;
+    int64_t* rw;         // [RW_COUNT][2^rep_lg] per-replica windows (batched LP device loop), else null
     int64_t lookahead;
     uint64_t* hash_g;    // [Ntot << rep_lg] this context's additions to every node's hash
     uint4* inbox;        // delivery records addressed to local lanes: entry k of lane r at
@@ -160,6 +161,13 @@ struct Dev {
     int64_t* wake;       // [R] device loop: the lane's next event time (INT64_MAX: none); a
                          // window lists only lanes due in it, the others' minimum bounds the next
     uint32_t* listed;    // [R]
+    // 256-lane blocks of the work-list scan (TW_SUB): a block is rescanned only
+    // when one of its lanes was marked (sb_mark), had lanes listed in the last
+    // window (sb_scan, both window ids) or holds a wake due in the window
+    // (sb_min: the minimum wake of its lanes left unlisted at its last scan)
+    uint32_t* sb_mark;   // [R / TW_SUB]
+    uint32_t* sb_scan;   // [R / TW_SUB]
+    int64_t* sb_min;     // [R / TW_SUB]
     uint32_t* inlist;    // [R] window id whose work list holds the lane (batched mode: a
                          // spawn target is appended to the running window's list once)
     uint32_t act_cur, wid;
@@ -213,8 +221,21 @@ __device__ __forceinline__ int64_t tx_us(const Dev& c, uint64_t link, uint32_t k
 // WN_XMAX: the largest per-rank record demand of one tick since the host last
 // cleared it (from the all-reduced words, so identical on every rank: the
 // ranks agree on the next exchange block size without talking)
+// WN_SPN_HERE, WN_REPS, WN_STEP: per-replica windows (Dev::rw) -- a spawn fell
+// inside its replica's window (the window reruns); replicas still running
+// after the last advance; what tw_lp_ctl decided this tick (RS_*)
 enum { WN_T, WN_L, WN_REC_MIN, WN_WINDOWS, WN_TICKS, WN_FLAGS, WN_ACT, WN_WID, WN_PHASE, WN_NT0, WN_SPN_MIN,
-       WN_SLEEP_MIN, WN_XMAX, WN_COUNT };
+       WN_SLEEP_MIN, WN_XMAX, WN_SPN_HERE, WN_REPS, WN_STEP, WN_COUNT };
+// Per-replica windows (batched LP, Dev::rw, [RW_*][2^rep_lg]): the window
+// machinery (ticks, reruns, phases, work lists) stays common to the batch,
+// but every replica's window is [RW_T, RW_T + L) from its own next event, so a
+// window covers what its own replica has due, not the union of all replicas'
+// event times.  RW_TICK (u64 min, reset every tick): next events of the lanes
+// that ran, spawn times; RW_WIN (u64 min, reset with the window): delivery
+// records, records a heavy lane left pending, unlisted lanes' wakes; RW_NT0:
+// phase 0's next time while phase 1 runs.
+enum { RW_T, RW_TICK, RW_WIN, RW_NT0, RW_COUNT };
+enum : int64_t { RS_RERUN = 0, RS_PHASE1 = 1, RS_ADVANCE = 2, RS_STOP = 3 };
 // reduction words of the device loop (all-reduced with MIN between ranks)
 enum { RD_NEXT, RD_ACTIVE, RD_ERR, RD_DEMAND, RD_COUNT };
 // spawn record markers in the kind field of an outbox entry pair (message kinds are < 256)
@@ -245,8 +266,20 @@ __device__ __forceinline__ uint32_t ib_cap(const Dev& c, uint32_t r) {
 
 // mark node r for the next window's work list (tw_lp_compact builds the list
 // from the marks, in node order within each wave: coalesced node state)
-__device__ __forceinline__ void lp_list_next(const Dev& c, uint32_t r) {
-    gp(c.listed)[r] = c.wid;
+#define TW_SUB_LG 8  // work-list scan blocks of 256 lanes
+__device__ __forceinline__ void lp_mark(const Dev& c, uint32_t r, uint32_t wid) {
+    gp(c.listed)[r] = wid;
+    gp(c.sb_mark)[r >> TW_SUB_LG] = wid;  // (lanes of one block store the same value)
+}
+__device__ __forceinline__ void lp_list_next(const Dev& c, uint32_t r) { lp_mark(c, r, c.wid); }
+// per-replica window words of lane r's replica (batched LP, Dev::rw)
+__device__ __forceinline__ int64_t GAS* rw_at(const Dev& c, int w, uint32_t r) {
+    return gp(c.rw) + ((size_t)w << c.rep_lg) + ((c.lp0 + r) & ((1u << c.rep_lg) - 1u));
+}
+// the last µs of lane r's replica window (INT64_MIN: the replica is done)
+__device__ __forceinline__ int64_t rw_tend(const Dev& c, uint32_t r, int64_t L) {
+    const int64_t T = *rw_at(c, RW_T, r);
+    return T == INT64_MAX ? INT64_MIN : T + L - 1;
 }
 
 // ------------------------------------------------------------------ hashing
