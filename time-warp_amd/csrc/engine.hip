@@ -1843,6 +1843,7 @@ __global__ void __launch_bounds__(TW_WG) tw_init_kernel(Dev c, uint32_t main_pc,
         if (c.lpb) gp(c.spawn_n)[r] = 0;
         gp(c.wake)[r] = INT64_MAX;
         lp_mark(c, r, 0);  // marked for the first window: it serves every node
+        if (c.rw && (((r >> c.rep_lg) & ((1u << TW_CHUNK_LG) - 1u)) == 0)) gp(c.cw_min)[cw_idx(c, r)] = INT64_MAX;
         if ((r & ((1u << TW_SUB_LG) - 1u)) == 0) {
             gp(c.sb_scan)[r >> TW_SUB_LG] = 0xFFFFFFFFu;
             gp(c.sb_min)[r >> TW_SUB_LG] = INT64_MAX;
@@ -1873,7 +1874,7 @@ __host__ __device__ constexpr size_t fixed_lds_bytes() {
 // RUNS = false (the compact geometry): no far runs, and built for two waves
 // per SIMD (<= 256 registers, half the LDS of a dense lane), so 1M-replica
 // batches keep two workgroups per CU
-template <bool LP, int WG, int NC, int TPW = 64, bool RUNS = true, bool GS = false>
+template <bool LP, int WG, int NC, int TPW = 64, bool RUNS = true, bool GS = false, bool PRW = false>
 __global__ void __launch_bounds__(WG * 64 / TPW)
     __attribute__((amdgpu_waves_per_eu((LP || !RUNS) ? 2 : (WG * 64 / TPW + 255) / 256, 2)))
 tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
@@ -1940,7 +1941,8 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
             uint64_t* sc = gp(c.scal) + r;
             const size_t R = c.R;
             if (sc[SC_STATUS * R] != TW_REP_RUNNING) break;  // (the next block of the work list)
-            const int64_t te = (LP && c.rw && c.win) ? rw_tend(c, r, lwin) : t_end;  // this lane's window end
+            // this lane's window end (PRW: per-replica windows, Dev::rw -- a per-lane value)
+            const int64_t te = (LP && PRW) ? rw_tend(c, r, lwin) : t_end;
             // LP: a node with no live thread, nothing to drain, no due run and no
             // spawn record has nothing to do in this window (every live thread holds
             // its one queued event; a superseded entry left behind pops without effect
@@ -2291,7 +2293,7 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
             if (LP) {
                 sc[SC_DUE_H * R] = L.dg(DW_HN) & 0xFFFFu;
                 if (L.dg(DW_IB) >> 31)  // sent records straight into inboxes (Lane::emit)
-                    min_hot((uint64_t GAS*)(c.rw ? rw_at(c, RW_WIN, r) : gp(c.win) + WN_REC_MIN), (uint64_t)(te + 1));
+                    min_hot((uint64_t GAS*)(PRW ? rw_at(c, RW_WIN, r) : gp(c.win) + WN_REC_MIN), (uint64_t)(te + 1));
             }
             sc[SC_DELIVERED * R] += L.cg(CW_DL); sc[SC_DROPPED * R] += L.cg(CW_DR);
             sc[SC_UNDELIV * R] += L.cg(CW_UD); sc[SC_THREADS * R] += L.d_th;
@@ -2315,7 +2317,7 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
             if (L.fsrc >= 0 && L.fmt < tn) tn = L.fmt;
             if (active && (tn == INT64_MAX || tn > te) && !pending_main) active = false;  // parked beyond t_end
             if (LP && L.status == TW_REP_RUNNING && tn != INT64_MAX)
-                min_hot((c.rw && c.win) ? (uint64_t GAS*)rw_at(c, RW_TICK, r) : gp(c.next_t), (uint64_t)tn);
+                min_hot(PRW ? (uint64_t GAS*)rw_at(c, RW_TICK, r) : gp(c.next_t), (uint64_t)tn);
             {   // lanes still active: one atomic per wave
                 const uint64_t am = __builtin_amdgcn_ballot_w64(active);
                 const uint64_t ex = __builtin_amdgcn_ballot_w64(true);
@@ -2327,7 +2329,12 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
                 // device loop: the lane is listed again by the window its next event
                 // falls in (tw_lp_compact); host loop: for the next window
                 const bool more = L.status == TW_REP_RUNNING && (L.live || pending_main);
-                if (c.win) gp(c.wake)[r] = more ? (pending_main ? L.now : tn) : INT64_MAX;
+                if (c.win) {
+                    const int64_t wk = more ? (pending_main ? L.now : tn) : INT64_MAX;
+                    gp(c.wake)[r] = wk;
+                    // per-replica windows: the lane's chunk keeps a lower bound of its wakes
+                    if (PRW && wk != INT64_MAX) min_hot((uint64_t GAS*)gp(c.cw_min) + cw_idx(c, r), (uint64_t)wk);
+                }
                 else if (more) lp_list_next(c, r);
             }
         } while (0);
@@ -2652,6 +2659,13 @@ __global__ void __launch_bounds__(256) tw_lpb_rctl(Dev c) {
         } else if (step == RS_ADVANCE && (int64_t)rw[RW_T * nrep + q] != INT64_MAX) {
             uint64_t t = rw[RW_WIN * nrep + q];
             t = tk < t ? tk : t;
+            // the replica's lanes' next events: the minimum over its chunks
+            const uint32_t nk = ((c.R >> c.rep_lg) + (1u << TW_CHUNK_LG) - 1u) >> TW_CHUNK_LG;
+            const uint64_t GAS* cm = (const uint64_t GAS*)gp(c.cw_min) + q;
+            for (uint32_t k = 0; k < nk; ++k) {
+                const uint64_t v = cm[(size_t)k * nrep];
+                t = v < t ? v : t;
+            }
             if (c.has_ph1) {  // the window ran phase 1 last: phase 0's next time joins
                 const uint64_t n0 = rw[RW_NT0 * nrep + q];
                 t = n0 < t ? n0 : t;
@@ -2674,6 +2688,72 @@ __global__ void tw_lpb_fin(Dev c) {
     w[WN_T] = INT64_MAX;
     w[WN_FLAGS] = WN_DONE;
 }
+// Per-replica windows: the window's work list.  One wavefront per tile of 64
+// replicas x one chunk of 64 nodes, a lane per replica: a chunk is read only
+// where its replica's lanes were marked (records, spawns) in the previous
+// window or its lower bound of their next events falls in the replica's new
+// window; a due chunk's bound is recomputed from its unlisted lanes (the listed
+// ones add theirs when they run).  Lanes are appended node by node, so a
+// wavefront of the event kernel gets 64 replicas of one node.
+__global__ void __launch_bounds__(256) tw_lpb_compact(Dev c) {
+    const int64_t GAS* w = gp(c.win);
+    const int64_t fl = w[WN_FLAGS];
+    if (!(fl & WN_FRESH) || (fl & WN_DONE)) return;
+    const uint32_t mark = (uint32_t)w[WN_WID] - 1u, dst = (uint32_t)w[WN_ACT];
+    const int64_t L = w[WN_L];
+    const uint32_t nrep = 1u << c.rep_lg, nloc = c.R >> c.rep_lg;
+    const uint32_t tile = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const uint32_t ngrp = (nrep + 63) >> 6;
+    const uint32_t k = tile / ngrp, q = (tile - k * ngrp) * 64 + __lane_id();
+    if ((k << TW_CHUNK_LG) >= nloc) return;  // (wave-uniform)
+    const bool have = q < nrep;
+    const size_t ci = ((size_t)k << c.rep_lg) + q;
+    const int64_t te = have ? rw_tend(c, q, L) : INT64_MIN;
+    const int64_t cmv = have ? gp(c.cw_min)[ci] : INT64_MAX;
+    const bool due = have && cmv <= te;
+    const bool mk = have && gp(c.cw_mark)[ci] == mark;
+    if (!__builtin_amdgcn_ballot_w64(due || mk)) return;
+    // pass 1: which of the column's lanes are listed (a bit per node)
+    int64_t nm = INT64_MAX;
+    uint64_t bits = 0;
+    const uint32_t n0 = k << TW_CHUNK_LG;
+    const uint32_t nn = n0 + (1u << TW_CHUNK_LG) < nloc ? 1u << TW_CHUNK_LG : nloc - n0;
+    if (due || mk) {
+        for (uint32_t j = 0; j < nn; ++j) {
+            const uint32_t r = ((n0 + j) << c.rep_lg) | q;
+            bool b = mk && gp(c.listed)[r] == mark;
+            if (due) {
+                const int64_t wk = gp(c.wake)[r];
+                b = b || wk <= te;
+                if (!b && wk < nm) nm = wk;
+            }
+            bits |= (uint64_t)b << j;
+        }
+    }
+    // pass 2: one append per tile, then node-major positions
+    uint32_t tot = (uint32_t)__builtin_popcountll(bits);
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) tot += __shfl_xor(tot, d, 64);
+    if (tot) {
+        uint32_t base = 0;
+        if (__lane_id() == 0)
+            base = __hip_atomic_fetch_add(gp(c.act_n) + dst * TW_LP_NB, tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        base = (uint32_t)__builtin_amdgcn_readfirstlane((int)base);
+        uint32_t GAS* act = gp(c.act) + (size_t)dst * TW_LP_NB * c.R;
+        for (uint32_t j = 0; j < nn; ++j) {
+            const bool b = (bits >> j) & 1u;
+            const uint64_t m = __builtin_amdgcn_ballot_w64(b);
+            if (b) {
+                const uint32_t r = ((n0 + j) << c.rep_lg) | q;
+                act[base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] = r;
+                if (c.inlist) gp(c.inlist)[r] = mark + 1u;
+            }
+            base += (uint32_t)__builtin_popcountll(m);
+        }
+    }
+    if (due) gp(c.cw_min)[ci] = nm;
+}
+
 // The window's work list: every node marked during the previous window
 // (listed[r] == mark), split into TW_LP_NB buckets by the node's pending
 // delivery records (min(inbox_n, NB-1): a wave runs until its busiest lane is
@@ -3186,11 +3266,23 @@ template <bool LP, int WG, int NC, int TPW = 64, bool RUNS = true>
 static void launch_run(tw_shard* c, hipStream_t st, int64_t t_end, uint64_t limit, uint32_t budget) {
     const uint32_t blocks = (uint32_t)((c->d.R + WG - 1) / WG);
     if constexpr (LP) {
-        if (blocks > c->lp_grid) {  // many lanes, few listed: the work list walked grid-stride
-            hipLaunchKernelGGL((tw_run_kernel<LP, WG, NC, TPW, RUNS, true>), dim3(c->lp_grid), dim3(WG * 64 / TPW),
-                               c->lds_bytes, st, c->d, t_end, limit, budget);
-            return;
-        }
+        // many lanes, few listed: the work list walked grid-stride (GS); the
+        // batched device loop's per-replica windows (PRW)
+        const bool gs = blocks > c->lp_grid, prw = c->d.rw && c->d.win;
+        const dim3 g(gs ? c->lp_grid : blocks), b(WG * 64 / TPW);
+        if (gs && prw)
+            hipLaunchKernelGGL((tw_run_kernel<LP, WG, NC, TPW, RUNS, true, true>), g, b, c->lds_bytes, st, c->d, t_end,
+                               limit, budget);
+        else if (gs)
+            hipLaunchKernelGGL((tw_run_kernel<LP, WG, NC, TPW, RUNS, true, false>), g, b, c->lds_bytes, st, c->d, t_end,
+                               limit, budget);
+        else if (prw)
+            hipLaunchKernelGGL((tw_run_kernel<LP, WG, NC, TPW, RUNS, false, true>), g, b, c->lds_bytes, st, c->d, t_end,
+                               limit, budget);
+        else
+            hipLaunchKernelGGL((tw_run_kernel<LP, WG, NC, TPW, RUNS>), g, b, c->lds_bytes, st, c->d, t_end, limit,
+                               budget);
+        return;
     }
     hipLaunchKernelGGL((tw_run_kernel<LP, WG, NC, TPW, RUNS>), dim3(blocks), dim3(WG * 64 / TPW), c->lds_bytes, st,
                        c->d, t_end, limit, budget);
@@ -3543,7 +3635,14 @@ static int load_common(tw_shard* c, const tw_scenario_desc* s, bool lp, uint32_t
         if (lpb) ALLOC(d.inlist, R);
         // per-replica windows (TW_LPB_GLOBAL=1: one window for the whole batch)
         d.rw = nullptr;
-        if (lpb && !getenv("TW_LPB_GLOBAL")) ALLOC(d.rw, (size_t)RW_COUNT << rep_lg);
+        d.cw_min = nullptr;
+        d.cw_mark = nullptr;
+        if (lpb && !getenv("TW_LPB_GLOBAL")) {
+            ALLOC(d.rw, (size_t)RW_COUNT << rep_lg);
+            const size_t nk = ((R >> rep_lg) + (1u << TW_CHUNK_LG) - 1) >> TW_CHUNK_LG;
+            ALLOC(d.cw_min, nk << rep_lg);
+            ALLOC(d.cw_mark, nk << rep_lg);
+        }
         ALLOC(c->foreign, (size_t)d.out_cap * 2);
         ALLOC(c->n_foreign, 1);
         ALLOC(c->staging, (size_t)d.out_cap * 2);
@@ -4137,7 +4236,13 @@ int sh_lp_loop_begin(tw_shard* c) {
         hipLaunchKernelGGL(tw_lp_due, dim3(TW_DUE_GRID), dim3(256), 0, c->stream, c->dwin());
         HIPCHK(hipGetLastError());
     }
-    hipLaunchKernelGGL(tw_lp_compact, dim3(compact_blocks(c->d.R)), dim3(256), 0, c->stream, c->dwin(), 0u, 0u);
+    if (c->d.rw) {  // per-replica windows: tiles of 64 replicas x one chunk of nodes, four per workgroup
+        const uint32_t nk = ((c->d.R >> c->d.rep_lg) + (1u << TW_CHUNK_LG) - 1u) >> TW_CHUNK_LG;
+        const uint32_t tiles = nk * (((1u << c->d.rep_lg) + 63u) >> 6);
+        hipLaunchKernelGGL(tw_lpb_compact, dim3((tiles + 3) / 4), dim3(256), 0, c->stream, c->dwin());
+    } else {
+        hipLaunchKernelGGL(tw_lp_compact, dim3(compact_blocks(c->d.R)), dim3(256), 0, c->stream, c->dwin(), 0u, 0u);
+    }
     HIPCHK(hipGetLastError());
     HIPCHK(hipMemsetAsync(c->d.lp_err, 0, 4, c->stream));
     c->loop_ready = true;
@@ -4203,7 +4308,13 @@ int sh_lp_tick_end(tw_shard* c) {
         hipLaunchKernelGGL(tw_lp_due, dim3(TW_DUE_GRID), dim3(256), 0, c->stream, c->dwin());
         HIPCHK(hipGetLastError());
     }
-    hipLaunchKernelGGL(tw_lp_compact, dim3(compact_blocks(c->d.R)), dim3(256), 0, c->stream, c->dwin(), 0u, 0u);
+    if (c->d.rw) {  // per-replica windows: tiles of 64 replicas x one chunk of nodes, four per workgroup
+        const uint32_t nk = ((c->d.R >> c->d.rep_lg) + (1u << TW_CHUNK_LG) - 1u) >> TW_CHUNK_LG;
+        const uint32_t tiles = nk * (((1u << c->d.rep_lg) + 63u) >> 6);
+        hipLaunchKernelGGL(tw_lpb_compact, dim3((tiles + 3) / 4), dim3(256), 0, c->stream, c->dwin());
+    } else {
+        hipLaunchKernelGGL(tw_lp_compact, dim3(compact_blocks(c->d.R)), dim3(256), 0, c->stream, c->dwin(), 0u, 0u);
+    }
     HIPCHK(hipGetLastError());
     return TW_OK;
 }

@@ -117,6 +117,12 @@ struct Dev {
     uint32_t lp0, Ntot, IB, out_cap;
     uint32_t rep_lg, lpb;
     int64_t* rw;         // [RW_COUNT][2^rep_lg] per-replica windows (batched LP device loop), else null
+    // per-replica windows: the lanes of a replica in chunks of 2^TW_CHUNK_LG
+    // nodes, [chunk][replica]: cw_min = a lower bound of the chunk's lanes'
+    // next events (exact except after one of them ran: the chunk is then due
+    // and rescanned), cw_mark = the window id a lane of the chunk was last marked in
+    int64_t* cw_min;
+    uint32_t* cw_mark;
     int64_t lookahead;
     uint64_t* hash_g;    // [Ntot << rep_lg] this context's additions to every node's hash
     uint4* inbox;        // delivery records addressed to local lanes: entry k of lane r at
@@ -267,9 +273,14 @@ __device__ __forceinline__ uint32_t ib_cap(const Dev& c, uint32_t r) {
 // mark node r for the next window's work list (tw_lp_compact builds the list
 // from the marks, in node order within each wave: coalesced node state)
 #define TW_SUB_LG 8  // work-list scan blocks of 256 lanes
+#define TW_CHUNK_LG 6  // per-replica windows: 64 nodes per chunk
+__device__ __forceinline__ size_t cw_idx(const Dev& c, uint32_t r) {  // [chunk][replica] of lane r
+    return ((size_t)((r >> c.rep_lg) >> TW_CHUNK_LG) << c.rep_lg) | (r & ((1u << c.rep_lg) - 1u));
+}
 __device__ __forceinline__ void lp_mark(const Dev& c, uint32_t r, uint32_t wid) {
     gp(c.listed)[r] = wid;
-    gp(c.sb_mark)[r >> TW_SUB_LG] = wid;  // (lanes of one block store the same value)
+    if (c.rw) gp(c.cw_mark)[cw_idx(c, r)] = wid;
+    else gp(c.sb_mark)[r >> TW_SUB_LG] = wid;  // (lanes of one block store the same value)
 }
 __device__ __forceinline__ void lp_list_next(const Dev& c, uint32_t r) { lp_mark(c, r, c.wid); }
 // per-replica window words of lane r's replica (batched LP, Dev::rw)
