@@ -3200,6 +3200,12 @@ struct tw_shard {
     int64_t* win_buf = nullptr;       // the device loop's WN_* words
     int64_t* h_win = nullptr;         // pinned host copy of them + lp_err (tw_lp_progress)
     bool loop_ready = false;
+    // sh_lp_run_windows: TW_GRAPH_TICKS ticks + the progress copy captured as
+    // one hipGraph (a tick is 4-8 short kernels: launched one by one, the host's
+    // enqueue rate left the device idle between them), re-captured when the
+    // launch arguments it holds change (tick_gkey)
+    hipGraphExec_t tick_graph = nullptr;
+    std::vector<unsigned char> tick_gkey;
     // pops per lane per tick of the device loop (TW_LP_TICK_BUDGET overrides it,
     // for tests: a small budget makes windows take several ticks)
     uint32_t lp_budget = 1u << 14;
@@ -3257,6 +3263,9 @@ void free_all(tw_shard* c) {
     c->ex_world = 1;
     c->ex_rank = c->ex_cap = c->ex_cap_eff = 0;
     c->loop_ready = false;
+    if (c->tick_graph) (void)hipGraphExecDestroy(c->tick_graph);
+    c->tick_graph = nullptr;
+    c->tick_gkey.clear();
     c->loaded = false;
 }
 
@@ -4319,16 +4328,16 @@ int sh_lp_tick_end(tw_shard* c) {
     return TW_OK;
 }
 
-int sh_lp_progress(tw_shard* c, tw_lp_state* out) {
-    if (!c || !out) return TW_ERR_INVALID;
-    if (!c->loaded || !c->lp || !c->loop_ready) return TW_ERR_STATE;
-    HIPCHK(hipSetDevice(c->device));
-    if (!c->h_win) HIPCHK(hipHostMalloc((void**)&c->h_win, 8 * (WN_COUNT + 1)));
+// the window words + lp_err into the pinned host copy (stream-ordered)
+static int lp_progress_copy(tw_shard* c) {
     int64_t* w = c->h_win;  // pinned: plain DMA copies, no staging blit
-    w[WN_COUNT] = 0;        // lp_err fills its low 4 bytes
     HIPCHK(hipMemcpyAsync(w, c->win_buf, 8 * WN_COUNT, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipMemcpyAsync(w + WN_COUNT, c->d.lp_err, 4, hipMemcpyDeviceToHost, c->stream));
+    return TW_OK;
+}
+static int lp_progress_read(tw_shard* c, tw_lp_state* out) {
     HIPCHK(hipStreamSynchronize(c->stream));
+    const int64_t* w = c->h_win;
     const uint32_t err = (uint32_t)w[WN_COUNT];
     out->windows = (uint64_t)w[WN_WINDOWS];
     out->ticks = (uint64_t)w[WN_TICKS];
@@ -4337,21 +4346,117 @@ int sh_lp_progress(tw_shard* c, tw_lp_state* out) {
     out->err = err;
     return TW_OK;
 }
+static int lp_host_alloc(tw_shard* c) {
+    if (!c->h_win) HIPCHK(hipHostMalloc((void**)&c->h_win, 8 * (WN_COUNT + 1)));
+    return TW_OK;
+}
+
+int sh_lp_progress(tw_shard* c, tw_lp_state* out) {
+    if (!c || !out) return TW_ERR_INVALID;
+    if (!c->loaded || !c->lp || !c->loop_ready) return TW_ERR_STATE;
+    HIPCHK(hipSetDevice(c->device));
+    int rc = lp_host_alloc(c);
+    if (rc) return rc;
+    c->h_win[WN_COUNT] = 0;  // lp_err fills its low 4 bytes
+    rc = lp_progress_copy(c);
+    return rc ? rc : lp_progress_read(c, out);
+}
+
+#define TW_GRAPH_TICKS 16
+// the launch arguments a captured tick graph depends on
+static std::vector<unsigned char> tick_key(const tw_shard* c) {
+    struct K {
+        Dev d;
+        hipStream_t st;
+        int64_t *win, *h_win, *red;
+        uint4 *send, *recv;
+        uint32_t *starts, budget, grid, world, cap, cap_eff;
+        size_t lds;
+        bool heavy;
+    } k;
+    std::memset(&k, 0, sizeof(k));
+    std::memcpy(&k.d, &c->d, sizeof(Dev));
+    k.st = c->stream;
+    k.win = c->win_buf;
+    k.h_win = c->h_win;
+    k.red = c->ex_red;
+    k.send = c->ex_send;
+    k.recv = c->ex_recv;
+    k.starts = c->ex_starts;
+    k.budget = c->lp_budget;
+    k.grid = c->lp_grid;
+    k.world = c->ex_world;
+    k.cap = c->ex_cap;
+    k.cap_eff = c->ex_cap_eff;
+    k.lds = c->lds_bytes;
+    k.heavy = c->heavy_ok;
+    std::vector<unsigned char> v(sizeof(K));
+    std::memcpy(v.data(), &k, sizeof(K));
+    return v;
+}
+// TW_GRAPH_TICKS ticks and the progress copy, captured once per set of launch
+// arguments (every kernel of a tick reads its window from the device, so the
+// same graph serves every batch; ticks after the loop is done return at once)
+static int tick_graph_ready(tw_shard* c) {
+    std::vector<unsigned char> key = tick_key(c);
+    if (c->tick_graph && key == c->tick_gkey) return TW_OK;
+    if (c->tick_graph) (void)hipGraphExecDestroy(c->tick_graph);
+    c->tick_graph = nullptr;
+    c->tick_gkey.clear();
+    HIPCHK(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
+    int rc = TW_OK;
+    for (int i = 0; i < TW_GRAPH_TICKS && !rc; ++i) {
+        rc = sh_lp_tick(c);
+        if (!rc) rc = sh_lp_tick_import(c);
+        if (!rc) rc = sh_lp_tick_end(c);
+    }
+    if (!rc) rc = lp_progress_copy(c);
+    hipGraph_t g = nullptr;
+    const hipError_t e = hipStreamEndCapture(c->stream, &g);
+    if (rc || e != hipSuccess) {
+        if (g) (void)hipGraphDestroy(g);
+        (void)hipGetLastError();
+        return rc ? rc : TW_ERR_HIP;
+    }
+    const hipError_t ei = hipGraphInstantiate(&c->tick_graph, g, nullptr, nullptr, 0);
+    (void)hipGraphDestroy(g);
+    if (ei != hipSuccess) {
+        c->tick_graph = nullptr;
+        return TW_ERR_HIP;
+    }
+    c->tick_gkey = std::move(key);
+    return TW_OK;
+}
 
 int sh_lp_run_windows(tw_shard* c, uint64_t max_ticks, tw_lp_state* out) {
     if (!c || !out) return TW_ERR_INVALID;
     if (!c->loaded || !c->lp || !c->loop_ready) return TW_ERR_STATE;
     if (c->ex_world != 1) return TW_ERR_STATE;
+    HIPCHK(hipSetDevice(c->device));
+    int rc = lp_host_alloc(c);
+    if (rc) return rc;
+    const char* ng = getenv("TW_NO_GRAPH");  // (A/B: launch every kernel from the host)
+    const bool graph = !(ng && *ng && *ng != '0');
     for (uint64_t done_ticks = 0; done_ticks < max_ticks;) {
-        const uint64_t batch = max_ticks - done_ticks < 16 ? max_ticks - done_ticks : 16;
-        for (uint64_t i = 0; i < batch; ++i) {
-            int rc = sh_lp_tick(c);
-            if (!rc) rc = sh_lp_tick_import(c);
-            if (!rc) rc = sh_lp_tick_end(c);
+        const uint64_t batch =
+            max_ticks - done_ticks < TW_GRAPH_TICKS ? max_ticks - done_ticks : (uint64_t)TW_GRAPH_TICKS;
+        c->h_win[WN_COUNT] = 0;  // lp_err fills its low 4 bytes
+        if (graph && batch == TW_GRAPH_TICKS) {
+            rc = tick_graph_ready(c);
+            if (rc) return rc;
+            HIPCHK(hipGraphLaunch(c->tick_graph, c->stream));
+        } else {
+            for (uint64_t i = 0; i < batch; ++i) {
+                rc = sh_lp_tick(c);
+                if (!rc) rc = sh_lp_tick_import(c);
+                if (!rc) rc = sh_lp_tick_end(c);
+                if (rc) return rc;
+            }
+            rc = lp_progress_copy(c);
             if (rc) return rc;
         }
         done_ticks += batch;
-        int rc = sh_lp_progress(c, out);
+        rc = lp_progress_read(c, out);
         if (rc) return rc;
         if (out->err) return TW_ERR_REPLICA;
         if (out->done) return TW_OK;

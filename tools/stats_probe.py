@@ -56,10 +56,13 @@ def main():
                           "lane_efficiency": d["pop"] / max(d["iter"], 1),
                           "per_pop": {k: round(v / pops, 4) for k, v in d.items() if k != "pop"}, "counters": d}))
         return
-    if len(sys.argv) > 1 and sys.argv[1] == "lpb_hotspot":  # config 5, nodes as logical processes (tw_lpb_load)
-        R = int(sys.argv[2]) if len(sys.argv) > 2 else 4096
-        S = int(sys.argv[3]) if len(sys.argv) > 3 else 256
-        scn = scenarios.hotspot(n_senders=S, n_replicas=R, msg_num=1000)
+    if len(sys.argv) > 1 and sys.argv[1] in ("lpb_hotspot", "lpb_token"):  # C5 / C3 as logical processes
+        R = int(sys.argv[2]) if len(sys.argv) > 2 else (4096 if sys.argv[1] == "lpb_hotspot" else 8192)
+        if sys.argv[1] == "lpb_token":
+            scn = scenarios.token_ring(n_nodes=4096, n_replicas=R, launch_duration=120_000_000, drop_log2=10)
+        else:
+            S = int(sys.argv[3]) if len(sys.argv) > 3 else 256
+            scn = scenarios.hotspot(n_senders=S, n_replicas=R, msg_num=1000)
         eng = Engine(0).load(scn, geometry="lpb")
         read(eng)
         eng.reset()
@@ -67,7 +70,7 @@ def main():
         d = read(eng)
         pops = max(d["pop"], 1)
         w, t = eng.lpb_windows()
-        print(json.dumps({"phase": "lpb_hotspot", "events": st.events, "loop_ms": st.kernel_ms, "windows": w,
+        print(json.dumps({"phase": sys.argv[1], "events": st.events, "loop_ms": st.kernel_ms, "windows": w,
                           "ticks": t, "lane_efficiency": d["pop"] / max(d["iter"], 1),
                           "per_pop": {k: round(v / pops, 4) for k, v in d.items() if k != "pop"}, "counters": d}))
         return
