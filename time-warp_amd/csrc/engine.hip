@@ -100,7 +100,12 @@
 #endif
 #define TW_TAIL_VMEM 9          // vector-memory ops of every iteration after the record prefetch
 
-#define P_COUNT 29
+// LP event kernel: waves per SIMD it is built for (2: <= 256 registers, which
+// spills; 1: the AGPRs too, no scratch)
+#ifndef TW_LP_WAVES
+#define TW_LP_WAVES 2
+#endif
+#define P_COUNT 34
 // Diagnostic build (-DTW_STATS, lib/libtimewarp_stats.so): per-lane event-path
 // counters summed into Dev::prof at kernel end (tools/stats_probe.py).  The
 // product build compiles every STAT to nothing.
@@ -114,7 +119,8 @@
 enum { K_POP, K_SUPERSEDED, K_PEEK_PF, K_PEEK_HBM, K_PUT_HBM, K_PUT_DEAD, K_PF_ISSUE, K_HASH_IMM, K_HASH_FLUSH,
        K_NEAR_PUSH, K_RUN_PUSH, K_FAR_PUSH, K_INSN, K_CYC_POP, K_CYC_INTERP, K_CYC_TAIL,
        K_CYC_SEL, K_CYC_FETCH, K_CYC_QPOP, K_CYC_COMMIT, K_CYC_PF, K_CYC_TERM, K_CYC_STORE, K_CYC_HASH,
-       K_CYC_SPAWN, K_CYC_ENQ, K_SPAWN, K_ALLOC_LD, K_ITER };
+       K_CYC_SPAWN, K_CYC_ENQ, K_SPAWN, K_ALLOC_LD, K_ITER, K_CYC_SEND, K_CYC_DELIV, K_CYC_DUE, K_CYC_PRO,
+       K_CYC_EPI };
 #ifdef TW_STATS
 #define STIME(v) const uint64_t v = __builtin_amdgcn_s_memtime()
 #define STADD(i, v) (st[(i)] += (uint32_t)(v))
@@ -156,7 +162,9 @@ enum {
 };
 // LP-only cold words, after the CW_* block: the due run of a heavy lane
 // (head | count << 16, seq base, head time) and its inbox base index
-enum { DW_HN, DW_SQ0, DW_TL, DW_TH, DW_IB, DW_COUNT };
+// DW_BSET/BOWN/BREL: LP -- the lane's own listener binding (bind, bind_own,
+// bind_rel), cached at the lane's start: only this lane's threads change it
+enum { DW_HN, DW_SQ0, DW_TL, DW_TH, DW_IB, DW_BSET, DW_BOWN, DW_BREL, DW_COUNT };
 
 // Pre-decoded instruction class ("uop" flags, built once per launch in the
 // kernel prologue from the program image): the interpreter's hot pass computes
@@ -295,6 +303,7 @@ struct Lane {
     const uint2 LAS* P;   // program image
     const uint32_t LAS* PU;  // its uop flags
     const int64_t LAS* K; // constant pool
+    const uint32_t LAS* LPC;  // listener-set x kind -> handler pc (Dev::lpc), staged in LDS
     // near heap: count, time base, cached root
     uint32_t near_n;
     int64_t nbase;
@@ -969,16 +978,18 @@ struct Lane {
         const bool valid = s != 0xFFFFFFFFu && s != cur && s < c.S;
         STAT(K_PF_ISSUE);
         const uint4 GAS* p = hrec(valid ? s : 0u);
+        // (readfirstlane: the m0 operand is an SGPR whatever register the value was kept in)
+        const uint32_t pw = (uint32_t)__builtin_amdgcn_readfirstlane((int)pfs_wave);
         // the instruction offset of global_load_lds also offsets the LDS
         // destination, so each quad gets its own global address instead
-        asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(p), "s"(pfs_wave)
+        asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(p), "s"(pw)
                      : "memory", "m0");
         asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(p + c.RQ),
-                     "s"(pfs_wave + WG * 16) : "memory", "m0");
+                     "s"(pw + WG * 16) : "memory", "m0");
         asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(p + 2 * c.RQ),
-                     "s"(pfs_wave + 2 * WG * 16) : "memory", "m0");
+                     "s"(pw + 2 * WG * 16) : "memory", "m0");
         asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(p + 3 * c.RQ),
-                     "s"(pfs_wave + 3 * WG * 16) : "memory", "m0");
+                     "s"(pw + 3 * WG * 16) : "memory", "m0");
         pf_slot = valid ? s : 0xFFFFFFFFu;
     }
     // The popped thread's record: the prefetched copy, or (rarely) a fresh load
@@ -1189,18 +1200,22 @@ struct Lane {
 
     // Thread ends (END or uncaught exception): listener release, ref
     // invalidation, slot freed; the caller stores the header quad.
-    __device__ __forceinline__ void die_prep(Th& th, uint32_t slot) {
+    __device__ __forceinline__ void rel_bind(const Th& th) {
         // an owned listener (token-ring `serve`) is released when its thread
         // dies: recorded with a store, no read (DELIVER compares the owner)
-        if (th_flags(th) & F_OWNS) gp(c.bind_rel)[bix(th.w1)] = th.w2;
+        if (th_flags(th) & F_OWNS) {
+            gp(c.bind_rel)[bix(th.w1)] = th.w2;
+            if constexpr (LP) ds(DW_BREL, th.w2);
+        }
+    }
+    __device__ __forceinline__ void die_prep(Th& th, uint32_t slot) {
+        rel_bind(th);
         th.w2 = 0xFFFFFFFFu;  // invalidate refs to this slot
         th.w3 = 0;
         free_slot(slot);
     }
     __device__ __forceinline__ void die(Th& th, uint32_t slot) {
-        // an owned listener (token-ring `serve`) is released when its thread
-        // dies: recorded with a store, no read (DELIVER compares the owner)
-        if (th_flags(th) & F_OWNS) gp(c.bind_rel)[bix(th.w1)] = th.w2;
+        rel_bind(th);
         th.w2 = 0xFFFFFFFFu;  // invalidate refs to this slot
         th.w3 = 0;
         put_hdr(slot, th);
@@ -1496,7 +1511,8 @@ struct Lane {
                 tw_vm_drain();
                 break;
             }
-            case TW_OP_SEND:  // schedule (after d) (deliver ..) unless the link drops it
+            case TW_OP_SEND: {  // schedule (after d) (deliver ..) unless the link drops it
+                STIME(tsd0);
                 if (me) {
                     const uint64_t link = (uint64_t)ra;
                     if (link >= c.L) {
@@ -1507,10 +1523,15 @@ struct Lane {
                         const int64_t payload = rf[((b >> 8) & 3u) * WG];
                         // the link's ordinal and (LP) its destination entry: independent
                         // loads in flight together, one wait
-                        const uint32_t ord = gp(c.link_ord)[lix(link)];
+                        // (a one-deep table -- one delay per link, every scenario but
+                        // record-replay -- needs no ordinal: its entry is known now)
+                        uint32_t ord = 0;
+                        if (c.D > 1) {
+                            ord = gp(c.link_ord)[lix(link)];
+                            gp(c.link_ord)[lix(link)] = ord + 1;
+                        }
                         uint4 dh = make_uint4(0x80000000u, 0, 0, 0);
                         if (LP) dh = gp(c.link_dsth)[link];  // destination | heavy, its inbox
-                        gp(c.link_ord)[lix(link)] = ord + 1;
                         const uint32_t e = c.link_table ? gp(c.link_table)[tix(link, ord)] : 0u;
                         if (e & TW_LINK_DROP) {
                             cinc(CW_DR);
@@ -1546,23 +1567,32 @@ struct Lane {
                         }
                     }
                 }
-                tw_vm_drain();
+                // (LP: every load above was consumed; what is left in flight are the
+                // record's stores, which the next pop's counted wait covers)
+                if (!LP) tw_vm_drain();
+                STIME(tsd1);
+                STADD(K_CYC_SEND, tsd1 - tsd0);
                 break;
-            case TW_OP_DELIVER:  // listener dispatch, ForkStrategy fork_ (MonadDialog.hs:232-256,317)
+            }
+            case TW_OP_DELIVER: {  // listener dispatch, ForkStrategy fork_ (MonadDialog.hs:232-256,317)
+                STIME(tdl0);
                 if (me) {
                     const int64_t r0 = rf[0], r1 = rf[WG], r2 = rf[2 * WG], r3 = rf[3 * WG];
                     const uint64_t link = (uint64_t)r1;
                     const uint32_t kind = (uint32_t)r3;
-                    const uint32_t dst = gp(c.link_dst)[link];
-                    const uint32_t set0 = gp(c.bind)[bix(dst)];
-                    const uint32_t own = gp(c.bind_own)[bix(dst)], rel = gp(c.bind_rel)[bix(dst)];
-                    if (LP) {  // the reply link a handler's RLINK asks for, loaded with the binding
+                    // LP: the record reached its destination's lane, whose binding
+                    // words are cached in LDS; the handler table is staged in LDS
+                    const uint32_t dst = LP ? th.w1 : gp(c.link_dst)[link];
+                    const uint32_t set0 = LP ? dg(DW_BSET) : gp(c.bind)[bix(dst)];
+                    const uint32_t own = LP ? dg(DW_BOWN) : gp(c.bind_own)[bix(dst)];
+                    const uint32_t rel = LP ? dg(DW_BREL) : gp(c.bind_rel)[bix(dst)];
+                    if (LP) {  // the reply link a handler's RLINK asks for
                         rlc_rev = gp(c.link_rev)[link];
                         rlc_link = (uint32_t)link;
                     }
                     const uint32_t set = own == rel ? 0u : set0;  // owner died: released
                     uint32_t lpc = TW_PC_NONE;
-                    if (set && kind < c.n_kinds) lpc = gp(c.lpc)[(size_t)(set - 1) * c.n_kinds + kind];
+                    if (set && kind < c.n_kinds) lpc = LPC[(size_t)(set - 1) * c.n_kinds + kind];
                     if (lpc == TW_PC_NONE) {
                         cinc(CW_UD);
                         hash(dst, TW_KIND_UNDELIV | kind, r0);
@@ -1612,7 +1642,10 @@ struct Lane {
                     }
                 }
                 tw_vm_drain();
+                STIME(tdl1);
+                STADD(K_CYC_DELIV, tdl1 - tdl0);
                 break;
+            }
             case TW_OP_LISTEN: {
                 const bool bad = (uint32_t)imm >= c.n_sets;
                 pfail(me && bad, TW_REP_ERR_INSN);
@@ -1620,6 +1653,10 @@ struct Lane {
                 if (me && !bad) {
                     gp(c.bind)[bix(th.w1)] = (uint32_t)imm + 1;
                     gp(c.bind_own)[bix(th.w1)] = b ? th.w2 : 0xFFFFFFFFu;
+                    if constexpr (LP) {
+                        ds(DW_BSET, (uint32_t)imm + 1);
+                        ds(DW_BOWN, b ? th.w2 : 0xFFFFFFFFu);
+                    }
                 }
                 th.w0 = (me && !bad && b) ? th.w0 | (F_OWNS << FL_SHIFT) : th.w0;
                 break;
@@ -1628,6 +1665,10 @@ struct Lane {
                 if (me) {
                     gp(c.bind)[bix(th.w1)] = 0;
                     gp(c.bind_own)[bix(th.w1)] = 0xFFFFFFFFu;
+                    if constexpr (LP) {
+                        ds(DW_BSET, 0);
+                        ds(DW_BOWN, 0xFFFFFFFFu);
+                    }
                 }
                 break;
             case TW_OP_TMO_BEGIN:  // schedule (after t) watchdog (TimedT.hs:373-375)
@@ -1876,7 +1917,8 @@ __host__ __device__ constexpr size_t fixed_lds_bytes() {
 // batches keep two workgroups per CU
 template <bool LP, int WG, int NC, int TPW = 64, bool RUNS = true, bool GS = false, bool PRW = false>
 __global__ void __launch_bounds__(WG * 64 / TPW)
-    __attribute__((amdgpu_waves_per_eu((LP || !RUNS) ? 2 : (WG * 64 / TPW + 255) / 256, 2)))
+    __attribute__((amdgpu_waves_per_eu(LP ? TW_LP_WAVES : !RUNS ? 2 : (WG * 64 / TPW + 255) / 256,
+                                       LP ? TW_LP_WAVES : 2)))
 tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
     constexpr bool HR = !LP && RUNS;
     // device-driven windows: the window, its work list and whether this is the
@@ -1912,6 +1954,7 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
     uint2 LAS* s_p = (uint2 LAS*)(s_cw + (CW_COUNT + (LP ? DW_COUNT : 0)) * WG);
     int64_t LAS* s_c = (int64_t LAS*)(s_p + c.n_insns + 1);
     uint32_t LAS* s_u = (uint32_t LAS*)(s_c + c.n_consts);
+    uint32_t LAS* s_l = s_u + c.n_insns + 1;
     {
         for (uint32_t i = threadIdx.x; i <= c.n_insns; i += WG * 64 / TPW) {
             const uint2 in = gp(c.insns)[i];
@@ -1919,6 +1962,7 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
             s_u[i] = uop_of(in.x & 0xFFu);
         }
         for (uint32_t i = threadIdx.x; i < c.n_consts; i += WG * 64 / TPW) s_c[i] = gp(c.consts)[i];
+        for (uint32_t i = threadIdx.x; i < c.n_sets * c.n_kinds; i += WG * 64 / TPW) s_l[i] = gp(c.lpc)[i];
         __syncthreads();
     }
     if (TPW < 64 && (threadIdx.x & 63u) >= TPW) return;
@@ -1937,6 +1981,7 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
                 r = gp(c.act)[(size_t)c.act_cur * TW_LP_NB * c.R + i];
             }
             if (r >= c.R) break;  // (the next block of the work list)
+            STIME(tpro0);
             if (LP && c.phase && gp(c.phase)[(c.lp0 + r) >> c.rep_lg] != ph) break;  // the other phase's node
             uint64_t* sc = gp(c.scal) + r;
             const size_t R = c.R;
@@ -1974,6 +2019,7 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
             L.P = s_p;
             L.PU = s_u;
             L.K = s_c;
+            L.LPC = s_l;
             L.pf_slot = 0xFFFFFFFFu;
             L.prun = -1;
             L.hacc = 0;
@@ -2011,6 +2057,9 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
                 if (dh < dn) h = gp(c.due)[(ib + (size_t)dh * ib_stride(c)) * 2];
                 L.ds(DW_TL, h.x);
                 L.ds(DW_TH, h.y);
+                L.ds(DW_BSET, gp(c.bind)[r]);  // (LP: bix(node) = the lane itself)
+                L.ds(DW_BOWN, gp(c.bind_own)[r]);
+                L.ds(DW_BREL, gp(c.bind_rel)[r]);
             }
             if constexpr (HR) {
                 uint32_t rh4[TW_RUNS];
@@ -2153,6 +2202,10 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
 
         #ifdef TW_STATS
             for (int i = 0; i < P_COUNT; ++i) L.st[i] = 0;
+            {
+                STIME(tpro1);
+                STADDL(K_CYC_PRO, tpro1 - tpro0);
+            }
         #endif
             uint32_t pending_main = (uint32_t)sc[SC_PENDING_MAIN * R];
             // nothing loaded before the loop may stay pending into it (a loop-header
@@ -2208,7 +2261,8 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
                             if (due) L.due_pop(th, slot, sq);
                             else L.fetch_rec(slot, th);  // prefetched copy or HBM
                             STIME(ts2);
-                            STADDL(K_CYC_FETCH, ts2 - ts1);
+                            STADDL(K_CYC_FETCH, due ? 0 : ts2 - ts1);
+                            STADDL(K_CYC_DUE, due ? ts2 - ts1 : 0);
                             if (due) {
                             } else if (!use_far) L.near_pop();
                             else if (L.fsrc == TW_RUNS) L.far_pop();
@@ -2274,10 +2328,14 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
             __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
             L.run_commit();
         #ifdef TW_STATS
+            // (a second set of counters for heavy-inbox LP lanes alone: a hotspot
+            // receiver's chain bounds its windows)
+            const uint32_t pset = (LP && !ilight) ? P_COUNT : 0u;
             if (c.prof)
                 for (int i = 0; i < P_COUNT; ++i)
-                    __hip_atomic_fetch_add(gp(c.prof) + i, (unsigned long long)L.st[i], __ATOMIC_RELAXED,
+                    __hip_atomic_fetch_add(gp(c.prof) + pset + i, (unsigned long long)L.st[i], __ATOMIC_RELAXED,
                                            __HIP_MEMORY_SCOPE_AGENT);
+            STIME(tepi0);
         #endif
             sc[SC_PENDING_MAIN * R] = pending_main;
             if (!LP && L.status == TW_REP_RUNNING && L.live == 0) L.status = TW_REP_DONE;
@@ -2337,6 +2395,14 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
                 }
                 else if (more) lp_list_next(c, r);
             }
+        #ifdef TW_STATS
+            {
+                STIME(tepi1);
+                if (c.prof)
+                    __hip_atomic_fetch_add(gp(c.prof) + pset + K_CYC_EPI, (unsigned long long)(tepi1 - tepi0), __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+            }
+        #endif
         } while (0);
         if (!(LP && GS) || (size_t)(blk + gridDim.x) * WG >= lp_n) break;
     }
@@ -3477,7 +3543,7 @@ static int load_common(tw_shard* c, const tw_scenario_desc* s, bool lp, uint32_t
     c->tie_flags.assign(d.R, 0u);
     const size_t R = d.R;
     const size_t Rt = s->n_replicas;  // replica dimension of the host tables
-    const size_t prog_lds = 12ull * (d.n_insns + 1) + 8ull * d.n_consts;
+    const size_t prog_lds = 12ull * (d.n_insns + 1) + 8ull * d.n_consts + 4ull * d.n_sets * d.n_kinds;
     // geometry by replica count (TW_GEOMETRY overrides; LP mode is dense):
     // <= 4096: a wavefront per replica (C5: 0.32 G events/s vs 0.25 sparse,
     // 0.20 narrow); < 65536: narrow (C3 at 8192: 2.5 vs 0.99 sparse, 0.74
@@ -3562,8 +3628,8 @@ static int load_common(tw_shard* c, const tw_scenario_desc* s, bool lp, uint32_t
         ALLOC(lbw, d.L);
     }
 #ifdef TW_STATS
-    ALLOC(d.prof, P_COUNT);
-    HIPCHK(hipMemsetAsync(d.prof, 0, 8 * P_COUNT, c->stream));
+    ALLOC(d.prof, 2 * P_COUNT);
+    HIPCHK(hipMemsetAsync(d.prof, 0, 16 * P_COUNT, c->stream));
 #endif
     uint32_t* iboff = nullptr;
     std::vector<uint32_t> h_iboff;
@@ -4526,10 +4592,10 @@ int sh_lpb_windows(tw_shard* c, uint64_t* windows, uint64_t* ticks) {
 int sh_prof_read(tw_shard* c, unsigned long long* out, size_t cap, int reset) {
 #ifdef TW_STATS
     if (!c || !out || !c->loaded || !c->d.prof) return TW_ERR_STATE;
-    size_t n = cap < (size_t)P_COUNT ? cap : (size_t)P_COUNT;
+    size_t n = cap < (size_t)2 * P_COUNT ? cap : (size_t)2 * P_COUNT;  // all lanes, then heavy LP lanes
     HIPCHK(hipSetDevice(c->device));
     HIPCHK(hipMemcpy(out, c->d.prof, 8 * n, hipMemcpyDeviceToHost));
-    if (reset) HIPCHK(hipMemset(c->d.prof, 0, 8 * P_COUNT));
+    if (reset) HIPCHK(hipMemset(c->d.prof, 0, 16 * P_COUNT));
     return (int)n;
 #else
     (void)c; (void)out; (void)cap; (void)reset;

@@ -23,17 +23,20 @@ from timewarp.engine import Engine  # noqa: E402
 NAMES = ["pop", "superseded", "peek_pf", "peek_hbm", "put_hbm", "put_dead", "pf_issue", "hash_imm", "hash_flush",
          "near_push", "run_push", "far_push", "insn", "cyc_pop", "cyc_interp", "cyc_step_and_flush",
          "cyc_select", "cyc_fetch", "cyc_qpop", "cyc_commit", "cyc_prefetch", "cyc_terminal", "cyc_store", "cyc_hash",
-         "cyc_spawn", "cyc_enqueue", "spawn", "alloc_ld", "iter"]
+         "cyc_spawn", "cyc_enqueue", "spawn", "alloc_ld", "iter", "cyc_send", "cyc_deliver", "cyc_due", "cyc_pro",
+         "cyc_epi"]
 
 
-def read(eng):
-    buf = (C.c_ulonglong * len(NAMES))()
+def read(eng, heavy=False):
+    """the counters of every lane (heavy=True: of heavy-inbox LP lanes alone)"""
+    buf = (C.c_ulonglong * (2 * len(NAMES)))()
     fn = eng.lib.tw_prof_read
     fn.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]
-    n = fn(eng.ctx, buf, len(NAMES), 1)
+    n = fn(eng.ctx, buf, 2 * len(NAMES), 1)
     if n < 0:
         raise RuntimeError(f"tw_prof_read: {n}")
-    return {k: buf[i] for i, k in enumerate(NAMES)}
+    o = len(NAMES) if heavy else 0
+    return {k: buf[o + i] for i, k in enumerate(NAMES)}
 
 
 def main():
@@ -67,6 +70,14 @@ def main():
         read(eng)
         eng.reset()
         st = eng.run()
+        if sys.argv[1] == "lpb_hotspot":  # the receivers alone first (read() clears every counter)
+            d = read(eng, heavy=True)
+            pops = max(d["pop"], 1)
+            print(json.dumps({"phase": "lpb_hotspot_receivers", "lane_efficiency": d["pop"] / max(d["iter"], 1),
+                              "per_pop": {k: round(v / pops, 4) for k, v in d.items() if k != "pop"},
+                              "counters": d}))
+            eng.reset()
+            st = eng.run()
         d = read(eng)
         pops = max(d["pop"], 1)
         w, t = eng.lpb_windows()
