@@ -303,6 +303,15 @@ def main():
         # C5: a replica is one long chain in the replica geometries (0.32 G
         # events/s, wave); its nodes as logical processes run it in parallel
         args.geometry = "lpb"
+    if args.geometry is None and args.config == "token_ring":
+        # C3 split 8 ways (8,192 replicas per GPU): a replica's ~45.7k-event
+        # chain bounds the replica geometries (narrow 2.5 G events/s); its
+        # (node, replica) pairs as logical processes run it at 3.2-3.3 G.  From
+        # 16,384 replicas per GPU up, narrow/dense win (5.0 vs 4.4 G at 16k).
+        world0 = int(os.environ.get("WORLD_SIZE", "1"))
+        per = args.replicas if args.weak else args.replicas // max(world0, 1)
+        if per <= 8192 and per & (per - 1) == 0 and args.replicas % max(world0, 1) == 0:
+            args.geometry = "lpb"
     if args.workload_key:
         print(json.dumps({"bench_workload": workload_key(args), "engine_sha": engine_sha()}))
         return

@@ -102,6 +102,15 @@
 
 // LP event kernel: waves per SIMD it is built for (2: <= 256 registers, which
 // spills; 1: the AGPRs too, no scratch)
+// LP lanes: the per-lane interpreter pass (PL: a hot pass serves lanes at
+// different pcs) -- 0 for the A/B of the opcode-uniform pass
+#ifndef TW_LP_PL
+#define TW_LP_PL 0
+#endif
+// the record prefetch as the compiler's LDS-DMA builtin (1) or inline asm (0)
+#ifndef TW_DMA_BUILTIN
+#define TW_DMA_BUILTIN 0
+#endif
 #ifndef TW_LP_WAVES
 #define TW_LP_WAVES 2
 #endif
@@ -284,7 +293,7 @@ struct Lane {
     // lanes diverge -- logical processes and the few-replica sparse geometry; the
     // dense replica geometry runs lock-step programs and keeps the cheaper
     // opcode-uniform pass
-    static constexpr bool PL = LP || WG < 64;
+    static constexpr bool PL = (LP && TW_LP_PL) || WG < 64;
     Dev c;  // by value: kernel arguments stay in SGPRs
     uint32_t r;       // replica
     // LDS (lane-offset pointers; element j at [j * WG])
@@ -978,6 +987,17 @@ struct Lane {
         const bool valid = s != 0xFFFFFFFFu && s != cur && s < c.S;
         STAT(K_PF_ISSUE);
         const uint4 GAS* p = hrec(valid ? s : 0u);
+#if TW_DMA_BUILTIN
+        // the compiler's own LDS-DMA instruction: its vector-memory count is
+        // modelled (inline asm is opaque to the wait-count pass, which then
+        // guarded the address registers with vmcnt waits where they were reused)
+        const uint32_t pw = (uint32_t)__builtin_amdgcn_readfirstlane((int)pfs_wave);
+        uint4 LAS* d0 = (uint4 LAS*)(size_t)pw;
+        __builtin_amdgcn_global_load_lds((const void GAS*)p, (void LAS*)d0, 16, 0, 0);
+        __builtin_amdgcn_global_load_lds((const void GAS*)(p + c.RQ), (void LAS*)(d0 + WG), 16, 0, 0);
+        __builtin_amdgcn_global_load_lds((const void GAS*)(p + 2 * c.RQ), (void LAS*)(d0 + 2 * WG), 16, 0, 0);
+        __builtin_amdgcn_global_load_lds((const void GAS*)(p + 3 * c.RQ), (void LAS*)(d0 + 3 * WG), 16, 0, 0);
+#else
         // (readfirstlane: the m0 operand is an SGPR whatever register the value was kept in)
         const uint32_t pw = (uint32_t)__builtin_amdgcn_readfirstlane((int)pfs_wave);
         // the instruction offset of global_load_lds also offsets the LDS
@@ -990,6 +1010,7 @@ struct Lane {
                      "s"(pw + 2 * WG * 16) : "memory", "m0");
         asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(p + 3 * c.RQ),
                      "s"(pw + 3 * WG * 16) : "memory", "m0");
+#endif
         pf_slot = valid ? s : 0xFFFFFFFFu;
     }
     // The popped thread's record: the prefetched copy, or (rarely) a fresh load
@@ -1136,7 +1157,9 @@ struct Lane {
         th.w1 = (c.lp0 + r) >> c.rep_lg;
         th.w2 = 0xFFFFFFFEu;      // never a throwTo target
         th.w3 = ok ? sq : sq + 1; // no slot (the lane has failed): a pop without effect
-        th.f0 = th.f1 = th.xl = th.xh = 0;
+        th.f0 = th.f1 = 0;
+        th.xl = b.w;  // the reply link (tw_lp_due), flagged by xh: DELIVER takes it and clears both
+        th.xh = 1;
         th.r0 = (int64_t)(((uint64_t)a.w << 32) | a.z);  // payload
         th.r1 = b.x;                                     // link
         th.r2 = b.z;                                     // sending node
@@ -1178,6 +1201,10 @@ struct Lane {
         }
         Th t;
         peek_rec(ts, t);
+        // the whole record drained here, on every path out (a quad left in
+        // flight on the early return made the compiler wait at the top of
+        // every later interpreter pass)
+        tw_vm_drain();
         if (t.w2 != tid) return;  // dead (slot free or reused): the map entry is unobservable
         if (t.w3 != 0) {          // queued: wake to now with a fresh seq
             bool on_chip = (th_flags(t) & F_NEARQ) != 0;
@@ -1586,8 +1613,17 @@ struct Lane {
                     const uint32_t set0 = LP ? dg(DW_BSET) : gp(c.bind)[bix(dst)];
                     const uint32_t own = LP ? dg(DW_BOWN) : gp(c.bind_own)[bix(dst)];
                     const uint32_t rel = LP ? dg(DW_BREL) : gp(c.bind_rel)[bix(dst)];
-                    if (LP) {  // the reply link a handler's RLINK asks for
-                        rlc_rev = gp(c.link_rev)[link];
+                    if (LP) {
+                        // the reply link a handler's RLINK asks for: a due-run record
+                        // brought it (xh set); a light-inbox one loads it (drained in
+                        // place, so a pass where no lane loads waits for nothing)
+                        uint32_t rv = th.xl;
+                        if (!th.xh) {
+                            rv = gp(c.link_rev)[link];
+                            tw_vm_drain();
+                        }
+                        th.xl = th.xh = 0;
+                        rlc_rev = rv;
                         rlc_link = (uint32_t)link;
                     }
                     const uint32_t set = own == rel ? 0u : set0;  // owner died: released
@@ -1641,7 +1677,7 @@ struct Lane {
                         tc = T_SPAWN;
                     }
                 }
-                tw_vm_drain();
+                if (!LP) tw_vm_drain();  // (LP: its one load drained in place)
                 STIME(tdl1);
                 STADD(K_CYC_DELIV, tdl1 - tdl0);
                 break;
@@ -2265,8 +2301,15 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
                             STADDL(K_CYC_DUE, due ? ts2 - ts1 : 0);
                             if (due) {
                             } else if (!use_far) L.near_pop();
-                            else if (L.fsrc == TW_RUNS) L.far_pop();
-                            else L.run_pop(L.fsrc);
+                            else if (L.fsrc == TW_RUNS) {
+                                // (drained: the heap walk issues loads whose values go
+                                // unused; left in flight, they made the compiler wait
+                                // vmcnt(0) -- for the record prefetch and the last
+                                // pass's stores -- at the top of every interpreter
+                                // pass of every step, tools/waitcnt_audit.py)
+                                L.far_pop();
+                                tw_vm_drain();
+                            } else L.run_pop(L.fsrc);
                             STIME(ts3);
                             STADDL(K_CYC_QPOP, ts3 - ts2);
                             if (slot == L.pf_slot) L.pf_slot = 0xFFFFFFFFu;
@@ -3019,6 +3062,13 @@ __device__ __forceinline__ uint32_t wg_excl_scan(uint32_t v, uint32_t* wsum, uin
     __syncthreads();
     return base + x - v;
 }
+// A due-run record's second quad: {link, kind, src, reply link}.  Its
+// destination (b.w) is the lane itself, so the slot carries link_rev[link]
+// instead, looked up here off the lane's chain: DELIVER hands it to the
+// handler's RLINK without a load.
+__device__ __forceinline__ uint4 due_rec_b(const Dev& c, uint4 b) {
+    return make_uint4(b.x, b.y, b.z, b.x < c.L ? gp(c.link_rev)[b.x] : 0u);
+}
 __global__ void __launch_bounds__(256) tw_lp_due(Dev c) {
     const int64_t GAS* w = gp(c.win);
     const int64_t fl = w[WN_FLAGS];
@@ -3129,7 +3179,7 @@ __global__ void __launch_bounds__(256) tw_lp_due(Dev c) {
                 const uint32_t k = srt[i];
                 uint4 GAS* q = gp(c.due) + (ib + (size_t)i * st) * 2;
                 q[0] = ea[k];
-                q[1] = eb[k];
+                q[1] = due_rec_b(c, eb[k]);
             }
         } else {
             // long windows: rank of every due record among the due ones (ties by
@@ -3144,7 +3194,7 @@ __global__ void __launch_bounds__(256) tw_lp_due(Dev c) {
                 }
                 uint4 GAS* q = gp(c.due) + (ib + (size_t)rank * st) * 2;
                 q[0] = a;
-                q[1] = b;
+                q[1] = due_rec_b(c, b);
             }
         }
         if (tid == 0) {
@@ -3184,27 +3234,63 @@ __global__ void __launch_bounds__(256) tw_lp_due(Dev c) {
 // the worst error (else done), the main exception whichever lane holds one.
 // out: [8][n_rep] words (final_t, events, delivered, dropped, undeliverable,
 // status, main_exc, threads).
+// Batched LP: per-replica results over the replica's node lanes.  A wave
+// reads 64 replicas' words of one node (coalesced); the nodes are split over
+// the grid's y dimension and the four waves of a workgroup, the partials
+// combined in LDS and then by atomics into `out` (zeroed by the caller):
+// sums for the counters, max for final_t and the worst status (floored at
+// TW_REP_DONE), and for main_exc the last node with one -- (node + 1) << 32 |
+// code, its max -- as the serial loop over nodes chose.
+#define TW_RED_GROUPS 64  // node groups: grid.y x 4 waves
 __global__ void __launch_bounds__(256) tw_lpb_reduce(Dev c, uint64_t* out) {
-    const uint32_t q = blockIdx.x * 256 + threadIdx.x;
     const uint32_t nr = 1u << c.rep_lg;
-    if (q >= nr) return;
+    const uint32_t q = blockIdx.x * 64 + (threadIdx.x & 63u);
+    const uint32_t g = blockIdx.y * 4 + (threadIdx.x >> 6);
     const size_t R = c.R;
+    const uint32_t per = (c.Ntot + TW_RED_GROUPS - 1) / TW_RED_GROUPS;
+    const uint32_t n0 = g * per, n1 = n0 + per < c.Ntot ? n0 + per : c.Ntot;
     int64_t ft = 0;
     uint64_t ev = 0, dl = 0, dr = 0, ud = 0, th = 0, me = 0, st = TW_REP_DONE;
-    for (uint32_t n = 0; n < c.Ntot; ++n) {
-        const uint64_t GAS* sc = gp(c.scal) + ((size_t)n << c.rep_lg) + q;
-        const int64_t f = (int64_t)sc[SC_FINAL_T * R];
-        ft = f > ft ? f : ft;
-        ev += sc[SC_EVENTS * R]; dl += sc[SC_DELIVERED * R]; dr += sc[SC_DROPPED * R];
-        ud += sc[SC_UNDELIV * R]; th += sc[SC_THREADS * R];
-        const uint64_t x = sc[SC_MAIN_EXC * R], s2 = sc[SC_STATUS * R];
-        me = x ? x : me;
-        st = (s2 >= TW_REP_ABORTED && s2 > st) ? s2 : st;
+    if (q < nr) {
+        for (uint32_t n = n0; n < n1; ++n) {
+            const uint64_t GAS* sc = gp(c.scal) + ((size_t)n << c.rep_lg) + q;
+            const int64_t f = (int64_t)sc[SC_FINAL_T * R];
+            ft = f > ft ? f : ft;
+            ev += sc[SC_EVENTS * R]; dl += sc[SC_DELIVERED * R]; dr += sc[SC_DROPPED * R];
+            ud += sc[SC_UNDELIV * R]; th += sc[SC_THREADS * R];
+            const uint64_t x = sc[SC_MAIN_EXC * R], s2 = sc[SC_STATUS * R];
+            me = x ? ((uint64_t)(n + 1) << 32) | (x & 0xFFFFFFFFull) : me;
+            st = (s2 >= TW_REP_ABORTED && s2 > st) ? s2 : st;
+        }
     }
-    uint64_t GAS* o = gp(out);
-    o[0 * (size_t)nr + q] = (uint64_t)ft; o[1 * (size_t)nr + q] = ev; o[2 * (size_t)nr + q] = dl;
-    o[3 * (size_t)nr + q] = dr; o[4 * (size_t)nr + q] = ud; o[5 * (size_t)nr + q] = st;
-    o[6 * (size_t)nr + q] = me; o[7 * (size_t)nr + q] = th;
+    __shared__ uint64_t part[8][4][64];
+    const uint32_t w = threadIdx.x >> 6, l = threadIdx.x & 63u;
+    part[0][w][l] = (uint64_t)ft; part[1][w][l] = ev; part[2][w][l] = dl; part[3][w][l] = dr;
+    part[4][w][l] = ud; part[5][w][l] = st; part[6][w][l] = me; part[7][w][l] = th;
+    __syncthreads();
+    if (threadIdx.x < 64 && q < nr) {
+        for (int k = 1; k < 4; ++k) {
+            ft = (int64_t)part[0][k][l] > ft ? (int64_t)part[0][k][l] : ft;
+            ev += part[1][k][l]; dl += part[2][k][l]; dr += part[3][k][l]; ud += part[4][k][l];
+            st = part[5][k][l] > st ? part[5][k][l] : st;
+            me = part[6][k][l] > me ? part[6][k][l] : me;
+            th += part[7][k][l];
+        }
+        uint64_t GAS* o = gp(out);
+        auto add = [&](int f, uint64_t v) {
+            if (v) __hip_atomic_fetch_add((unsigned long long GAS*)(o + (size_t)f * nr + q), (unsigned long long)v,
+                                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        };
+        auto mx = [&](int f, uint64_t v) {
+            __hip_atomic_fetch_max((unsigned long long GAS*)(o + (size_t)f * nr + q), (unsigned long long)v,
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        };
+        mx(0, (uint64_t)(ft > 0 ? ft : 0));  // (final times are >= 0)
+        add(1, ev); add(2, dl); add(3, dr); add(4, ud);
+        mx(5, st);
+        mx(6, me);
+        add(7, th);
+    }
 }
 
 // Per-replica digest of the results and node hashes (tw_tie_audit compares
@@ -3242,6 +3328,7 @@ struct tw_shard {
     uint32_t n_rep = 1;             // replicas batched per node
     bool heavy_ok = false;          // some node's inbox can exceed TW_LIGHT (tw_lp_due runs)
     uint64_t lpb_windows = 0, lpb_ticks = 0;  // of the last batched-LP tw_run
+    bool lpb_fresh = false;         // tw_reset since the last batched-LP tw_run: every counter is 0
     bool has_ph1 = false;           // two-phase windows (Dev::phase)
     uint4* foreign = nullptr;      // [out_cap][2]
     uint32_t* n_foreign = nullptr;
@@ -3828,6 +3915,7 @@ int sh_reset(tw_shard* c) {
         c->d.act_cur = 0;
         c->d.wid = 0;
         HIPCHK(hipMemsetAsync(d.act_n, 0, 8 * TW_LP_NB, st));
+        c->lpb_fresh = c->lpb;
     }
     if (d.pq_hdr) {
         // empty MinQueues: no element, no node used, every rank a Skip
@@ -3957,7 +4045,8 @@ int sh_read_results(tw_shard* c, tw_replica_result* out, size_t n) {
         const uint32_t nr = c->n_rep;
         uint64_t* dd = nullptr;
         HIPCHK(hipMallocAsync((void**)&dd, 64ull * nr, c->stream));
-        hipLaunchKernelGGL(tw_lpb_reduce, dim3((nr + 255) / 256), dim3(256), 0, c->stream, d, dd);
+        HIPCHK(hipMemsetAsync(dd, 0, 64ull * nr, c->stream));
+        hipLaunchKernelGGL(tw_lpb_reduce, dim3((nr + 63) / 64, TW_RED_GROUPS / 4), dim3(256), 0, c->stream, d, dd);
         HIPCHK(hipGetLastError());
         std::vector<uint64_t> h(8ull * nr);
         HIPCHK(hipMemcpyAsync(h.data(), dd, 64ull * nr, hipMemcpyDeviceToHost, c->stream));
@@ -3968,7 +4057,8 @@ int sh_read_results(tw_shard* c, tw_replica_result* out, size_t n) {
             std::memset(&o, 0, sizeof(o));
             o.final_t = (int64_t)h[q]; o.events = h[nr + q]; o.delivered = h[2ull * nr + q];
             o.dropped = h[3ull * nr + q]; o.undeliverable = h[4ull * nr + q]; o.status = (uint32_t)h[5ull * nr + q];
-            o.main_exc = (uint32_t)h[6ull * nr + q]; o.threads = h[7ull * nr + q];
+            o.main_exc = (uint32_t)h[6ull * nr + q];  // (the node tag is in the high word)
+            o.threads = h[7ull * nr + q];
         }
         return TW_OK;
     }
@@ -4533,12 +4623,19 @@ int sh_lp_run_windows(tw_shard* c, uint64_t max_ticks, tw_lp_state* out) {
 // Batched LP: tw_run = the whole device window loop (one host sync per 16 ticks)
 static int lpb_run(tw_shard* c, tw_stats* out) {
     auto w0 = std::chrono::steady_clock::now();
+    // the run's counts are the results minus those before it: zero right
+    // after tw_reset (no reduction pass needed)
     std::vector<tw_replica_result> before;
     if (out) {
         before.resize(c->n_rep);
-        int rc = sh_read_results(c, before.data(), before.size());
-        if (rc) return rc;
+        if (c->lpb_fresh) {
+            std::memset(before.data(), 0, sizeof(tw_replica_result) * before.size());
+        } else {
+            int rc = sh_read_results(c, before.data(), before.size());
+            if (rc) return rc;
+        }
     }
+    c->lpb_fresh = false;
     while (c->ev_pool.size() < 2) {
         hipEvent_t e;
         HIPCHK(hipEventCreate(&e));
