@@ -902,7 +902,11 @@ struct Lane {
     // quad 0 of a record; quad q is c.RQ further ([quad][slot][replica]: the 64
     // lanes' same quad of the same slot is one contiguous 1 KiB, so a wave that
     // writes only its header quads still writes whole lines)
-    __device__ __forceinline__ uint4 GAS* hrec(uint32_t slot) const { return gp(c.slots) + ix(slot); }
+    // (LP lanes: a record's four quads contiguous, [slot][lane][quad], c.RQ = 1 --
+    // their work lists are sparse, so a record is one line instead of four)
+    __device__ __forceinline__ uint4 GAS* hrec(uint32_t slot) const {
+        return gp(c.slots) + (LP ? ix(slot) * 4 : ix(slot));
+    }
     __device__ __forceinline__ void hbm_load(uint32_t slot, Th& th) const {
         const uint4 GAS* p = hrec(slot);
         unpack(th, p[0], p[c.RQ], p[2 * c.RQ], p[3 * c.RQ]);
@@ -1893,14 +1897,14 @@ __global__ void __launch_bounds__(TW_WG) tw_init_kernel(Dev c, uint32_t main_pc,
     const uint32_t g = lp_mode ? (c.lp0 + r) >> c.rep_lg : 0u;
     const uint32_t rho = lp_mode ? (c.lp0 + r) & ((1u << c.rep_lg) - 1u) : r;
     const bool has_main = !lp_mode || g == main_node;
-    for (uint32_t f = 0; f < SC_COUNT; ++f) gp(c.scal)[(size_t)f * c.R + r] = 0;
-    gp(c.scal)[(size_t)SC_THREADS * c.R + r] = has_main ? 1 : 0;
-    gp(c.scal)[(size_t)SC_TIDC * c.R + r] = tid0;  // main is tid 0 (TimedT.hs:272-280)
-    gp(c.scal)[(size_t)SC_SEQ * c.R + r] = seq0;
-    gp(c.scal)[(size_t)SC_STATUS * c.R + r] = TW_REP_RUNNING;
-    gp(c.scal)[(size_t)SC_PENDING_MAIN * c.R + r] = has_main ? 1 : 0;
-    gp(c.scal)[(size_t)SC_BUMP * c.R + r] = has_main ? 1 : 0;  // slot 0 = main
-    uint4 GAS* p = gp(c.slots) + r;  // slot 0, quad-major (Lane::hrec)
+    for (uint32_t f = 0; f < SC_COUNT; ++f) gp(c.scal)[sc_ix(c, f, r)] = 0;
+    gp(c.scal)[sc_ix(c, SC_THREADS, r)] = has_main ? 1 : 0;
+    gp(c.scal)[sc_ix(c, SC_TIDC, r)] = tid0;  // main is tid 0 (TimedT.hs:272-280)
+    gp(c.scal)[sc_ix(c, SC_SEQ, r)] = seq0;
+    gp(c.scal)[sc_ix(c, SC_STATUS, r)] = TW_REP_RUNNING;
+    gp(c.scal)[sc_ix(c, SC_PENDING_MAIN, r)] = has_main ? 1 : 0;
+    gp(c.scal)[sc_ix(c, SC_BUMP, r)] = has_main ? 1 : 0;  // slot 0 = main
+    uint4 GAS* p = gp(c.slots) + (c.RQ == 1 ? (size_t)r * 4 : (size_t)r);  // slot 0 (Lane::hrec)
     uint32_t w0 = (main_pc & 0xFFFFu) | (F_MAIN << FL_SHIFT);
     p[0] = make_uint4(w0, main_node, has_main ? 0u : 0xFFFFFFFFu, 0u);
     p[c.RQ] = make_uint4(0u, 0u, 0u, 0u);
@@ -2019,9 +2023,14 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
             if (r >= c.R) break;  // (the next block of the work list)
             STIME(tpro0);
             if (LP && c.phase && gp(c.phase)[(c.lp0 + r) >> c.rep_lg] != ph) break;  // the other phase's node
-            uint64_t* sc = gp(c.scal) + r;
+            // the lane's scalar block: [field][replica] for replicas (a wave's
+            // lanes move in lock-step: one coalesced line per field), a
+            // contiguous [lane][SC_LP_STRIDE] block for LP lanes (work lists
+            // are sparse: one or two lines per lane instead of one per field)
+            uint64_t* sc = gp(c.scal) + (LP ? (size_t)r * SC_LP_STRIDE : (size_t)r);
+            const size_t SR = LP ? 1 : c.R;
             const size_t R = c.R;
-            if (sc[SC_STATUS * R] != TW_REP_RUNNING) break;  // (the next block of the work list)
+            if (sc[SC_STATUS * SR] != TW_REP_RUNNING) break;  // (the next block of the work list)
             // this lane's window end (PRW: per-replica windows, Dev::rw -- a per-lane value)
             const int64_t te = (LP && PRW) ? rw_tend(c, r, lwin) : t_end;
             // LP: a node with no live thread, nothing to drain, no due run and no
@@ -2037,7 +2046,7 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
                 ipar = (c.dpar && c.win && ilight) ? (c.wid & 1u) : 0u;  // the buffer the last window filled
                 n_in = gp(c.inbox_n)[(size_t)ipar * R + r];
                 const bool drain = fresh && n_in != 0 && ilight;
-                if (sc[SC_LIVE * R] == 0 && sc[SC_PENDING_MAIN * R] == 0 && !drain && sc[SC_DUE_H * R] >= sc[SC_DUE_N * R] &&
+                if (sc[SC_LIVE * SR] == 0 && sc[SC_PENDING_MAIN * SR] == 0 && !drain && sc[SC_DUE_H * SR] >= sc[SC_DUE_N * SR] &&
                     !(c.lpb && gp(c.spawn_n)[r]))
                     break;  // (the next block of the work list)
             }
@@ -2060,18 +2069,18 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
             L.prun = -1;
             L.hacc = 0;
             L.hnode = 0xFFFFFFFFu;
-            L.now = (int64_t)sc[SC_NOW * R]; L.final_t = (int64_t)sc[SC_FINAL_T * R];
-            L.seq = (uint32_t)sc[SC_SEQ * R]; L.tidc = (uint32_t)sc[SC_TIDC * R]; L.live = (uint32_t)sc[SC_LIVE * R];
-            const uint32_t near_n0 = (uint32_t)sc[SC_NEAR_N * R];
-            L.far_n = (uint32_t)sc[SC_FAR_N * R];
-            L.status = (uint32_t)sc[SC_STATUS * R];
-            L.free_n = (uint32_t)sc[SC_FREE_N * R]; L.ftop = (uint32_t)sc[SC_FTOP * R]; L.bump = (uint32_t)sc[SC_BUMP * R];
+            L.now = (int64_t)sc[SC_NOW * SR]; L.final_t = (int64_t)sc[SC_FINAL_T * SR];
+            L.seq = (uint32_t)sc[SC_SEQ * SR]; L.tidc = (uint32_t)sc[SC_TIDC * SR]; L.live = (uint32_t)sc[SC_LIVE * SR];
+            const uint32_t near_n0 = (uint32_t)sc[SC_NEAR_N * SR];
+            L.far_n = (uint32_t)sc[SC_FAR_N * SR];
+            L.status = (uint32_t)sc[SC_STATUS * SR];
+            L.free_n = (uint32_t)sc[SC_FREE_N * SR]; L.ftop = (uint32_t)sc[SC_FTOP * SR]; L.bump = (uint32_t)sc[SC_BUMP * SR];
         #pragma unroll
             for (int w = 0; w < CW_COUNT; ++w) L.cs(w, 0);
-            L.cs(CW_MAINEXC, (uint32_t)sc[SC_MAIN_EXC * R]);
-            L.cs(CW_TMO, (uint32_t)sc[SC_TMO_CTR * R]);
-            L.cs(CW_TRN, (uint32_t)sc[SC_TRACE_N * R]);
-            const uint64_t events0 = sc[SC_EVENTS * R];
+            L.cs(CW_MAINEXC, (uint32_t)sc[SC_MAIN_EXC * SR]);
+            L.cs(CW_TMO, (uint32_t)sc[SC_TMO_CTR * SR]);
+            L.cs(CW_TRN, (uint32_t)sc[SC_TRACE_N * SR]);
+            const uint64_t events0 = sc[SC_EVENTS * SR];
             const uint64_t ev_room64 = max_events > events0 ? max_events - events0 : 0;
             const uint32_t ev_room = ev_room64 > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)ev_room64;
             L.t_end = te;
@@ -2084,11 +2093,11 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
             L.oo = 0;
             if constexpr (LP) {
                 L.oo = gp(c.out_off)[(c.lp0 + r) >> c.rep_lg];  // (the lane's node: every thread of an LP lane runs on it)
-                const uint32_t dn = (uint32_t)sc[SC_DUE_N * R], dh = (uint32_t)sc[SC_DUE_H * R];
+                const uint32_t dn = (uint32_t)sc[SC_DUE_N * SR], dh = (uint32_t)sc[SC_DUE_H * SR];
                 const size_t ib = ib_base(c, r);
                 L.ds(DW_IB, (uint32_t)ib);
                 L.ds(DW_HN, dh | (dn << 16));
-                L.ds(DW_SQ0, (uint32_t)sc[SC_DUE_SEQ * R]);
+                L.ds(DW_SQ0, (uint32_t)sc[SC_DUE_SEQ * SR]);
                 uint4 h = make_uint4(0, 0, 0, 0);
                 if (dh < dn) h = gp(c.due)[(ib + (size_t)dh * ib_stride(c)) * 2];
                 L.ds(DW_TL, h.x);
@@ -2102,8 +2111,8 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
         #pragma unroll
                 for (int j = 0; j < TW_RUNS; ++j) {
                     // (no far runs configured, e.g. LP nodes: nothing to load)
-                    const uint32_t rh = c.Cr ? (uint32_t)sc[(SC_RH0 + j) * R] : 0u;
-                    const uint32_t rn = c.Cr ? (uint32_t)sc[(SC_RC0 + j) * R] : 0u;
+                    const uint32_t rh = c.Cr ? (uint32_t)sc[(SC_RH0 + j) * SR] : 0u;
+                    const uint32_t rn = c.Cr ? (uint32_t)sc[(SC_RC0 + j) * SR] : 0u;
                     rh4[j] = rh;
                     uint4 h = make_uint4(0, 0, 0, 0), s2 = h, u = h;
                     if (rn) {
@@ -2243,7 +2252,7 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
                 STADDL(K_CYC_PRO, tpro1 - tpro0);
             }
         #endif
-            uint32_t pending_main = (uint32_t)sc[SC_PENDING_MAIN * R];
+            uint32_t pending_main = (uint32_t)sc[SC_PENDING_MAIN * SR];
             // nothing loaded before the loop may stay pending into it (a loop-header
             // wait would otherwise drain the counter on every iteration)
             __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
@@ -2380,30 +2389,30 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
                                            __HIP_MEMORY_SCOPE_AGENT);
             STIME(tepi0);
         #endif
-            sc[SC_PENDING_MAIN * R] = pending_main;
+            sc[SC_PENDING_MAIN * SR] = pending_main;
             if (!LP && L.status == TW_REP_RUNNING && L.live == 0) L.status = TW_REP_DONE;
 
-            sc[SC_NOW * R] = (uint64_t)L.now; sc[SC_FINAL_T * R] = (uint64_t)L.final_t;
-            sc[SC_SEQ * R] = L.seq; sc[SC_TIDC * R] = L.tidc; sc[SC_LIVE * R] = L.live;
-            sc[SC_NEAR_N * R] = L.near_n; sc[SC_FAR_N * R] = L.far_n;
-            sc[SC_STATUS * R] = L.status; sc[SC_MAIN_EXC * R] = L.cg(CW_MAINEXC);
-            sc[SC_FREE_N * R] = L.free_n; sc[SC_FTOP * R] = L.ftop; sc[SC_BUMP * R] = L.bump;
-            sc[SC_TMO_CTR * R] = L.cg(CW_TMO);
-            sc[SC_TRACE_N * R] = L.cg(CW_TRN);
-            sc[SC_EVENTS * R] = events0 + L.d_ev;
+            sc[SC_NOW * SR] = (uint64_t)L.now; sc[SC_FINAL_T * SR] = (uint64_t)L.final_t;
+            sc[SC_SEQ * SR] = L.seq; sc[SC_TIDC * SR] = L.tidc; sc[SC_LIVE * SR] = L.live;
+            sc[SC_NEAR_N * SR] = L.near_n; sc[SC_FAR_N * SR] = L.far_n;
+            sc[SC_STATUS * SR] = L.status; sc[SC_MAIN_EXC * SR] = L.cg(CW_MAINEXC);
+            sc[SC_FREE_N * SR] = L.free_n; sc[SC_FTOP * SR] = L.ftop; sc[SC_BUMP * SR] = L.bump;
+            sc[SC_TMO_CTR * SR] = L.cg(CW_TMO);
+            sc[SC_TRACE_N * SR] = L.cg(CW_TRN);
+            sc[SC_EVENTS * SR] = events0 + L.d_ev;
             if (LP) {
-                sc[SC_DUE_H * R] = L.dg(DW_HN) & 0xFFFFu;
+                sc[SC_DUE_H * SR] = L.dg(DW_HN) & 0xFFFFu;
                 if (L.dg(DW_IB) >> 31)  // sent records straight into inboxes (Lane::emit)
                     min_hot((uint64_t GAS*)(PRW ? rw_at(c, RW_WIN, r) : gp(c.win) + WN_REC_MIN), (uint64_t)(te + 1));
             }
-            sc[SC_DELIVERED * R] += L.cg(CW_DL); sc[SC_DROPPED * R] += L.cg(CW_DR);
-            sc[SC_UNDELIV * R] += L.cg(CW_UD); sc[SC_THREADS * R] += L.d_th;
+            sc[SC_DELIVERED * SR] += L.cg(CW_DL); sc[SC_DROPPED * SR] += L.cg(CW_DR);
+            sc[SC_UNDELIV * SR] += L.cg(CW_UD); sc[SC_THREADS * SR] += L.d_th;
             if (HR && c.Cr) {
                 const uint4 ix4 = *L.rqp(RQ_IDX);
         #pragma unroll
                 for (int j = 0; j < TW_RUNS; ++j) {
-                    sc[(SC_RH0 + j) * R] = Lane<LP, WG, NC, RUNS>::q_at(ix4, j);
-                    sc[(SC_RC0 + j) * R] = L.rqp(RQ_TAIL + j)->w;
+                    sc[(SC_RH0 + j) * SR] = Lane<LP, WG, NC, RUNS>::q_at(ix4, j);
+                    sc[(SC_RC0 + j) * SR] = L.rqp(RQ_TAIL + j)->w;
                 }
             }
             for (uint32_t i = 0, j = 0; i < NC; ++i) {
@@ -3200,17 +3209,17 @@ __global__ void __launch_bounds__(256) tw_lp_due(Dev c) {
         if (tid == 0) {
             const uint32_t left = n - nd;
             gp(c.inbox_n)[r] = left;
-            uint64_t* sc = gp(c.scal) + r;
+            uint64_t* sc = gp(c.scal) + (size_t)r * SC_LP_STRIDE;  // (LP: the lane's block)
             const size_t R = c.R;
-            const uint64_t s0 = sc[SC_SEQ * R];
+            const uint64_t s0 = sc[SC_SEQ];
             if (s0 + nd >= 0xFFFFFFFFull) {
-                if (sc[SC_STATUS * R] == TW_REP_RUNNING) sc[SC_STATUS * R] = TW_REP_ERR_COUNTER;
+                if (sc[SC_STATUS] == TW_REP_RUNNING) sc[SC_STATUS] = TW_REP_ERR_COUNTER;
             } else {
-                sc[SC_SEQ * R] = s0 + nd;  // the due run's queue seqs: s0 + 1 .. s0 + nd
+                sc[SC_SEQ] = s0 + nd;  // the due run's queue seqs: s0 + 1 .. s0 + nd
             }
-            sc[SC_DUE_SEQ * R] = s0;
-            sc[SC_DUE_N * R] = nd;
-            sc[SC_DUE_H * R] = 0;
+            sc[SC_DUE_SEQ] = s0;
+            sc[SC_DUE_N] = nd;
+            sc[SC_DUE_H] = 0;
             if (smin != ~0ull)
                 __hip_atomic_fetch_min(c.rw ? (uint64_t GAS*)rw_at(c, RW_WIN, r) : gp(c.pend_min), (uint64_t)smin,
                                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -3253,12 +3262,12 @@ __global__ void __launch_bounds__(256) tw_lpb_reduce(Dev c, uint64_t* out) {
     uint64_t ev = 0, dl = 0, dr = 0, ud = 0, th = 0, me = 0, st = TW_REP_DONE;
     if (q < nr) {
         for (uint32_t n = n0; n < n1; ++n) {
-            const uint64_t GAS* sc = gp(c.scal) + ((size_t)n << c.rep_lg) + q;
-            const int64_t f = (int64_t)sc[SC_FINAL_T * R];
+            const uint64_t GAS* sc = gp(c.scal) + ((((size_t)n << c.rep_lg) + q) * SC_LP_STRIDE);
+            const int64_t f = (int64_t)sc[SC_FINAL_T];
             ft = f > ft ? f : ft;
-            ev += sc[SC_EVENTS * R]; dl += sc[SC_DELIVERED * R]; dr += sc[SC_DROPPED * R];
-            ud += sc[SC_UNDELIV * R]; th += sc[SC_THREADS * R];
-            const uint64_t x = sc[SC_MAIN_EXC * R], s2 = sc[SC_STATUS * R];
+            ev += sc[SC_EVENTS]; dl += sc[SC_DELIVERED]; dr += sc[SC_DROPPED];
+            ud += sc[SC_UNDELIV]; th += sc[SC_THREADS];
+            const uint64_t x = sc[SC_MAIN_EXC], s2 = sc[SC_STATUS];
             me = x ? ((uint64_t)(n + 1) << 32) | (x & 0xFFFFFFFFull) : me;
             st = (s2 >= TW_REP_ABORTED && s2 > st) ? s2 : st;
         }
@@ -3301,7 +3310,7 @@ __global__ void __launch_bounds__(256) tw_digest_kernel(Dev c, uint64_t* out) {
     uint64_t d = 0;
     const int fields[8] = {SC_FINAL_T, SC_EVENTS, SC_DELIVERED, SC_DROPPED, SC_UNDELIV, SC_STATUS, SC_MAIN_EXC,
                            SC_THREADS};
-    for (int i = 0; i < 8; ++i) d = mix64(d ^ gp(c.scal)[(size_t)fields[i] * c.R + r]) + (uint64_t)i;
+    for (int i = 0; i < 8; ++i) d = mix64(d ^ gp(c.scal)[sc_ix(c, fields[i], r)]) + (uint64_t)i;
     for (uint32_t n = 0; n < c.N; ++n) d += mix64(gp(c.hash)[(size_t)n * c.R + r] ^ ((uint64_t)n * 0x9e3779b97f4a7c15ull));
     gp(out)[r] = d;
 }
@@ -3612,7 +3621,7 @@ static int load_common(tw_shard* c, const tw_scenario_desc* s, bool lp, uint32_t
     d.lpb = lpb ? 1u : 0u;
     d.R = lp ? lp_count : s->n_replicas;
     d.S = s->max_slots; d.Q = s->queue_capacity;
-    d.RQ = (uint64_t)d.S * d.R;
+    d.RQ = lp ? 1u : (uint64_t)d.S * d.R;  // quad stride: LP records contiguous (Lane::hrec)
     d.N = lp ? 1 : s->n_nodes;  // per-lane node arrays
     d.Ntot = s->n_nodes;
     d.lp0 = lp ? lp_begin : 0;
@@ -3690,7 +3699,8 @@ static int load_common(tw_shard* c, const tw_scenario_desc* s, bool lp, uint32_t
     ALLOC(ldst, d.L);
     ALLOC(lrev, d.L);
     if (s->link_table) ALLOC(ltab, (size_t)d.L * d.D * Rt);
-    ALLOC(d.scal, (size_t)SC_COUNT * R);
+    d.sc_lp = lp ? 1u : 0u;  // LP lanes: one contiguous scalar block per lane (sc_ix)
+    ALLOC(d.scal, (size_t)(lp ? SC_LP_STRIDE : SC_COUNT) * R);
     ALLOC(d.slots, (size_t)d.S * R * 4);
     ALLOC(d.free_stk, (size_t)d.S * R);
     ALLOC(d.far, (size_t)d.Q * R);
@@ -3953,7 +3963,11 @@ int sh_run(tw_shard* c, int64_t t_end_us, uint64_t max_events, tw_stats* out) {
     std::vector<uint64_t> ev0;
     if (out) {
         ev0.resize(d.R);
-        HIPCHK(hipMemcpyAsync(ev0.data(), d.scal + (size_t)SC_EVENTS * d.R, 8ull * d.R, hipMemcpyDeviceToHost, st));
+        if (d.sc_lp)  // (the events word of every lane's block: one strided copy)
+            HIPCHK(hipMemcpy2DAsync(ev0.data(), 8, d.scal + SC_EVENTS, 8ull * SC_LP_STRIDE, 8, d.R,
+                                    hipMemcpyDeviceToHost, st));
+        else
+            HIPCHK(hipMemcpyAsync(ev0.data(), d.scal + (size_t)SC_EVENTS * d.R, 8ull * d.R, hipMemcpyDeviceToHost, st));
         HIPCHK(hipStreamSynchronize(st));
     }
     const uint64_t limit = max_events;  // cumulative per-replica cap
@@ -4062,10 +4076,11 @@ int sh_read_results(tw_shard* c, tw_replica_result* out, size_t n) {
         }
         return TW_OK;
     }
-    std::vector<uint64_t> sc((size_t)SC_COUNT * d.R);
-    HIPCHK(hipMemcpyAsync(sc.data(), d.scal, 8ull * SC_COUNT * d.R, hipMemcpyDeviceToHost, c->stream));
+    const size_t nsc = (size_t)(d.sc_lp ? SC_LP_STRIDE : SC_COUNT) * d.R;
+    std::vector<uint64_t> sc(nsc);
+    HIPCHK(hipMemcpyAsync(sc.data(), d.scal, 8ull * nsc, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
-    auto F = [&](int f, uint32_t i) { return sc[(size_t)f * d.R + i]; };
+    auto F = [&](int f, uint32_t i) { return d.sc_lp ? sc[(size_t)i * SC_LP_STRIDE + f] : sc[(size_t)f * d.R + i]; };
     for (uint32_t i = 0; i < d.R; ++i) {
         out[i].final_t = (int64_t)F(SC_FINAL_T, i); out[i].events = F(SC_EVENTS, i);
         out[i].delivered = F(SC_DELIVERED, i); out[i].dropped = F(SC_DROPPED, i);

@@ -78,6 +78,9 @@ enum {
     SC_DUE_N, SC_DUE_H, SC_DUE_SEQ, SC_COUNT
 };
 
+#define SC_LP_STRIDE 32  // an LP lane's scalar block: 256 B, two 128-B lines
+static_assert(SC_COUNT <= SC_LP_STRIDE, "LP scalar block too small");
+
 struct Dev {
     // shape
     uint32_t R, S, Q, N, L, D, T, Cr;
@@ -116,6 +119,7 @@ struct Dev {
     // travel as spawn records)
     uint32_t lp0, Ntot, IB, out_cap;
     uint32_t rep_lg, lpb;
+    uint32_t sc_lp;      // LP context: scal is [lane][SC_LP_STRIDE] (sc_ix), else [SC_COUNT][R]
     int64_t* rw;         // [RW_COUNT][2^rep_lg] per-replica windows (batched LP device loop), else null
     // per-replica windows: the lanes of a replica in chunks of 2^TW_CHUNK_LG
     // nodes, [chunk][replica]: cw_min = a lower bound of the chunk's lanes'
@@ -202,6 +206,11 @@ struct Dev {
     uint4* pq_scr;
     uint32_t* pq_hdr;
 };
+// index of scalar field f of lane / replica r
+__host__ __device__ __forceinline__ size_t sc_ix(const Dev& c, uint32_t f, size_t r) {
+    return c.sc_lp ? r * SC_LP_STRIDE + f : (size_t)f * c.R + r;
+}
+
 // pqueue header words (per replica, [r * PQ_WORDS + w])
 enum { PQ_N, PQ_NFREE, PQ_BUMP, PQ_FLEN, PQ_MIN, PQ_FOREST = PQ_MIN + 4, PQ_WORDS = PQ_FOREST + 32 };
 
