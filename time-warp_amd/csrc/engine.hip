@@ -1458,6 +1458,33 @@ struct Lane {
                         csp(p, CW_CNODE, node);
                         csp(p, CW_CRA, a);
                         csp(p, CW_CDEL, 2u);  // the child's registers are the parent's
+                        if constexpr (LP) {
+                            // batched LP, a fork onto another node of the replica
+                            // (TimedT.hs:326-342): the child goes out as a spawn record
+                            // right here, with the registers it captures now, and the
+                            // parent's `wait (for 1 mcs)` becomes an ordinary yield --
+                            // which the inline continuation below resumes in this pass
+                            // when nothing on the node is due before it (a main thread
+                            // forking every node of the scenario runs its loop without a
+                            // queue round trip per fork)
+                            const bool xs = p && c.lpb && node != th.w1;
+                            if (__builtin_amdgcn_ballot_w64(xs)) {
+                                bool ph1 = false;
+                                if (xs && c.phase) {
+                                    ph1 = gp(c.phase)[th.w1] != 0;  // (not from a phase-1 node)
+                                    tw_vm_drain();
+                                }
+                                const bool go = xs && !ph1;
+                                pfail(xs && ph1, TW_REP_ERR_INSN);
+                                tc = (xs && ph1) ? (uint32_t)T_STOP : tc;
+                                if (go) {
+                                    emit_spawn(now, (uint32_t)imm, lane_of(node), rf[0], rf[WG], rf[2 * WG], rf[3 * WG]);
+                                    rf[a * WG] = -1;  // the ref is opaque (refs name engine slots)
+                                }
+                                tc = go ? (uint32_t)T_YIELD : tc;
+                                yt = go ? now + 1 : yt;
+                            }
+                        }
                     }
                     const bool wt = tk == TK_WREL || tk == TK_WABS || tk == TK_WREG;
                     if (need(wt)) {

@@ -244,7 +244,7 @@ def ping_pong(n_replicas: int = 1, round_trips: int = 1, network_delay=(ms(1), m
 def hotspot(n_senders: int = 256, n_replicas: int = 1, msg_num: int = 1000, msg_rate: int = 1000,
             duration_s: int = 10, network_delay=(ms(1), ms(5)), seed_base: int = 0,
             near_horizon_us: int = sec(10), fork_strategy: str = "fork", payload_bytes: int = 0,
-            bandwidth_bytes_per_s: float = 0.0, probe_traces: int = 0) -> Scenario:
+            bandwidth_bytes_per_s: float = 0.0, probe_traces: int = 0, probe_loads: int = 0) -> Scenario:
     """bench/Network many-senders -> one-receiver request/response.
 
     Sender (Sender/Main.hs:34-64): listen for Pong, then per message
@@ -258,8 +258,9 @@ def hotspot(n_senders: int = 256, n_replicas: int = 1, msg_num: int = 1000, msg_
     delivering thread (ForkStrategy `const id`, MonadDialog.hs:114-117) instead
     of the default `fork_` (MonadDialog.hs:317): two pops fewer per delivery.
 
-    ``probe_traces`` (diagnostics only, tools/pass_probe.py) adds that many
-    trace instructions to the Ping handler: the receiver's per-instruction cost.
+    ``probe_traces`` / ``probe_loads`` (diagnostics only, tools/pass_probe.py)
+    add that many trace / node-variable load instructions to the Ping handler:
+    the receiver's cost per instruction pass and per dependent memory load.
 
     ``bandwidth_bytes_per_s > 0`` adds each message's transmission time to its
     link delay: the BinaryP wire size of `Ping/Pong MsgId Payload` with a
@@ -294,6 +295,8 @@ def hotspot(n_senders: int = 256, n_replicas: int = 1, msg_num: int = 1000, msg_
     c = p.function("on_ping")                         # Ping -> logMeasure; reply Pong
     for _ in range(int(probe_traces)):
         c.trace(TAG_PING, 0)
+    for _ in range(int(probe_loads)):
+        c.nload(3, 2)
     c.trace(TAG_PING, 0)                              # logMeasure PingReceived mid
     c.trace(TAG_PONG_SENT, 0)                         # logMeasure PongSent mid
     c.reply_link(2, 1).send(2, K_PONG, 0)
