@@ -3237,7 +3237,6 @@ __global__ void __launch_bounds__(256) tw_lp_due(Dev c) {
             const uint32_t left = n - nd;
             gp(c.inbox_n)[r] = left;
             uint64_t* sc = gp(c.scal) + (size_t)r * SC_LP_STRIDE;  // (LP: the lane's block)
-            const size_t R = c.R;
             const uint64_t s0 = sc[SC_SEQ];
             if (s0 + nd >= 0xFFFFFFFFull) {
                 if (sc[SC_STATUS] == TW_REP_RUNNING) sc[SC_STATUS] = TW_REP_ERR_COUNTER;
@@ -3282,7 +3281,6 @@ __global__ void __launch_bounds__(256) tw_lpb_reduce(Dev c, uint64_t* out) {
     const uint32_t nr = 1u << c.rep_lg;
     const uint32_t q = blockIdx.x * 64 + (threadIdx.x & 63u);
     const uint32_t g = blockIdx.y * 4 + (threadIdx.x >> 6);
-    const size_t R = c.R;
     const uint32_t per = (c.Ntot + TW_RED_GROUPS - 1) / TW_RED_GROUPS;
     const uint32_t n0 = g * per, n1 = n0 + per < c.Ntot ? n0 + per : c.Ntot;
     int64_t ft = 0;
@@ -3329,6 +3327,51 @@ __global__ void __launch_bounds__(256) tw_lpb_reduce(Dev c, uint64_t* out) {
     }
 }
 
+// tw_run's statistics on the device, instead of copying every replica's
+// results to the host (248 MB for C2's million replicas): out[0] the events
+// of this run (the events word minus its value at the run's start), [1..3]
+// delivered / dropped / undeliverable, [4] the largest final time, [5] / [6]
+// replicas done / in an error status.  A wave reduces its 64 replicas, its
+// first lane adds them in with atomics (out zeroed by the caller).
+__device__ __forceinline__ unsigned long long shx64(unsigned long long v, int m) {
+    const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)v, m, 64);
+    const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(v >> 32), m, 64);
+    return ((unsigned long long)hi << 32) | lo;
+}
+__global__ void __launch_bounds__(256) tw_stats_kernel(Dev c, const uint64_t* ev0, unsigned long long* out) {
+    const size_t r = (size_t)blockIdx.x * 256 + threadIdx.x;
+    unsigned long long v[7] = {0ull, 0ull, 0ull, 0ull, 0ull, 0ull, 0ull};
+    if (r < c.R) {
+        const uint64_t GAS* s = gp(c.scal);
+        v[0] = s[sc_ix(c, SC_EVENTS, r)] - gp(ev0)[r];
+        v[1] = s[sc_ix(c, SC_DELIVERED, r)];
+        v[2] = s[sc_ix(c, SC_DROPPED, r)];
+        v[3] = s[sc_ix(c, SC_UNDELIV, r)];
+        const int64_t ft = (int64_t)s[sc_ix(c, SC_FINAL_T, r)];
+        v[4] = ft > 0 ? (unsigned long long)ft : 0ull;
+        const uint32_t st = (uint32_t)s[sc_ix(c, SC_STATUS, r)];
+        v[5] = st == TW_REP_DONE ? 1ull : 0ull;
+        v[6] = st >= TW_REP_ERR_SLOTS ? 1ull : 0ull;
+    }
+#pragma unroll
+    for (int k = 0; k < 7; ++k) {
+#pragma unroll
+        for (int m = 32; m >= 1; m >>= 1) {
+            const unsigned long long o = shx64(v[k], m);
+            v[k] = k == 4 ? (o > v[k] ? o : v[k]) : v[k] + o;
+        }
+    }
+    if (__lane_id() == 0) {
+#pragma unroll
+        for (int k = 0; k < 7; ++k) {
+            if (k == 4)
+                __hip_atomic_fetch_max(gp(out) + k, v[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            else if (v[k])
+                __hip_atomic_fetch_add(gp(out) + k, v[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+}
+
 // Per-replica digest of the results and node hashes (tw_tie_audit compares
 // runs under different tie orders without copying every hash to the host).
 __global__ void __launch_bounds__(256) tw_digest_kernel(Dev c, uint64_t* out) {
@@ -3352,6 +3395,11 @@ struct tw_shard {
     bool loaded = false;
     std::vector<void*> allocs;
     uint32_t* h_active = nullptr;  // pinned
+    // tw_run's statistics reduced on the device (tw_stats_kernel): the events
+    // column at the run's start, the 8 result words, their pinned host copy
+    uint64_t* st_ev0 = nullptr;
+    unsigned long long* st_out = nullptr;
+    unsigned long long* h_st = nullptr;
     uint32_t main_pc = 0, main_node = 0;
     int64_t* main_regs = nullptr;  // device copies for tw_reset
     int64_t* nv_init = nullptr;
@@ -3452,6 +3500,10 @@ void free_all(tw_shard* c) {
     c->ex_world = 1;
     c->ex_rank = c->ex_cap = c->ex_cap_eff = 0;
     c->loop_ready = false;
+    if (c->st_ev0) (void)hipFree(c->st_ev0);
+    if (c->st_out) (void)hipFree(c->st_out);
+    c->st_ev0 = nullptr;
+    c->st_out = nullptr;
     if (c->tick_graph) (void)hipGraphExecDestroy(c->tick_graph);
     c->tick_graph = nullptr;
     c->tick_gkey.clear();
@@ -3519,6 +3571,7 @@ void sh_destroy(tw_shard* c) {
     free_all(c);
     for (hipEvent_t e : c->ev_pool) (void)hipEventDestroy(e);
     if (c->h_active) (void)hipHostFree(c->h_active);
+    if (c->h_st) (void)hipHostFree(c->h_st);
     if (c->h_win) (void)hipHostFree(c->h_win);
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
     delete c;
@@ -3987,15 +4040,18 @@ int sh_run(tw_shard* c, int64_t t_end_us, uint64_t max_events, tw_stats* out) {
     const Dev& d = c->d;
     // events before this call (to report per-call deltas; only when asked
     // for: an LP window would otherwise copy 8 B per node every window)
-    std::vector<uint64_t> ev0;
+    // (a device-side copy of the events column; tw_stats_kernel reduces the
+    // run's statistics on the device at the end)
     if (out) {
-        ev0.resize(d.R);
+        if (!c->st_ev0) HIPCHK(hipMalloc((void**)&c->st_ev0, 8ull * (d.R ? d.R : 1)));
+        if (!c->st_out) HIPCHK(hipMalloc((void**)&c->st_out, 64));
+        if (!c->h_st) HIPCHK(hipHostMalloc((void**)&c->h_st, 64));
         if (d.sc_lp)  // (the events word of every lane's block: one strided copy)
-            HIPCHK(hipMemcpy2DAsync(ev0.data(), 8, d.scal + SC_EVENTS, 8ull * SC_LP_STRIDE, 8, d.R,
-                                    hipMemcpyDeviceToHost, st));
+            HIPCHK(hipMemcpy2DAsync(c->st_ev0, 8, d.scal + SC_EVENTS, 8ull * SC_LP_STRIDE, 8, d.R,
+                                    hipMemcpyDeviceToDevice, st));
         else
-            HIPCHK(hipMemcpyAsync(ev0.data(), d.scal + (size_t)SC_EVENTS * d.R, 8ull * d.R, hipMemcpyDeviceToHost, st));
-        HIPCHK(hipStreamSynchronize(st));
+            HIPCHK(hipMemcpyAsync(c->st_ev0, d.scal + (size_t)SC_EVENTS * d.R, 8ull * d.R, hipMemcpyDeviceToDevice,
+                                  st));
     }
     const uint64_t limit = max_events;  // cumulative per-replica cap
     c->launch_ms.clear();
@@ -4056,18 +4112,20 @@ int sh_run(tw_shard* c, int64_t t_end_us, uint64_t max_events, tw_stats* out) {
     }
     if (out) {
         std::memset(out, 0, sizeof(*out));
-        std::vector<tw_replica_result> rr(d.R);
-        int rc = sh_read_results(c, rr.data(), d.R);
-        if (rc) return rc;
-        for (uint32_t i = 0; i < d.R; ++i) {
-            out->events += rr[i].events - ev0[i];
-            out->delivered += rr[i].delivered;
-            out->dropped += rr[i].dropped;
-            out->undeliverable += rr[i].undeliverable;
-            if (rr[i].final_t > out->max_final_t) out->max_final_t = rr[i].final_t;
-            if (rr[i].status == TW_REP_DONE) ++out->replicas_done;
-            if (rr[i].status >= TW_REP_ERR_SLOTS) ++out->replicas_error;
-        }
+        HIPCHK(hipMemsetAsync(c->st_out, 0, 64, st));
+        hipLaunchKernelGGL(tw_stats_kernel, dim3((uint32_t)((d.R + 255) / 256)), dim3(256), 0, st, d,
+                           (const uint64_t*)c->st_ev0, c->st_out);
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipMemcpyAsync(c->h_st, c->st_out, 64, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+        const unsigned long long* h = c->h_st;
+        out->events = h[0];
+        out->delivered = h[1];
+        out->dropped = h[2];
+        out->undeliverable = h[3];
+        out->max_final_t = (int64_t)h[4];
+        out->replicas_done = (uint32_t)h[5];
+        out->replicas_error = (uint32_t)h[6];
         out->sends = out->delivered + out->dropped + out->undeliverable;
         out->launches = launches;
         out->kernel_ms = kms;
