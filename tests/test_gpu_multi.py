@@ -97,6 +97,26 @@ def test_one_rank_rccl_replicas(engine_mod, oracle_mod):
     assert st.max_final_t == int(ores["final_t"].max())
 
 
+def test_one_rank_rccl_lpb(engine_mod, oracle_mod):
+    """bench.py's C3 at 8 GPUs: each rank runs its replica block as batched
+    logical processes (tw_lpb_load on a tw_create_rank context); tw_run's
+    statistics come back through the library's all-reduce."""
+    jid = engine_mod.comm_id()
+    scn = scenarios.token_ring(n_nodes=16, n_replicas=32, launch_duration=40_000_000, drop_log2=4)
+    with engine_mod.Engine(0, comm=(1, 0, jid)) as e:
+        e.load(scn, geometry="lpb")
+        assert e.geometry() == "lpb"
+        st = e.run()
+        res, h = e.results(), e.hashes()
+        e.reset()
+        st2 = e.run()
+    ores, oh = oracle_mod.run_batch(scn, threads=8)
+    _same_batch(res, h, ores, oh, "rccl x1 lpb")
+    assert st.events == st2.events == int(ores["events"].sum())
+    assert st.delivered == int(ores["delivered"].sum()) and st.dropped == int(ores["dropped"].sum())
+    assert st.max_final_t == int(ores["final_t"].max())
+
+
 def test_one_rank_rccl_lp_loop(engine_mod, oracle_mod):
     """tw_lp_run over a one-rank RCCL communicator: the record blocks go
     through ncclSend/ncclRecv to itself, the window words through

@@ -1,6 +1,6 @@
 # round-3 final pass, part 2: C2 / C4 / C5 / C3-at-8,192 bench lines (with CPU baselines) and traffic passes
 export TMPDIR=/tmp
-O=gpurun_out/r03f2
+O=gpurun_out/r03final2
 mkdir -p $O
 run() {  # run NAME SECONDS CMD...
   local name=$1 secs=$2; shift 2
@@ -9,6 +9,7 @@ run() {  # run NAME SECONDS CMD...
   echo "$name=$rc"
   [ $rc -eq 0 ] || exit $rc
 }
+timeout -k 10 300 python -u -m pytest tests/test_gpu_multi.py -x -q --timeout 300 --timeout-method thread > $O/tests_multi.log 2>&1; echo "tests_multi=$?"
 run bench_c2 300 python3 -u bench.py --config ping_pong
 run bench_c4 300 python3 -u bench.py --config gossip
 run bench_c5 400 python3 -u bench.py --config hotspot --steps 2 --warmup 1
