@@ -161,6 +161,15 @@ enum tw_op {
  * thread takes the handler's registers {payload, link, sender, kind}, moves to
  * the destination node and continues at the handler's pc. */
 #define TW_LPC_INLINE 0x80000000u
+/* SEND fused with the LINK / RLINK that computes its link (b flags; made by
+ * Program.finalize from a `LINK a,k ; SEND a,..` or `RLINK a,r ; SEND a,..`
+ * pair, whose SEND stays in the image for jumps to it).  The fused SEND first
+ * does what the pair's first instruction does -- VIA_LINK: r[a] = out_off[node]
+ * + imm; VIA_RLINK: r[a] = link_rev[r[(b >> 12) & 3]], an out-of-range link
+ * stopping the replica as RLINK does -- then sends over r[a] and continues at
+ * pc + 2: one instruction (one interpreter pass, one step) instead of two. */
+#define TW_SEND_VIA_LINK 0x400u
+#define TW_SEND_VIA_RLINK 0x800u
 
 typedef struct tw_insn {
     uint32_t w0;  /* op | a<<8 | b<<16 */

@@ -461,6 +461,17 @@ struct Sim {
                 break;
             }
             case TW_OP_SEND: {
+                // fused LINK / RLINK (timewarp.h TW_SEND_VIA_*): the pair's first
+                // instruction, then this send, then past the pair's SEND
+                if (b & TW_SEND_VIA_LINK) {
+                    r[ra] = (int64_t)d->out_off[th->node] + imm;
+                    ++th->pc;
+                } else if (b & TW_SEND_VIA_RLINK) {
+                    uint64_t l = (uint64_t)r[(b >> 12) & 3];
+                    if (l >= d->n_links) { fail(TW_REP_ERR_INSN); return; }
+                    r[ra] = (int64_t)d->link_rev[l];
+                    ++th->pc;
+                }
                 uint64_t link = (uint64_t)r[ra];
                 if (link >= d->n_links) { fail(TW_REP_ERR_INSN); return; }
                 uint32_t kind = b & 0xFF;

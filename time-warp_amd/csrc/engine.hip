@@ -1571,14 +1571,32 @@ struct Lane {
             }
             case TW_OP_SEND: {  // schedule (after d) (deliver ..) unless the link drops it
                 STIME(tsd0);
+                wr = true;
+                wm = false;
                 if (me) {
-                    const uint64_t link = (uint64_t)ra;
-                    if (link >= c.L) {
+                    // fused LINK / RLINK (TW_SEND_VIA_*): the pair's first instruction
+                    // here, the pass continues past the pair's SEND (LP: the lane's
+                    // out-link base and last reply link are cached)
+                    uint64_t link = (uint64_t)ra;
+                    bool lbad = false;
+                    const bool fz = (b & (TW_SEND_VIA_LINK | TW_SEND_VIA_RLINK)) != 0;
+                    if (b & TW_SEND_VIA_LINK) {
+                        link = (uint64_t)((int64_t)(LP ? oo : gp(c.out_off)[th.w1]) + imm);
+                    } else if (b & TW_SEND_VIA_RLINK) {
+                        const uint64_t rin = (uint64_t)rf[((b >> 12) & 3u) * WG];
+                        lbad = rin >= c.L;
+                        if (!lbad) link = (LP && (uint32_t)rin == rlc_link) ? rlc_rev : gp(c.link_rev)[rin];
+                    }
+                    wm = fz && !lbad;
+                    wv = (int64_t)link;
+                    tgt = fz ? pc + 2 : tgt;
+                    if (lbad || link >= c.L) {
                         fail(TW_REP_ERR_INSN);
                         tc = T_STOP;
                     } else {
                         const uint32_t kind = b & 0xFFu;
-                        const int64_t payload = rf[((b >> 8) & 3u) * WG];
+                        const uint32_t pr = (b >> 8) & 3u;
+                        const int64_t payload = (fz && pr == a) ? (int64_t)link : rf[pr * WG];
                         // the link's ordinal and (LP) its destination entry: independent
                         // loads in flight together, one wait
                         // (a one-deep table -- one delay per link, every scenario but

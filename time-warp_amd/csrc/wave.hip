@@ -835,10 +835,20 @@ struct Wave {
                 wr = true; wv = (int64_t)cp(dv->link_rev)[rb];
                 break;
             case TW_OP_SEND: {  // schedule (after d) (deliver ..) unless the link drops it
-                const uint64_t link = (uint64_t)ra;
+                uint64_t link = (uint64_t)ra;
+                const bool fz = (b & (TW_SEND_VIA_LINK | TW_SEND_VIA_RLINK)) != 0;
+                if (b & TW_SEND_VIA_LINK) {  // fused LINK a, imm
+                    link = (uint64_t)((int64_t)cp(dv->out_off)[th.w1] + imm);
+                } else if (b & TW_SEND_VIA_RLINK) {  // fused RLINK a, r
+                    const uint64_t rin = (uint64_t)th.reg((b >> 12) & 3u);
+                    if (rin >= dv->L) { fail(TW_REP_ERR_INSN); fin = W_STOP; break; }
+                    link = cp(dv->link_rev)[rin];
+                }
+                if (fz) { wr = true; wv = (int64_t)link; npc = pc + 2; }
                 if (link >= dv->L) { fail(TW_REP_ERR_INSN); fin = W_STOP; break; }
                 const uint32_t kind = b & 0xFFu;
-                const int64_t payload = th.reg((b >> 8) & 3u);
+                const uint32_t pr = (b >> 8) & 3u;
+                const int64_t payload = (fz && pr == a) ? (int64_t)link : th.reg(pr);
                 uint32_t GAS* op_ = gp(dv->link_ord) + ix(link);
                 const uint32_t ord = rfl(*op_);
                 st32(op_, ord + 1);

@@ -39,6 +39,7 @@ opaque register value usable only by throw_to / kill_thread.
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass, field
 from typing import Callable, Dict, List, Optional, Sequence, Union
 
@@ -64,6 +65,28 @@ Imm = Union[int, Label]
 
 def _enc(op: int, a: int = 0, b: int = 0) -> int:
     return (op & 0xFF) | ((a & 0xFF) << 8) | ((b & 0xFFFF) << 16)
+
+
+def _fuse_sends(insns: np.ndarray) -> None:
+    """Peephole: `LINK a,k ; SEND a,..` / `RLINK a,r ; SEND a,..` -> a fused
+    SEND in the pair's first slot (TW_SEND_VIA_LINK / _RLINK, timewarp.h).
+    The pair's SEND stays where it is, so a jump to it still sends over r[a];
+    pcs, yields and trace terms are those of the unfused image.  A pair whose
+    SEND's payload register is `a` is left alone (the payload would be the
+    link the fused half just computed)."""
+    for i in range(len(insns) - 1):
+        w, w2 = int(insns[i, 0]), int(insns[i + 1, 0])
+        op, op2 = w & 0xFF, w2 & 0xFF
+        if op2 != isa.OP_SEND or op not in (isa.OP_LINK, isa.OP_RLINK):
+            continue
+        a, a2, b, b2 = (w >> 8) & 0xFF, (w2 >> 8) & 0xFF, w >> 16, w2 >> 16
+        if a != a2 or (b2 >> 10) != 0 or ((b2 >> 8) & 3) == (a & 3):
+            continue
+        if op == isa.OP_LINK:
+            insns[i, 0] = _enc(isa.OP_SEND, a, b2 | isa.SEND_VIA_LINK)  # imm: LINK's k
+        else:
+            insns[i, 0] = _enc(isa.OP_SEND, a, b2 | isa.SEND_VIA_RLINK | ((b & 3) << 12))
+            insns[i, 1] = 0
 
 
 class Program:
@@ -216,6 +239,8 @@ class Program:
                 imm = imm.pc
             insns[i, 0] = w0
             insns[i, 1] = np.uint32(int(imm) & 0xFFFFFFFF)
+        if os.environ.get("TW_FUSE_SEND", "1") != "0":
+            _fuse_sends(insns)
         nk = max(1, len(self.msg_kinds))
         ls = np.full((max(1, len(self.listener_sets)), nk), isa.PC_NONE, dtype=np.uint32)
         for si, s in enumerate(self.listener_sets):
