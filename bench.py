@@ -19,6 +19,7 @@ scenario by node (strong scaling, RCCL all-to-all per window).
 from __future__ import annotations
 
 import argparse
+import functools
 import hashlib
 import json
 import os
@@ -31,6 +32,7 @@ sys.path.insert(0, os.path.join(ROOT, "time-warp_amd"))
 
 import numpy as np  # noqa: E402
 
+TABLE_CHECK_REPLICAS = 64     # replicas of a device-drawn link table re-drawn on the host
 HBM_PEAK_GBS = 8000.0           # MI355X HBM3E peak (MI355X_MICROARCH.md)
 BYTES_PER_EVENT = 64            # 16 B event read + 16 B event write + 32 B thread/node state r/w
 BYTES_PER_SEND = 8              # link-table entry + ordinal
@@ -47,21 +49,27 @@ def replica_block(args, rank: int, world: int):
     return r0, r1 - r0
 
 
-def build_scenario(args, rank: int, world: int):
+def build_scenario(args, rank: int, world: int, drawer=None, max_replicas=None):
+    """This rank's scenario; `drawer` = engine.draw_link_table draws its link
+    table on the GPU (tw_draw_link_table) instead of the host StdGen loop;
+    `max_replicas` caps the block (the host-drawn table check)."""
     from timewarp import scenarios
 
     base, R = replica_block(args, rank, world)
+    if max_replicas is not None:
+        R = min(R, max_replicas)
     if args.config == "token_ring":
         return scenarios.token_ring(n_nodes=args.nodes, n_replicas=R, launch_duration=args.duration_s * 1_000_000,
-                                    drop_log2=args.drop_log2, seed_base=base), (
+                                    drop_log2=args.drop_log2, seed_base=base, drawer=drawer), (
             f"token-ring (examples/token-ring) {args.nodes} nodes x {R} replicas/GPU, delay U[1,5] ms, "
             f"drop 2^-{args.drop_log2}, launchDuration {args.duration_s} s")
     if args.config == "ping_pong":
-        return scenarios.ping_pong(n_replicas=R, round_trips=args.round_trips, seed_base=base), (
+        return scenarios.ping_pong(n_replicas=R, round_trips=args.round_trips, seed_base=base, drawer=drawer), (
             f"ping-pong (examples/ping-pong) 2 nodes x {R} replicas/GPU, {args.round_trips} round trips, "
             "per-link delay U[1,5] ms")
     if args.config == "hotspot":
-        return scenarios.hotspot(n_senders=args.nodes, n_replicas=R, msg_num=args.msg_num, seed_base=base), (
+        return scenarios.hotspot(n_senders=args.nodes, n_replicas=R, msg_num=args.msg_num, seed_base=base,
+                                 drawer=drawer), (
             f"hotspot (bench/Network) {args.nodes} senders -> 1 receiver x {R} replicas/GPU, "
             f"{args.msg_num} msgs @1000/s")
     if args.config == "gossip":
@@ -286,6 +294,8 @@ def main():
     ap.add_argument("--msg-num", type=int, default=1000)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--host-tables", action="store_true",
+                    help="draw the link tables with the host StdGen loop instead of on the GPU")
     ap.add_argument("--geometry", default=None, choices=["dense", "sparse", "half", "wave", "narrow", "compact", "lpb"],
                     help="replica configs: kernel geometry (default: the library's choice by replica count); "
                          "lpb = every (node, replica) a logical process in one window loop (the replicas per "
@@ -340,7 +350,23 @@ def main():
         if r_rank & (r_rank - 1):
             raise SystemExit(f"--geometry lpb needs a power-of-two replica count per GPU (lanes are node << log2(R) "
                              f"| replica); rank {rank} of {world} would get {r_rank} of {args.replicas} replicas")
-    scn, workload = build_scenario(args, rank, world)
+    # scenario set-up (outside the timed region): the link table drawn on the
+    # GPU, checked against the host StdGen draw on its first replicas
+    drawer = None
+    if not args.host_tables and args.config != "gossip":
+        from timewarp.engine import draw_link_table
+        drawer = functools.partial(draw_link_table, device=local)
+    t_setup = time.perf_counter()
+    scn, workload = build_scenario(args, rank, world, drawer=drawer)
+    setup = {"table_draw": "host" if drawer is None else "device (tw_draw_link_table)",
+             "build_s": time.perf_counter() - t_setup}
+    if drawer is not None and scn.link_table is not None:
+        ref, _ = build_scenario(args, rank, world, max_replicas=TABLE_CHECK_REPLICAS)
+        n_chk = ref.link_table.shape[2]
+        setup["host_check_replicas"] = n_chk
+        setup["host_check_equal"] = bool(np.array_equal(scn.link_table[:, :, :n_chk], ref.link_table))
+        if not setup["host_check_equal"]:
+            raise SystemExit("device-drawn link table differs from the host StdGen draw")
     if args.config == "gossip":
         return bench_gossip(args, scn, workload, world, rank, local, dist_on, barrier)
     # one rank of the job: the library's RCCL communicator over the ranks
@@ -429,6 +455,7 @@ def main():
             },
         }
         out["roofline"]["algorithmic_per_event"] = alg_bytes / max(1, loc_events)
+        out["setup"] = setup
         if eng.geometry() == "lpb":
             out["config"]["parallelism"] = (f"replica-sharded x{world}; inside a GPU every (node, replica) pair is a "
                                             "logical process: one device window loop, lookahead = min link delay")

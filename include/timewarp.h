@@ -394,6 +394,30 @@ void tw_destroy(tw_ctx* ctx);
 const char* tw_strerror(int code);
 const char* tw_version(void);
 
+/* ---------------------------------------------- link tables drawn on the GPU
+ * The scenario builders' network-delay draws (examples/token-ring/Main.hs:60,77:
+ * `mkStdGen` + `getRandomTR`, random-1.1's StdGen) for every replica at once:
+ * replica r's generator is mkStdGen(seed_base + r); it walks the links with
+ * drawn[l] != 0 in ascending order and, for each, draws link_depth entries,
+ * each randomR(lo[l], hi[l]) followed -- when drop_log2 > 0 -- by a drop coin
+ * randomR(0, 2^drop_log2 - 1) that marks the entry TW_LINK_DROP when 0.  Links
+ * with drawn[l] == 0 hold lo[l] in every entry.  Output: the table tw_load
+ * takes, [n_links][link_depth][n_replicas] in host memory, equal entry for
+ * entry to the host draw (time-warp_amd/timewarp/stdgen.py); one GPU thread
+ * per replica replaces a host loop of n_links x link_depth vector steps.
+ * Ranges must need one StdGen digit (hi - lo + 1 <= 2147483). */
+typedef struct tw_table_draw {
+    uint32_t n_links;
+    uint32_t link_depth;
+    uint32_t n_replicas;
+    int32_t drop_log2;         /* 0 = no drop coins, else 1..21 (one digit) */
+    int64_t seed_base;
+    const uint8_t* drawn;      /* [n_links] */
+    const int64_t* lo;         /* [n_links] µs */
+    const int64_t* hi;         /* [n_links] µs (drawn links) */
+} tw_table_draw;
+int tw_draw_link_table(int device, const tw_table_draw* spec, uint32_t* out);
+
 /* ------------------------------------------------- node-partitioned (LP) mode
  * One huge scenario (n_replicas = 1) split by node across contexts / GPUs
  * (BASELINE config 4).  Each lane runs one node as a logical process with its

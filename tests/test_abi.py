@@ -51,9 +51,10 @@ CHECK_C = r"""
 #include "timewarp.h"
 #define F(T, f) printf(#T "." #f " %zu\n", offsetof(T, f));
 int main(void) {
-  printf("tw_scenario_desc %zu\ntw_replica_result %zu\ntw_stats %zu\ntw_insn %zu\ntw_lp_state %zu\n",
+  printf("tw_scenario_desc %zu\ntw_replica_result %zu\ntw_stats %zu\ntw_insn %zu\ntw_lp_state %zu\n"
+         "tw_table_draw %zu\n",
          sizeof(tw_scenario_desc), sizeof(tw_replica_result), sizeof(tw_stats), sizeof(tw_insn),
-         sizeof(tw_lp_state));
+         sizeof(tw_lp_state), sizeof(tw_table_draw));
   %FIELDS%
   return 0;
 }
@@ -63,7 +64,8 @@ int main(void) {
 def test_struct_layout_matches_ctypes(tmp_path):
     fields = []
     for T, cls in (("tw_scenario_desc", abi.TwScenarioDesc), ("tw_replica_result", abi.TwReplicaResult),
-                   ("tw_stats", abi.TwStats), ("tw_lp_state", abi.TwLpState)):
+                   ("tw_stats", abi.TwStats), ("tw_lp_state", abi.TwLpState),
+                   ("tw_table_draw", abi.TwTableDraw)):
         for f, _ in cls._fields_:
             fields.append(f"F({T}, {f})")
     src = tmp_path / "chk.c"
@@ -76,7 +78,9 @@ def test_struct_layout_matches_ctypes(tmp_path):
     assert int(got["tw_stats"]) == C.sizeof(abi.TwStats)
     assert int(got["tw_insn"]) == 8
     assert int(got["tw_lp_state"]) == C.sizeof(abi.TwLpState)
+    assert int(got["tw_table_draw"]) == C.sizeof(abi.TwTableDraw)
     for T, cls in (("tw_scenario_desc", abi.TwScenarioDesc), ("tw_replica_result", abi.TwReplicaResult),
-                   ("tw_stats", abi.TwStats), ("tw_lp_state", abi.TwLpState)):
+                   ("tw_stats", abi.TwStats), ("tw_lp_state", abi.TwLpState),
+                   ("tw_table_draw", abi.TwTableDraw)):
         for f, _ in cls._fields_:
             assert int(got[f"{T}.{f}"]) == getattr(cls, f).offset, (T, f)

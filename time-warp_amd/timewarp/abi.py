@@ -84,6 +84,20 @@ class TwLpState(C.Structure):
     ]
 
 
+class TwTableDraw(C.Structure):
+    """tw_table_draw: a link-table draw on the GPU (tw_draw_link_table)."""
+    _fields_ = [
+        ("n_links", C.c_uint32),
+        ("link_depth", C.c_uint32),
+        ("n_replicas", C.c_uint32),
+        ("drop_log2", C.c_int32),
+        ("seed_base", C.c_int64),
+        ("drawn", C.c_void_p),
+        ("lo", C.c_void_p),
+        ("hi", C.c_void_p),
+    ]
+
+
 RESULT_FIELDS = ["final_t", "events", "delivered", "dropped", "undeliverable", "status", "main_exc", "threads"]
 
 # numpy dtype with the same layout as tw_replica_result (for bulk reads)

@@ -16,7 +16,7 @@ from typing import Optional
 
 import numpy as np
 
-from .abi import RESULT_DTYPE, TwLpState, TwStats
+from .abi import RESULT_DTYPE, TwLpState, TwStats, TwTableDraw
 from .scenario import Scenario
 
 _PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -29,7 +29,8 @@ EXPORTS = ["tw_create", "tw_comm_id", "tw_create_rank", "tw_ctx_info", "tw_lp_ru
            "tw_lp_load", "tw_lp_window", "tw_lp_take_outbox", "tw_lp_inject", "tw_lp_results",
            "tw_set_trace", "tw_read_trace", "tw_tie_audit", "tw_set_counter_base", "tw_geometry",
            "tw_set_stream", "tw_lp_exchange_setup", "tw_lp_loop_begin", "tw_lp_tick", "tw_lp_tick_import",
-           "tw_lp_tick_end", "tw_lp_progress", "tw_lp_run_windows", "tw_lpb_load", "tw_lpb_windows"]
+           "tw_lp_tick_end", "tw_lp_progress", "tw_lp_run_windows", "tw_lpb_load", "tw_lpb_windows",
+           "tw_draw_link_table"]
 GEOMETRIES = ("dense", "sparse", "half", "wave", "lp", "narrow", "lpb", "compact")  # TW_GEO_* order
 
 # tw_trace_rec (include/timewarp.h)
@@ -103,16 +104,38 @@ def load_library(path: Optional[str] = None):
     lib.tw_lp_run_windows.argtypes = [C.c_void_p, C.c_uint64, C.POINTER(TwLpState)]
     lib.tw_lpb_load.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p, C.c_uint32, C.c_uint32]
     lib.tw_lpb_windows.argtypes = [C.c_void_p, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
+    lib.tw_draw_link_table.argtypes = [C.c_int, C.POINTER(TwTableDraw), C.c_void_p]
     for name in ("tw_create", "tw_comm_id", "tw_create_rank", "tw_ctx_info", "tw_lp_run", "tw_set_tie_mode", "tw_load", "tw_reset", "tw_run", "tw_read_results", "tw_read_hashes", "tw_read_final",
                  "tw_last_launch_ms", "tw_lp_load", "tw_lp_window", "tw_lp_take_outbox", "tw_lp_inject",
                  "tw_lp_results", "tw_set_trace", "tw_read_trace", "tw_tie_audit", "tw_set_counter_base",
                  "tw_geometry", "tw_set_stream", "tw_lp_exchange_setup", "tw_lp_loop_begin", "tw_lp_tick",
                  "tw_lp_tick_import", "tw_lp_tick_end", "tw_lp_progress", "tw_lp_run_windows", "tw_lpb_load",
-                 "tw_lpb_windows"):
+                 "tw_lpb_windows", "tw_draw_link_table"):
         getattr(lib, name).restype = C.c_int
     if path is None:
         _lib = lib
     return lib
+
+
+def draw_link_table(n_replicas: int, drawn, lo, hi, link_depth: int = 1, drop_log2: int = 0,
+                    seed_base: int = 0, device: int = 0) -> np.ndarray:
+    """The scenario builders' StdGen delay draws on the GPU (tw_draw_link_table):
+    replica r's generator mkStdGen(seed_base + r) walks the links with
+    drawn[l] in ascending order, link_depth entries each (a randomR(lo, hi)
+    delay, then a drop coin when drop_log2 > 0); other links hold lo[l].
+    Returns the [n_links][link_depth][n_replicas] uint32 table tw_load takes,
+    entry for entry the host draw of timewarp/stdgen.py."""
+    drawn = np.ascontiguousarray(drawn, dtype=np.uint8)
+    lo = np.ascontiguousarray(lo, dtype=np.int64)
+    hi = np.ascontiguousarray(hi, dtype=np.int64)
+    L = drawn.shape[0]
+    if lo.shape != (L,) or hi.shape != (L,):
+        raise ValueError("drawn, lo and hi need one entry per link")
+    out = np.empty((L, int(link_depth), int(n_replicas)), dtype=np.uint32)
+    spec = TwTableDraw(n_links=L, link_depth=int(link_depth), n_replicas=int(n_replicas), drop_log2=int(drop_log2),
+                       seed_base=int(seed_base), drawn=drawn.ctypes.data, lo=lo.ctypes.data, hi=hi.ctypes.data)
+    _check(load_library().tw_draw_link_table(int(device), C.byref(spec), out.ctypes.data), "tw_draw_link_table")
+    return out
 
 
 def _check(rc: int, what: str):

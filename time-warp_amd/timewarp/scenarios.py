@@ -1,9 +1,10 @@
 """Scenario builders for the BASELINE.json configs, lowered to thread programs.
 
 Each builder restates a reference scenario as per-node handler state machines
-(see program.py for the API mapping) and draws its link tables host-side from
-random-1.1 StdGen (stdgen.py), one generator per replica, so every trace is
-deterministic.
+(see program.py for the API mapping) and draws its link tables from random-1.1
+StdGen, one generator per replica, so every trace is deterministic: on the
+host (stdgen.py) or, with ``drawer=engine.draw_link_table``, the same draw on
+the GPU (tw_draw_link_table).
 
   token_ring  — examples/token-ring/Main.hs (configs 1 and 3)
   ping_pong   — examples/ping-pong/Main.hs re-hosted on emulation (config 2)
@@ -37,11 +38,40 @@ def _capped(n: int) -> int:
     return int(min(n, 0xFFFFFFFF))
 
 
+# -------------------------------------------------------------- link tables
+def draw_table(n_links: int, n_replicas: int, drawn_links, lo, hi, link_depth: int = 1, drop_log2: int = 0,
+               seed_base: int = 0, drawer=None) -> np.ndarray:
+    """The scenarios' link-table draw (examples/token-ring/Main.hs:60,77:
+    ``mkStdGen`` + ``getRandomTR``), one StdGen per replica (seed_base + r):
+    for each link of ``drawn_links`` in ascending order, ``link_depth``
+    entries, each a randomR(lo, hi) delay followed by a drop coin when
+    drop_log2 > 0 (dropped when 0).  Other links hold ``lo``.  ``drawer`` =
+    ``engine.draw_link_table`` runs the same draw on the GPU
+    (tw_draw_link_table); the default is the host draw of stdgen.py."""
+    drawn = np.zeros(n_links, np.uint8)
+    drawn[np.asarray(drawn_links, dtype=np.int64)] = 1
+    lo = np.broadcast_to(np.asarray(lo, dtype=np.int64), (n_links,)).copy()
+    hi = np.broadcast_to(np.asarray(hi, dtype=np.int64), (n_links,)).copy()
+    if drawer is not None:
+        return drawer(n_replicas, drawn, lo, hi, link_depth=link_depth, drop_log2=drop_log2, seed_base=seed_base)
+    table = np.empty((n_links, link_depth, n_replicas), np.uint32)
+    table[:] = lo.astype(np.uint32)[:, None, None]
+    g = StdGenVec(seed_base + np.arange(n_replicas, dtype=np.int64))
+    for l in np.nonzero(drawn)[0].tolist():
+        for k in range(link_depth):
+            dly = g.range(int(lo[l]), int(hi[l])).astype(np.uint32)
+            if drop_log2:
+                u = g.range(0, (1 << drop_log2) - 1)
+                dly = np.where(u == 0, dly | np.uint32(isa.LINK_DROP), dly)
+            table[l, k, :] = dly
+    return table
+
+
 # --------------------------------------------------------------- token ring
 def token_ring(n_nodes: int = 16, n_replicas: int = 1, launch_duration: int = sec(20),
                token_passing_delay: int = sec(3), allowed_progress_delay: int = sec(5),
                network_delay=(ms(1), ms(5)), drop_log2: int = 0, seed_base: int = 0,
-               link_depth: int = 1, near_horizon_us: int = sec(10)) -> Scenario:
+               link_depth: int = 1, near_horizon_us: int = sec(10), drawer=None) -> Scenario:
     """examples/token-ring/Main.hs lowered.
 
     Node ids: ring nodes 0..N-1 are the reference's ``no = 1..N``
@@ -137,24 +167,16 @@ def token_ring(n_nodes: int = 16, n_replicas: int = 1, launch_duration: int = se
     L = topo.n_links
 
     # Delays: ring links (even ids) random, observer links (odd ids) 0
-    live_kind = np.zeros(L, np.uint32)
-    live_lo = np.zeros(L, np.int64)
-    live_hi = np.zeros(L, np.int64)
     ring_links = np.arange(0, 2 * N, 2)
+    lo = np.zeros(L, np.int64)
+    hi = np.zeros(L, np.int64)
+    lo[ring_links], hi[ring_links] = network_delay
+    live_kind = np.zeros(L, np.uint32)
     live_kind[ring_links] = 2
-    live_lo[ring_links] = network_delay[0]
-    live_hi[ring_links] = network_delay[1]
     live_kind[ring_links + 1] = 1
-
-    table = np.zeros((L, link_depth, n_replicas), np.uint32)
-    g = StdGenVec(seed_base + np.arange(n_replicas, dtype=np.int64))
-    for l in ring_links.tolist():
-        for k in range(link_depth):
-            dly = g.range(network_delay[0], network_delay[1]).astype(np.uint32)
-            if drop_log2:
-                u = g.range(0, (1 << drop_log2) - 1)
-                dly = np.where(u == 0, dly | np.uint32(isa.LINK_DROP), dly)
-            table[l, k, :] = dly
+    live_lo, live_hi = lo.copy(), hi.copy()
+    table = draw_table(L, n_replicas, ring_links, lo, hi, link_depth=link_depth, drop_log2=drop_log2,
+                       seed_base=seed_base, drawer=drawer)
 
     hops = launch_duration // max(1, token_passing_delay) + 2
     max_slots = 3 * N + 64
@@ -182,7 +204,7 @@ def token_ring(n_nodes: int = 16, n_replicas: int = 1, launch_duration: int = se
 
 # ---------------------------------------------------------------- ping-pong
 def ping_pong(n_replicas: int = 1, round_trips: int = 1, network_delay=(ms(1), ms(5)),
-              seed_base: int = 0, near_horizon_us: int = sec(10)) -> Scenario:
+              seed_base: int = 0, near_horizon_us: int = sec(10), drawer=None) -> Scenario:
     """examples/ping-pong/Main.hs re-hosted on the emulated transfer.
 
     Node 0 = "ping" (listens AtPort 4444), node 1 = "pong" (AtPort 5555),
@@ -228,10 +250,7 @@ def ping_pong(n_replicas: int = 1, round_trips: int = 1, network_delay=(ms(1), m
 
     img = p.finalize()
     topo = Topology.from_out_lists(3, [[1], [0], []])
-    g = StdGenVec(seed_base + np.arange(n_replicas, dtype=np.int64))
-    table = np.zeros((2, 1, n_replicas), np.uint32)
-    table[0, 0, :] = g.range(*network_delay)
-    table[1, 0, :] = g.range(*network_delay)
+    table = draw_table(2, n_replicas, [0, 1], *network_delay, seed_base=seed_base, drawer=drawer)
     return Scenario(
         name="ping_pong", image=img, topo=topo, n_replicas=n_replicas,
         main_pc=img.pc_of("main"), main_node=2, link_table=table,
@@ -244,7 +263,8 @@ def ping_pong(n_replicas: int = 1, round_trips: int = 1, network_delay=(ms(1), m
 def hotspot(n_senders: int = 256, n_replicas: int = 1, msg_num: int = 1000, msg_rate: int = 1000,
             duration_s: int = 10, network_delay=(ms(1), ms(5)), seed_base: int = 0,
             near_horizon_us: int = sec(10), fork_strategy: str = "fork", payload_bytes: int = 0,
-            bandwidth_bytes_per_s: float = 0.0, probe_traces: int = 0, probe_loads: int = 0) -> Scenario:
+            bandwidth_bytes_per_s: float = 0.0, probe_traces: int = 0, probe_loads: int = 0,
+            drawer=None) -> Scenario:
     """bench/Network many-senders -> one-receiver request/response.
 
     Sender (Sender/Main.hs:34-64): listen for Pong, then per message
@@ -327,10 +347,8 @@ def hotspot(n_senders: int = 256, n_replicas: int = 1, msg_num: int = 1000, msg_
     img = p.finalize()
     out = [[RECV] for _ in range(S)] + [list(range(S)), []]
     topo = Topology.from_out_lists(S + 2, out)
-    g = StdGenVec(seed_base + np.arange(n_replicas, dtype=np.int64))
-    table = np.zeros((topo.n_links, 1, n_replicas), np.uint32)
-    for l in range(topo.n_links):
-        table[l, 0, :] = g.range(*network_delay)
+    table = draw_table(topo.n_links, n_replicas, np.arange(topo.n_links), *network_delay, seed_base=seed_base,
+                       drawer=drawer)
     if bandwidth_bytes_per_s > 0:
         from .wire import bench_message_size, transmission_us
         table[:S] += transmission_us(bench_message_size("Ping", payload_bytes), bandwidth_bytes_per_s)
@@ -363,7 +381,7 @@ TAG_ACK = 12
 
 def gatekeeper(n_clients: int = 4, n_replicas: int = 1, msg_num: int = 20, junk_every: int = 4,
                network_delay=(ms(1), ms(5)), seed_base: int = 0, raw: bool = True,
-               near_horizon_us: int = sec(10)) -> Scenario:
+               near_horizon_us: int = sec(10), drawer=None) -> Scenario:
     """A ``listenR`` server (MonadDialog.hs:226-256): the raw listener logs
     every message that reaches the port and returns True only for even
     payloads; the typed listener for `Req` then replies `Ack`.  Clients also
@@ -433,10 +451,8 @@ def gatekeeper(n_clients: int = 4, n_replicas: int = 1, msg_num: int = 20, junk_
     img = p.finalize()
     out = [[SRV] for _ in range(C)] + [list(range(C)), []]
     topo = Topology.from_out_lists(C + 2, out)
-    g = StdGenVec(seed_base + np.arange(n_replicas, dtype=np.int64))
-    table = np.zeros((topo.n_links, 1, n_replicas), np.uint32)
-    for l in range(topo.n_links):
-        table[l, 0, :] = g.range(*network_delay)
+    table = draw_table(topo.n_links, n_replicas, np.arange(topo.n_links), *network_delay, seed_base=seed_base,
+                       drawer=drawer)
     max_slots = C * 24 + 64
     return Scenario(
         name=f"gatekeeper_c{C}" + ("" if raw else "_plain"), image=img, topo=topo, n_replicas=n_replicas,
