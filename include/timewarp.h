@@ -170,6 +170,16 @@ enum tw_op {
  * pc + 2: one instruction (one interpreter pass, one step) instead of two. */
 #define TW_SEND_VIA_LINK 0x400u
 #define TW_SEND_VIA_RLINK 0x800u
+/* Two more pairs fused the same way (the pair's second instruction stays in
+ * the image; the fused one continues at pc + 2):
+ * TW_ALU_NSTORE (b flag of SETI / SETK / ADDI / MULI / NOW / NODE, whose b is
+ *   otherwise unused): `op a,.. ; NSTORE a, var` -- after r[a] is computed,
+ *   v[node][b & 3] = r[a];
+ * TW_TRACE_PAIR (b flag of TRACE): `TRACE a, tag ; TRACE a2, tag2` -- then
+ *   node hash += term(now, 0x30000 | tag2, r[a2]) with a2 = (b >> 13) & 3 and
+ *   tag2 = b & 0x1FFF (< 8192). */
+#define TW_ALU_NSTORE 0x8000u
+#define TW_TRACE_PAIR 0x8000u
 
 typedef struct tw_insn {
     uint32_t w0;  /* op | a<<8 | b<<16 */

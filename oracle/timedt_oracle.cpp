@@ -383,6 +383,13 @@ struct Sim {
             int64_t* r = th->r;
             uint32_t ra = a & 3;
             ++th->pc;
+            // fused `NSTORE a` after an ALU op (TW_ALU_NSTORE, timewarp.h)
+            auto alu_nstore = [&] {
+                if (b & TW_ALU_NSTORE) {
+                    node_vars[(size_t)th->node * 4 + (b & 3)] = r[ra];
+                    ++th->pc;
+                }
+            };
             switch (op) {
             case TW_OP_NOP: break;
             case TW_OP_END:
@@ -421,10 +428,10 @@ struct Sim {
                 if (th->nfr == 0 || th->fr[th->nfr - 1].mask == 0) { fail(TW_REP_ERR_INSN); return; }
                 --th->nfr;
                 break;
-            case TW_OP_SETI: r[ra] = imm; break;
-            case TW_OP_SETK: r[ra] = K[imm]; break;
-            case TW_OP_ADDI: r[ra] += imm; break;
-            case TW_OP_MULI: r[ra] *= imm; break;
+            case TW_OP_SETI: r[ra] = imm; alu_nstore(); break;
+            case TW_OP_SETK: r[ra] = K[imm]; alu_nstore(); break;
+            case TW_OP_ADDI: r[ra] += imm; alu_nstore(); break;
+            case TW_OP_MULI: r[ra] *= imm; alu_nstore(); break;
             case TW_OP_MOV: r[ra] = r[b & 3]; break;
             case TW_OP_ADD: r[ra] += r[b & 3]; break;
             case TW_OP_SUB: r[ra] -= r[b & 3]; break;
@@ -440,8 +447,8 @@ struct Sim {
             case TW_OP_JLE: if (r[ra] <= r[b & 3]) th->pc = (uint32_t)imm; break;
             case TW_OP_JEQI: if (r[ra] == (int16_t)b) th->pc = (uint32_t)imm; break;
             case TW_OP_JNEI: if (r[ra] != (int16_t)b) th->pc = (uint32_t)imm; break;
-            case TW_OP_NOW: r[ra] = cur; break;
-            case TW_OP_NODE: r[ra] = th->node; break;
+            case TW_OP_NOW: r[ra] = cur; alu_nstore(); break;
+            case TW_OP_NODE: r[ra] = th->node; alu_nstore(); break;
             case TW_OP_NLOAD: r[ra] = node_vars[(size_t)th->node * 4 + (b & 3)]; break;
             case TW_OP_NSTORE: node_vars[(size_t)th->node * 4 + (b & 3)] = r[ra]; break;
             case TW_OP_NLOADX:
@@ -532,6 +539,14 @@ struct Sim {
                 if (o->traces && o->traces_n < o->traces_cap)
                     o->traces[o->traces_n] = two_term{cur, th->node, (uint32_t)imm, r[ra]};
                 if (o->traces) ++o->traces_n;
+                if (b & TW_TRACE_PAIR) {  // fused second TRACE (timewarp.h)
+                    const uint32_t t2 = b & 0x1FFF, a2 = (b >> 13) & 3;
+                    hash(th->node, TW_KIND_TRACE | t2, r[a2]);
+                    if (o->traces && o->traces_n < o->traces_cap)
+                        o->traces[o->traces_n] = two_term{cur, th->node, t2, r[a2]};
+                    if (o->traces) ++o->traces_n;
+                    ++th->pc;
+                }
                 break;
             case TW_OP_TMO_BEGIN: {
                 if (tmo_ctr >= d->max_timeouts) { fail(TW_REP_ERR_INSN); return; }

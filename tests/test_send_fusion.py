@@ -1,7 +1,8 @@
-"""SEND fused with its LINK / RLINK (include/timewarp.h TW_SEND_VIA_*,
-Program.finalize's peephole): the fused image must run exactly as the unfused
-one -- same pcs, yields, events and trace hashes; only the instruction count
-per step shrinks.  CPU tests pin the peephole and the oracle's fused SEND;
+"""Fused instruction pairs (Program.finalize's peephole, include/timewarp.h):
+SEND with its LINK / RLINK (TW_SEND_VIA_*), an ALU op with the NSTORE of its
+result (TW_ALU_NSTORE) and two TRACEs (TW_TRACE_PAIR).  The fused image must
+run exactly as the unfused one -- same pcs, yields, events and trace hashes;
+only the instruction count per step shrinks.  CPU tests pin the peephole and the oracle's fused SEND;
 GPU tests run fused and unfused images through the event, LP and batched-LP
 kernels and require bit-equal results."""
 import numpy as np
@@ -11,6 +12,7 @@ from timewarp import isa, scenarios
 from timewarp.abi import RESULT_FIELDS
 from timewarp.program import Program
 from timewarp.scenario import Scenario, Topology
+from timewarp.timeunits import for_
 
 SCENARIOS = {
     "hotspot": lambda: scenarios.hotspot(n_senders=8, n_replicas=4, msg_num=30),
@@ -24,15 +26,53 @@ SCENARIOS = {
 
 def _pair(name, monkeypatch):
     fused = SCENARIOS[name]()
-    monkeypatch.setenv("TW_FUSE_SEND", "0")
+    monkeypatch.setenv("TW_FUSE_PAIRS", "0")
     plain = SCENARIOS[name]()
-    monkeypatch.delenv("TW_FUSE_SEND")
+    monkeypatch.delenv("TW_FUSE_PAIRS")
     return fused, plain
 
 
 def _n_fused(img):
     w = img.insns[:, 0].astype(np.int64)
     return int((((w & 0xFF) == isa.OP_SEND) & (((w >> 16) & (isa.SEND_VIA_LINK | isa.SEND_VIA_RLINK)) != 0)).sum())
+
+
+def _n_flag(img, ops, flag=0x8000):
+    w = img.insns[:, 0].astype(np.int64)
+    return int((np.isin(w & 0xFF, ops) & (((w >> 16) & flag) != 0)).sum())
+
+
+def _pair_prog(jump_into=False, n_traces=3):
+    """main: SETI/NOW/ADDI results stored to node vars through fused pairs, a
+    run of TRACEs (overlapping pairs), optionally a second lap that jumps to
+    the pairs' second instructions; the node vars are traced at the end."""
+    p = Program()
+    c = p.function("main")
+    c.seti(3, 0)
+    top = c.here()
+    c.seti(0, 41)
+    nst = p.label("nst")
+    p.bind(nst)
+    c.nstore(0, 0)
+    c.now(1).nstore(1, 1).addi(0, 1).nstore(0, 2)
+    c.wait(for_(1000))
+    tr2 = p.label("tr2")
+    c.trace(11, 0)
+    p.bind(tr2)
+    for k in range(1, n_traces):
+        c.trace(11 + k, k % 4)
+    c.nload(2, 0).trace(20, 2).nload(2, 1).trace(21, 2).nload(2, 2).trace(22, 2)
+    if jump_into:
+        c.addi(3, 1).jeqi(3, 2, "done").jeqi(3, 1, "second")
+        c.jmp(top)
+        c2 = p.function("second")
+        c2.seti(0, 7).jmp(nst)
+        p.bind(p.label("done"))
+    c.end()
+    img = p.finalize()
+    topo = Topology.from_out_lists(1, [[]])
+    return Scenario(name="pairs", image=img, topo=topo, n_replicas=3, main_pc=img.pc_of("main"), main_node=0,
+                    max_slots=8, queue_capacity=32, run_capacity=8, max_timeouts=2)
 
 
 def _send_prog(payload_reg=0, jump_to_send=False, rlink_from=None):
@@ -90,12 +130,33 @@ def test_peephole_shapes(monkeypatch):
     assert k.size == 1 and ((int(w[k[0]]) >> 28) & 3) == 2 and int(r.insns[k[0], 1]) == 0
 
 
+def test_peephole_alu_and_trace_pairs(monkeypatch):
+    img = _pair_prog().image
+    assert _n_flag(img, [isa.OP_SETI, isa.OP_NOW, isa.OP_ADDI]) == 3
+    assert _n_flag(img, [isa.OP_TRACE]) == 2  # 3 TRACEs in a row: two overlapping pairs
+    monkeypatch.setenv("TW_FUSE_PAIRS", "0")
+    assert _n_flag(_pair_prog().image, [isa.OP_SETI, isa.OP_NOW, isa.OP_ADDI, isa.OP_TRACE]) == 0
+
+
+@pytest.mark.parametrize("kw", [{}, {"jump_into": True}, {"n_traces": 2}, {"n_traces": 5, "jump_into": True}])
+def test_oracle_alu_trace_pairs(oracle_mod, monkeypatch, kw):
+    fused = _pair_prog(**kw)
+    monkeypatch.setenv("TW_FUSE_PAIRS", "0")
+    plain = _pair_prog(**kw)
+    rf, hf = oracle_mod.run_batch(fused, threads=1)
+    rp, hp = oracle_mod.run_batch(plain, threads=1)
+    for f in RESULT_FIELDS:
+        assert np.array_equal(rf[f], rp[f]), f
+    assert np.array_equal(hf, hp)
+    assert (rf["status"] == isa.REP_DONE).all()
+
+
 @pytest.mark.parametrize("kw", [{}, {"payload_reg": 1}, {"jump_to_send": True}, {"rlink_from": 0}, {"rlink_from": 99}])
 def test_oracle_pair_programs(oracle_mod, monkeypatch, kw):
     """A jump into the pair's SEND sends over r1 as before; an out-of-range
     reply link stops the replica in both images."""
     fused = _send_prog(**kw)
-    monkeypatch.setenv("TW_FUSE_SEND", "0")
+    monkeypatch.setenv("TW_FUSE_PAIRS", "0")
     plain = _send_prog(**kw)
     rf, hf = oracle_mod.run_batch(fused, threads=1)
     rp, hp = oracle_mod.run_batch(plain, threads=1)
@@ -139,6 +200,21 @@ def test_gpu_fused_equals_unfused(engine_mod, oracle_mod, monkeypatch, name, geo
         assert np.array_equal(rf[f], rp[f]), (f, rf[f][:4], rp[f][:4])
         assert np.array_equal(rf[f], ro[f]), (f, rf[f][:4], ro[f][:4])
     assert np.array_equal(hf, hp) and np.array_equal(hf, ho)
+
+
+@pytest.mark.gpu
+@pytest.mark.one_geometry
+@pytest.mark.parametrize("geometry", [None, "dense", "sparse", "wave", "narrow", "compact"])
+@pytest.mark.parametrize("kw", [{}, {"jump_into": True}, {"n_traces": 5, "jump_into": True}])
+def test_gpu_alu_trace_pairs(engine_mod, oracle_mod, kw, geometry):
+    scn = _pair_prog(**kw)
+    rf, hf = _gpu_run(engine_mod, scn, geometry)
+    ro, ho = oracle_mod.run_batch(scn, threads=1)
+    for f in RESULT_FIELDS:
+        if f == "tie_flags":
+            continue
+        assert np.array_equal(rf[f], ro[f]), (f, rf[f], ro[f])
+    assert np.array_equal(hf, ho)
 
 
 @pytest.mark.gpu

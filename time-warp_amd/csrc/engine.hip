@@ -195,6 +195,12 @@ enum : uint32_t {
 #define U_LD(f) (((f) >> 14) & 3u)     // table load into r[a]
 #define U_JM(f) (((f) >> 16) & 0xFFu)
 enum : uint32_t { LD_NONE, LD_NV, LD_OUT, LD_RL };  // node var / out-link base / reverse link
+// fused pairs (timewarp.h TW_ALU_NSTORE / TW_TRACE_PAIR): the pass also stores
+// r[a] to node var b & 3 / adds the second TRACE's term, and skips the pair's
+// second instruction
+#define U_NS (1u << 24)
+#define U_TR2 (1u << 25)
+#define U_P2 (1u << 26)
 __device__ __forceinline__ uint32_t uop_of(uint32_t op) {
     auto u = [](uint32_t alu, uint32_t jm, uint32_t tk) { return alu | (tk << 8) | (jm << 16); };
     switch (op) {
@@ -227,6 +233,17 @@ __device__ __forceinline__ uint32_t uop_of(uint32_t op) {
     case TW_OP_RLINK: return LD_RL << 14;
     default: return U_FX;  // every other opcode (and invalid ones) takes the switch
     }
+}
+__device__ __forceinline__ uint32_t uop_insn(uint32_t w0) {
+    const uint32_t op = w0 & 0xFFu, b = w0 >> 16;
+    uint32_t f = uop_of(op);
+    if (b & TW_ALU_NSTORE) {
+        if (op == TW_OP_SETI || op == TW_OP_SETK || op == TW_OP_ADDI || op == TW_OP_MULI || op == TW_OP_NOW ||
+            op == TW_OP_NODE)
+            f |= U_NS | U_P2;
+        if (op == TW_OP_TRACE) f |= U_TR2 | U_P2;
+    }
+    return f;
 }
 
 // A load's result consumed in a branch of the interpreter must not stay
@@ -1351,8 +1368,10 @@ struct Lane {
             // hot-class op, each with its own uop fields; a rare op serves the
             // lanes holding that opcode
             const bool hot = !(fl & U_FX);
+            // (opcode-uniform pass: the lanes holding the first lane's opcode and uop
+            // flags -- a fused pair's flags depend on b, not only on the opcode)
             const bool at = PL ? (running & ((hot & !(lfl & U_FX)) | (!hot & ((in.x & 0xFFu) == op))))
-                               : (running && (in.x & 0xFFu) == op);
+                               : (running && (in.x & 0xFFu) == op && lfl == fl);
             n += at ? 1u : 0u;
             const bool capped = at && n > TW_STEP_CAP;  // TW_REP_ERR_INSN before executing it
             const bool me = at && !capped;
@@ -1436,10 +1455,20 @@ struct Lane {
                     wv = v;
                 }
                 wm = me && lw;
+                if (need((f & U_NS) != 0)) {  // fused NSTORE of the ALU result
+                    if (me && (f & U_NS)) gp(c.nvars)[nix(th.w1, b & 3u)] = wv;
+                }
                 if (need((f & U_TR) != 0)) {  // the popped node's term joins hacc
                     hacc += (me && (f & U_TR)) ? term(now, TW_KIND_TRACE | ((uint32_t)imm & 0xFFFFu), ra) : 0ull;
                     if (c.trace_cap && me && (f & U_TR)) trace_rec(th.w1, imm, ra);
                 }
+                if (need((f & U_TR2) != 0)) {  // fused second TRACE
+                    const bool t2l = me && (f & U_TR2);
+                    const int64_t r2 = rf[((b >> 13) & 3u) * WG];
+                    hacc += t2l ? term(now, TW_KIND_TRACE | (b & 0x1FFFu), r2) : 0ull;
+                    if (c.trace_cap && t2l) trace_rec(th.w1, (int32_t)(b & 0x1FFFu), r2);
+                }
+                if (need((f & U_P2) != 0)) tgt = (f & U_P2) ? pc + 2 : tgt;
                 if (need(jm != JM_NONE)) {
                     const int64_t b16 = (int64_t)(int16_t)b;
                     const uint32_t ci = (ra == rb ? 1u : 0u) | (ra < rb ? 2u : 0u) | (ra == b16 ? 4u : 0u);
@@ -2044,7 +2073,7 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
         for (uint32_t i = threadIdx.x; i <= c.n_insns; i += WG * 64 / TPW) {
             const uint2 in = gp(c.insns)[i];
             s_p[i] = in;
-            s_u[i] = uop_of(in.x & 0xFFu);
+            s_u[i] = uop_insn(in.x);
         }
         for (uint32_t i = threadIdx.x; i < c.n_consts; i += WG * 64 / TPW) s_c[i] = gp(c.consts)[i];
         for (uint32_t i = threadIdx.x; i < c.n_sets * c.n_kinds; i += WG * 64 / TPW) s_l[i] = gp(c.lpc)[i];

@@ -907,6 +907,13 @@ struct Wave {
             case TW_OP_TRACE:
                 hacc += term(now, TW_KIND_TRACE | ((uint32_t)imm & 0xFFFFu), ra);
                 if (dv->trace_cap) trace_rec(th.w1, imm, ra);
+                if (b & TW_TRACE_PAIR) {  // fused second TRACE
+                    const uint32_t t2 = b & 0x1FFFu;
+                    const int64_t r2 = th.reg((b >> 13) & 3u);
+                    hacc += term(now, TW_KIND_TRACE | t2, r2);
+                    if (dv->trace_cap) trace_rec(th.w1, (int32_t)t2, r2);
+                    npc = pc + 2;
+                }
                 break;
             case TW_OP_TMO_BEGIN: {  // schedule (after t) watchdog (TimedT.hs:373-375)
                 const uint32_t tmo = rfl(cw->tmo);
@@ -937,6 +944,12 @@ struct Wave {
                 fail(TW_REP_ERR_INSN);
                 fin = W_STOP;
                 break;
+            }
+            // an ALU op fused with the NSTORE of its result (TW_ALU_NSTORE)
+            if ((b & TW_ALU_NSTORE) && (op == TW_OP_SETI || op == TW_OP_SETK || op == TW_OP_ADDI ||
+                                        op == TW_OP_MULI || op == TW_OP_NOW || op == TW_OP_NODE)) {
+                st_i64(gp(dv->nvars) + ix((size_t)th.w1 * 4 + (b & 3u)), wv);
+                npc = pc + 2;
             }
             if (wr) th.set_reg(a, wv);
             if (thr) throw_to(th, slot, tref, tcode, tval);

@@ -67,26 +67,43 @@ def _enc(op: int, a: int = 0, b: int = 0) -> int:
     return (op & 0xFF) | ((a & 0xFF) << 8) | ((b & 0xFFFF) << 16)
 
 
-def _fuse_sends(insns: np.ndarray) -> None:
-    """Peephole: `LINK a,k ; SEND a,..` / `RLINK a,r ; SEND a,..` -> a fused
-    SEND in the pair's first slot (TW_SEND_VIA_LINK / _RLINK, timewarp.h).
-    The pair's SEND stays where it is, so a jump to it still sends over r[a];
-    pcs, yields and trace terms are those of the unfused image.  A pair whose
-    SEND's payload register is `a` is left alone (the payload would be the
-    link the fused half just computed)."""
-    for i in range(len(insns) - 1):
-        w, w2 = int(insns[i, 0]), int(insns[i + 1, 0])
+_ALU_B_FREE = (isa.OP_SETI, isa.OP_SETK, isa.OP_ADDI, isa.OP_MULI, isa.OP_NOW, isa.OP_NODE)
+
+
+def _fuse_pairs(insns: np.ndarray) -> None:
+    """Peephole over the resolved image: an instruction pair becomes one
+    instruction in the pair's first slot (include/timewarp.h):
+
+      LINK a,k ; SEND a,..    -> SEND with TW_SEND_VIA_LINK (imm = k)
+      RLINK a,r ; SEND a,..   -> SEND with TW_SEND_VIA_RLINK (r in b bits 12-13)
+      op a,.. ; NSTORE a,v    -> op with TW_ALU_NSTORE | v  (op: SETI SETK ADDI
+                                 MULI NOW NODE, whose b is otherwise unused)
+      TRACE a,t ; TRACE a2,t2 -> TRACE with TW_TRACE_PAIR | a2 << 13 | t2 (t2 < 8192)
+
+    The fused instruction continues at pc + 2.  The pair's second instruction
+    stays where it is, so a jump to it still runs it alone; pcs, yields and
+    trace terms are those of the unfused image (one instruction, one
+    interpreter pass and one step count fewer per pair).  A SEND pair whose
+    payload register is `a` is left alone (the payload would be the link the
+    fused half just computed).  Every rewrite reads the original image, so
+    overlapping pairs (three TRACEs in a row) fuse consistently."""
+    orig = insns.copy()
+    for i in range(len(orig) - 1):
+        w, w2 = int(orig[i, 0]), int(orig[i + 1, 0])
         op, op2 = w & 0xFF, w2 & 0xFF
-        if op2 != isa.OP_SEND or op not in (isa.OP_LINK, isa.OP_RLINK):
-            continue
         a, a2, b, b2 = (w >> 8) & 0xFF, (w2 >> 8) & 0xFF, w >> 16, w2 >> 16
-        if a != a2 or (b2 >> 10) != 0 or ((b2 >> 8) & 3) == (a & 3):
-            continue
-        if op == isa.OP_LINK:
-            insns[i, 0] = _enc(isa.OP_SEND, a, b2 | isa.SEND_VIA_LINK)  # imm: LINK's k
-        else:
-            insns[i, 0] = _enc(isa.OP_SEND, a, b2 | isa.SEND_VIA_RLINK | ((b & 3) << 12))
-            insns[i, 1] = 0
+        if op2 == isa.OP_SEND and op in (isa.OP_LINK, isa.OP_RLINK):
+            if a != a2 or (b2 >> 10) != 0 or ((b2 >> 8) & 3) == (a & 3):
+                continue
+            if op == isa.OP_LINK:
+                insns[i, 0] = _enc(isa.OP_SEND, a, b2 | isa.SEND_VIA_LINK)  # imm: LINK's k
+            else:
+                insns[i, 0] = _enc(isa.OP_SEND, a, b2 | isa.SEND_VIA_RLINK | ((b & 3) << 12))
+                insns[i, 1] = 0
+        elif op2 == isa.OP_NSTORE and op in _ALU_B_FREE and b == 0 and (a & 3) == (a2 & 3):
+            insns[i, 0] = _enc(op, a, isa.ALU_NSTORE | (b2 & 3))
+        elif op == isa.OP_TRACE and op2 == isa.OP_TRACE and b == 0 and 0 <= int(orig[i + 1, 1]) < 0x2000:
+            insns[i, 0] = _enc(op, a, isa.TRACE_PAIR | ((a2 & 3) << 13) | int(orig[i + 1, 1]))
 
 
 class Program:
@@ -239,8 +256,8 @@ class Program:
                 imm = imm.pc
             insns[i, 0] = w0
             insns[i, 1] = np.uint32(int(imm) & 0xFFFFFFFF)
-        if os.environ.get("TW_FUSE_SEND", "1") != "0":
-            _fuse_sends(insns)
+        if os.environ.get("TW_FUSE_PAIRS", "1") != "0":
+            _fuse_pairs(insns)
         nk = max(1, len(self.msg_kinds))
         ls = np.full((max(1, len(self.listener_sets)), nk), isa.PC_NONE, dtype=np.uint32)
         for si, s in enumerate(self.listener_sets):
