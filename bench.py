@@ -302,6 +302,9 @@ def main():
                          "GPU must be a power of two: lanes are node << log2(R) | replica)")
     ap.add_argument("--host-windows", action="store_true",
                     help="gossip: the host-driven window loop (round-1 path) instead of the device loop")
+    ap.add_argument("--jit", type=int, default=0, choices=[0, 1],
+                    help="1: the scenario compiler (tw_set_jit) -- the program image compiled into the event "
+                         "kernel at load (outside the timed region); 0: the interpreter")
     ap.add_argument("--workload-key", action="store_true",
                     help="print the workload key and engine digest (tools/pmc.sh provenance) and exit")
     args = ap.parse_args()
@@ -372,7 +375,16 @@ def main():
     # one rank of the job: the library's RCCL communicator over the ranks
     # (tw_create_rank) all-reduces every tw_run's statistics
     comm = twd.library_comm(world, rank) if dist_on else None
-    eng = Engine(local, comm=comm).load(scn, geometry=args.geometry)
+    eng = Engine(local, comm=comm)
+    t_load = time.perf_counter()
+    if args.jit:
+        eng.set_jit(True)
+    eng.load(scn, geometry=args.geometry)
+    setup["load_s"] = time.perf_counter() - t_load
+    jit_on, jit_ms = eng.jit_status()
+    if args.jit and not jit_on:
+        raise SystemExit("--jit 1: the scenario compiler did not produce the kernel")
+    setup["jit"] = {"on": jit_on, "compile_ms": jit_ms}
 
     for _ in range(args.warmup):
         eng.reset()

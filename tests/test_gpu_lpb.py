@@ -92,6 +92,22 @@ def test_lpb_token_ring_many_nodes(engine_mod, oracle_mod):
     _compare_lpb(scn, engine_mod, oracle_mod)
 
 
+def test_lpb_token_ring_c3_per_gpu_shape(engine_mod, oracle_mod):
+    # the path bench.py takes for C3 at <= 8,192 replicas per GPU (BASELINE's
+    # 64k over 8 GPUs) at its real shape: 4,096 nodes, launchDuration 120 s
+    # (start-up fork chain, ~40 token hops, the teardown kills), drop 2^-10
+    scn = scenarios.token_ring(n_nodes=4096, n_replicas=4, launch_duration=120_000_000, drop_log2=10)
+    st, ores, windows = _compare_lpb(scn, engine_mod, oracle_mod)
+    assert (ores["status"] == 1).all() and ores["delivered"].sum() > 0
+
+
+def test_lpb_token_ring_c3_per_gpu_shape_64(engine_mod, oracle_mod):
+    # the same shape over 64 replicas (lanes = node << 6 | replica: waves of 64
+    # replicas of one node, as at 8,192 replicas per GPU)
+    scn = scenarios.token_ring(n_nodes=4096, n_replicas=64, launch_duration=120_000_000, drop_log2=10)
+    _compare_lpb(scn, engine_mod, oracle_mod)
+
+
 def test_lpb_rejects_short_link_out_of_phase1(engine_mod):
     # a link shorter than the lookahead out of a node that itself is fed by one
     # would need a third phase: tw_lpb_load refuses it

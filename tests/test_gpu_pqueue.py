@@ -77,6 +77,20 @@ def test_token_ring_in_pqueue_order(engine_mod, oracle_mod):
         _check(res, h, oracle_mod.run(scn, mode=1, replica=r), "token_ring", r)
 
 
+def test_token_ring_c3_nodes_in_pqueue_order(engine_mod, oracle_mod):
+    # C3's 4,096 nodes: by 10.5 s the queue holds ~12k events (every node's
+    # sleeping worker and server, its killer at launchDuration) and each token
+    # hop's throwTo rebuilds all of it (TimedT.hs:361-368).  Cut at 10.5 s
+    # (start-up + the first hops): the teardown's 8,192 rebuilds in the wave
+    # kernel's scalar MinQueue would take minutes
+    scn = scenarios.token_ring(n_nodes=4096, n_replicas=1, launch_duration=120_000_000, drop_log2=10)
+    t_end = 10_500_000
+    res, h = _gpu_pq(engine_mod, scn, t_end=t_end)
+    o = oracle_mod.run(scn, mode=1, replica=0, t_end=t_end)
+    _check(res, h, o, "token_ring_4096")
+    assert o.result["delivered"] >= 3 and o.result["events"] > 30_000
+
+
 def test_pqueue_mode_needs_the_wave_geometry(engine_mod):
     scn = progs.random_program(0)
     with engine_mod.Engine(0) as e:

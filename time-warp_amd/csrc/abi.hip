@@ -158,6 +158,43 @@ int job_reduce(tw_ctx* c, std::vector<std::vector<uint64_t>>& sums, std::vector<
     return TW_OK;
 }
 
+// Status codes ranked by severity for the job-wide reduction (MAX): a hard
+// runtime, communicator or state failure on one shard outranks a replica
+// error or an incomplete run on another, whatever their numeric values
+int64_t sev_of(int rc) {
+    switch (rc) {
+    case TW_OK: return 0;
+    case TW_ERR_REPLICA: return 1;
+    case TW_ERR_INCOMPLETE: return 2;
+    case TW_ERR_INVALID: return 3;
+    case TW_ERR_STATE: return 4;
+    case TW_ERR_JIT: return 5;
+    case TW_ERR_COMM: return 6;
+    case TW_ERR_OOM: return 7;
+    case TW_ERR_HIP: return 8;
+    default: return 9;  // TW_ERR_NO_DEVICE and anything unknown
+    }
+}
+int rc_of_sev(int64_t s) {
+    static const int rcs[] = {TW_OK, TW_ERR_REPLICA, TW_ERR_INCOMPLETE, TW_ERR_INVALID, TW_ERR_STATE,
+                              TW_ERR_JIT, TW_ERR_COMM, TW_ERR_OOM, TW_ERR_HIP, TW_ERR_NO_DEVICE};
+    return s >= 0 && s <= 9 ? rcs[s] : TW_ERR_HIP;
+}
+
+// Every shard of every rank learns the worst of the shards' local codes (one
+// small all-reduce): a rank that failed locally joins the collective instead
+// of leaving the others waiting in the next one
+int job_agree(tw_ctx* c, const std::vector<int>& local, int* worst) {
+    const size_t n = c->sh.size();
+    std::vector<std::vector<uint64_t>> sums(n, std::vector<uint64_t>{0});
+    std::vector<std::vector<int64_t>> maxs(n);
+    for (size_t i = 0; i < n; ++i) maxs[i] = {sev_of(local[i])};
+    const int rc = job_reduce(c, sums, maxs);
+    if (rc) return rc;
+    *worst = rc_of_sev(maxs[0][0]);
+    return TW_OK;
+}
+
 int64_t dbits(double v) {
     int64_t b;
     std::memcpy(&b, &v, 8);
@@ -179,7 +216,7 @@ int reduce_stats(tw_ctx* c, std::vector<tw_stats>& st, std::vector<int>& rcs, tw
         const tw_stats& s = st[i];
         sums[i] = {s.events, s.sends, s.delivered, s.dropped, s.undeliverable, s.replicas_done, s.replicas_error,
                    s.launches};
-        maxs[i] = {s.max_final_t, dbits(s.kernel_ms), dbits(s.wall_ms), (int64_t)-rcs[i]};
+        maxs[i] = {s.max_final_t, dbits(s.kernel_ms), dbits(s.wall_ms), sev_of(rcs[i])};
     }
     int rc = job_reduce(c, sums, maxs);
     if (rc) return rc;
@@ -190,7 +227,7 @@ int reduce_stats(tw_ctx* c, std::vector<tw_stats>& st, std::vector<int>& rcs, tw
         out->replicas_error = (uint32_t)sums[0][6]; out->launches = (uint32_t)sums[0][7];
         out->max_final_t = maxs[0][0]; out->kernel_ms = bitsd(maxs[0][1]); out->wall_ms = bitsd(maxs[0][2]);
     }
-    *rc_out = (int)-maxs[0][3];
+    *rc_out = rc_of_sev(maxs[0][3]);
     return TW_OK;
 }
 
@@ -239,12 +276,16 @@ bool single(tw_ctx* c) { return c->sh.size() == 1; }
 
 }  // namespace
 
+static_assert(TW_ABI_VERSION == 3u, "tw_version names ABI 3");
+static_assert(RD_N == TW_LP_RED_WORDS, "the caller-owned reduction buffer (timewarp.h)");
+
 extern "C" {
 
 const char* tw_version(void) {
     return "timewarp-mi355x 0.6 (gfx950; lane-per-replica dense/narrow/sparse kernels, wavefront-per-replica kernel, "
            "node-partitioned LP kernel with device-driven windows, batched logical processes (tw_lpb_load); "
-           "multi-GPU contexts with library-owned RCCL communicators; ABI 3)";
+           "multi-GPU contexts with library-owned RCCL communicators; scenario compiler (tw_set_jit); "
+           "ABI 3)";
 }
 
 const char* tw_strerror(int code) {
@@ -526,6 +567,36 @@ int tw_set_tie_mode(tw_ctx* c, uint32_t mode) {
     return TW_OK;
 }
 
+int tw_set_jit(tw_ctx* c, uint32_t on) {
+    if (!c) return TW_ERR_INVALID;
+    for (tw_shard* s : c->sh) {
+        int rc = sh_set_jit(s, on);
+        if (rc) return rc;
+    }
+    return TW_OK;
+}
+
+int tw_jit_status(tw_ctx* c, uint32_t* on, double* compile_ms) {
+    if (!c) return TW_ERR_INVALID;
+    uint32_t all = 1;
+    double ms = 0.0;
+    for (tw_shard* s : c->sh) {
+        uint32_t o = 0;
+        double m = 0.0;
+        int rc = sh_jit_status(s, &o, &m);
+        if (rc) return rc;
+        all &= o;
+        ms += m;
+    }
+    if (on) *on = all;
+    if (compile_ms) *compile_ms = ms;
+    return TW_OK;
+}
+
+int tw_jit_precompile(const tw_scenario_desc* desc, int geometry, double* compile_ms) {
+    return sh_jit_precompile(desc, geometry, compile_ms);
+}
+
 int tw_geometry(tw_ctx* c) {
     if (!c) return TW_ERR_INVALID;
     return sh_geometry(c->sh[0]);
@@ -659,13 +730,15 @@ int tw_lp_results(tw_ctx* c, tw_replica_result* agg, uint64_t* node_hashes, size
     for (size_t i = 0; i < n; ++i) {
         tw_replica_result a{};
         hs[i].assign(n_nodes, 0);
-        int rc = sh_lp_results(c->sh[i], &a, node_hashes ? hs[i].data() : nullptr, n_nodes);
-        if (rc) return rc;
+        // a local failure joins the reduction (every rank returns it) instead
+        // of leaving the other ranks in the all-reduce
+        const int lrc = sh_lp_results(c->sh[i], &a, node_hashes ? hs[i].data() : nullptr, n_nodes);
         sums[i] = {a.events, a.delivered, a.dropped, a.undeliverable, a.threads};
-        maxs[i] = {a.final_t, (int64_t)a.status, (int64_t)a.main_exc};
+        maxs[i] = {a.final_t, (int64_t)a.status, (int64_t)a.main_exc, sev_of(lrc)};
     }
     int rc = job_reduce(c, sums, maxs);
     if (rc) return rc;
+    if (maxs[0][3]) return rc_of_sev(maxs[0][3]);
     std::memset(agg, 0, sizeof(*agg));
     agg->events = sums[0][0]; agg->delivered = sums[0][1]; agg->dropped = sums[0][2];
     agg->undeliverable = sums[0][3]; agg->threads = sums[0][4];
@@ -711,6 +784,18 @@ int tw_lp_results(tw_ctx* c, tw_replica_result* agg, uint64_t* node_hashes, size
 int tw_lp_run(tw_ctx* c, uint64_t max_ticks, tw_lp_state* out) {
     if (!c || !out) return TW_ERR_INVALID;
     const size_t n = c->sh.size();
+    std::vector<int> lrc(n, TW_OK);  // each shard's first local failure
+    // the worst local code of the job (RCCL: agreed over every rank first)
+    auto agreed = [&](int* worst) -> int {
+        if (c->tp != TP_RCCL) {
+            int w = TW_OK;
+            for (int r : lrc)
+                if (sev_of(r) > sev_of(w)) w = r;
+            *worst = w;
+            return TW_OK;
+        }
+        return job_agree(c, lrc, worst);
+    };
     for (tw_shard* s : c->sh)
         if (!sh_is_lp(s)) return TW_ERR_STATE;
     if (n == 1 && c->tp == TP_NONE) {
@@ -753,11 +838,11 @@ int tw_lp_run(tw_ctx* c, uint64_t max_ticks, tw_lp_state* out) {
             const long v = strtol(x, nullptr, 10);
             if (v >= 1 && v <= (1 << 22)) c->xcap = (uint32_t)v;
         }
-        for (size_t i = 0; i < n; ++i) {
-            int rc = sh_lp_exchange_own(c->sh[i], (uint32_t)c->world, (uint32_t)(c->rank0 + i), c->starts.data(),
-                                        c->xcap);
-            if (rc) return rc;
-        }
+        // (a shard's local failure from here on is carried to every rank by
+        // job_agree before the next collective: no rank is left waiting in one)
+        for (size_t i = 0; i < n; ++i)
+            if (!lrc[i]) lrc[i] = sh_lp_exchange_own(c->sh[i], (uint32_t)c->world, (uint32_t)(c->rank0 + i),
+                                                     c->starts.data(), c->xcap);
         if (c->tp == TP_COPY) {
             c->red_all.assign(n, nullptr);
             c->ev_a.assign(n, nullptr);
@@ -774,14 +859,20 @@ int tw_lp_run(tw_ctx* c, uint64_t max_ticks, tw_lp_state* out) {
     std::vector<ShardXchg> x(n);
     uint32_t cap_eff = 0;
     for (size_t i = 0; i < n; ++i) {
-        int rc = sh_lp_loop_begin(c->sh[i]);
-        if (rc) return rc;
-        sh_lp_exchange_info(c->sh[i], &x[i]);
-        cap_eff = std::min<uint32_t>(x[i].stride, 4096u);
+        if (!lrc[i]) lrc[i] = sh_lp_loop_begin(c->sh[i]);
+        if (!lrc[i]) sh_lp_exchange_info(c->sh[i], &x[i]);
+        if (!lrc[i]) cap_eff = std::min<uint32_t>(x[i].stride, 4096u);
     }
-    for (size_t i = 0; i < n; ++i) {
-        int rc = sh_lp_set_block(c->sh[i], cap_eff);
+    for (size_t i = 0; i < n; ++i)
+        if (!lrc[i]) lrc[i] = sh_lp_set_block(c->sh[i], cap_eff);
+    {
+        int worst = TW_OK;
+        const int rc = agreed(&worst);
         if (rc) return rc;
+        if (worst) {
+            if (c->lp_ready) c->lp_ready = false;  // (set up again by the next call)
+            return worst;
+        }
     }
     const size_t stride_b = 32ull * ((size_t)x[0].stride + 1);
     std::vector<tw_lp_state> st(n);
@@ -789,10 +880,10 @@ int tw_lp_run(tw_ctx* c, uint64_t max_ticks, tw_lp_state* out) {
         const uint64_t batch = std::min<uint64_t>(max_ticks - done_ticks, 16);
         const size_t bytes = 32ull * ((size_t)cap_eff + 1);
         for (uint64_t k = 0; k < batch; ++k) {
-            for (size_t i = 0; i < n; ++i) {
-                int rc = sh_lp_tick(c->sh[i]);
-                if (rc) return rc;
-            }
+            // a shard that failed stops launching but keeps taking part in the
+            // exchange and the reduction until the batch's agreement
+            for (size_t i = 0; i < n; ++i)
+                if (!lrc[i]) lrc[i] = sh_lp_tick(c->sh[i]);
             // record blocks: block g of rank r's send -> block r of rank g's recv
             if (c->tp == TP_RCCL) {
                 NCCLCHK(ncclGroupStart());
@@ -820,10 +911,8 @@ int tw_lp_run(tw_ctx* c, uint64_t max_ticks, tw_lp_state* out) {
                     }
                 }
             }
-            for (size_t i = 0; i < n; ++i) {
-                int rc = sh_lp_tick_import(c->sh[i]);
-                if (rc) return rc;
-            }
+            for (size_t i = 0; i < n; ++i)
+                if (!lrc[i]) lrc[i] = sh_lp_tick_import(c->sh[i]);
             // window words: all-reduce(min)
             if (c->tp == TP_RCCL) {
                 NCCLCHK(ncclGroupStart());
@@ -863,18 +952,21 @@ int tw_lp_run(tw_ctx* c, uint64_t max_ticks, tw_lp_state* out) {
                     HIPCHK_A(hipGetLastError());
                 }
             }
-            for (size_t i = 0; i < n; ++i) {
-                int rc = sh_lp_tick_end(c->sh[i]);
-                if (rc) return rc;
-            }
+            for (size_t i = 0; i < n; ++i)
+                if (!lrc[i]) lrc[i] = sh_lp_tick_end(c->sh[i]);
         }
         done_ticks += batch;
         bool err = false, done = true;
         for (size_t i = 0; i < n; ++i) {
-            int rc = sh_lp_progress(c->sh[i], &st[i]);
-            if (rc) return rc;
+            if (!lrc[i]) lrc[i] = sh_lp_progress(c->sh[i], &st[i]);
             err = err || st[i].err;
             done = done && st[i].done;
+        }
+        {
+            int worst = TW_OK;
+            const int rc = agreed(&worst);
+            if (rc) return rc;
+            if (worst) return worst;
         }
         *out = st[0];
         for (size_t i = 1; i < n; ++i) out->err |= st[i].err;
@@ -888,12 +980,14 @@ int tw_lp_run(tw_ctx* c, uint64_t max_ticks, tw_lp_state* out) {
         want = std::min(want, x[0].stride);
         if (want > cap_eff || want * 4 <= cap_eff) cap_eff = want;
         for (size_t i = 0; i < n; ++i) {
-            int rc = sh_lp_set_block(c->sh[i], cap_eff);
-            if (!rc) rc = sh_lp_clear_xmax(c->sh[i]);
-            if (rc) return rc;
+            if (!lrc[i]) lrc[i] = sh_lp_set_block(c->sh[i], cap_eff);
+            if (!lrc[i]) lrc[i] = sh_lp_clear_xmax(c->sh[i]);
         }
     }
-    return TW_ERR_INCOMPLETE;
+    int worst = TW_OK;
+    const int rc = agreed(&worst);
+    if (rc) return rc;
+    return worst ? worst : TW_ERR_INCOMPLETE;
 }
 
 #ifdef TW_STATS

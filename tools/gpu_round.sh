@@ -24,6 +24,11 @@ for s in "$@"; do
     stats_c5) step stats_c5 400 env TW_LIB=$PWD/time-warp_amd/lib/libtimewarp_stats.so python -u tools/stats_probe.py hotspot 4096 256 ;;
     probe2) step probe2 300 env TW_LIB=$PWD/time-warp_amd/lib/libtimewarp_prof2.so python tools/kernel_probe.py 65536 4096 ;;
     bench)  step bench 500 python bench.py ;;
+    jit_c3) step jit_c3 400 python -u tools/jit_probe.py token_ring 65536 ;;
+    jit_c3_8k) step jit_c3_8k 400 python -u tools/jit_probe.py token_ring 8192 narrow ;;
+    jit_c2) step jit_c2 400 python -u tools/jit_probe.py ping_pong 1048576 ;;
+    jit_c5) step jit_c5 400 python -u tools/jit_probe.py hotspot 4096 sparse ;;
+    benchj) step benchj 400 python bench.py --steps 3 --jit 1 ;;
     benchq) step benchq 300 python bench.py --steps 2 --no-cpu-baseline ;;
     bench_c2) step bench_c2 400 python bench.py --config ping_pong ;;
     bench_c4) step bench_c4 500 python bench.py --config gossip ;;
