@@ -584,7 +584,12 @@ int tw_lp_run_windows(tw_ctx* ctx, uint64_t max_ticks, tw_lp_state* out);
  * the ranks last agreed on -- the largest per-rank demand of a tick, rounded
  * up, re-chosen every 16 ticks from the reduced words (TW_LP_XCAP caps it,
  * default 16384 records); records beyond it wait a tick in a carry buffer
- * (the window reruns), so an exchange never overflows.  The multi-GPU
+ * (the window reruns) and go first at the next tick.  The carry holds up to
+ * min(outbox capacity, 2^20) records: a demand above the agreed block size
+ * for long enough to outgrow it stops every rank at the same tick with the
+ * replica error (tw_lp_state.err bit 8) rather than losing a record.  A local
+ * failure on one rank is agreed over the job before the next collective, so
+ * every rank returns the same code at the same point.  The multi-GPU
  * replacement of MonadDialog's cross-node send path (MonadDialog.hs:149-166)
  * with runTimedT's loop around it.  The caller-driven primitives
  * (tw_lp_exchange_setup / tw_lp_tick ...) remain for one-device contexts. */

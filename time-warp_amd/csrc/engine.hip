@@ -1333,6 +1333,11 @@ int sh_lp_tick(tw_shard* c) {
     c->d.win = nullptr;
     HIPCHK(hipGetLastError());
     if (c->jit_missing) return TW_ERR_JIT;
+    if (c->ex_world > 1 && d.carry) {  // the previous tick's carry claims block slots first
+        hipLaunchKernelGGL(tw_lp_pack_carry, dim3(lp_grid(d.carry_cap)), dim3(256), 0, st, d, c->ex_send,
+                           (const uint32_t*)c->ex_starts, c->ex_world, c->ex_cap, c->ex_cap_eff);
+        HIPCHK(hipGetLastError());
+    }
     hipLaunchKernelGGL(tw_lp_pack, dim3(lp_grid(d.out_cap)), dim3(256), 0, st, d, c->ex_send,
                        (const uint32_t*)c->ex_starts, c->ex_world, c->ex_cap, c->ex_cap_eff);
     HIPCHK(hipGetLastError());

@@ -106,7 +106,10 @@ enum { K_POP, K_SUPERSEDED, K_PEEK_PF, K_PEEK_HBM, K_PUT_HBM, K_PUT_DEAD, K_PF_I
 #endif
 
 // m0 is set by the LDS-DMA (global_load_lds) inline asm only; no other code of
-// these kernels uses it.
+// these kernels uses it.  Each LDS-DMA load and each hand-counted wait that
+// proves one landed carries a `; tw:<stream>` comment (pf: the record
+// prefetch, run: a far run's next entry) for tools/waitcnt_audit.py, which
+// checks every counted wait against the compiled code's paths.
 #pragma clang diagnostic ignored "-Winline-asm"
 
 namespace {
@@ -763,7 +766,7 @@ struct Lane {
     __device__ __forceinline__ void run_commit() {
         if constexpr (!HR) return;
         if (prun >= 0) {
-            asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+            asm volatile("s_waitcnt vmcnt(4) ; tw:run" ::: "memory");
             *rqp(RQ_SEC + prun) = pfs[4 * WG];
             prun = -1;
         }
@@ -824,7 +827,7 @@ struct Lane {
         if (n >= 2) {
             const uint32_t p2 = h + 1 == c.Cr ? 0 : h + 1;
             // into LDS staging quad 4 (no register left pending across the step)
-            asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(run_at(sel, p2)),
+            asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off ; tw:run" ::"v"(run_at(sel, p2)),
                          "s"(pfs_wave + 4 * WG * 16) : "memory", "m0");
             prun = sel;
         }
@@ -1013,13 +1016,13 @@ struct Lane {
         const uint32_t pw = (uint32_t)__builtin_amdgcn_readfirstlane((int)pfs_wave);
         // the instruction offset of global_load_lds also offsets the LDS
         // destination, so each quad gets its own global address instead
-        asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(p), "s"(pw)
+        asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off ; tw:pf" ::"v"(p), "s"(pw)
                      : "memory", "m0");
-        asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(p + c.RQ),
+        asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off ; tw:pf" ::"v"(p + c.RQ),
                      "s"(pw + WG * 16) : "memory", "m0");
-        asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(p + 2 * c.RQ),
+        asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off ; tw:pf" ::"v"(p + 2 * c.RQ),
                      "s"(pw + 2 * WG * 16) : "memory", "m0");
-        asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(p + 3 * c.RQ),
+        asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off ; tw:pf" ::"v"(p + 3 * c.RQ),
                      "s"(pw + 3 * WG * 16) : "memory", "m0");
 #endif
         pf_slot = valid ? s : 0xFFFFFFFFu;
@@ -1038,7 +1041,7 @@ struct Lane {
         } else {
             STAT(K_PEEK_PF);
         }
-        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(TW_TAIL_VMEM) : "memory");
+        asm volatile("s_waitcnt vmcnt(%0) ; tw:pf" ::"n"(TW_TAIL_VMEM) : "memory");
         unpack(th, pfs[0], pfs[WG], pfs[2 * WG], pfs[3 * WG]);
     }
 
@@ -2002,7 +2005,7 @@ struct Lane {
             // younger than that prefetch, so vmcnt(8) proves it has landed and
             // cannot overwrite these LDS writes.
             if (cslot != 0xFFFFFFFFu && near_n != 0 && nrs == cslot) {
-                asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+                asm volatile("s_waitcnt vmcnt(8) ; tw:pf" ::: "memory");
                 pfs[0] = make_uint4(ch.w0, ch.w1, ch.w2, ch.w3);
                 pfs[WG] = make_uint4(ch.f0, ch.f1, ch.xl, ch.xh);
                 pfs[2 * WG] = make_uint4((uint32_t)ch.r0, (uint32_t)((uint64_t)ch.r0 >> 32), (uint32_t)ch.r1,
@@ -2708,9 +2711,12 @@ __device__ __forceinline__ bool win_enter(Dev& c) {
 // `stride` records apart; this tick sends the first `cap` of each (the size
 // the ranks agreed on, <= stride).  A block's header counts every record
 // meant for that rank (the demand, reduced as RD_DEMAND); records beyond cap
-// -- and the carry of the previous tick, sent first -- wait in the carry
-// buffer for the next tick, which keeps the window running (lp_fill), so an
-// exchange never overflows and never loses a record.
+// wait in the carry buffer for the next tick, which keeps the window running
+// (lp_fill).  The previous tick's carry goes first: tw_lp_pack_carry claims
+// its block slots in a launch of its own before tw_lp_pack's outbox loop.  A
+// carry that outgrows its capacity (demand above the agreed block size for
+// many ticks in a row: the block size follows the demand every 16 ticks) is
+// lp_err bit 8, which stops every rank at the same tick.
 __device__ __forceinline__ void lp_foreign(const Dev& c, uint4 a, uint4 b, uint4* send, const uint32_t* starts,
                                            uint32_t world, uint32_t stride, uint32_t cap, uint32_t cout) {
     const uint32_t dst = b.w;
@@ -2735,6 +2741,20 @@ __device__ __forceinline__ void lp_foreign(const Dev& c, uint4 a, uint4 b, uint4
     q[0] = a;
     q[1] = b;
 }
+// The records the previous tick's blocks had no room for claim this tick's
+// block slots first (multi-rank exchanges only; launched before tw_lp_pack)
+__global__ void __launch_bounds__(256) tw_lp_pack_carry(Dev c, uint4* send, const uint32_t* starts, uint32_t world,
+                                                        uint32_t stride, uint32_t cap) {
+    if (!win_enter(c) || !c.carry || !send || world <= 1) return;
+    // carry buffers by tick parity: read the previous tick's, write this one's
+    const uint32_t tk = (uint32_t)gp(c.win)[WN_TICKS], cout = tk & 1u, cin = cout ^ 1u;
+    uint32_t nc = *gp(c.carry_n + cin);
+    nc = nc < c.carry_cap ? nc : c.carry_cap;
+    for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < nc; i += gridDim.x * 256) {
+        const uint4 GAS* q = gp(c.carry) + ((size_t)cin * c.carry_cap + i) * 2;
+        lp_foreign(c, q[0], q[1], send, starts, world, stride, cap, cout);
+    }
+}
 __global__ void __launch_bounds__(256) tw_lp_pack(Dev c, uint4* send, const uint32_t* starts, uint32_t world,
                                                   uint32_t stride, uint32_t cap) {
     if (!win_enter(c)) return;
@@ -2742,19 +2762,8 @@ __global__ void __launch_bounds__(256) tw_lp_pack(Dev c, uint4* send, const uint
     n = n < c.out_cap ? n : c.out_cap;
     uint64_t GAS* tmin = (uint64_t GAS*)(gp(c.win) + WN_REC_MIN);
     const int64_t wend = gp(c.win)[WN_T] + gp(c.win)[WN_L];
-    // carry buffers by tick parity: read the previous tick's, write this one's
-    const uint32_t tk = (uint32_t)gp(c.win)[WN_TICKS], cout = tk & 1u, cin = cout ^ 1u;
-    uint32_t nc = 0;
-    if (c.carry && send && world > 1) {
-        nc = *gp(c.carry_n + cin);
-        nc = nc < c.carry_cap ? nc : c.carry_cap;
-    }
-    for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n + nc; i += gridDim.x * 256) {
-        if (i >= n) {  // a record the previous tick's blocks had no room for
-            const uint4 GAS* q = gp(c.carry) + ((size_t)cin * c.carry_cap + (i - n)) * 2;
-            lp_foreign(c, q[0], q[1], send, starts, world, stride, cap, cout);
-            continue;
-        }
+    const uint32_t cout = (uint32_t)gp(c.win)[WN_TICKS] & 1u;  // this tick's carry buffer
+    for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
         const uint4 a = gp(c.outbox)[(size_t)i * 2], b = gp(c.outbox)[(size_t)i * 2 + 1];
         const uint32_t dst = b.w;
         if (b.y == TW_SPAWN_CONT) continue;  // second half of a spawn pair

@@ -108,6 +108,10 @@ extern "C" int tw_draw_link_table(int device, const tw_table_draw* s, uint32_t* 
     }
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) return TW_ERR_NO_DEVICE;
+    // the calling thread's current device is restored on every return below
+    // (a torch or multi-GPU host process keeps its own device selection)
+    int prev = -1;
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
     if (hipSetDevice(device) != hipSuccess) return TW_ERR_NO_DEVICE;
     const size_t n = (size_t)L * D * R;
     uint32_t* d_out = nullptr;
@@ -144,5 +148,6 @@ extern "C" int tw_draw_link_table(int device, const tw_table_draw* s, uint32_t* 
     if (d_links) (void)hipFree(d_links);
     if (d_out) (void)hipFree(d_out);
     if (st) (void)hipStreamDestroy(st);
+    if (prev >= 0 && prev != device) (void)hipSetDevice(prev);
     return rc;
 }
