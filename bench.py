@@ -128,6 +128,8 @@ def engine_sha() -> str:
     h = hashlib.sha256()
     d = os.path.join(ROOT, "time-warp_amd", "csrc")
     for f in sorted(os.listdir(d)):
+        if f == "jit_src.inc":  # (generated from the others at build time)
+            continue
         h.update(f.encode())
         h.update(open(os.path.join(d, f), "rb").read())
     return h.hexdigest()[:16]
@@ -174,7 +176,8 @@ def measured_traffic(args, launches_per_step: float, events_per_step: float, who
 def workload_key(args) -> str:
     return (f"{args.config}:nodes={args.nodes}:replicas={args.replicas}:weak={int(args.weak)}:"
             f"dur={args.duration_s}:drop={args.drop_log2}:rt={args.round_trips}:msgs={args.msg_num}"
-            + (f":geo={args.geometry}" if getattr(args, "geometry", None) else ""))
+            + (f":geo={args.geometry}" if getattr(args, "geometry", None) else "")
+            + (":jit=1" if getattr(args, "jit", 0) else ""))
 
 
 def bench_gossip(args, scn, workload, world, rank, local, dist_on, barrier):

@@ -384,16 +384,20 @@ struct Lane {
     __device__ __forceinline__ void fail(uint32_t st) {
         if (status == TW_REP_RUNNING) status = st;
     }
-    static_assert(!(JIT && TW_DIRTY_TAIL), "the dirty store tail compares the LDS register file with the record");
+#ifndef TW_JIT_RF_VGPR
+#define TW_JIT_RF_VGPR 1  // compiled scenario: registers in VGPRs (1) or the LDS register file (0)
+#endif
+    static constexpr bool RFV = JIT && TW_JIT_RF_VGPR;
+    static_assert(!(RFV && TW_DIRTY_TAIL), "the dirty store tail compares the LDS register file with the record");
     // The running thread's registers r0..r3: the LDS register file (the
     // interpreter's operand indices are per lane) or, in a compiled scenario,
     // the record's own fields held in VGPRs (every index is a constant there)
     __device__ __forceinline__ int64_t rg(const Th& th, uint32_t i) const {
-        if constexpr (JIT) return i == 0 ? th.r0 : i == 1 ? th.r1 : i == 2 ? th.r2 : th.r3;
+        if constexpr (RFV) return i == 0 ? th.r0 : i == 1 ? th.r1 : i == 2 ? th.r2 : th.r3;
         else return rf[i * WG];
     }
     __device__ __forceinline__ void rs(Th& th, uint32_t i, int64_t v) {
-        if constexpr (JIT) {
+        if constexpr (RFV) {
             th.r0 = i == 0 ? v : th.r0;
             th.r1 = i == 1 ? v : th.r1;
             th.r2 = i == 2 ? v : th.r2;
@@ -827,8 +831,10 @@ struct Lane {
         if (n >= 2) {
             const uint32_t p2 = h + 1 == c.Cr ? 0 : h + 1;
             // into LDS staging quad 4 (no register left pending across the step)
+            // (readfirstlane: the m0 operand is an SGPR whatever register the value was kept in)
+            const uint32_t pw4 = (uint32_t)__builtin_amdgcn_readfirstlane((int)(pfs_wave + 4 * WG * 16));
             asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off ; tw:run" ::"v"(run_at(sel, p2)),
-                         "s"(pfs_wave + 4 * WG * 16) : "memory", "m0");
+                         "s"(pw4) : "memory", "m0");
             prun = sel;
         }
     }
@@ -1337,7 +1343,6 @@ struct Lane {
     // CT (the compiled scenario, jop): the opcode OPC and uop flags FLC are
     // template constants, so the front end emits only this instruction's class
     // code and, for a rare op, only its case of the per-opcode switch
-#define TW_RC(X) (CT ? OPC == (uint32_t)(X) : op == (uint32_t)(X))
     template <bool CT = false, uint32_t OPC = 0, uint32_t FLC = 0>
     __device__ __forceinline__ void pass(Th& th, uint32_t slot, St& s, bool at, uint32_t uw, int32_t imm, uint32_t op,
                                          uint32_t fl, uint32_t lfl) {
@@ -1511,15 +1516,15 @@ struct Lane {
             }
         }
         if (CT ? (FLC & U_FX) != 0 : (fl & U_FX) != 0) {
-        // the rare ops, one `if` each (CT: the front end keeps only OPC's);
-        // a case body's `break` leaves the do-while
-        do {
-        if (TW_RC(TW_OP_THROW_TO)) {
+        // the rare ops (CT: OPC is a template constant, so the front end emits
+        // only its case)
+        switch (CT ? OPC : op) {
+        case TW_OP_THROW_TO: {
             thr_any = true; thr = me;
             tref = ra; tcode = b & 0xFFu; tval = rg(th, ((b >> 8) & 3u));
             break;
         }
-        if (TW_RC(TW_OP_THROW)) {
+        case TW_OP_THROW: {
             if (me) {
                 th_set_pc(th, pc + 1);
                 if (unwind(th, slot, b & 0xFFu, rg(th, ((b >> 8) & 3u)))) tgt = th_pc(th);
@@ -1527,7 +1532,8 @@ struct Lane {
             }
             break;
         }
-        if (TW_RC(TW_OP_CATCH) || TW_RC(TW_OP_TMO_PUSH)) {
+        case TW_OP_CATCH:
+        case TW_OP_TMO_PUSH: {
             const uint32_t nf = th_nfr(th);
             const bool bad = nf >= c.max_frames;
             pfail(me && bad, TW_REP_ERR_FRAMES);
@@ -1541,7 +1547,7 @@ struct Lane {
             th.w0 = ok ? (th.w0 & ~(15u << 16)) | ((nf + 1) << 16) : th.w0;
             break;
         }
-        if (TW_RC(TW_OP_UNCATCH)) {
+        case TW_OP_UNCATCH: {
             const uint32_t nf = th_nfr(th);
             const bool bad = nf == 0 || (frame(th, slot, nf > 0 && me ? nf - 1 : 0) >> 16) == 0;
             pfail(me && bad, TW_REP_ERR_INSN);
@@ -1549,17 +1555,18 @@ struct Lane {
             th.w0 = (me && !bad) ? (th.w0 & ~(15u << 16)) | ((nf - 1) << 16) : th.w0;
             break;
         }
-        if (TW_RC(TW_OP_MODI)) {
+        case TW_OP_MODI: {
             const int64_t m = ra % (int64_t)imm;
             wr = true;
             wv = m < 0 ? m + imm : m;
             break;
         }
-        if (TW_RC(TW_OP_NSTORE)) {
+        case TW_OP_NSTORE: {
             if (me) gp(c.nvars)[nix(th.w1, b & 3)] = ra;
             break;
         }
-        if (TW_RC(TW_OP_NLOADX) || TW_RC(TW_OP_NSTOREX)) {
+        case TW_OP_NLOADX:
+        case TW_OP_NSTOREX: {
             const uint64_t node = (uint64_t)rg(th, ((b >> 8) & 3u));
             const bool bad = LP ? node != th.w1 : node >= c.N;
             pfail(me && bad, TW_REP_ERR_INSN);
@@ -1574,7 +1581,7 @@ struct Lane {
             tw_vm_drain();
             break;
         }
-        if (TW_RC(TW_OP_SEND)) {  // schedule (after d) (deliver ..) unless the link drops it
+        case TW_OP_SEND: {  // schedule (after d) (deliver ..) unless the link drops it
             STIME(tsd0);
             wr = true;
             wm = false;
@@ -1655,7 +1662,7 @@ struct Lane {
             STADD(K_CYC_SEND, tsd1 - tsd0);
             break;
         }
-        if (TW_RC(TW_OP_DELIVER)) {  // listener dispatch, ForkStrategy fork_ (MonadDialog.hs:232-256,317)
+        case TW_OP_DELIVER: {  // listener dispatch, ForkStrategy fork_ (MonadDialog.hs:232-256,317)
             STIME(tdl0);
             if (me) {
                 const int64_t r0 = rg(th, 0), r1 = rg(th, 1), r2 = rg(th, 2), r3 = rg(th, 3);
@@ -1736,7 +1743,7 @@ struct Lane {
             STADD(K_CYC_DELIV, tdl1 - tdl0);
             break;
         }
-        if (TW_RC(TW_OP_LISTEN)) {
+        case TW_OP_LISTEN: {
             const bool bad = (uint32_t)imm >= c.n_sets;
             pfail(me && bad, TW_REP_ERR_INSN);
             tc = bad ? T_STOP : T_NONE;
@@ -1751,7 +1758,7 @@ struct Lane {
             th.w0 = (me && !bad && b) ? th.w0 | (F_OWNS << FL_SHIFT) : th.w0;
             break;
         }
-        if (TW_RC(TW_OP_UNLISTEN)) {
+        case TW_OP_UNLISTEN: {
             if (me) {
                 gp(c.bind)[bix(th.w1)] = 0;
                 gp(c.bind_own)[bix(th.w1)] = 0xFFFFFFFFu;
@@ -1762,7 +1769,7 @@ struct Lane {
             }
             break;
         }
-        if (TW_RC(TW_OP_TMO_BEGIN)) {  // schedule (after t) watchdog (TimedT.hs:373-375)
+        case TW_OP_TMO_BEGIN: {  // schedule (after t) watchdog (TimedT.hs:373-375)
             if (me) {
                 const uint32_t tmo = cg(CW_TMO);
                 if (tmo >= c.T) {
@@ -1781,7 +1788,7 @@ struct Lane {
             }
             break;
         }
-        if (TW_RC(TW_OP_TMO_END)) {
+        case TW_OP_TMO_END: {
             if (me) {
                 const uint32_t nf = th_nfr(th);
                 const uint32_t fr = nf ? frame(th, slot, nf - 1) : 0u;
@@ -1796,7 +1803,7 @@ struct Lane {
             }
             break;
         }
-        if (TW_RC(TW_OP_TMO_FIRE)) {
+        case TW_OP_TMO_FIRE: {
             const uint64_t e = (uint64_t)rg(th, 1);
             const bool ok = me && e < c.T;
             thr_any = true;
@@ -1805,12 +1812,12 @@ struct Lane {
             tw_vm_drain();
             break;
         }
-        {  // an invalid opcode
+        default: {  // an invalid opcode
             pfail(me, TW_REP_ERR_INSN);
             tc = T_STOP;
             break;
         }
-        } while (0);
+        }
         }  // U_FX
         if (wr) rs(th, a, wm ? wv : ra);
         (void)lfl;
@@ -2413,7 +2420,7 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
                         pending_main = 0;
                         L.pf_slot = 0xFFFFFFFFu;
                         L.fetch_rec(0, th);
-                        if constexpr (!JIT) { L.rf[0] = th.r0; L.rf[WG] = th.r1; L.rf[2 * WG] = th.r2; L.rf[3 * WG] = th.r3; }
+                        if constexpr (!decltype(L)::RFV) { L.rf[0] = th.r0; L.rf[WG] = th.r1; L.rf[2 * WG] = th.r2; L.rf[3 * WG] = th.r3; }
                         L.hnode = th.w1;
                         run = true;
                     } else if (rare) {  // whileM_ notDone, or this launch's event cap
@@ -2470,7 +2477,7 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
                                 L.now = t;
                                 if (t - L.nbase > (int64_t)0x7FFFFFFF) L.near_rebase(t);
                                 L.hnode = th.w1;
-                                if constexpr (!JIT) { L.rf[0] = th.r0; L.rf[WG] = th.r1; L.rf[2 * WG] = th.r2; L.rf[3 * WG] = th.r3; }
+                                if constexpr (!decltype(L)::RFV) { L.rf[0] = th.r0; L.rf[WG] = th.r1; L.rf[2 * WG] = th.r2; L.rf[3 * WG] = th.r3; }
                                 // LP phantom = the deliverer's wake, already counted and hashed by the sender
                                 const bool phantom = LP && (th_flags(th) & F_PHANTOM);
                                 if (!phantom) {

@@ -82,9 +82,10 @@ bool shared_op(uint32_t w0) {
 std::string dispatch_src(const tw_insn* insns, uint32_t n) {
     std::string s;
     s.reserve(128 * (size_t)n + 512);
+    s += "#ifndef TW_JIT_DISPATCH_ATTR\n#define TW_JIT_DISPATCH_ATTR __forceinline__\n#endif\n";
     s += "namespace {\n"
          "template <class LT, class ST>\n"
-         "__device__ __forceinline__ void tw_jit_dispatch(LT& L, Th& th, uint32_t slot, ST& s, uint32_t fpc) {\n"
+         "__device__ TW_JIT_DISPATCH_ATTR void tw_jit_dispatch(LT& L, Th& th, uint32_t slot, ST& s, uint32_t fpc) {\n"
          "    switch (fpc) {\n";
     char buf[200];
     for (uint32_t pc = 0; pc < n; ++pc) {
@@ -167,6 +168,18 @@ int jit_compile(const tw_insn* insns, uint32_t n_insns, const std::vector<std::s
     std::vector<std::string> opts = {"--offload-arch=gfx950", "-O3", "-std=c++17",
                                      std::string("-I") + (rocm && *rocm ? rocm : "/opt/rocm") + "/include"};
     for (const std::string& d : defs) opts.push_back(d);
+    if (const char* x = getenv("TW_JIT_OPTS")) {  // (experiments: extra options, space-separated)
+        std::string o;
+        for (const char* p = x;; ++p) {
+            if (*p == ' ' || *p == 0) {
+                if (!o.empty()) opts.push_back(o);
+                o.clear();
+                if (!*p) break;
+            } else {
+                o += *p;
+            }
+        }
+    }
     std::string key_s = src;
     for (const std::string& o : opts) key_s += "\n" + o;
     const uint64_t key = fnv1a(key_s);
@@ -239,6 +252,10 @@ int jit_compile(const tw_insn* insns, uint32_t n_insns, const std::vector<std::s
     std::string co(cs, '\0');
     hiprtcGetCode(prog, &co[0]);
     hiprtcDestroyProgram(&prog);
+    if (const char* dump = getenv("TW_JIT_DUMP")) {  // (inspection: the source and the code object)
+        (void)write_file(std::string(dump) + ".hip", src);
+        (void)write_file(std::string(dump) + ".co", co);
+    }
     if (cdir && *cdir) {
         std::string nm;
         for (const std::string& x : ns) nm += x + "\n";

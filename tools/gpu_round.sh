@@ -45,6 +45,8 @@ for s in "$@"; do
     benchq_c3_8k) step benchq_c3_8k 300 python bench.py --replicas 8192 --steps 2 --warmup 1 --no-cpu-baseline ;;
     benchq_c2) step benchq_c2 300 python bench.py --config ping_pong --steps 2 --warmup 1 --no-cpu-baseline ;;
     geo=*) export TW_GEOMETRY=${s#geo=}; SFX=_${s#geo=} ;;
+    env=*) kv=${s#env=}; export "${kv%%=*}=${kv#*=}" ;;
+    sfx=*) SFX=_${s#sfx=} ;;
     pytest_geo) step pytest_geo 600 python -u -m pytest tests/ -q -m gpu -x --timeout 120 --timeout-method thread -k "$TW_GEOMETRY" ;;
     lib=default) unset TW_LIB; SFX="" ;;
     lib=*) export TW_LIB=$PWD/time-warp_amd/lib/libtimewarp_${s#lib=}.so; SFX=_${s#lib=} ;;
