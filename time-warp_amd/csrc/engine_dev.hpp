@@ -1190,8 +1190,11 @@ struct Lane {
 
     // Create a thread queued at now (fork, TimedT.hs:326-339): its record is
     // left in `ch` for the store tail.  Returns its ref.
+    // queue = false: the child is the very next pop and runs in place (step):
+    // its queue entry's insertion counter value is taken, the entry itself and
+    // the live count's +1 / -1 of its push and pop are left out
     __device__ __forceinline__ bool spawn(uint32_t pc, uint32_t node, int64_t q0, int64_t q1, int64_t q2, int64_t q3,
-                                          int64_t& ref, Th& ch, uint32_t& cs_out) {
+                                          int64_t& ref, Th& ch, uint32_t& cs_out, bool queue = true) {
         uint32_t s = alloc_slot();
         if (s == 0xFFFFFFFFu) return false;
         if (tidc == 0xFFFFFFFFu) { fail(TW_REP_ERR_COUNTER); return false; }  // getNextThreadId, TimedT.hs:288-289
@@ -1203,7 +1206,8 @@ struct Lane {
         ch.w3 = 0;
         ch.f0 = ch.f1 = ch.xl = ch.xh = 0;
         ch.r0 = q0; ch.r1 = q1; ch.r2 = q2; ch.r3 = q3;
-        enqueue(ch, s, now);
+        if (queue) enqueue(ch, s, now);
+        else (void)next_seq();
         cs_out = s;
         ref = (int64_t)(((uint64_t)tid << 32) | s);
         return true;
@@ -1894,6 +1898,81 @@ struct Lane {
         s.fin = at ? (uint32_t)T_STOP : s.fin;
         s.running = s.running && !at;
     }
+    // A fork whose child is the very next pop runs the child in place, in this
+    // iteration (replica kernels).  TimedT's fork queues the child at now and
+    // the parent at now + 1 (TimedT.hs:326-342); the child is PQ.minView's
+    // next pick (TimedT.hs:242) when its queue key (now, key of the next
+    // insertion counter value) is below every queued event's: under the
+    // engine's (t, seq) order only if nothing else is queued at now, under
+    // TW_TIE_LIFO always -- which is what pqueue's MinQueue does too, where an
+    // insert whose key is <= the held minimum's becomes the new minimum.  For
+    // those lanes the fork is carried out here exactly as the terminal and the
+    // next pop would: the child's thread id, slot and insertion counter value,
+    // then the parent's queue entry at now + 1 and its record; the child's pop
+    // is counted (event, clock, resume hash term on its node) and it becomes
+    // the running thread, without its queue entry, the pop phase or a store
+    // tail in between.  Returns true if some lane has a child to run.
+    __device__ __forceinline__ bool fork_in_place(Th& th, uint32_t& slot, St& s) {
+        const uint32_t kc = c.tie_mode ? seq_key(c.tie_mode, seq + 1u) : seq + 1u;
+        bool ip = s.fin == T_SPAWN && status == TW_REP_RUNNING && d_ev < ev_room && seq < 0xFFFFFFFEu &&
+                  tidc != 0xFFFFFFFFu;
+        if (!__builtin_amdgcn_ballot_w64(ip)) return false;
+        if (far_dirty) far_min();
+        bool has = near_n != 0;
+        int64_t qt = nbase + (int64_t)(nrk >> 32);
+        uint32_t qs = (uint32_t)nrk;
+        const bool uf = fsrc >= 0 && (!has || tless(fmt, fms, qt, qs));
+        qt = uf ? fmt : qt;
+        qs = uf ? fms : qs;
+        has = has || fsrc >= 0;
+        ip = ip && (!has || tless(now, kc, qt, qs));
+        if (!__builtin_amdgcn_ballot_w64(ip)) return false;
+        if (ip) {
+            STAT(K_SPAWN);
+            const uint32_t cdel = cg(CW_CDEL), cra = cg(CW_CRA);
+            int64_t ref;
+            Th ch;
+            uint32_t cslot = 0xFFFFFFFFu;
+            const bool ok =
+                (cdel & 2u) ? spawn(cg(CW_CPC), cg(CW_CNODE), rg(th, 0), rg(th, 1), rg(th, 2), rg(th, 3), ref, ch, cslot,
+                                    false)
+                            : spawn(cg(CW_CPC), cg(CW_CNODE), cg64(CW_Q0, CW_Q0 + 1), cg64(CW_Q0 + 2, CW_Q0 + 3),
+                                    cg64(CW_Q0 + 4, CW_Q0 + 5), cg64(CW_Q0 + 6, CW_Q7), ref, ch, cslot, false);
+            if (ok) {
+                // the parent: `wait (for 1 mcs)` (TimedT.hs:340) -- queued, record stored
+                if (cra < 4) rs(th, cra, ref);
+                th_set_pc(th, s.pc);
+                enqueue(th, slot, now + 1);
+                th.r0 = rg(th, 0); th.r1 = rg(th, 1); th.r2 = rg(th, 2); th.r3 = rg(th, 3);
+                put_rec(slot, th);
+                // the child's pop (TimedT.hs:241-247): counted, its resume term on its node
+                STAT(K_POP);
+                ++d_ev;
+                final_t = now;
+                if (ch.w1 != hnode) {
+                    hash_flush();
+                    hnode = ch.w1;
+                }
+                hacc += term0(now, TW_KIND_RESUME | th_pc(ch));
+                th = ch;
+                slot = cslot;
+                if constexpr (!RFV) {
+                    rf[0] = ch.r0; rf[WG] = ch.r1; rf[2 * WG] = ch.r2; rf[3 * WG] = ch.r3;
+                }
+                s.pc = th_pc(th);
+                th.w0 |= F_STARTED << FL_SHIFT;
+                s.running = s.pc < c.n_insns;
+                pfail(!s.running, TW_REP_ERR_INSN);
+                s.fin = s.running ? (uint32_t)T_NONE : (uint32_t)T_STOP;
+                s.n = 0;
+                s.yt = 0;
+            } else {
+                s.fin = T_STOP;  // (a slot or counter failure: the terminal stores the parent)
+            }
+        }
+        return true;
+    }
+
     // Run the popped threads' continuations until each yields or ends (the
     // ContT continuation of TimedT.hs:343-355).  Called by every lane of the
     // wave (`run` = this lane popped a runnable thread), so the loop is
@@ -1920,7 +1999,14 @@ struct Lane {
         STIME(ti0);
         for (;;) {
             const uint64_t mask = __builtin_amdgcn_ballot_w64(s.running);
-            if (mask == 0) break;
+            if (mask == 0) {
+                // (replica kernels) a fork whose child is the very next pop: the
+                // child runs in place, its lanes running again
+                if constexpr (!LP) {
+                    if (fork_in_place(th, slot, s)) continue;
+                }
+                break;
+            }
             const uint32_t first = (uint32_t)__builtin_ctzll(mask);
             if constexpr (JIT) {
                 // the compiled scenario (jit.cpp): the first running lane's pc picks

@@ -25,6 +25,9 @@ for s in "$@"; do
     probe2) step probe2 300 env TW_LIB=$PWD/time-warp_amd/lib/libtimewarp_prof2.so python tools/kernel_probe.py 65536 4096 ;;
     bench)  step bench 500 python bench.py ;;
     jit_c3) step jit_c3 400 python -u tools/jit_probe.py token_ring 65536 ;;
+    tie_c3) step tie_c3 400 python -u tools/ab_probe.py token_ring 65536 auto tie=fifo tie=lifo ;;
+    tie_c2) step tie_c2 400 python -u tools/ab_probe.py ping_pong 1048576 auto tie=fifo tie=lifo ;;
+    tie_c3_8k) step tie_c3_8k 400 python -u tools/ab_probe.py token_ring 8192 narrow tie=fifo tie=lifo ;;
     jit_c3_8k) step jit_c3_8k 400 python -u tools/jit_probe.py token_ring 8192 narrow ;;
     jit_c2) step jit_c2 400 python -u tools/jit_probe.py ping_pong 1048576 ;;
     jit_c5) step jit_c5 400 python -u tools/jit_probe.py hotspot 4096 sparse ;;
