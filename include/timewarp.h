@@ -80,11 +80,20 @@ enum {
     TW_TIE_FIFO = 0,
     TW_TIE_LIFO = 1,
     TW_TIE_SCRAMBLE = 2,
-    TW_TIE_PQUEUE = 3   /* TimedT's own order: the queue is pqueue-1.3.1.1's
+    TW_TIE_PQUEUE = 3,  /* TimedT's own order: the queue is pqueue-1.3.1.1's
                            binomial MinQueue ordered by timestamp only
                            (TimedT.hs:100-104, 242), throwTo rebuilds it with
                            fromList . map . toList (TimedT.hs:361-368); the
                            wave geometry only (tw_set_tie_mode) */
+    TW_TIE_FORKFIRST = 4 /* TW_TIE_FIFO, except that a forked child (fork, a
+                           send's deliverer, a delivery's handler, a timeout's
+                           watchdog) is always the next pop, ahead of events
+                           queued earlier at the same time -- pqueue's rule for
+                           an insert whose key is <= the held minimum
+                           (TimedT.hs:242, 326-342).  The replica kernels run
+                           that child in place, without a queue round trip.
+                           Insertion counter values are 31-bit in this mode.
+                           Replica geometries but wave (tw_set_tie_mode) */
 };
 
 /* ------------------------------------------------------------- exceptions */

@@ -29,6 +29,7 @@ MODE_CANONICAL = 0
 MODE_PQUEUE = 1
 MODE_LIFO = 2        # canonical queue, equal timestamps in reverse insertion order (TW_TIE_LIFO)
 MODE_SCRAMBLE = 3    # canonical queue, equal timestamps in scrambled order (TW_TIE_SCRAMBLE)
+MODE_FORKFIRST = 5   # canonical queue, a forked child always the next pop (TW_TIE_FORKFIRST)
 
 
 class TwoLiveDelays(C.Structure):

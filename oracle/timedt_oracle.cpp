@@ -34,6 +34,11 @@
 //   modes 2, 3: the canonical queue with equal timestamps in reverse insertion
 //          order (TW_TIE_LIFO) or a scrambled order (TW_TIE_SCRAMBLE): the
 //          engine's tie probes (tw_tie_audit), mirrored for the parity tests.
+//   mode 5: the canonical queue, but a forked child is always the next pop
+//          (TW_TIE_FORKFIRST): its entry takes the key of its insertion counter
+//          value alone, every other entry the value with bit 31 set, so it
+//          sorts before everything queued at the same time -- what pqueue's
+//          MinQueue does with an insert whose key is <= the held minimum.
 #include <algorithm>
 #include <atomic>
 #include <cstdint>
@@ -122,8 +127,12 @@ struct EvLEq {  // Event's Ord: compare timestamps only (TimedT.hs:100-104)
 };
 
 // The key an insertion counter takes under a tie mode (== the engine's seq_key).
+// (TW_TIE_FORKFIRST: a forked child's entry is marked by bit 40 of its seq and
+// keeps the bare value, CanonQueue::key)
+constexpr uint64_t kChildMark = 1ull << 40;
 inline uint32_t seq_key32(int tie, uint32_t s) {
     if (tie == TW_TIE_FIFO) return s;
+    if (tie == TW_TIE_FORKFIRST) return s | 0x80000000u;
     if (tie == TW_TIE_LIFO) return 0u - s;
     uint32_t x = s;
     x ^= x >> 16; x *= 0x7feb352du; x ^= x >> 15; x *= 0x846ca68bu; x ^= x >> 16;
@@ -163,10 +172,14 @@ class CanonQueue {
     }
 
   private:
+    uint32_t key(const Event& e) const {
+        if (tie == TW_TIE_FORKFIRST && (e.seq & kChildMark)) return (uint32_t)e.seq;
+        return seq_key32(tie, (uint32_t)e.seq);
+    }
     bool less(const Event& a, const Event& b) const {
         if (a.t != b.t) return a.t < b.t;
         if (tie == TW_TIE_FIFO) return a.seq < b.seq;
-        return seq_key32(tie, (uint32_t)a.seq) < seq_key32(tie, (uint32_t)b.seq);
+        return key(a) < key(b);
     }
     void set(size_t i, const Event& e) {
         h_[i] = e;
@@ -229,7 +242,7 @@ struct Sim {
 
     Sim(const tw_scenario_desc* d_, uint32_t rep, two_opts* o_, uint64_t* hashes_)
         : d(d_), replica(rep), o(o_), mode(o_->mode == 1 ? 1 : 0), hashes(hashes_) {
-        cq.tie = o_->mode >= 2 ? o_->mode - 1 : TW_TIE_FIFO;
+        cq.tie = o_->mode == 5 ? TW_TIE_FORKFIRST : o_->mode >= 2 ? o_->mode - 1 : TW_TIE_FIFO;
         max_frames = d->max_frames ? d->max_frames : 2u;
         node_vars.assign((size_t)d->n_nodes * 4, 0);
         if (d->node_vars) std::memcpy(node_vars.data(), d->node_vars, node_vars.size() * 8);
@@ -260,13 +273,14 @@ struct Sim {
     // The engine's counters are 32-bit; reaching the top is a status, never a
     // silent wrap (the reference's counters are unbounded Integers).
     uint64_t next_seq() {
-        if (seq >= 0xFFFFFFFFull) fail(TW_REP_ERR_COUNTER);
+        // (TW_TIE_FORKFIRST keys spend bit 31 on the child mark: 31-bit counter)
+        if (seq >= (cq.tie == TW_TIE_FORKFIRST ? 0x7FFFFFFFull : 0xFFFFFFFFull)) fail(TW_REP_ERR_COUNTER);
         else ++seq;
         return seq;
     }
 
-    void enqueue(Thread* th, int64_t t) {
-        Event e{t, next_seq(), th};
+    void enqueue(Thread* th, int64_t t, bool child = false) {
+        Event e{t, next_seq() | (child && cq.tie == TW_TIE_FORKFIRST ? kChildMark : 0ull), th};
         if (mode == 0) cq.insert(e);
         else pq.insert(e);
     }
@@ -307,7 +321,7 @@ struct Sim {
         Thread* c = new_thread(pc, node);
         if (!c) return nullptr;
         for (int i = 0; i < 4; ++i) c->r[i] = regs[i];
-        enqueue(c, cur);
+        enqueue(c, cur, true);
         return c;
     }
 

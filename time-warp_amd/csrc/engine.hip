@@ -1027,7 +1027,10 @@ int sh_geometry(tw_shard* c) {
 int sh_set_tie_mode(tw_shard* c, uint32_t mode) {
     if (!c) return TW_ERR_INVALID;
     if (!c->loaded) return TW_ERR_STATE;
-    if (mode > TW_TIE_PQUEUE) return TW_ERR_INVALID;
+    if (mode > TW_TIE_FORKFIRST) return TW_ERR_INVALID;
+    // a forked child first: the lane-per-replica kernels (their fork_in_place);
+    // the wave and logical-process kernels keep the other orders
+    if (mode == TW_TIE_FORKFIRST && (c->lp || c->geo == 3)) return TW_ERR_INVALID;
     if (mode == TW_TIE_PQUEUE) {
         if (c->lp || c->geo != 3) return TW_ERR_INVALID;  // the wave kernel only
         HIPCHK(hipSetDevice(c->device));

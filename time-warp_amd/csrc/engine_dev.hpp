@@ -882,14 +882,20 @@ struct Lane {
     // A fresh insertion counter value, as the key the tie mode gives it.  The
     // counter is 32-bit: reaching its top is a TW_REP_ERR_COUNTER status (the
     // replica stops after this step), never a silent wrap.
-    __device__ __forceinline__ uint32_t next_seq() {
-        if (seq == 0xFFFFFFFFu) fail(TW_REP_ERR_COUNTER);
+    // (TW_TIE_FORKFIRST: 31 bits -- bit 31 of a key marks every entry but a
+    // forked child's, `child`, which sorts first among its time's entries)
+    __device__ __forceinline__ uint32_t seq_top() const {
+        return c.tie_mode == TW_TIE_FORKFIRST ? 0x7FFFFFFFu : 0xFFFFFFFFu;
+    }
+    __device__ __forceinline__ uint32_t next_seq(bool child = false) {
+        if (seq == seq_top()) fail(TW_REP_ERR_COUNTER);
         else ++seq;
+        if (child && c.tie_mode == TW_TIE_FORKFIRST) return seq;
         return c.tie_mode ? seq_key(c.tie_mode, seq) : seq;
     }
     // Queue the thread at t with a fresh seq; returns true if the entry is on chip.
-    __device__ __forceinline__ bool enqueue(Th& th, uint32_t slot, int64_t t) {
-        uint32_t s = next_seq();
+    __device__ __forceinline__ bool enqueue(Th& th, uint32_t slot, int64_t t, bool child = false) {
+        uint32_t s = next_seq(child);
         if (th.w3 == 0) ++live;
         th.w3 = s;
         if (near_fits(t)) {
@@ -1206,8 +1212,8 @@ struct Lane {
         ch.w3 = 0;
         ch.f0 = ch.f1 = ch.xl = ch.xh = 0;
         ch.r0 = q0; ch.r1 = q1; ch.r2 = q2; ch.r3 = q3;
-        if (queue) enqueue(ch, s, now);
-        else (void)next_seq();
+        if (queue) enqueue(ch, s, now, true);
+        else (void)next_seq(true);
         cs_out = s;
         ref = (int64_t)(((uint64_t)tid << 32) | s);
         return true;
@@ -1907,14 +1913,16 @@ struct Lane {
     // TW_TIE_LIFO always -- which is what pqueue's MinQueue does too, where an
     // insert whose key is <= the held minimum's becomes the new minimum.  For
     // those lanes the fork is carried out here exactly as the terminal and the
-    // next pop would: the child's thread id, slot and insertion counter value,
+    // next pop would (TW_TIE_FORKFIRST: always the case, the child's key sorts
+    // first): the child's thread id, slot and insertion counter value,
     // then the parent's queue entry at now + 1 and its record; the child's pop
     // is counted (event, clock, resume hash term on its node) and it becomes
     // the running thread, without its queue entry, the pop phase or a store
     // tail in between.  Returns true if some lane has a child to run.
     __device__ __forceinline__ bool fork_in_place(Th& th, uint32_t& slot, St& s) {
-        const uint32_t kc = c.tie_mode ? seq_key(c.tie_mode, seq + 1u) : seq + 1u;
-        bool ip = s.fin == T_SPAWN && status == TW_REP_RUNNING && d_ev < ev_room && seq < 0xFFFFFFFEu &&
+        const uint32_t kc = c.tie_mode == TW_TIE_FORKFIRST ? seq + 1u : c.tie_mode ? seq_key(c.tie_mode, seq + 1u)
+                                                                                   : seq + 1u;
+        bool ip = s.fin == T_SPAWN && status == TW_REP_RUNNING && d_ev < ev_room && seq + 1u < seq_top() &&
                   tidc != 0xFFFFFFFFu;
         if (!__builtin_amdgcn_ballot_w64(ip)) return false;
         if (far_dirty) far_min();
@@ -2001,8 +2009,10 @@ struct Lane {
             const uint64_t mask = __builtin_amdgcn_ballot_w64(s.running);
             if (mask == 0) {
                 // (replica kernels) a fork whose child is the very next pop: the
-                // child runs in place, its lanes running again
-                if constexpr (!LP) {
+                // child runs in place, its lanes running again.  Not in the
+                // sparse geometry, whose kernel would spill for it (there the
+                // child takes its queue round trip: the same order either way)
+                if constexpr (!LP && !PL) {
                     if (fork_in_place(th, slot, s)) continue;
                 }
                 break;

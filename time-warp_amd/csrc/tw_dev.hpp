@@ -219,8 +219,11 @@ enum { PQ_N, PQ_NFREE, PQ_BUMP, PQ_FLEN, PQ_MIN, PQ_FOREST = PQ_MIN + 4, PQ_WORD
 // The key an insertion counter value takes in the queues (equal timestamps pop
 // in key order): FIFO (canonical), reverse (LIFO) or a scrambled bijection.
 // Every mode maps 0 to 0 and nothing else to 0 (wake_seq 0 = not queued).
+// TW_TIE_FORKFIRST: bit 31 set on every key but a forked child's (Lane::next_seq),
+// so a child sorts before everything queued at the same time.
 __device__ __forceinline__ uint32_t seq_key(uint32_t mode, uint32_t s) {
     if (mode == TW_TIE_FIFO || mode == TW_TIE_PQUEUE) return s;  // (pqueue: seq only names the entry)
+    if (mode == TW_TIE_FORKFIRST) return s | 0x80000000u;
     if (mode == TW_TIE_LIFO) return 0u - s;
     uint32_t x = s;  // xorshift-multiply: a bijection of u32 with x(0) = 0
     x ^= x >> 16; x *= 0x7feb352du; x ^= x >> 15; x *= 0x846ca68bu; x ^= x >> 16;

@@ -323,7 +323,7 @@ class Engine:
                "tw_tie_audit")
         return RunStats(**{f: getattr(st, f) for f, _ in TwStats._fields_ if f != "reserved"})
 
-    TIE_MODES = {"fifo": 0, "lifo": 1, "scramble": 2, "pqueue": 3}  # TW_TIE_*
+    TIE_MODES = {"fifo": 0, "lifo": 1, "scramble": 2, "pqueue": 3, "forkfirst": 4}  # TW_TIE_*
 
     def set_jit(self, on: bool = True) -> "Engine":
         """The scenario compiler (tw_set_jit): later loads (and the loaded
@@ -342,7 +342,10 @@ class Engine:
         """Equal-timestamp order of later runs: "fifo" (the engine's (t, seq)),
         the audit probes "lifo" / "scramble", or "pqueue": TimedT's own order
         (pqueue's MinQueue by timestamp only, TimedT.hs:100-104, with the
-        throwTo rebuild of TimedT.hs:361-368), wave geometry only."""
+        throwTo rebuild of TimedT.hs:361-368), wave geometry only, or
+        "forkfirst": fifo with a forked child always the next pop (pqueue's
+        held-minimum rule; the replica kernels run it in place), lane-per-
+        replica geometries only."""
         _check(self.lib.tw_set_tie_mode(self.ctx, self.TIE_MODES[mode]), "tw_set_tie_mode")
         return self
 
