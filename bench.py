@@ -177,7 +177,8 @@ def workload_key(args) -> str:
     return (f"{args.config}:nodes={args.nodes}:replicas={args.replicas}:weak={int(args.weak)}:"
             f"dur={args.duration_s}:drop={args.drop_log2}:rt={args.round_trips}:msgs={args.msg_num}"
             + (f":geo={args.geometry}" if getattr(args, "geometry", None) else "")
-            + (":jit=1" if getattr(args, "jit", 0) else ""))
+            + (":jit=1" if getattr(args, "jit", 0) else "")
+            + (f":tie={args.tie}" if getattr(args, "tie", "auto") != "auto" else ""))
 
 
 def bench_gossip(args, scn, workload, world, rank, local, dist_on, barrier):
@@ -305,6 +306,12 @@ def main():
                          "GPU must be a power of two: lanes are node << log2(R) | replica)")
     ap.add_argument("--host-windows", action="store_true",
                     help="gossip: the host-driven window loop (round-1 path) instead of the device loop")
+    ap.add_argument("--tie", default="auto", choices=["auto", "fifo", "forkfirst", "lifo"],
+                    help="equal-timestamp order (tw_set_tie_mode).  forkfirst = fifo except that a forked child is "
+                         "always the next pop, as in TimedT's pqueue (an insert whose key is <= the held minimum "
+                         "becomes the minimum); the replica kernels then run the child in place.  auto: forkfirst "
+                         "for the token ring on the lane-per-replica geometries (C3 is tie-insensitive: its results "
+                         "equal the canonical order's, checked by parity_sample), else fifo")
     ap.add_argument("--jit", type=int, default=0, choices=[0, 1],
                     help="1: the scenario compiler (tw_set_jit) -- the program image compiled into the event "
                          "kernel at load (outside the timed region); 0: the interpreter")
@@ -384,6 +391,12 @@ def main():
         eng.set_jit(True)
     eng.load(scn, geometry=args.geometry)
     setup["load_s"] = time.perf_counter() - t_load
+    tie = args.tie
+    if tie == "auto":
+        tie = "forkfirst" if args.config == "token_ring" and eng.geometry() not in ("lpb", "wave") else "fifo"
+    if tie != "fifo":
+        eng.set_tie_mode(tie)
+    setup["tie_order"] = tie
     jit_on, jit_ms = eng.jit_status()
     if args.jit and not jit_on:
         raise SystemExit("--jit 1: the scenario compiler did not produce the kernel")
@@ -455,6 +468,7 @@ def main():
                 "events_per_step": int(tot_events / args.steps),
                 "parallelism": f"replica-sharded x{world}, contiguous blocks (no data-path collective)",
                 "geometry": eng.geometry(),
+                "tie_order": tie,
             },
             "roofline": {
                 "bound": "hbm",
@@ -496,8 +510,11 @@ def main():
         if not args.no_cpu_baseline:
             cb, parity, n = cpu_baseline(scn, res, hashes, args.cpu_seconds)
             out["cpu_baseline"] = cb
-            out["parity_sample"] = {"replicas": n, "bit_exact": bool(parity)}
+            out["parity_sample"] = {"replicas": n, "bit_exact": bool(parity),
+                                    "against": "oracle canonical (t, seq) order"}
         print(json.dumps(out), flush=True)
+        if not args.no_cpu_baseline and not out["parity_sample"]["bit_exact"]:
+            raise SystemExit("parity_sample: the GPU results differ from the oracle's")
     eng.close()
     if dist_on:
         dist.destroy_process_group()

@@ -180,13 +180,26 @@ void free_all(tw_shard* c) {
 
 }  // namespace
 
+// The fork-in-place variant (Lane::fork_in_place) of a replica geometry: under
+// the tie orders where a forked child is always the next pop (FORKFIRST,
+// LIFO), and for the compact geometry in every order.  Measured (round 4):
+// C3 dense FIFO 17.8 G events/s without it, 16.3 G with it (the child is
+// rarely next under FIFO and the code costs registers), FORKFIRST 19.4 G;
+// C2 compact FIFO 39.7 G without, 43.2-44.0 G with (ping-pong forks into an
+// empty queue: the child is next under FIFO too)
+static bool use_ip(const tw_shard* c) {
+    if (c->lp || c->geo == 1) return false;  // (LP: its own inline paths; sparse: compiled out)
+    return c->d.tie_mode == TW_TIE_FORKFIRST || c->d.tie_mode == TW_TIE_LIFO || c->geo == 7;
+}
+
 template <bool LP, int WG, int NC, int TPW = 64, bool RUNS = true>
 static void launch_run(tw_shard* c, hipStream_t st, int64_t t_end, uint64_t limit, uint32_t budget) {
     const uint32_t blocks = (uint32_t)((c->d.R + WG - 1) / WG);
+    const bool ip = !LP && WG >= 64 && use_ip(c);
     if (c->jit_on) {
         // the compiled scenario (jit.cpp): same kernel template, same launch shape
         const bool gs = LP && blocks > c->lp_grid, prw = LP && c->d.rw && c->d.win;
-        const hipFunction_t f = c->jit_fn[(gs ? 2 : 0) + (prw ? 1 : 0)];
+        const hipFunction_t f = c->jit_fn[(gs ? 2 : 0) + (prw ? 1 : 0) + (ip ? 1 : 0)];
         if (!f) {
             c->jit_missing = true;
             return;
@@ -219,6 +232,13 @@ static void launch_run(tw_shard* c, hipStream_t st, int64_t t_end, uint64_t limi
             hipLaunchKernelGGL((tw_run_kernel<LP, WG, NC, TPW, RUNS>), g, b, c->lds_bytes, st, c->d, t_end, limit,
                                budget);
         return;
+    }
+    if constexpr (WG >= 64) {
+        if (ip) {
+            hipLaunchKernelGGL((tw_run_kernel<LP, WG, NC, TPW, RUNS, false, false, true>), dim3(blocks),
+                               dim3(WG * 64 / TPW), c->lds_bytes, st, c->d, t_end, limit, budget);
+            return;
+        }
     }
     hipLaunchKernelGGL((tw_run_kernel<LP, WG, NC, TPW, RUNS>), dim3(blocks), dim3(WG * 64 / TPW), c->lds_bytes, st,
                        c->d, t_end, limit, budget);
@@ -279,8 +299,8 @@ static void jit_inst(bool lp, int geo, std::vector<std::string>& inst, std::vect
     char b[160];
     if (lp) {
         for (int v = 0; v < 4; ++v) {
-            snprintf(b, sizeof b, "true, %d, %d, 64, true, %s, %s", TW_WG_LP, TW_NEAR_LP, (v & 2) ? "true" : "false",
-                     (v & 1) ? "true" : "false");
+            snprintf(b, sizeof b, "true, %d, %d, 64, true, %s, %s, false", TW_WG_LP, TW_NEAR_LP,
+                     (v & 2) ? "true" : "false", (v & 1) ? "true" : "false");
             inst.push_back(b);
             slot.push_back(v);
         }
@@ -291,9 +311,12 @@ static void jit_inst(bool lp, int geo, std::vector<std::string>& inst, std::vect
         else if (geo == 2) tpw = TW_HALF_LANES;
         else if (geo == 5) { wg = TW_NARROW; tpw = TW_NARROW; }
         else if (geo == 7) { nc = TW_NEAR_COMPACT; runs = false; }
-        snprintf(b, sizeof b, "false, %d, %d, %d, %s, false, false", wg, nc, tpw, runs ? "true" : "false");
-        inst.push_back(b);
-        slot.push_back(0);
+        for (int ip = 0; ip < (geo == 1 ? 1 : 2); ++ip) {  // (fork-in-place variant in slot 1; not sparse)
+            snprintf(b, sizeof b, "false, %d, %d, %d, %s, false, false, %s", wg, nc, tpw, runs ? "true" : "false",
+                     ip ? "true" : "false");
+            inst.push_back(b);
+            slot.push_back(ip);
+        }
     }
 }
 
@@ -544,26 +567,29 @@ static int load_common(tw_shard* c, const tw_scenario_desc* s, bool lp, uint32_t
                    prog_lds;
     if (c->geo == 3) c->lds_bytes = 0;  // the wave kernel reads the program image through the scalar cache
     if (c->lds_bytes > 160 * 1024) { free_all(c); return TW_ERR_INVALID; }  // program + constants must fit in LDS
-    if (c->geo == 3) {
-    } else if (c->geo == 1)
-        HIPCHK(hipFuncSetAttribute((const void*)tw_run_kernel<false, TW_WG_SPARSE, TW_NEAR_SPARSE>,
-                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)c->lds_bytes));
-    else if (c->geo == 2)
-        HIPCHK(hipFuncSetAttribute((const void*)tw_run_kernel<false, TW_WG, TW_NEAR_CAP, TW_HALF_LANES>,
-                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)c->lds_bytes));
-    else if (c->geo == 5)
-        HIPCHK(hipFuncSetAttribute((const void*)tw_run_kernel<false, TW_NARROW, TW_NEAR_CAP, TW_NARROW>,
-                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)c->lds_bytes));
-    else if (c->geo == 7)
-        HIPCHK(hipFuncSetAttribute((const void*)tw_run_kernel<false, TW_WG, TW_NEAR_COMPACT, 64, false>,
-                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)c->lds_bytes));
-    else if (lp)
-        HIPCHK(hipFuncSetAttribute((const void*)tw_run_kernel<true, TW_WG_LP, TW_NEAR_LP>,
-                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)c->lds_bytes));
-
-    else
-        HIPCHK(hipFuncSetAttribute((const void*)tw_run_kernel<false, TW_WG, TW_NEAR_CAP>,
-                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)c->lds_bytes));
+    {
+        // (the kernel and, for the lane-per-replica geometries, its fork-in-place variant)
+        auto lds = [&](const void* k) { return hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                                    (int)c->lds_bytes); };
+        if (c->geo == 3) {
+        } else if (lp) {
+            HIPCHK(lds((const void*)tw_run_kernel<true, TW_WG_LP, TW_NEAR_LP>));
+        } else if (c->geo == 1) {
+            HIPCHK(lds((const void*)tw_run_kernel<false, TW_WG_SPARSE, TW_NEAR_SPARSE>));
+        } else if (c->geo == 2) {
+            HIPCHK(lds((const void*)tw_run_kernel<false, TW_WG, TW_NEAR_CAP, TW_HALF_LANES>));
+            HIPCHK(lds((const void*)tw_run_kernel<false, TW_WG, TW_NEAR_CAP, TW_HALF_LANES, true, false, false, true>));
+        } else if (c->geo == 5) {
+            HIPCHK(lds((const void*)tw_run_kernel<false, TW_NARROW, TW_NEAR_CAP, TW_NARROW>));
+            HIPCHK(lds((const void*)tw_run_kernel<false, TW_NARROW, TW_NEAR_CAP, TW_NARROW, true, false, false, true>));
+        } else if (c->geo == 7) {
+            HIPCHK(lds((const void*)tw_run_kernel<false, TW_WG, TW_NEAR_COMPACT, 64, false>));
+            HIPCHK(lds((const void*)tw_run_kernel<false, TW_WG, TW_NEAR_COMPACT, 64, false, false, false, true>));
+        } else {
+            HIPCHK(lds((const void*)tw_run_kernel<false, TW_WG, TW_NEAR_CAP>));
+            HIPCHK(lds((const void*)tw_run_kernel<false, TW_WG, TW_NEAR_CAP, 64, true, false, false, true>));
+        }
+    }
     int e;
 #define ALLOC(p, n) if ((e = dalloc(c, &p, (n))) != TW_OK) { free_all(c); return e; }
     uint2* insns; int64_t* consts; uint32_t *lpc, *out_off, *ldst, *lrev, *ltab = nullptr;

@@ -275,7 +275,9 @@ __device__ void tw_jit_dispatch(LT& L, Th& th, uint32_t slot, ST& s, uint32_t fp
 
 // JIT: the event loop of a compiled scenario (jit.cpp) -- instruction decode
 // folded into per-pc code, the running thread's registers in VGPRs
-template <bool LP, int WG, int NC, bool RUNS = true, bool JIT = false>
+// IP: fork children run in place (fork_in_place) -- the variant the host
+// launches under the tie orders where a forked child is always the next pop
+template <bool LP, int WG, int NC, bool RUNS = true, bool IP = false, bool JIT = false>
 struct Lane {
     // the replica kernels keep monotone far runs (LDS bookkeeping + HBM FIFOs)
     // unless built without them (the compact geometry: far events go to the
@@ -2012,7 +2014,7 @@ struct Lane {
                 // child runs in place, its lanes running again.  Not in the
                 // sparse geometry, whose kernel would spill for it (there the
                 // child takes its queue round trip: the same order either way)
-                if constexpr (!LP && !PL) {
+                if constexpr (!LP && !PL && IP) {
                     if (fork_in_place(th, slot, s)) continue;
                 }
                 break;
@@ -2196,7 +2198,8 @@ __host__ __device__ constexpr size_t fixed_lds_bytes() {
 // RUNS = false (the compact geometry): no far runs, and built for two waves
 // per SIMD (<= 256 registers, half the LDS of a dense lane), so 1M-replica
 // batches keep two workgroups per CU
-template <bool LP, int WG, int NC, int TPW = 64, bool RUNS = true, bool GS = false, bool PRW = false, bool JIT = false>
+template <bool LP, int WG, int NC, int TPW = 64, bool RUNS = true, bool GS = false, bool PRW = false, bool IP = false,
+          bool JIT = false>
 __global__ void __launch_bounds__(WG * 64 / TPW)
     __attribute__((amdgpu_waves_per_eu(LP ? TW_LP_WAVES : !RUNS ? 2 : (WG * 64 / TPW + 255) / 256,
                                        LP ? TW_LP_WAVES : 2)))
@@ -2292,7 +2295,7 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
                     break;  // (the next block of the work list)
             }
 
-            Lane<LP, WG, NC, RUNS, JIT> L;
+            Lane<LP, WG, NC, RUNS, IP, JIT> L;
             L.c = c;
             L.r = r;
             L.nk = s_k + li;
@@ -2652,7 +2655,7 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
                 const uint4 ix4 = *L.rqp(RQ_IDX);
         #pragma unroll
                 for (int j = 0; j < TW_RUNS; ++j) {
-                    sc[(SC_RH0 + j) * SR] = Lane<LP, WG, NC, RUNS, JIT>::q_at(ix4, j);
+                    sc[(SC_RH0 + j) * SR] = Lane<LP, WG, NC, RUNS, IP, JIT>::q_at(ix4, j);
                     sc[(SC_RC0 + j) * SR] = L.rqp(RQ_TAIL + j)->w;
                 }
             }
