@@ -1875,6 +1875,14 @@ struct Lane {
                     n = 0;                       // TW_STEP_CAP counts per pop
                     tc = T_NONE;
                     if (now - nbase > (int64_t)0x7FFFFFFF) near_rebase(now);
+                    // the resumed instruction is END (a handler's last send, a
+                    // gossip node's last forward): the thread ends in this pass
+                    // instead of one more -- END's count, pc and exit as its pass
+                    if (pc < c.n_insns && (P[pc].x & 0xFFu) == TW_OP_END) {
+                        n = 1;
+                        pc = pc + 1;
+                        tc = T_EXIT;
+                    }
                 }
             }
         }

@@ -97,6 +97,8 @@ def main():
         scn = scenarios.token_ring(n_nodes=N, n_replicas=R, launch_duration=Ld, drop_log2=10)
         phases = [("startup<1s", 999_999), ("token<L", Ld - 1), ("teardown", (1 << 63) - 1)]
     eng = Engine(0).load(scn)
+    if os.environ.get("TW_PROBE_TIE"):  # e.g. forkfirst (bench.py's C3 order)
+        eng.set_tie_mode(os.environ["TW_PROBE_TIE"])
     if not hasattr(eng.lib, "tw_prof_read"):
         raise SystemExit("TW_LIB is not the diagnostic build (tw_prof_read missing)")
     read(eng)
