@@ -37,6 +37,9 @@ def test_library_loads_without_device():
     lib = load_library()
     assert b"gfx950" in lib.tw_version()
     assert lib.tw_strerror(-2) == b"no HIP device"
+    # every status the header declares has its own message
+    for name, val in re.findall(r"(TW_(?:OK|ERR_[A-Z_]+))\s*=\s*(-?\d+)", open(HEADER).read()):
+        assert lib.tw_strerror(int(val)) != b"unknown error", name
 
 
 def test_isa_mirror_in_sync():

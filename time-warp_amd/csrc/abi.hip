@@ -299,6 +299,7 @@ const char* tw_strerror(int code) {
     case TW_ERR_REPLICA: return "replica error";
     case TW_ERR_INCOMPLETE: return "relaunch cap reached before every replica stopped";
     case TW_ERR_COMM: return "RCCL error";
+    case TW_ERR_JIT: return "scenario compiler failed to build the kernel";
     default: return "unknown error";
     }
 }
