@@ -231,17 +231,17 @@ static void launch_run(tw_shard* c, hipStream_t st, int64_t t_end, uint64_t limi
         else
             hipLaunchKernelGGL((tw_run_kernel<LP, WG, NC, TPW, RUNS>), g, b, c->lds_bytes, st, c->d, t_end, limit,
                                budget);
-        return;
-    }
-    if constexpr (WG >= 64) {
-        if (ip) {
-            hipLaunchKernelGGL((tw_run_kernel<LP, WG, NC, TPW, RUNS, false, false, true>), dim3(blocks),
-                               dim3(WG * 64 / TPW), c->lds_bytes, st, c->d, t_end, limit, budget);
-            return;
+    } else {
+        if constexpr (WG >= 64) {
+            if (ip) {
+                hipLaunchKernelGGL((tw_run_kernel<LP, WG, NC, TPW, RUNS, false, false, true>), dim3(blocks),
+                                   dim3(WG * 64 / TPW), c->lds_bytes, st, c->d, t_end, limit, budget);
+                return;
+            }
         }
+        hipLaunchKernelGGL((tw_run_kernel<LP, WG, NC, TPW, RUNS>), dim3(blocks), dim3(WG * 64 / TPW), c->lds_bytes, st,
+                           c->d, t_end, limit, budget);
     }
-    hipLaunchKernelGGL((tw_run_kernel<LP, WG, NC, TPW, RUNS>), dim3(blocks), dim3(WG * 64 / TPW), c->lds_bytes, st,
-                       c->d, t_end, limit, budget);
 }
 
 namespace tw {

@@ -1934,9 +1934,6 @@ struct Lane {
                                                                                    : seq + 1u;
         bool ip = s.fin == T_SPAWN && status == TW_REP_RUNNING && d_ev < ev_room && seq + 1u < seq_top() &&
                   tidc != 0xFFFFFFFFu;
-        // (LP: a fork on the lane's own node -- not the deliverer a delivery
-        // record stands for, cdel bit 0; a cross-node fork never reaches here)
-        if constexpr (LP) ip = ip && !(cg(CW_CDEL) & 1u) && cg(CW_CNODE) == th.w1;
         if (!__builtin_amdgcn_ballot_w64(ip)) return false;
         if (far_dirty) far_min();
         bool has = near_n != 0;
@@ -1969,7 +1966,7 @@ struct Lane {
                 // the child's pop (TimedT.hs:241-247): counted, its resume term on its node
                 STAT(K_POP);
                 ++d_ev;
-                final_t = LP ? (now > final_t ? now : final_t) : now;
+                final_t = now;
                 if (ch.w1 != hnode) {
                     hash_flush();
                     hnode = ch.w1;
@@ -2025,10 +2022,7 @@ struct Lane {
                 // child runs in place, its lanes running again.  Not in the
                 // sparse geometry, whose kernel would spill for it (there the
                 // child takes its queue round trip: the same order either way)
-#ifndef TW_LP_IP
-#define TW_LP_IP 0  // (the LP kernels with fork_in_place: an A/B build, lib/libtimewarp_lpip1.so)
-#endif
-                if constexpr ((!LP && !PL && IP) || (LP && TW_LP_IP)) {
+                if constexpr (!LP && !PL && IP) {
                     if (fork_in_place(th, slot, s)) continue;
                 }
                 break;
