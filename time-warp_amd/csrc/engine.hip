@@ -607,7 +607,7 @@ static int load_common(tw_shard* c, const tw_scenario_desc* s, bool lp, uint32_t
     ALLOC(d.far, (size_t)d.Q * R);
     ALLOC(d.runs, (size_t)(d.Cr ? TW_RUNS * (size_t)d.Cr : 1) * R);
     if (c->geo == 3) d.wave_k = (uint32_t)wave_near_k(d.R);
-    ALLOC(d.near_spill, (size_t)(c->geo == 1 ? TW_NEAR_SPARSE : c->geo == 3 ? wave_spill_entries(d.wave_k) : TW_NEAR_CAP) * R);
+    ALLOC(d.near_spill, (size_t)(lp ? TW_NEAR_LP : c->geo == 1 ? TW_NEAR_SPARSE : c->geo == 3 ? wave_spill_entries(d.wave_k) : TW_NEAR_CAP) * R);
     ALLOC(d.dummy, (size_t)TW_DUMMY_REC + R);
     ALLOC(d.nvars, (size_t)d.N * 4 * R);
     ALLOC(d.hash, (size_t)d.N * R);

@@ -194,9 +194,12 @@ def token_ring(n_nodes: int = 16, n_replicas: int = 1, launch_duration: int = se
                   # launchNode's threads (worker, server, killer, the token's
                   # deliverer and handler), the observer its server, checker, killer
                   # and note deliveries; main's spawn pairs are a tick's records.
-                  # The observer's 0 µs links make it a phase-1 node.
+                  # The observer's 0 µs links make it a phase-1 node.  At most
+                  # six threads and their events per node: 8 slots and 8 far
+                  # entries behind the 8 on-chip ones (~1.7 KB per lane, so
+                  # 32,768 replicas x 4,098 nodes fit one GPU's HBM)
                   lp_inbox_cap=np.array([4] * N + [8, 1], np.uint32),
-                  lp_max_slots=12, lp_queue_capacity=16,
+                  lp_max_slots=8, lp_queue_capacity=8,
                   lp_outbox_cap=min(1 << 27, (2 * (N + 2) + 64) * n_replicas)),
         live_kind=live_kind, live_lo=live_lo, live_hi=live_hi,
     )

@@ -66,6 +66,10 @@ for s in "$@"; do
     stats_c5_lpb) step stats_c5_lpb 400 env TW_LIB=$PWD/time-warp_amd/lib/libtimewarp_stats.so python -u tools/stats_probe.py lpb_hotspot 4096 256 ;;
     prof_c5) step prof_c5 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_c5 -o run -- python3 bench.py --config hotspot --steps 1 --warmup 0 --no-cpu-baseline ;;
     prof_c3_8k_lpb) step prof_c3_8k_lpb 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_c3_8k_lpb -o run -- python3 bench.py --replicas 8192 --geometry lpb --steps 1 --warmup 0 --no-cpu-baseline ;;
+    benchq_c3_32k) step benchq_c3_32k 300 python bench.py --replicas 32768 --steps 2 --warmup 1 --no-cpu-baseline ;;
+    benchq_c3_16k) step benchq_c3_16k 300 python bench.py --replicas 16384 --steps 2 --warmup 1 --no-cpu-baseline ;;
+    benchq_c3_32k_lpb) step benchq_c3_32k_lpb 400 python bench.py --replicas 32768 --geometry lpb --steps 1 --warmup 1 --no-cpu-baseline ;;
+    benchq_c3_16k_lpb) step benchq_c3_16k_lpb 300 python bench.py --replicas 16384 --geometry lpb --steps 2 --warmup 1 --no-cpu-baseline ;;
     benchq_c3_8k_lpb) step benchq_c3_8k_lpb 300 python bench.py --replicas 8192 --geometry lpb --steps 2 --warmup 1 --no-cpu-baseline ;;
     pmct_c5) bash tools/pmc_traffic.sh gpurun_out/pmct_c5$SFX --config hotspot > gpurun_out/pmct_c5$SFX.log 2>&1; rc=$?; echo "pmct_c5=$rc"; [ $rc -eq 0 ] || exit $rc ;;
     pmct_c2) bash tools/pmc_traffic.sh gpurun_out/pmct_c2$SFX --config ping_pong > gpurun_out/pmct_c2$SFX.log 2>&1; rc=$?; echo "pmct_c2=$rc"; [ $rc -eq 0 ] || exit $rc ;;
