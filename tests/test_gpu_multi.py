@@ -138,6 +138,34 @@ def test_one_rank_rccl_lp_loop(engine_mod, oracle_mod):
             assert lp.done == 1 and lp.err == 0
 
 
+@pytest.mark.parametrize("mode", ["copy", "rccl"])
+def test_lp_run_local_failure_agreed(engine_mod, oracle_mod, monkeypatch, mode):
+    """A failure local to one shard (injected: TW_TEST_FAIL_TICK=shard:tick
+    fails that shard's launches at that tick, as a HIP error would) does not
+    strand the others in the exchange: every shard keeps exchanging and
+    reducing until the batch's agreement, and tw_lp_run returns the agreed
+    code (TW_ERR_STATE) on all of them.  The next call sets the loop up again
+    and runs the scenario to the oracle's result."""
+    scn = scenarios.gossip(3000, drop_log2=4, seed=5)
+    L = int(scn.meta["lookahead_us"])
+    s = engine_mod.lp_scenario(scn)
+    kw = dict(devices=[0, 0]) if mode == "copy" else dict(comm=(1, 0, engine_mod.comm_id()))
+    with engine_mod.LPEngine(s, 0, scn.n_nodes, L, **kw) as e:
+        e.reset()
+        monkeypatch.setenv("TW_TEST_FAIL_TICK", "1:5" if mode == "copy" else "0:5")
+        with pytest.raises(engine_mod.EngineError, match=r"tw_lp_run failed: -5 "):
+            e.run_lp()
+        monkeypatch.delenv("TW_TEST_FAIL_TICK")
+        e.reset()
+        lp = e.run_lp()
+        agg, hashes = e.lp_results()
+    o = oracle_mod.run(scn, trace_cap=0)
+    for f in ("final_t", "events", "delivered", "dropped", "undeliverable", "status", "threads"):
+        assert int(agg[f]) == int(o.result[f]), (mode, f, int(agg[f]), o.result[f])
+    assert np.array_equal(hashes, o.hashes)
+    assert lp.done == 1 and lp.err == 0
+
+
 def test_multi_shard_refuses_caller_loop(engine_mod):
     """The caller-driven window primitives speak for one device only."""
     scn = scenarios.gossip(256, seed=1)

@@ -877,14 +877,25 @@ int tw_lp_run(tw_ctx* c, uint64_t max_ticks, tw_lp_state* out) {
     }
     const size_t stride_b = 32ull * ((size_t)x[0].stride + 1);
     std::vector<tw_lp_state> st(n);
+    // testing hook: TW_TEST_FAIL_TICK=shard:tick makes that local shard's
+    // launches at that tick fail (TW_ERR_STATE), as a HIP or launch error
+    // would -- the other shards and ranks must still leave together
+    long fail_sh = -1, fail_tk = -1;
+    if (const char* f = getenv("TW_TEST_FAIL_TICK")) {
+        char* e = nullptr;
+        fail_sh = strtol(f, &e, 10);
+        fail_tk = (e && *e == ':') ? strtol(e + 1, nullptr, 10) : -1;
+    }
     for (uint64_t done_ticks = 0; done_ticks < max_ticks;) {
         const uint64_t batch = std::min<uint64_t>(max_ticks - done_ticks, 16);
         const size_t bytes = 32ull * ((size_t)cap_eff + 1);
         for (uint64_t k = 0; k < batch; ++k) {
             // a shard that failed stops launching but keeps taking part in the
             // exchange and the reduction until the batch's agreement
-            for (size_t i = 0; i < n; ++i)
+            for (size_t i = 0; i < n; ++i) {
                 if (!lrc[i]) lrc[i] = sh_lp_tick(c->sh[i]);
+                if (!lrc[i] && (long)i == fail_sh && (long)(done_ticks + k) == fail_tk) lrc[i] = TW_ERR_STATE;
+            }
             // record blocks: block g of rank r's send -> block r of rank g's recv
             if (c->tp == TP_RCCL) {
                 NCCLCHK(ncclGroupStart());

@@ -1322,6 +1322,10 @@ int sh_lp_loop_begin(tw_shard* c) {
     c->d.wid = 0;
     hipLaunchKernelGGL(tw_lp_begin, dim3(1), dim3(1), 0, c->stream, c->dwin(), c->d.lookahead);
     HIPCHK(hipGetLastError());
+    // the record blocks' counts (tw_lp_ctl clears them every tick; a loop that
+    // stopped inside a tick -- a failure on some rank -- may have left some)
+    for (uint32_t g = 0; c->ex_send && g < c->ex_world; ++g)
+        HIPCHK(hipMemsetAsync(c->ex_send + (size_t)g * (c->ex_cap + 1) * 2, 0, sizeof(uint4), c->stream));
     if (c->d.rw) {  // every replica's first window starts at 0; minima empty
         const size_t nrep = (size_t)1 << c->d.rep_lg;
         HIPCHK(hipMemsetAsync(c->d.rw + RW_T * nrep, 0, 8 * nrep, c->stream));
