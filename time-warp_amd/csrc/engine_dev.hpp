@@ -2644,21 +2644,31 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
             sc[SC_PENDING_MAIN * SR] = pending_main;
             if (!LP && L.status == TW_REP_RUNNING && L.live == 0) L.status = TW_REP_DONE;
 
-            sc[SC_NOW * SR] = (uint64_t)L.now; sc[SC_FINAL_T * SR] = (uint64_t)L.final_t;
+            // (the compact geometry's replica lanes: curTime after the last pop is
+            // the clock -- every pop sets both --, and every thread this launch
+            // created took a thread id, so neither count is carried through the
+            // loop in a register; neither is the launch's starting event count, in
+            // any geometry but those with far runs.  Measured: C2 +3 %, the LP
+            // kernels without scratch; the run geometries' allocation lost 1.4 % on
+            // C3 with it, so they keep the registers)
+            constexpr bool KEEP = !LP && RUNS;
+            const uint64_t threads_add = (LP || KEEP) ? (uint64_t)L.d_th : (uint64_t)(L.tidc - (uint32_t)sc[SC_TIDC * SR]);
+            sc[SC_NOW * SR] = (uint64_t)L.now; sc[SC_FINAL_T * SR] = (uint64_t)((LP || KEEP) ? L.final_t : L.now);
             sc[SC_SEQ * SR] = L.seq; sc[SC_TIDC * SR] = L.tidc; sc[SC_LIVE * SR] = L.live;
             sc[SC_NEAR_N * SR] = L.near_n; sc[SC_FAR_N * SR] = L.far_n;
             sc[SC_STATUS * SR] = L.status; sc[SC_MAIN_EXC * SR] = L.cg(CW_MAINEXC);
             sc[SC_FREE_N * SR] = L.free_n; sc[SC_FTOP * SR] = L.ftop; sc[SC_BUMP * SR] = L.bump;
             sc[SC_TMO_CTR * SR] = L.cg(CW_TMO);
             sc[SC_TRACE_N * SR] = L.cg(CW_TRN);
-            sc[SC_EVENTS * SR] = events0 + L.d_ev;
+            if constexpr (KEEP) sc[SC_EVENTS * SR] = events0 + L.d_ev;
+            else sc[SC_EVENTS * SR] += L.d_ev;
             if (LP) {
                 sc[SC_DUE_H * SR] = L.dg(DW_HN) & 0xFFFFu;
                 if (L.dg(DW_IB) >> 31)  // sent records straight into inboxes (Lane::emit)
                     min_hot((uint64_t GAS*)(PRW ? rw_at(c, RW_WIN, r) : gp(c.win) + WN_REC_MIN), (uint64_t)(te + 1));
             }
             sc[SC_DELIVERED * SR] += L.cg(CW_DL); sc[SC_DROPPED * SR] += L.cg(CW_DR);
-            sc[SC_UNDELIV * SR] += L.cg(CW_UD); sc[SC_THREADS * SR] += L.d_th;
+            sc[SC_UNDELIV * SR] += L.cg(CW_UD); sc[SC_THREADS * SR] += threads_add;
             if (HR && c.Cr) {
                 const uint4 ix4 = *L.rqp(RQ_IDX);
         #pragma unroll
