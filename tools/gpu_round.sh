@@ -63,6 +63,8 @@ for s in "$@"; do
     calib) mkdir -p gpurun_out/calib && timeout -k 10 120 ./tools/ubench/pmc_calib > gpurun_out/calib/run.log 2>&1 && timeout -s KILL 60 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d gpurun_out/calib/f -o run -- ./tools/ubench/pmc_calib > gpurun_out/calib/f.log 2>&1 && timeout -s KILL 60 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d gpurun_out/calib/w -o run -- ./tools/ubench/pmc_calib > gpurun_out/calib/w.log 2>&1 && python3 tools/pmc_calib.py gpurun_out/calib/pmc_calibration.json gpurun_out/calib/run.log gpurun_out/calib/f gpurun_out/calib/w > gpurun_out/calib/summary.log 2>&1; rc=$?; echo "calib=$rc"; [ $rc -eq 0 ] || exit $rc ;;
     pmc) bash tools/pmc.sh gpurun_out/pmc$SFX > gpurun_out/pmc$SFX.log 2>&1; rc=$?; echo "pmc=$rc"; [ $rc -eq 0 ] || exit $rc ;;
     multi_tests) step multi_tests 400 python -u -m pytest tests/test_gpu_multi.py -x -v --timeout 200 --timeout-method thread ;;
+    fusion_tests) step fusion_tests 400 python -u -m pytest tests/test_send_fusion.py -x -q -m gpu --timeout 200 --timeout-method thread ;;
+    throw_tests) step throw_tests 300 python -u -m pytest tests/test_gpu_throw_sequences.py -x -q -m gpu --timeout 120 --timeout-method thread ;;
     lpb_tests) step lpb_tests 500 python -u -m pytest tests/test_gpu_lpb.py -x -v --timeout 200 --timeout-method thread ;;
     stats_c3_lpb) step stats_c3_lpb 400 env TW_LIB=$PWD/time-warp_amd/lib/libtimewarp_stats.so python -u tools/stats_probe.py lpb_token 8192 ;;
     stats_c5_lpb) step stats_c5_lpb 400 env TW_LIB=$PWD/time-warp_amd/lib/libtimewarp_stats.so python -u tools/stats_probe.py lpb_hotspot 4096 256 ;;
