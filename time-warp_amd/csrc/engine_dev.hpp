@@ -935,7 +935,21 @@ struct Lane {
         const uint4 GAS* p = hrec(slot);
         unpack(th, p[0], p[c.RQ], p[2 * c.RQ], p[3 * c.RQ]);
     }
-    __device__ __forceinline__ void peek_rec(uint32_t slot, Th& th) { hbm_load(slot, th); }
+    // a record's header and frames / exception quads (a throwTo victim: its
+    // registers are neither read nor written, so quads 2-3 stay in HBM)
+    __device__ __forceinline__ void peek_q01(uint32_t slot, Th& th) const {
+        const uint4 GAS* p = hrec(slot);
+        const uint4 a = p[0], b = p[c.RQ];
+        th.w0 = a.x; th.w1 = a.y; th.w2 = a.z; th.w3 = a.w;
+        th.f0 = b.x; th.f1 = b.y; th.xl = b.z; th.xh = b.w;
+    }
+    __device__ __forceinline__ void put_q01(uint32_t slot, const Th& th) {
+        if (slot == pf_slot) pf_slot = 0xFFFFFFFFu;
+        STAT(K_PUT_HBM);
+        uint4 GAS* p = hrec(slot);
+        p[0] = make_uint4(th.w0, th.w1, th.w2, th.w3);
+        p[c.RQ] = make_uint4(th.f0, th.f1, th.xl, th.xh);
+    }
     // mode ST_THROUGH: the full record; ST_DEAD: only the header quad (the tid
     // that invalidates stale refs)
     __device__ __forceinline__ void put_hdr(uint32_t slot, const Th& th) {
@@ -1232,8 +1246,8 @@ struct Lane {
             return;
         }
         Th t;
-        peek_rec(ts, t);
-        // the whole record drained here, on every path out (a quad left in
+        peek_q01(ts, t);
+        // the loads drained here, on every path out (a quad left in
         // flight on the early return made the compiler wait at the top of
         // every later interpreter pass)
         tw_vm_drain();
@@ -1254,7 +1268,7 @@ struct Lane {
             th_set_exc(t, code);
             th_set_xval(t, val);
         }
-        put_rec(ts, t);
+        put_q01(ts, t);
     }
 
     // Thread ends (END or uncaught exception): listener release, ref
