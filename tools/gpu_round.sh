@@ -70,6 +70,7 @@ for s in "$@"; do
     stats_c5_lpb) step stats_c5_lpb 400 env TW_LIB=$PWD/time-warp_amd/lib/libtimewarp_stats.so python -u tools/stats_probe.py lpb_hotspot 4096 256 ;;
     prof_c5) step prof_c5 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_c5 -o run -- python3 bench.py --config hotspot --steps 1 --warmup 0 --no-cpu-baseline ;;
     prof_c3_8k_lpb) step prof_c3_8k_lpb 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_c3_8k_lpb -o run -- python3 bench.py --replicas 8192 --geometry lpb --steps 1 --warmup 0 --no-cpu-baseline ;;
+    bench_c3_8k) step bench_c3_8k 400 python bench.py --replicas 8192 ;;
     benchq_c3_32k) step benchq_c3_32k 300 python bench.py --replicas 32768 --steps 2 --warmup 1 --no-cpu-baseline ;;
     benchq_c3_16k) step benchq_c3_16k 300 python bench.py --replicas 16384 --steps 2 --warmup 1 --no-cpu-baseline ;;
     benchq_c3_32k_lpb) step benchq_c3_32k_lpb 400 python bench.py --replicas 32768 --geometry lpb --steps 1 --warmup 1 --no-cpu-baseline ;;
