@@ -128,8 +128,6 @@ def engine_sha() -> str:
     h = hashlib.sha256()
     d = os.path.join(ROOT, "time-warp_amd", "csrc")
     for f in sorted(os.listdir(d)):
-        if f == "jit_src.inc":  # (generated from the others at build time)
-            continue
         h.update(f.encode())
         h.update(open(os.path.join(d, f), "rb").read())
     return h.hexdigest()[:16]
@@ -177,7 +175,6 @@ def workload_key(args) -> str:
     return (f"{args.config}:nodes={args.nodes}:replicas={args.replicas}:weak={int(args.weak)}:"
             f"dur={args.duration_s}:drop={args.drop_log2}:rt={args.round_trips}:msgs={args.msg_num}"
             + (f":geo={args.geometry}" if getattr(args, "geometry", None) else "")
-            + (":jit=1" if getattr(args, "jit", 0) else "")
             + (f":tie={args.tie}" if getattr(args, "tie", "auto") != "auto" else ""))
 
 
@@ -312,9 +309,6 @@ def main():
                          "becomes the minimum); the replica kernels then run the child in place.  auto: forkfirst "
                          "for the token ring on the lane-per-replica geometries (C3 is tie-insensitive: its results "
                          "equal the canonical order's, checked by parity_sample), else fifo")
-    ap.add_argument("--jit", type=int, default=0, choices=[0, 1],
-                    help="1: the scenario compiler (tw_set_jit) -- the program image compiled into the event "
-                         "kernel at load (outside the timed region); 0: the interpreter")
     ap.add_argument("--workload-key", action="store_true",
                     help="print the workload key and engine digest (tools/pmc.sh provenance) and exit")
     args = ap.parse_args()
@@ -387,8 +381,6 @@ def main():
     comm = twd.library_comm(world, rank) if dist_on else None
     eng = Engine(local, comm=comm)
     t_load = time.perf_counter()
-    if args.jit:
-        eng.set_jit(True)
     eng.load(scn, geometry=args.geometry)
     setup["load_s"] = time.perf_counter() - t_load
     tie = args.tie
@@ -397,10 +389,6 @@ def main():
     if tie != "fifo":
         eng.set_tie_mode(tie)
     setup["tie_order"] = tie
-    jit_on, jit_ms = eng.jit_status()
-    if args.jit and not jit_on:
-        raise SystemExit("--jit 1: the scenario compiler did not produce the kernel")
-    setup["jit"] = {"on": jit_on, "compile_ms": jit_ms}
 
     for _ in range(args.warmup):
         eng.reset()

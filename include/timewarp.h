@@ -30,13 +30,16 @@
 extern "C" {
 #endif
 
-/* ABI 3: tw_create(devices, ndev) (was tw_create(device)); the caller-owned
- * reduction buffer of tw_lp_exchange_setup holds TW_LP_RED_WORDS int64 words
- * (was 2).  The scenario descriptor's layout is ABI 2's, but tw_load refuses
- * a descriptor stamped with another version, so a caller built against an
- * older header fails there (TW_ERR_INVALID) instead of handing a red buffer
- * of the old size to the device loop. */
-#define TW_ABI_VERSION 3u
+/* ABI 4: the scenario compiler of ABI 3 (tw_set_jit / tw_jit_status /
+ * tw_jit_precompile and TW_ERR_JIT) is gone -- measured slower than the
+ * interpreter on every configuration.  ABI 3: tw_create(devices,
+ * ndev) (was tw_create(device)); the caller-owned reduction buffer of
+ * tw_lp_exchange_setup holds TW_LP_RED_WORDS int64 words (was 2).  The scenario
+ * descriptor's layout is ABI 2's, but tw_load refuses a descriptor stamped with
+ * another version, so a caller built against an older header fails there
+ * (TW_ERR_INVALID) instead of handing a red buffer of the old size to the
+ * device loop. */
+#define TW_ABI_VERSION 4u
 #define TW_LP_RED_WORDS 4
 /* Async exception payloads (throwTo's value, `SomeException` in the
  * reference's asyncExceptions map, TimedT.hs:113,359) are carried as int64. */
@@ -52,8 +55,7 @@ typedef enum tw_status {
     TW_ERR_REPLICA = -6,      /* one or more replicas ended in error status */
     TW_ERR_INCOMPLETE = -7,   /* tw_run's relaunch cap was reached before every
                                  replica stopped (quiescence / t_end / cap)  */
-    TW_ERR_COMM = -8,         /* RCCL error (communicator setup or a collective) */
-    TW_ERR_JIT = -9           /* the scenario compiler (tw_set_jit) failed to build the kernel */
+    TW_ERR_COMM = -8          /* RCCL error (communicator setup or a collective) */
 } tw_status;
 
 /* per-replica status (tw_replica_result.status) */
@@ -392,26 +394,6 @@ int tw_tie_audit(tw_ctx* ctx, int64_t t_end_us, uint64_t max_events, uint32_t pr
  * wave geometry (TW_ERR_INVALID otherwise) and a queue_capacity covering the
  * replica's pending events. */
 int tw_set_tie_mode(tw_ctx* ctx, uint32_t mode);
-
-/* The scenario compiler: on = 1 makes every later tw_load / tw_lp_load /
- * tw_lpb_load (and, when a scenario is loaded, this call itself) compile the
- * loaded program image into the event kernel -- each instruction becomes
- * device code with its operands as constants, the running thread's registers
- * stay in VGPRs -- with hiprtc, in process, for gfx950 (a few seconds per
- * image; cached per process, and under $TW_JIT_CACHE when set).  Results are
- * bit-identical to the interpreter's (on = 0, the default unless TW_JIT=1 is
- * in the environment at tw_create).  The wave geometry has no compiled form
- * (TW_ERR_INVALID); a failed compile is TW_ERR_JIT and leaves the context
- * interpreting. */
-int tw_set_jit(tw_ctx* ctx, uint32_t on);
-/* on: 1 when every shard runs a compiled kernel; compile_ms: the last
- * compiles' time summed over shards (0 after a cache hit). */
-int tw_jit_status(tw_ctx* ctx, uint32_t* on, double* compile_ms);
-/* The scenario compiler alone, no device needed: compile desc's program image
- * for a geometry (TW_GEO_DENSE/SPARSE/HALF/NARROW/COMPACT, or TW_GEO_LP/LPB for
- * the logical-process kernels) into the caches a later tw_load uses.  Needs
- * only desc->insns / n_insns. */
-int tw_jit_precompile(const tw_scenario_desc* desc, int geometry, double* compile_ms);
 
 /* Testing hook: from the next tw_reset on, start every replica's insertion
  * counter at seq0 and its thread counter at tid0 (>= 1; main is tid 0), so the

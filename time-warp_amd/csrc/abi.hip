@@ -168,17 +168,16 @@ int64_t sev_of(int rc) {
     case TW_ERR_INCOMPLETE: return 2;
     case TW_ERR_INVALID: return 3;
     case TW_ERR_STATE: return 4;
-    case TW_ERR_JIT: return 5;
-    case TW_ERR_COMM: return 6;
-    case TW_ERR_OOM: return 7;
-    case TW_ERR_HIP: return 8;
-    default: return 9;  // TW_ERR_NO_DEVICE and anything unknown
+    case TW_ERR_COMM: return 5;
+    case TW_ERR_OOM: return 6;
+    case TW_ERR_HIP: return 7;
+    default: return 8;  // TW_ERR_NO_DEVICE and anything unknown
     }
 }
 int rc_of_sev(int64_t s) {
     static const int rcs[] = {TW_OK, TW_ERR_REPLICA, TW_ERR_INCOMPLETE, TW_ERR_INVALID, TW_ERR_STATE,
-                              TW_ERR_JIT, TW_ERR_COMM, TW_ERR_OOM, TW_ERR_HIP, TW_ERR_NO_DEVICE};
-    return s >= 0 && s <= 9 ? rcs[s] : TW_ERR_HIP;
+                              TW_ERR_COMM, TW_ERR_OOM, TW_ERR_HIP, TW_ERR_NO_DEVICE};
+    return s >= 0 && s <= 8 ? rcs[s] : TW_ERR_HIP;
 }
 
 // Every shard of every rank learns the worst of the shards' local codes (one
@@ -276,7 +275,7 @@ bool single(tw_ctx* c) { return c->sh.size() == 1; }
 
 }  // namespace
 
-static_assert(TW_ABI_VERSION == 3u, "tw_version names ABI 3");
+static_assert(TW_ABI_VERSION == 4u, "tw_version names ABI 4");
 static_assert(RD_N == TW_LP_RED_WORDS, "the caller-owned reduction buffer (timewarp.h)");
 
 extern "C" {
@@ -284,8 +283,8 @@ extern "C" {
 const char* tw_version(void) {
     return "timewarp-mi355x 0.6 (gfx950; lane-per-replica dense/narrow/sparse kernels, wavefront-per-replica kernel, "
            "node-partitioned LP kernel with device-driven windows, batched logical processes (tw_lpb_load); "
-           "multi-GPU contexts with library-owned RCCL communicators; scenario compiler (tw_set_jit); "
-           "ABI 3)";
+           "multi-GPU contexts with library-owned RCCL communicators; "
+           "ABI 4)";
 }
 
 const char* tw_strerror(int code) {
@@ -299,7 +298,6 @@ const char* tw_strerror(int code) {
     case TW_ERR_REPLICA: return "replica error";
     case TW_ERR_INCOMPLETE: return "relaunch cap reached before every replica stopped";
     case TW_ERR_COMM: return "RCCL error";
-    case TW_ERR_JIT: return "scenario compiler failed to build the kernel";
     default: return "unknown error";
     }
 }
@@ -566,36 +564,6 @@ int tw_set_tie_mode(tw_ctx* c, uint32_t mode) {
         if (rc) return rc;
     }
     return TW_OK;
-}
-
-int tw_set_jit(tw_ctx* c, uint32_t on) {
-    if (!c) return TW_ERR_INVALID;
-    for (tw_shard* s : c->sh) {
-        int rc = sh_set_jit(s, on);
-        if (rc) return rc;
-    }
-    return TW_OK;
-}
-
-int tw_jit_status(tw_ctx* c, uint32_t* on, double* compile_ms) {
-    if (!c) return TW_ERR_INVALID;
-    uint32_t all = 1;
-    double ms = 0.0;
-    for (tw_shard* s : c->sh) {
-        uint32_t o = 0;
-        double m = 0.0;
-        int rc = sh_jit_status(s, &o, &m);
-        if (rc) return rc;
-        all &= o;
-        ms += m;
-    }
-    if (on) *on = all;
-    if (compile_ms) *compile_ms = ms;
-    return TW_OK;
-}
-
-int tw_jit_precompile(const tw_scenario_desc* desc, int geometry, double* compile_ms) {
-    return sh_jit_precompile(desc, geometry, compile_ms);
 }
 
 int tw_geometry(tw_ctx* c) {

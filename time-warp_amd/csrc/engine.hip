@@ -42,7 +42,6 @@
 #include "shard.hpp"
 
 #include "engine_dev.hpp"
-#include "jit.hpp"
 
 // ======================================================================= C ABI
 struct tw_shard {
@@ -104,14 +103,6 @@ struct tw_shard {
     // for tests: a small budget makes windows take several ticks)
     uint32_t lp_budget = 1u << 14;
     uint32_t lp_grid = TW_LP_GRID;  // LP launches above this many workgroups walk the list (TW_LP_GRID env)
-    // scenario compiler (tw_set_jit, jit.cpp): the loaded program image compiled
-    // into the event kernel; jit_fn[v] is launch variant v (LP: gs * 2 + prw)
-    bool jit_on = false;
-    bool jit_missing = false;         // a launch found no compiled variant (sh_run fails)
-    std::vector<tw_insn> h_insns;
-    hipModule_t jit_mod = nullptr;
-    hipFunction_t jit_fn[4] = {};
-    double jit_ms = 0.0;              // the last compile (0: cache hit)
     Dev dwin() const {                // the descriptor the device loop's kernels get
         Dev x = d;
         x.win = win_buf;
@@ -172,9 +163,6 @@ void free_all(tw_shard* c) {
     if (c->tick_graph) (void)hipGraphExecDestroy(c->tick_graph);
     c->tick_graph = nullptr;
     c->tick_gkey.clear();
-    if (c->jit_mod) (void)hipModuleUnload(c->jit_mod);
-    c->jit_mod = nullptr;
-    for (hipFunction_t& f : c->jit_fn) f = nullptr;
     c->loaded = false;
 }
 
@@ -196,24 +184,6 @@ template <bool LP, int WG, int NC, int TPW = 64, bool RUNS = true>
 static void launch_run(tw_shard* c, hipStream_t st, int64_t t_end, uint64_t limit, uint32_t budget) {
     const uint32_t blocks = (uint32_t)((c->d.R + WG - 1) / WG);
     const bool ip = !LP && WG >= 64 && use_ip(c);
-    if (c->jit_on) {
-        // the compiled scenario (jit.cpp): same kernel template, same launch shape
-        const bool gs = LP && blocks > c->lp_grid, prw = LP && c->d.rw && c->d.win;
-        const hipFunction_t f = c->jit_fn[(gs ? 2 : 0) + (prw ? 1 : 0) + (ip ? 1 : 0)];
-        if (!f) {
-            c->jit_missing = true;
-            return;
-        }
-        Dev dv = c->d;
-        int64_t te = t_end;
-        uint64_t lim = limit;
-        uint32_t bud = budget;
-        void* args[] = {&dv, &te, &lim, &bud};
-        if (hipModuleLaunchKernel(f, gs ? c->lp_grid : blocks, 1, 1, WG * 64 / TPW, 1, 1, (unsigned)c->lds_bytes, st,
-                                  args, nullptr) != hipSuccess)
-            c->jit_missing = true;
-        return;
-    }
     if constexpr (LP) {
         // many lanes, few listed: the work list walked grid-stride (GS); the
         // batched device loop's per-replica windows (PRW)
@@ -246,114 +216,6 @@ static void launch_run(tw_shard* c, hipStream_t st, int64_t t_end, uint64_t limi
 
 namespace tw {
 
-// The library's own configuration of the event kernel, handed to the scenario
-// compiler so both builds of tw_run_kernel agree
-static std::vector<std::string> jit_defs() {
-    std::vector<std::string> d;
-#ifdef TW_STATS
-    d.push_back("-DTW_STATS=1");
-#endif
-    auto def = [&](const char* n, long v) { d.push_back(std::string("-D") + n + "=" + std::to_string(v)); };
-    def("TW_DIRTY_TAIL", TW_DIRTY_TAIL);
-    def("TW_NARROW", TW_NARROW);
-    def("TW_LP_WAVES", TW_LP_WAVES);
-    def("TW_LP_PL", TW_LP_PL);
-    def("TW_CW_REGS", TW_CW_REGS);
-    def("TW_DMA_BUILTIN", TW_DMA_BUILTIN);
-    def("TW_LP_NB", TW_LP_NB);
-    def("TW_RUNS", TW_RUNS);
-    return d;
-}
-
-static void jit_inst(bool lp, int geo, std::vector<std::string>& inst, std::vector<int>& slot);
-
-// Compile the loaded image into the event kernel of the shard's geometry
-// (every launch variant it can take) and load it on the shard's device.
-static int jit_build(tw_shard* c) {
-    if (c->jit_mod) (void)hipModuleUnload(c->jit_mod);
-    c->jit_mod = nullptr;
-    for (hipFunction_t& f : c->jit_fn) f = nullptr;
-    c->jit_missing = false;
-    if (!c->jit_on || !c->loaded) return TW_OK;
-    if (!c->lp && c->geo == 3) return TW_ERR_INVALID;  // the wave kernel has no compiled form
-    std::vector<std::string> inst;
-    std::vector<int> slot;
-    jit_inst(c->lp, c->geo, inst, slot);
-    std::string code;
-    std::vector<std::string> names;
-    int rc = jit_compile(c->h_insns.data(), (uint32_t)c->h_insns.size(), inst, jit_defs(), &code, &names, &c->jit_ms);
-    if (rc != TW_OK) return rc;
-    HIPCHK(hipSetDevice(c->device));
-    HIPCHK(hipModuleLoadData(&c->jit_mod, code.data()));
-    for (size_t i = 0; i < names.size(); ++i) {
-        hipFunction_t f = nullptr;
-        HIPCHK(hipModuleGetFunction(&f, c->jit_mod, names[i].c_str()));
-        c->jit_fn[slot[i]] = f;
-    }
-    return TW_OK;
-}
-
-// The tw_run_kernel instantiations (template arguments but the last) of a
-// geometry and their launch-variant slots (LP: gs * 2 + prw)
-static void jit_inst(bool lp, int geo, std::vector<std::string>& inst, std::vector<int>& slot) {
-    char b[160];
-    if (lp) {
-        for (int v = 0; v < 4; ++v) {
-            snprintf(b, sizeof b, "true, %d, %d, 64, true, %s, %s, false", TW_WG_LP, TW_NEAR_LP,
-                     (v & 2) ? "true" : "false", (v & 1) ? "true" : "false");
-            inst.push_back(b);
-            slot.push_back(v);
-        }
-    } else {
-        int wg = TW_WG, nc = TW_NEAR_CAP, tpw = 64;
-        bool runs = true;
-        if (geo == 1) { wg = TW_WG_SPARSE; nc = TW_NEAR_SPARSE; }
-        else if (geo == 2) tpw = TW_HALF_LANES;
-        else if (geo == 5) { wg = TW_NARROW; tpw = TW_NARROW; }
-        else if (geo == 7) { nc = TW_NEAR_COMPACT; runs = false; }
-        for (int ip = 0; ip < (geo == 1 ? 1 : 2); ++ip) {  // (fork-in-place variant in slot 1; not sparse)
-            snprintf(b, sizeof b, "false, %d, %d, %d, %s, false, false, %s", wg, nc, tpw, runs ? "true" : "false",
-                     ip ? "true" : "false");
-            inst.push_back(b);
-            slot.push_back(ip);
-        }
-    }
-}
-
-// tw_jit_precompile: the compile alone (no device needed), into the caches
-int sh_jit_precompile(const tw_scenario_desc* s, int geometry, double* compile_ms) {
-    if (!s || !s->insns || s->n_insns == 0) return TW_ERR_INVALID;
-    const bool lp = geometry == TW_GEO_LP || geometry == TW_GEO_LPB;
-    if (!lp && geometry != TW_GEO_DENSE && geometry != TW_GEO_SPARSE && geometry != TW_GEO_HALF &&
-        geometry != TW_GEO_NARROW && geometry != TW_GEO_COMPACT)
-        return TW_ERR_INVALID;
-    std::vector<std::string> inst;
-    std::vector<int> slot;
-    jit_inst(lp, geometry, inst, slot);
-    std::string code;
-    std::vector<std::string> names;
-    double ms = 0.0;
-    const int rc = jit_compile(s->insns, s->n_insns, inst, jit_defs(), &code, &names, &ms);
-    if (compile_ms) *compile_ms = ms;
-    return rc;
-}
-
-int sh_set_jit(tw_shard* c, uint32_t on) {
-    if (!c || on > 1) return TW_ERR_INVALID;
-    c->jit_on = on != 0;
-    if (!c->loaded) return TW_OK;  // (compiled by the next load)
-    const int rc = jit_build(c);
-    if (rc != TW_OK) c->jit_on = false;
-    return rc;
-}
-
-int sh_jit_status(tw_shard* c, uint32_t* on, double* compile_ms) {
-    if (!c) return TW_ERR_INVALID;
-    if (on) *on = c->jit_on && c->jit_mod ? 1u : 0u;
-    if (compile_ms) *compile_ms = c->jit_ms;
-    return TW_OK;
-}
-
 int sh_create(int device, tw_shard** out) {
     if (!out) return TW_ERR_INVALID;
     *out = nullptr;
@@ -374,10 +236,6 @@ int sh_create(int device, tw_shard** out) {
         return TW_ERR_HIP;
     }
     c->own_stream = c->stream;
-    {
-        const char* j = getenv("TW_JIT");  // (tests: the whole suite through the scenario compiler)
-        c->jit_on = j && j[0] == '1';
-    }
     *out = c;
     return TW_OK;
 }
@@ -784,12 +642,7 @@ static int load_common(tw_shard* c, const tw_scenario_desc* s, bool lp, uint32_t
     c->main_regs = mregs;
     c->nv_init = nvi;
     c->listen_init = lsi;
-    c->h_insns.assign(s->insns, s->insns + s->n_insns);
     c->loaded = true;
-    if (c->jit_on && !(c->geo == 3 && !lp)) {
-        const int jr = jit_build(c);
-        if (jr != TW_OK) { free_all(c); return jr; }
-    }
     int rc = sh_reset(c);
     if (rc) return rc;
     HIPCHK(hipStreamSynchronize(st));
@@ -923,7 +776,6 @@ int sh_run(tw_shard* c, int64_t t_end_us, uint64_t max_events, tw_stats* out) {
             else
                 launch_run<false, TW_WG, TW_NEAR_CAP>(c, st, t_end_us, limit, budget);
             HIPCHK(hipGetLastError());
-            if (c->jit_missing) return TW_ERR_JIT;
             HIPCHK(hipEventRecord(c->ev_pool[2 * i + 1], st));
             ++launches;
         }
@@ -1365,7 +1217,6 @@ int sh_lp_tick(tw_shard* c) {
     launch_run<true, TW_WG_LP, TW_NEAR_LP>(c, st, 0, UINT64_MAX, c->lp_budget);
     c->d.win = nullptr;
     HIPCHK(hipGetLastError());
-    if (c->jit_missing) return TW_ERR_JIT;
     if (c->ex_world > 1 && d.carry) {  // the previous tick's carry claims block slots first
         hipLaunchKernelGGL(tw_lp_pack_carry, dim3(lp_grid(d.carry_cap)), dim3(256), 0, st, d, c->ex_send,
                            (const uint32_t*)c->ex_starts, c->ex_world, c->ex_cap, c->ex_cap_eff);

@@ -1,8 +1,6 @@
 // engine_dev.hpp — the device code of libtimewarp.so's event engine (engine.hip):
 // the lane-per-replica / logical-process event loop (Lane, tw_run_kernel) and
-// the window-loop kernels.  Included by engine.hip, and compiled a second time
-// by the scenario compiler (jit.cpp: hiprtc, __HIPCC_RTC__ defined), which
-// needs only the event kernel: the other kernels stay out of that compile.
+// the window-loop kernels.  Included by engine.hip.
 #pragma once
 #include "tw_dev.hpp"
 
@@ -268,16 +266,9 @@ struct BoolC {
     static constexpr bool value = B;
 };
 
-// The compiled scenario's block dispatch (generated by jit.cpp, compiled by
-// hiprtc together with this file; never instantiated in the static library)
-template <class LT, class ST>
-__device__ void tw_jit_dispatch(LT& L, Th& th, uint32_t slot, ST& s, uint32_t fpc);
-
-// JIT: the event loop of a compiled scenario (jit.cpp) -- instruction decode
-// folded into per-pc code, the running thread's registers in VGPRs
 // IP: fork children run in place (fork_in_place) -- the variant the host
 // launches under the tie orders where a forked child is always the next pop
-template <bool LP, int WG, int NC, bool RUNS = true, bool IP = false, bool JIT = false>
+template <bool LP, int WG, int NC, bool RUNS = true, bool IP = false>
 struct Lane {
     // the replica kernels keep monotone far runs (LDS bookkeeping + HBM FIFOs)
     // unless built without them (the compact geometry: far events go to the
@@ -386,28 +377,10 @@ struct Lane {
     __device__ __forceinline__ void fail(uint32_t st) {
         if (status == TW_REP_RUNNING) status = st;
     }
-#ifndef TW_JIT_RF_VGPR
-#define TW_JIT_RF_VGPR 1  // compiled scenario: registers in VGPRs (1) or the LDS register file (0)
-#endif
-    static constexpr bool RFV = JIT && TW_JIT_RF_VGPR;
-    static_assert(!(RFV && TW_DIRTY_TAIL), "the dirty store tail compares the LDS register file with the record");
     // The running thread's registers r0..r3: the LDS register file (the
-    // interpreter's operand indices are per lane) or, in a compiled scenario,
-    // the record's own fields held in VGPRs (every index is a constant there)
-    __device__ __forceinline__ int64_t rg(const Th& th, uint32_t i) const {
-        if constexpr (RFV) return i == 0 ? th.r0 : i == 1 ? th.r1 : i == 2 ? th.r2 : th.r3;
-        else return rf[i * WG];
-    }
-    __device__ __forceinline__ void rs(Th& th, uint32_t i, int64_t v) {
-        if constexpr (RFV) {
-            th.r0 = i == 0 ? v : th.r0;
-            th.r1 = i == 1 ? v : th.r1;
-            th.r2 = i == 2 ? v : th.r2;
-            th.r3 = i == 3 ? v : th.r3;
-        } else {
-            rf[i * WG] = v;
-        }
-    }
+    // interpreter's operand indices are per lane)
+    __device__ __forceinline__ int64_t rg(const Th& th, uint32_t i) const { return rf[i * WG]; }
+    __device__ __forceinline__ void rs(Th& th, uint32_t i, int64_t v) { rf[i * WG] = v; }
 
     // ---------------------------------------------------------- near heap (LDS)
     // 4-ary min-heap of unique 64-bit keys; a free position holds ~0, so no
@@ -1355,8 +1328,7 @@ struct Lane {
     }
 
     enum { T_NONE, T_YIELD, T_SPAWN, T_EXIT, T_STOP, T_DIED };
-    // The step's per-lane loop state, shared by the interpreter's passes and the
-    // scenario compiler's instruction blocks (jit.cpp)
+    // The step's per-lane loop state, shared by the interpreter's passes
     struct St {
         uint32_t pc, fin, n;
         bool running;
@@ -1364,12 +1336,7 @@ struct Lane {
     };
 
     // One interpreter pass: the instruction (uw, imm; op and uop flags fl of the
-    // first running lane, lfl of this lane's own) for the lanes `at` it.  The
-    // scenario compiler calls it with constants (jop), which folds the decode.
-    // CT (the compiled scenario, jop): the opcode OPC and uop flags FLC are
-    // template constants, so the front end emits only this instruction's class
-    // code and, for a rare op, only its case of the per-opcode switch
-    template <bool CT = false, uint32_t OPC = 0, uint32_t FLC = 0>
+    // first running lane, lfl of this lane's own) for the lanes `at` it.
     __device__ __forceinline__ void pass(Th& th, uint32_t slot, St& s, bool at, uint32_t uw, int32_t imm, uint32_t op,
                                          uint32_t fl, uint32_t lfl) {
         uint32_t& pc = s.pc;
@@ -1377,7 +1344,7 @@ struct Lane {
         uint32_t& n = s.n;
         int64_t& yt = s.yt;
         uint32_t& fin = s.fin;
-        const bool hot = CT ? !(FLC & U_FX) : !(fl & U_FX);
+        const bool hot = !(fl & U_FX);
         n += at ? 1u : 0u;
         const bool capped = at && n > TW_STEP_CAP;  // TW_REP_ERR_INSN before executing it
         const bool me = at && !capped;
@@ -1532,7 +1499,7 @@ struct Lane {
             }
         };
         if (hot) {
-            if constexpr (PL && !JIT) {
+            if constexpr (PL) {
                 if (__builtin_expect(__builtin_amdgcn_ballot_w64(at && lfl != fl) == 0, 1))
                     hot_body(BoolC<true>{}, fl);
                 else
@@ -1541,10 +1508,9 @@ struct Lane {
                 hot_body(BoolC<true>{}, fl);
             }
         }
-        if (CT ? (FLC & U_FX) != 0 : (fl & U_FX) != 0) {
-        // the rare ops (CT: OPC is a template constant, so the front end emits
-        // only its case)
-        switch (CT ? OPC : op) {
+        if ((fl & U_FX) != 0) {
+        // the rare ops
+        switch (op) {
         case TW_OP_THROW_TO: {
             thr_any = true; thr = me;
             tref = ra; tcode = b & 0xFFu; tval = rg(th, ((b >> 8) & 3u));
@@ -1903,31 +1869,6 @@ struct Lane {
         fin = at ? tc : fin;
         running = running && !(at && tc != T_NONE);
     }
-    // The scenario compiler's instruction at `pc`: word W, immediate I (jit.cpp
-    // emits one call per pc of the image); true if some running lane goes on at pc + 1
-    template <uint32_t W, int32_t I>
-    __device__ __forceinline__ bool jop(Th& th, uint32_t slot, St& s, uint32_t pc) {
-        const bool at = s.running && s.pc == pc;
-        pass<true, W & 0xFFu, uop_insn(W)>(th, slot, s, at, W, I, W & 0xFFu, uop_insn(W), uop_insn(W));
-        return __builtin_amdgcn_ballot_w64(s.running && s.pc == pc + 1u) != 0;
-    }
-    // The compiled scenario's heavy rare instructions (throwTo, throw, the
-    // timeout watchdog: each inlines the queue re-stamp or the unwinder) all
-    // run through this one interpreter pass, a single copy in the dispatch,
-    // with the instruction from the LDS image
-    __device__ __forceinline__ void jrare(Th& th, uint32_t slot, St& s, uint32_t pc) {
-        const bool at = s.running && s.pc == pc;
-        const uint2 in = P[pc];
-        const uint32_t fl = PU[pc];
-        pass(th, slot, s, at, in.x, (int32_t)in.y, in.x & 0xFFu, fl, fl);
-    }
-    // a pc outside the compiled image (unreachable: a running lane's pc is checked)
-    __device__ __forceinline__ void jbad(St& s, uint32_t pc) {
-        const bool at = s.running && s.pc == pc;
-        pfail(at, TW_REP_ERR_INSN);
-        s.fin = at ? (uint32_t)T_STOP : s.fin;
-        s.running = s.running && !at;
-    }
     // A fork whose child is the very next pop runs the child in place, in this
     // iteration (replica kernels).  TimedT's fork queues the child at now and
     // the parent at now + 1 (TimedT.hs:326-342); the child is PQ.minView's
@@ -1988,9 +1929,7 @@ struct Lane {
                 hacc += term0(now, TW_KIND_RESUME | th_pc(ch));
                 th = ch;
                 slot = cslot;
-                if constexpr (!RFV) {
-                    rf[0] = ch.r0; rf[WG] = ch.r1; rf[2 * WG] = ch.r2; rf[3 * WG] = ch.r3;
-                }
+                rf[0] = ch.r0; rf[WG] = ch.r1; rf[2 * WG] = ch.r2; rf[3 * WG] = ch.r3;
                 s.pc = th_pc(th);
                 th.w0 |= F_STARTED << FL_SHIFT;
                 s.running = s.pc < c.n_insns;
@@ -2042,14 +1981,6 @@ struct Lane {
                 break;
             }
             const uint32_t first = (uint32_t)__builtin_ctzll(mask);
-            if constexpr (JIT) {
-                // the compiled scenario (jit.cpp): the first running lane's pc picks
-                // the block; each of its instructions runs for the lanes at that pc
-                // (operands and uop flags are constants), falling through to the
-                // next instruction while some lane continues there
-                tw_jit_dispatch(*this, th, slot, s, (uint32_t)__builtin_amdgcn_readlane(pc, first));
-                continue;
-            } else {
             // every lane fetches its own instruction; the pass runs the first running
             // lane's opcode in all lanes holding that opcode (their operands and
             // immediates stay per lane), so divergent lanes at different pcs still
@@ -2068,7 +1999,6 @@ struct Lane {
             const bool at = PL ? (s.running & ((hot & !(lfl & U_FX)) | (!hot & ((in.x & 0xFFu) == op))))
                                : (s.running && (in.x & 0xFFu) == op && lfl == fl);
             pass(th, slot, s, at, in.x, (int32_t)in.y, op, fl, lfl);
-            }
         }
         STIME(ti1);
         STADD(K_CYC_INTERP, ti1 - ti0);
@@ -2147,7 +2077,6 @@ struct Lane {
     }
 };
 
-#ifndef __HIPCC_RTC__
 // ------------------------------------------------------------------ kernels
 __global__ void __launch_bounds__(TW_WG) tw_init_kernel(Dev c, uint32_t main_pc, uint32_t main_node,
                                                        const int64_t* main_regs, const int64_t* nv_init,
@@ -2204,8 +2133,6 @@ __global__ void __launch_bounds__(TW_WG) tw_init_kernel(Dev c, uint32_t main_pc,
         for (uint32_t n = 0; n < c.N; ++n) gp(c.bind)[(size_t)n * c.R + r] = listen_init[n];
 }
 
-#endif  // __HIPCC_RTC__
-
 // LDS per workgroup: near heap keys + slots, the running threads' register
 // files, the cold words, then the program image and constant pool, so
 // instruction fetch and time constants never leave the CU.
@@ -2220,8 +2147,7 @@ __host__ __device__ constexpr size_t fixed_lds_bytes() {
 // RUNS = false (the compact geometry): no far runs, and built for two waves
 // per SIMD (<= 256 registers, half the LDS of a dense lane), so 1M-replica
 // batches keep two workgroups per CU
-template <bool LP, int WG, int NC, int TPW = 64, bool RUNS = true, bool GS = false, bool PRW = false, bool IP = false,
-          bool JIT = false>
+template <bool LP, int WG, int NC, int TPW = 64, bool RUNS = true, bool GS = false, bool PRW = false, bool IP = false>
 __global__ void __launch_bounds__(WG * 64 / TPW)
     __attribute__((amdgpu_waves_per_eu(LP ? TW_LP_WAVES : !RUNS ? 2 : (WG * 64 / TPW + 255) / 256,
                                        LP ? TW_LP_WAVES : 2)))
@@ -2317,7 +2243,7 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
                     break;  // (the next block of the work list)
             }
 
-            Lane<LP, WG, NC, RUNS, IP, JIT> L;
+            Lane<LP, WG, NC, RUNS, IP> L;
             L.c = c;
             L.r = r;
             L.nk = s_k + li;
@@ -2541,7 +2467,7 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
                         pending_main = 0;
                         L.pf_slot = 0xFFFFFFFFu;
                         L.fetch_rec(0, th);
-                        if constexpr (!decltype(L)::RFV) { L.rf[0] = th.r0; L.rf[WG] = th.r1; L.rf[2 * WG] = th.r2; L.rf[3 * WG] = th.r3; }
+                        L.rf[0] = th.r0; L.rf[WG] = th.r1; L.rf[2 * WG] = th.r2; L.rf[3 * WG] = th.r3;
                         L.hnode = th.w1;
                         run = true;
                     } else if (rare) {  // whileM_ notDone, or this launch's event cap
@@ -2598,7 +2524,7 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
                                 L.now = t;
                                 if (t - L.nbase > (int64_t)0x7FFFFFFF) L.near_rebase(t);
                                 L.hnode = th.w1;
-                                if constexpr (!decltype(L)::RFV) { L.rf[0] = th.r0; L.rf[WG] = th.r1; L.rf[2 * WG] = th.r2; L.rf[3 * WG] = th.r3; }
+                                L.rf[0] = th.r0; L.rf[WG] = th.r1; L.rf[2 * WG] = th.r2; L.rf[3 * WG] = th.r3;
                                 // LP phantom = the deliverer's wake, already counted and hashed by the sender
                                 const bool phantom = LP && (th_flags(th) & F_PHANTOM);
                                 if (!phantom) {
@@ -2687,7 +2613,7 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
                 const uint4 ix4 = *L.rqp(RQ_IDX);
         #pragma unroll
                 for (int j = 0; j < TW_RUNS; ++j) {
-                    sc[(SC_RH0 + j) * SR] = Lane<LP, WG, NC, RUNS, IP, JIT>::q_at(ix4, j);
+                    sc[(SC_RH0 + j) * SR] = Lane<LP, WG, NC, RUNS, IP>::q_at(ix4, j);
                     sc[(SC_RC0 + j) * SR] = L.rqp(RQ_TAIL + j)->w;
                 }
             }
@@ -2737,7 +2663,6 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
 }
 
 
-#ifndef __HIPCC_RTC__
 // A delivery record for local node dst: claim an inbox slot (the drain at the
 // window's first tick sorts them), lower *tmin to its time, list the node for
 // the next window.
@@ -3641,6 +3566,5 @@ __global__ void __launch_bounds__(256) tw_digest_kernel(Dev c, uint64_t* out) {
     gp(out)[r] = d;
 }
 
-#endif  // __HIPCC_RTC__
 
 }  // namespace

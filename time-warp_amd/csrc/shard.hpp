@@ -32,9 +32,6 @@ TW_HIDDEN int sh_tie_audit(tw_shard* c, int64_t t_end_us, uint64_t max_events, u
 TW_HIDDEN int sh_geometry(tw_shard* c);
 TW_HIDDEN int sh_set_counter_base(tw_shard* c, uint32_t seq0, uint32_t tid0);
 TW_HIDDEN int sh_set_tie_mode(tw_shard* c, uint32_t mode);
-TW_HIDDEN int sh_set_jit(tw_shard* c, uint32_t on);
-TW_HIDDEN int sh_jit_status(tw_shard* c, uint32_t* on, double* compile_ms);
-TW_HIDDEN int sh_jit_precompile(const tw_scenario_desc* s, int geometry, double* compile_ms);
 TW_HIDDEN int sh_set_trace(tw_shard* c, uint32_t cap);
 TW_HIDDEN int sh_read_trace(tw_shard* c, uint32_t replica, tw_trace_rec* out, size_t cap, uint64_t* n_emitted);
 TW_HIDDEN int sh_last_launch_ms(tw_shard* c, double* out, size_t cap);

@@ -3,11 +3,9 @@
 // wave.hip: wave-per-replica kernel): the thread record, the per-replica
 // scalar block, the device context and the hash terms.
 #pragma once
-#ifndef __HIPCC_RTC__  // (the scenario compiler's hiprtc source: jit.cpp)
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
-#endif
 
 #include "../../include/timewarp.h"
 
@@ -357,12 +355,10 @@ __device__ __forceinline__ void atom_add64(unsigned long long GAS* p, uint64_t v
                  "s_mov_b64 exec, %0" : "=&s"(sv) : "v"(p), "v"(v), "s"(mask) : "memory", "scc");
 }
 
-#ifndef __HIPCC_RTC__
 // wave.hip: the wave-per-replica kernel (geometry TW_GEO_WAVE)
 int wave_near_k(uint32_t R);                // near-queue entries per lane (K) for R replicas (tw_load)
 size_t wave_spill_entries(uint32_t K);      // near-queue spill entries per replica
 hipError_t wave_launch(const Dev& d, const Dev* d_dev, hipStream_t st, int64_t t_end, uint64_t limit,
                        uint32_t budget);
-#endif
 
 }  // namespace tw

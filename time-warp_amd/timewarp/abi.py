@@ -109,4 +109,4 @@ RESULT_DTYPE = _np.dtype([
     ("main_exc", _np.uint32), ("threads", _np.uint64), ("tie_flags", _np.uint32), ("reserved", _np.uint32),
 ])
 assert RESULT_DTYPE.itemsize == C.sizeof(TwReplicaResult)
-assert isa.ABI_VERSION == 3
+assert isa.ABI_VERSION == 4

@@ -30,7 +30,7 @@ EXPORTS = ["tw_create", "tw_comm_id", "tw_create_rank", "tw_ctx_info", "tw_lp_ru
            "tw_set_trace", "tw_read_trace", "tw_tie_audit", "tw_set_counter_base", "tw_geometry",
            "tw_set_stream", "tw_lp_exchange_setup", "tw_lp_loop_begin", "tw_lp_tick", "tw_lp_tick_import",
            "tw_lp_tick_end", "tw_lp_progress", "tw_lp_run_windows", "tw_lpb_load", "tw_lpb_windows",
-           "tw_draw_link_table", "tw_set_jit", "tw_jit_status", "tw_jit_precompile"]
+           "tw_draw_link_table"]
 GEOMETRIES = ("dense", "sparse", "half", "wave", "lp", "narrow", "lpb", "compact")  # TW_GEO_* order
 
 # tw_trace_rec (include/timewarp.h)
@@ -105,15 +105,12 @@ def load_library(path: Optional[str] = None):
     lib.tw_lpb_load.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p, C.c_uint32, C.c_uint32]
     lib.tw_lpb_windows.argtypes = [C.c_void_p, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
     lib.tw_draw_link_table.argtypes = [C.c_int, C.POINTER(TwTableDraw), C.c_void_p]
-    lib.tw_set_jit.argtypes = [C.c_void_p, C.c_uint32]
-    lib.tw_jit_status.argtypes = [C.c_void_p, C.POINTER(C.c_uint32), C.POINTER(C.c_double)]
-    lib.tw_jit_precompile.argtypes = [C.c_void_p, C.c_int, C.POINTER(C.c_double)]
     for name in ("tw_create", "tw_comm_id", "tw_create_rank", "tw_ctx_info", "tw_lp_run", "tw_set_tie_mode", "tw_load", "tw_reset", "tw_run", "tw_read_results", "tw_read_hashes", "tw_read_final",
                  "tw_last_launch_ms", "tw_lp_load", "tw_lp_window", "tw_lp_take_outbox", "tw_lp_inject",
                  "tw_lp_results", "tw_set_trace", "tw_read_trace", "tw_tie_audit", "tw_set_counter_base",
                  "tw_geometry", "tw_set_stream", "tw_lp_exchange_setup", "tw_lp_loop_begin", "tw_lp_tick",
                  "tw_lp_tick_import", "tw_lp_tick_end", "tw_lp_progress", "tw_lp_run_windows", "tw_lpb_load",
-                 "tw_lpb_windows", "tw_draw_link_table", "tw_set_jit", "tw_jit_status", "tw_jit_precompile"):
+                 "tw_lpb_windows", "tw_draw_link_table"):
         getattr(lib, name).restype = C.c_int
     if path is None:
         _lib = lib
@@ -139,19 +136,6 @@ def draw_link_table(n_replicas: int, drawn, lo, hi, link_depth: int = 1, drop_lo
                        seed_base=int(seed_base), drawn=drawn.ctypes.data, lo=lo.ctypes.data, hi=hi.ctypes.data)
     _check(load_library().tw_draw_link_table(int(device), C.byref(spec), out.ctypes.data), "tw_draw_link_table")
     return out
-
-
-def jit_precompile(scn: Scenario, geometry: str) -> float:
-    """The scenario compiler alone (tw_jit_precompile, no device needed):
-    compile `scn`'s program image into the event kernel of `geometry`
-    ("dense", "sparse", "half", "narrow", "compact", "lp" or "lpb") into the
-    process's cache (and $TW_JIT_CACHE).  Returns the compile time in ms (0 on
-    a cache hit)."""
-    d = scn.desc()
-    ms = C.c_double()
-    _check(load_library().tw_jit_precompile(C.addressof(d), GEOMETRIES.index(geometry), C.byref(ms)),
-           "tw_jit_precompile")
-    return float(ms.value)
 
 
 def _check(rc: int, what: str):
@@ -324,19 +308,6 @@ class Engine:
         return RunStats(**{f: getattr(st, f) for f, _ in TwStats._fields_ if f != "reserved"})
 
     TIE_MODES = {"fifo": 0, "lifo": 1, "scramble": 2, "pqueue": 3, "forkfirst": 4}  # TW_TIE_*
-
-    def set_jit(self, on: bool = True) -> "Engine":
-        """The scenario compiler (tw_set_jit): later loads (and the loaded
-        scenario, now) run the program image compiled into the event kernel
-        instead of the interpreter; bit-identical results."""
-        _check(self.lib.tw_set_jit(self.ctx, 1 if on else 0), "tw_set_jit")
-        return self
-
-    def jit_status(self):
-        """(compiled kernel running on every shard, last compile time in ms)."""
-        on, ms = C.c_uint32(), C.c_double()
-        _check(self.lib.tw_jit_status(self.ctx, C.byref(on), C.byref(ms)), "tw_jit_status")
-        return bool(on.value), float(ms.value)
 
     def set_tie_mode(self, mode: str) -> "Engine":
         """Equal-timestamp order of later runs: "fifo" (the engine's (t, seq)),

@@ -5,7 +5,7 @@ kernel time per step.
 
 usage: python tools/ab_probe.py CONFIG REPLICAS GEOMETRY SETTING_A SETTING_B
   CONFIG: token_ring | ping_pong | hotspot;  GEOMETRY: a geometry or "auto"
-  SETTING: comma list of tie=fifo|lifo, jit=0|1   e.g.  tie=fifo tie=lifo
+  SETTING: comma list of tie=fifo|lifo|forkfirst   e.g.  tie=fifo tie=lifo
 """
 import json
 import os
@@ -33,8 +33,6 @@ def run(scn, geo, setting, steps):
     kv = dict(x.split("=") for x in setting.split(",") if x)
     eng = Engine(0)
     t0 = time.perf_counter()
-    if kv.get("jit", "0") == "1":
-        eng.set_jit(True)
     eng.load(scn, geometry=None if geo == "auto" else geo)
     load_s = time.perf_counter() - t0
     if "tie" in kv:

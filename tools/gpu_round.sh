@@ -19,7 +19,6 @@ step() {  # step NAME SECONDS CMD...
 for s in "$@"; do
   case $s in
     pytest) step pytest_gpu 1000 python -u -m pytest tests/ -q -m gpu -x --timeout 300 --timeout-method thread ;;
-    pytest_new) step pytest_new 600 python -u -m pytest tests/test_gpu_tie_orders.py tests/test_gpu_jit.py -q -m gpu -x --timeout 300 --timeout-method thread ;;
     smoke)  step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     phase)  step phase 300 python tools/phase_probe.py 65536 4096 ;;
     micro)  step micro 300 python tools/micro_probe.py 65536 8 ;;
@@ -29,12 +28,9 @@ for s in "$@"; do
     stats_c5) step stats_c5 400 env TW_LIB=$PWD/time-warp_amd/lib/libtimewarp_stats.so python -u tools/stats_probe.py hotspot 4096 256 ;;
     probe2) step probe2 300 env TW_LIB=$PWD/time-warp_amd/lib/libtimewarp_prof2.so python tools/kernel_probe.py 65536 4096 ;;
     bench)  step bench 500 python bench.py ;;
-    jit_c3) step jit_c3 400 python -u tools/ab_probe.py token_ring 65536 auto jit=0 jit=1 ;;
     tie_c3) step tie_c3 400 python -u tools/ab_probe.py token_ring 65536 auto tie=fifo tie=forkfirst ;;
     tie_c2) step tie_c2 400 python -u tools/ab_probe.py ping_pong 1048576 auto tie=fifo tie=forkfirst ;;
     tie_c3_8k) step tie_c3_8k 400 python -u tools/ab_probe.py token_ring 8192 narrow tie=fifo tie=forkfirst ;;
-    jit_c2) step jit_c2 400 python -u tools/ab_probe.py ping_pong 1048576 auto jit=0 jit=1 ;;
-    benchj) step benchj 400 python bench.py --steps 3 --jit 1 ;;
     benchq) step benchq 300 python bench.py --steps 2 --no-cpu-baseline ;;
     bench_c2) step bench_c2 400 python bench.py --config ping_pong ;;
     bench_c4) step bench_c4 500 python bench.py --config gossip ;;
