@@ -8,7 +8,8 @@ Lane::fetch_rec, run_commit, the LP child staging).  tools/waitcnt_audit.py
 walks every instantiation's control-flow graph and fails if some path reaches
 such a wait after fewer than N vector-memory instructions since the load it
 guards -- e.g. a compiler change that merged or dropped a store of the
-fixed-shape store tail."""
+fixed-shape store tail.  The victim headers a throwTo step stages at its pop
+(Lane::stage_victims, stream `vic`) are checked the same way."""
 import os
 import subprocess
 import sys
@@ -58,5 +59,17 @@ def test_audit_flags_a_short_wait(engine_asm, tmp_path, capsys):
     assert "s_waitcnt vmcnt(9) ; tw:pf" in s
     bad = tmp_path / "short.s"
     bad.write_text(s.replace("s_waitcnt vmcnt(9) ; tw:pf", "s_waitcnt vmcnt(12) ; tw:pf"))
+    rc, out = _audit(str(bad), capsys)
+    assert rc == 1 and "SHORT" in out, out
+
+
+def test_audit_flags_a_short_victim_wait(engine_asm, tmp_path, capsys):
+    # throw_to's wait for the victim headers stage_victims loaded at the pop:
+    # vmcnt(4) is proved by the record prefetch's four loads issued after them;
+    # vmcnt(6) would not be
+    s = open(engine_asm).read()
+    assert "s_waitcnt vmcnt(4) ; tw:vic" in s
+    bad = tmp_path / "short_vic.s"
+    bad.write_text(s.replace("s_waitcnt vmcnt(4) ; tw:vic", "s_waitcnt vmcnt(6) ; tw:vic"))
     rc, out = _audit(str(bad), capsys)
     assert rc == 1 and "SHORT" in out, out

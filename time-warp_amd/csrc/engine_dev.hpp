@@ -129,12 +129,19 @@ enum {
     CW_FTL = 0,                     // far heap top (t, seq, slot)
     CW_FTH, CW_FS, CW_FSL,
     CW_DL, CW_DR, CW_UD, CW_MAINEXC, CW_TMO,          // counters
-    CW_YTL, CW_YTH, CW_CPC, CW_CNODE, CW_CRA, CW_CDEL, // step staging: wake time, child
-    CW_Q0, CW_Q7 = CW_Q0 + 7,                          // child registers (4 x int64)
+    CW_CPC, CW_CNODE, CW_CRA, CW_CDEL,                 // step staging: the child (its registers: Lane::qq)
+    CW_F2L, CW_F2H, CW_F2S,  // the far sources' runner-up key (t, seq): the least but the chosen source's
+    CW_VS,                   // victim headers staged at this pop: d_ev << 3 | n0 << 2 | quads (stage_victims)
     CW_TRN,                                            // TRACE records emitted (tw_set_trace)
     CW_DUMMY,                                          // target of idle lanes' predicated stores
     CW_COUNT
 };
+// byte offset of the child-register quads (Lane::qq) from the record staging
+template <int WG, int NC, bool HR>
+__host__ __device__ constexpr uint32_t qq_lds_offset() {
+    return (uint32_t)(((HR ? 5 : 4) + (HR ? RQ_COUNT : 0)) * WG * 16 + NC * WG * 8 + 4 * WG * 8);
+}
+
 // LP-only cold words, after the CW_* block: the due run of a heavy lane
 // (head | count << 16, seq base, head time) and its inbox base index
 // DW_BSET/BOWN/BREL: LP -- the lane's own listener binding (bind, bind_own,
@@ -288,6 +295,10 @@ struct Lane {
     uint4 LAS* pfs;       // prefetch staging: quad q of the next pop's record at [q * WG]
     uint32_t pfs_wave;    // LDS byte address of this wave's staging (quad 0), wave-uniform
     uint32_t LAS* cw;     // cold words [CW_*] in LDS (TW_CW_REGS=0)
+    // a spawning instruction's child registers (4 x int64) as two lane-contiguous
+    // quads [2][WG]: one 16-B LDS access per pair, and at a pop whose step opens
+    // with throwTo the LDS-DMA target of the victims' header quads (stage_victims)
+    uint4 LAS* qq;
     // cold words in registers (replica kernels): every index is a constant, so no
     // LDS round trip; the allocator parks them in AGPRs when tight.  The LP
     // kernel runs two waves per SIMD (no AGPR room) and keeps them in LDS.
@@ -373,6 +384,16 @@ struct Lane {
         cs(wh, (uint32_t)((uint64_t)v >> 32));
     }
     __device__ __forceinline__ void cinc(int w) { cs(w, cg(w) + 1); }
+    // the child registers (qq): two int64 per quad
+    __device__ __forceinline__ static uint4 q2(int64_t a, int64_t b) {
+        return make_uint4((uint32_t)a, (uint32_t)((uint64_t)a >> 32), (uint32_t)b, (uint32_t)((uint64_t)b >> 32));
+    }
+    __device__ __forceinline__ static int64_t qa(uint4 q) { return (int64_t)(((uint64_t)q.y << 32) | q.x); }
+    __device__ __forceinline__ static int64_t qb(uint4 q) { return (int64_t)(((uint64_t)q.w << 32) | q.z); }
+    __device__ __forceinline__ void qset(int64_t r0, int64_t r1, int64_t r2, int64_t r3) {
+        qq[0] = q2(r0, r1);
+        qq[WG] = q2(r2, r3);
+    }
 
     __device__ __forceinline__ void fail(uint32_t st) {
         if (status == TW_REP_RUNNING) status = st;
@@ -789,20 +810,33 @@ struct Lane {
     }
     // The head moves to the second entry; the entry after it is loaded now, by
     // LDS-DMA into staging quad 4, and committed before the store tail.
+    // The popped run is the far minimum (fsrc); its new head stays the minimum
+    // when it is below the runner-up far_min recorded (the least key of the
+    // other far sources), so a stream of pops from one run -- C3's teardown: the
+    // 4,096 kill wakes at 120 s and the 8,192 victims re-stamped behind them --
+    // keeps far_min's eight-quad scan off every pop.
     __device__ __forceinline__ void run_pop(int sel) {
         if constexpr (!HR) return;  // unreachable: fsrc is never a run without runs
         run_commit();
-        far_dirty = true;
         uint4 ix4 = *rqp(RQ_IDX);
         uint32_t h = q_at(ix4, sel) + 1;
         h = h == c.Cr ? 0 : h;
         ix4.x = sel == 0 ? h : ix4.x; ix4.y = sel == 1 ? h : ix4.y;
         ix4.z = sel == 2 ? h : ix4.z; ix4.w = sel == 3 ? h : ix4.w;
         *rqp(RQ_IDX) = ix4;
-        *rqp(RQ_HEAD + sel) = *rqp(RQ_SEC + sel);
+        const uint4 nh = *rqp(RQ_SEC + sel);
+        *rqp(RQ_HEAD + sel) = nh;
         uint4 tl = *rqp(RQ_TAIL + sel);
         const uint32_t n = --tl.w;
         *rqp(RQ_TAIL + sel) = tl;
+        {
+            const int64_t t = ent_t(nh);
+            const bool keep = !far_dirty && fsrc == sel && n != 0 && tless(t, nh.w, cg64(CW_F2L, CW_F2H), cg(CW_F2S));
+            fmt = keep ? t : fmt;
+            fms = keep ? nh.w : fms;
+            fmsl = keep ? nh.z : fmsl;
+            far_dirty = !keep;
+        }
         if (n >= 2) {
             const uint32_t p2 = h + 1 == c.Cr ? 0 : h + 1;
             // into LDS staging quad 4 (no register left pending across the step)
@@ -833,15 +867,28 @@ struct Lane {
         uint4 hd[TW_RUNS], tl[TW_RUNS];
 #pragma unroll
         for (int j = 0; j < TW_RUNS; ++j) { hd[j] = *rqp(RQ_HEAD + j); tl[j] = *rqp(RQ_TAIL + j); }
+        // (and the runner-up: the least key of the sources but the chosen one;
+        // none = (INT64_MAX, ~0), above every key)
+        int64_t t2 = INT64_MAX;
+        uint32_t s2 = 0xFFFFFFFFu;
 #pragma unroll
         for (int j = 0; j < TW_RUNS; ++j) {
             const int64_t t = ent_t(hd[j]);
-            const bool b = tl[j].w != 0 && (fsrc < 0 || tless(t, hd[j].w, fmt, fms));
+            const bool v = tl[j].w != 0;
+            const bool b = v && (fsrc < 0 || tless(t, hd[j].w, fmt, fms));
+            // a new minimum demotes the old one (when there was one); otherwise
+            // the head may still be the runner-up
+            const bool d = b && fsrc >= 0 && tless(fmt, fms, t2, s2);
+            const bool u = v && !b && tless(t, hd[j].w, t2, s2);
+            t2 = d ? fmt : (u ? t : t2);
+            s2 = d ? fms : (u ? hd[j].w : s2);
             fsrc = b ? j : fsrc;
             fmt = b ? t : fmt;
             fms = b ? hd[j].w : fms;
             fmsl = b ? hd[j].z : fmsl;
         }
+        cs64(CW_F2L, CW_F2H, t2);
+        cs(CW_F2S, s2);
     }
     // every queued event (near heap, far sources, LP due run) is later than t
     __device__ __forceinline__ bool queue_after(int64_t t) {
@@ -907,21 +954,6 @@ struct Lane {
     __device__ __forceinline__ void hbm_load(uint32_t slot, Th& th) const {
         const uint4 GAS* p = hrec(slot);
         unpack(th, p[0], p[c.RQ], p[2 * c.RQ], p[3 * c.RQ]);
-    }
-    // a record's header and frames / exception quads (a throwTo victim: its
-    // registers are neither read nor written, so quads 2-3 stay in HBM)
-    __device__ __forceinline__ void peek_q01(uint32_t slot, Th& th) const {
-        const uint4 GAS* p = hrec(slot);
-        const uint4 a = p[0], b = p[c.RQ];
-        th.w0 = a.x; th.w1 = a.y; th.w2 = a.z; th.w3 = a.w;
-        th.f0 = b.x; th.f1 = b.y; th.xl = b.z; th.xh = b.w;
-    }
-    __device__ __forceinline__ void put_q01(uint32_t slot, const Th& th) {
-        if (slot == pf_slot) pf_slot = 0xFFFFFFFFu;
-        STAT(K_PUT_HBM);
-        uint4 GAS* p = hrec(slot);
-        p[0] = make_uint4(th.w0, th.w1, th.w2, th.w3);
-        p[c.RQ] = make_uint4(th.f0, th.f1, th.xl, th.xh);
     }
     // mode ST_THROUGH: the full record; ST_DEAD: only the header quad (the tid
     // that invalidates stale refs)
@@ -1208,40 +1240,118 @@ struct Lane {
         return true;
     }
 
-    // throwTo (TimedT.hs:357-368): re-stamp target's event to now, first exception wins.
-    __device__ __forceinline__ void throw_to(Th& self, uint32_t self_slot, int64_t ref, uint32_t code, int64_t val) {
-        uint32_t ts = (uint32_t)ref;
-        uint32_t tid = (uint32_t)((uint64_t)ref >> 32);
-        if (ts >= c.S) return;
-        if (ts == self_slot) {  // the running thread: its record lives in registers
-            if (self.w2 != tid) return;
-            if (th_exc(self) == 0) { th_set_exc(self, code); th_set_xval(self, val); q1d = true; }
-            return;
+    // throwTo (TimedT.hs:357-368) for the lanes `thr` of an interpreter pass
+    // (n: the instruction's count in the step): the target's event is
+    // re-stamped to now, the first exception wins.  Only the victim's header
+    // quad is read and written (pc, flags, exception code, tid, queued seq); a
+    // fresh exception's value goes to the upper half of its frames quad with
+    // one 8-B store.  The header comes from the quad stage_victims loaded at the
+    // pop when this is the step's first or second instruction, else from HBM
+    // here (drained in place on every path).
+    __device__ __forceinline__ void throw_to(Th& self, uint32_t self_slot, uint32_t n, bool thr, int64_t ref,
+                                            uint32_t code, int64_t val) {
+        const uint32_t ts = (uint32_t)ref;
+        const uint32_t tid = (uint32_t)((uint64_t)ref >> 32);
+        bool go = thr && ts < c.S;
+        if (go && ts == self_slot) {  // the running thread: its record lives in registers
+            if (self.w2 == tid && th_exc(self) == 0) { th_set_exc(self, code); th_set_xval(self, val); q1d = true; }
+            go = false;
         }
+        uint32_t k = 2u;  // the staged quad holding this lane's victim header (2: none)
+        if constexpr (!LP) {
+            if (__builtin_amdgcn_ballot_w64(go && n <= 3u)) {
+                // (CW_VS: d_ev << 3 | the step's first pass count n0 << 2 | quads)
+                const uint32_t vs = cg(CW_VS);
+                const uint32_t j = n - 1u - ((vs >> 2) & 1u);  // 0, 1: the step's first / second pass
+                const bool st = go && j < 2u && (vs >> 3) == d_ev && ((vs >> j) & 1u);
+                k = st ? j : 2u;
+            }
+        }
+        uint4 h = make_uint4(0u, 0u, 0xFFFFFFFFu, 0u);
+        if (__builtin_amdgcn_ballot_w64(k < 2u)) {
+            // every vector-memory op since the staging load is younger: the record
+            // prefetch's four at least
+            asm volatile("s_waitcnt vmcnt(4) ; tw:vic" ::: "memory");
+            if (k < 2u) h = qq[k * WG];
+        }
+        if (__builtin_amdgcn_ballot_w64(go && k == 2u)) {
+            if (go && k == 2u) h = hrec(ts)[0];
+            tw_vm_drain();
+        }
+        if (!go || h.z != tid) return;  // dead (slot free or reused): the map entry is unobservable
         Th t;
-        peek_q01(ts, t);
-        // the loads drained here, on every path out (a quad left in
-        // flight on the early return made the compiler wait at the top of
-        // every later interpreter pass)
-        tw_vm_drain();
-        if (t.w2 != tid) return;  // dead (slot free or reused): the map entry is unobservable
+        t.w0 = h.x; t.w1 = h.y; t.w2 = h.z; t.w3 = h.w;
         if (t.w3 != 0) {          // queued: wake to now with a fresh seq
             bool on_chip = (th_flags(t) & F_NEARQ) != 0;
             uint32_t s = next_seq();
             if (!(on_chip && near_rekey(t.w3, now, s, ts))) {
                 on_chip = near_fits(now);
-                if (on_chip) near_push(now, s, ts);
-                else push_far(now, s, ts);
+                if (on_chip) {
+                    near_push(now, s, ts);
+                } else if (!run_push(now, s, ts)) {
+                    far_push(now, s, ts);
+                    // (the heap's ancestor loads whose values go unused must not stay
+                    // in flight into the next pass; the stores of every other path
+                    // need no wait: a wave's later loads of the same words see them)
+                    tw_vm_drain();
+                }
             }
             if (on_chip) th_or_flags(t, F_NEARQ);
             else th_clr_flags(t, F_NEARQ);
             t.w3 = s;
         }
-        if (th_exc(t) == 0) {
-            th_set_exc(t, code);
-            th_set_xval(t, val);
-        }
-        put_q01(ts, t);
+        const bool fresh = th_exc(t) == 0;
+        if (fresh) th_set_exc(t, code);
+        if (ts == pf_slot) pf_slot = 0xFFFFFFFFu;
+        STAT(K_PUT_HBM);
+        uint4 GAS* p = hrec(ts);
+        p[0] = make_uint4(t.w0, t.w1, t.w2, t.w3);
+        if (fresh)  // (xl, xh: the frames quad's upper half)
+            *(uint2 GAS*)((uint32_t GAS*)(p + c.RQ) + 2) = make_uint2((uint32_t)val, (uint32_t)((uint64_t)val >> 32));
+    }
+
+    // A thread resumed at an unconditional JMP -- every `schedule`'s stub
+    // (`wait spec >> jmp action`, program.py Code.schedule; MonadTimed.hs:162-163)
+    // -- goes to the jump's target at the pop: the JMP counts as the step's
+    // first instruction (returns n0 = 1) without an interpreter pass of its own.
+    __device__ __forceinline__ uint32_t jump_at_pop(Th& th, bool run) const {
+        const uint32_t pc = th_pc(th);
+        const bool ok = run && pc < c.n_insns;
+        const uint2 in = P[ok ? pc : 0u];
+        const bool j = ok && (in.x & 0xFFu) == TW_OP_JMP && (uint32_t)in.y < c.n_insns;
+        th.w0 = j ? (th.w0 & 0xFFFF0000u) | (uint32_t)in.y : th.w0;
+        return j ? 1u : 0u;
+    }
+
+    // Victim prefetch (replica kernels).  A step that opens with throwTo -- C3's
+    // kill pair `mapM_ killThread [r1, r2]` at 120 s, 4,096 per replica
+    // (examples/token-ring/Main.hs:124-127) -- waited a full HBM round trip for
+    // each victim's header in its interpreter pass.  The victims are known at
+    // the pop (the refs sit in the popped record's registers), so their header
+    // quads are loaded here, by LDS-DMA into the child-register quads (qq: free
+    // until a spawning instruction later in the step), for the step's first two
+    // instructions when they are throwTo.  Issued before the record prefetch,
+    // so throw_to's counted vmcnt(4) proves they landed without waiting for
+    // it.  CW_VS names this pop (d_ev: every counted pop and in-place child
+    // changes it), the step's starting instruction count n0 and the staged quads.
+    __device__ __forceinline__ void stage_victims(const Th& th, uint32_t slot, bool run, uint32_t n0) {
+        const uint32_t pc = th_pc(th);
+        const bool ok = run && pc < c.n_insns;
+        const uint32_t w0 = P[ok ? pc : 0u].x, w1 = P[ok ? pc + 1u : 0u].x;  // (the image is padded by one NOP)
+        const bool t0 = ok && (w0 & 0xFFu) == TW_OP_THROW_TO;
+        if (!__builtin_amdgcn_ballot_w64(t0)) return;
+        const uint32_t v0 = (uint32_t)rf[((w0 >> 8) & 3u) * WG];
+        const uint32_t v1 = (uint32_t)rf[((w1 >> 8) & 3u) * WG];
+        const bool s0 = t0 && v0 < c.S && v0 != slot;
+        const bool s1 = t0 && (w1 & 0xFFu) == TW_OP_THROW_TO && v1 < c.S && v1 != slot && v1 != v0;
+        // (readfirstlane: the m0 operand is an SGPR whatever register the value was kept in)
+        const uint32_t qw = (uint32_t)__builtin_amdgcn_readfirstlane((int)(pfs_wave + qq_lds_offset<WG, NC, HR>()));
+        asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off ; tw:vic" ::"v"(hrec(s0 ? v0 : 0u)),
+                     "s"(qw) : "memory", "m0");
+        if (__builtin_amdgcn_ballot_w64(s1))
+            asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off ; tw:vic" ::"v"(hrec(s1 ? v1 : 0u)),
+                         "s"(qw + WG * 16) : "memory", "m0");
+        cs(CW_VS, (d_ev << 3) | (n0 << 2) | (s0 ? 1u : 0u) | (s1 ? 2u : 0u));
     }
 
     // Thread ends (END or uncaught exception): listener release, ref
@@ -1640,9 +1750,7 @@ struct Lane {
                         }
                     } else {
                         cs(CW_CPC, TW_PC_DELIVER_STUB); cs(CW_CNODE, th.w1); cs(CW_CRA, 4); cs(CW_CDEL, 0);
-                        cs64(CW_Q0, CW_Q0 + 1, payload); cs64(CW_Q0 + 2, CW_Q0 + 3, (int64_t)link);
-                        cs64(CW_Q0 + 4, CW_Q0 + 5, (int64_t)(e & 0x7FFFFFFFu) + tx_us(c, link, kind));
-                        cs64(CW_Q0 + 6, CW_Q7, (int64_t)kind);
+                        qset(payload, (int64_t)link, (int64_t)(e & 0x7FFFFFFFu) + tx_us(c, link, kind), (int64_t)kind);
                         tc = T_SPAWN;
                     }
                 }
@@ -1725,8 +1833,7 @@ struct Lane {
                     cinc(CW_DL);
                     hash(dst, TW_KIND_RECV | kind, r0);
                     cs(CW_CPC, lpc); cs(CW_CNODE, dst); cs(CW_CRA, 4); cs(CW_CDEL, LP ? 1u : 0u);
-                    cs64(CW_Q0, CW_Q0 + 1, r0); cs64(CW_Q0 + 2, CW_Q0 + 3, (int64_t)link);
-                    cs64(CW_Q0 + 4, CW_Q0 + 5, LP ? r2 : (int64_t)th.w1); cs64(CW_Q0 + 6, CW_Q7, (int64_t)kind);
+                    qset(r0, (int64_t)link, LP ? r2 : (int64_t)th.w1, (int64_t)kind);
                     tc = T_SPAWN;
                 }
             }
@@ -1772,9 +1879,7 @@ struct Lane {
                     gp(c.tmo_done)[ix(tmo)] = 0;
                     rs(th, a, tmo);
                     cs(CW_CPC, TW_PC_WATCHDOG_STUB); cs(CW_CNODE, th.w1); cs(CW_CRA, 4); cs(CW_CDEL, 0);
-                    cs64(CW_Q0, CW_Q0 + 1, (int64_t)(((uint64_t)th.w2 << 32) | slot));
-                    cs64(CW_Q0 + 2, CW_Q0 + 3, (int64_t)tmo);
-                    cs64(CW_Q0 + 4, CW_Q0 + 5, K[imm]); cs64(CW_Q0 + 6, CW_Q7, 0);
+                    qset((int64_t)(((uint64_t)th.w2 << 32) | slot), (int64_t)tmo, K[imm], 0);
                     tc = T_SPAWN;
                 }
             }
@@ -1813,10 +1918,7 @@ struct Lane {
         }  // U_FX
         if (wr) rs(th, a, wm ? wv : ra);
         (void)lfl;
-        if (thr_any) {
-            if (thr) throw_to(th, slot, tref, tcode, tval);
-            tw_vm_drain();
-        }
+        if (thr_any) throw_to(th, slot, n, thr, tref, tcode, tval);
         // per-lane epilogue of the pass
         pc = me ? tgt : pc;
         pfail(capped, TW_REP_ERR_INSN);
@@ -1906,11 +2008,13 @@ struct Lane {
             int64_t ref;
             Th ch;
             uint32_t cslot = 0xFFFFFFFFu;
-            const bool ok =
-                (cdel & 2u) ? spawn(cg(CW_CPC), cg(CW_CNODE), rg(th, 0), rg(th, 1), rg(th, 2), rg(th, 3), ref, ch, cslot,
-                                    false)
-                            : spawn(cg(CW_CPC), cg(CW_CNODE), cg64(CW_Q0, CW_Q0 + 1), cg64(CW_Q0 + 2, CW_Q0 + 3),
-                                    cg64(CW_Q0 + 4, CW_Q0 + 5), cg64(CW_Q0 + 6, CW_Q7), ref, ch, cslot, false);
+            bool ok;
+            if (cdel & 2u) {
+                ok = spawn(cg(CW_CPC), cg(CW_CNODE), rg(th, 0), rg(th, 1), rg(th, 2), rg(th, 3), ref, ch, cslot, false);
+            } else {
+                const uint4 a = qq[0], b = qq[WG];
+                ok = spawn(cg(CW_CPC), cg(CW_CNODE), qa(a), qb(a), qa(b), qb(b), ref, ch, cslot, false);
+            }
             if (ok) {
                 // the parent: `wait (for 1 mcs)` (TimedT.hs:340) -- queued, record stored
                 if (cra < 4) rs(th, cra, ref);
@@ -1955,7 +2059,7 @@ struct Lane {
     // divergent region).  Lanes in lock-step take one pass per instruction.
     // Yield / fork / exit are recorded per lane and carried out after the
     // loop for all lanes at once.
-    __device__ __forceinline__ void step(Th& th, uint32_t slot, bool run) {
+    __device__ __forceinline__ void step(Th& th, uint32_t slot, bool run, uint32_t n0 = 0) {
         St s;
         uint32_t& pc = s.pc;
         uint32_t& fin = s.fin;
@@ -1965,7 +2069,7 @@ struct Lane {
         s.running = run && pc < c.n_insns;
         pfail(run && !s.running, TW_REP_ERR_INSN);
         fin = (run && !s.running) ? (uint32_t)T_STOP : (uint32_t)T_NONE;
-        s.n = 0;
+        s.n = n0;  // (a JMP taken at the pop: jump_at_pop)
         yt = 0;
         STIME(ti0);
         for (;;) {
@@ -2024,11 +2128,12 @@ struct Lane {
                 if (ok) emit_spawn(now, cg(CW_CPC), lane_of(cg(CW_CNODE)), rg(th, 0), rg(th, 1), rg(th, 2), rg(th, 3));
                 else fail(TW_REP_ERR_INSN);
                 ref = -1;
-            } else if (cdel & 2u)
+            } else if (cdel & 2u) {
                 ok = spawn(cg(CW_CPC), cg(CW_CNODE), rg(th, 0), rg(th, 1), rg(th, 2), rg(th, 3), ref, ch, cslot);
-            else
-                ok = spawn(cg(CW_CPC), cg(CW_CNODE), cg64(CW_Q0, CW_Q0 + 1), cg64(CW_Q0 + 2, CW_Q0 + 3),
-                           cg64(CW_Q0 + 4, CW_Q0 + 5), cg64(CW_Q0 + 6, CW_Q7), ref, ch, cslot);
+            } else {
+                const uint4 a = qq[0], b = qq[WG];
+                ok = spawn(cg(CW_CPC), cg(CW_CNODE), qa(a), qb(a), qa(b), qb(b), ref, ch, cslot);
+            }
             if (!ok) {
                 fin = T_STOP;
             } else {
@@ -2139,7 +2244,7 @@ __global__ void __launch_bounds__(TW_WG) tw_init_kernel(Dev c, uint32_t main_pc,
 template <int WG, int NC, bool LP = false, bool RUNS = true>
 __host__ __device__ constexpr size_t fixed_lds_bytes() {
     return (size_t)(LP || !RUNS ? 4 : 5) * WG * 16 + (size_t)(LP || !RUNS ? 0 : RQ_COUNT) * WG * 16 + (size_t)NC * WG * 12 +
-           (size_t)4 * WG * 8 + (size_t)(CW_COUNT + (LP ? DW_COUNT : 0)) * WG * 4;
+           (size_t)4 * WG * 8 + (size_t)2 * WG * 16 + (size_t)(CW_COUNT + (LP ? DW_COUNT : 0)) * WG * 4;
 }
 
 // WG replicas per workgroup share its LDS; TPW of each wave's 64 lanes carry a
@@ -2181,7 +2286,8 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
     uint4 LAS* s_rq = s_pf + (HR ? 5 : 4) * WG;  // (staging quad 4 holds a far run's next entry: runs only)
     uint64_t LAS* s_k = (uint64_t LAS*)(s_rq + (HR ? RQ_COUNT : 0) * WG);
     int64_t LAS* s_rf = (int64_t LAS*)(s_k + NC * WG);
-    uint32_t LAS* s_s = (uint32_t LAS*)(s_rf + 4 * WG);
+    uint4 LAS* s_q = (uint4 LAS*)((uint8_t LAS*)s_pf + qq_lds_offset<WG, NC, HR>());  // (= s_rf + 4 * WG)
+    uint32_t LAS* s_s = (uint32_t LAS*)(s_q + 2 * WG);
     uint32_t LAS* s_cw = s_s + NC * WG;
     uint2 LAS* s_p = (uint2 LAS*)(s_cw + (CW_COUNT + (LP ? DW_COUNT : 0)) * WG);
     int64_t LAS* s_c = (int64_t LAS*)(s_p + c.n_insns + 1);
@@ -2249,6 +2355,7 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
             L.nk = s_k + li;
             L.ns = s_s + li;
             L.rf = s_rf + li;
+            L.qq = s_q + li;
             L.cw = s_cw + li;
             L.pfs = s_pf + li;
             L.rq = s_rq + li;
@@ -2554,12 +2661,14 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
                     }
                 }
                 if (!popping) slot = 0u;  // main's first run is slot 0; idle lanes do not use it
+                const uint32_t n0 = L.jump_at_pop(th, run);
+                if constexpr (!LP) L.stage_victims(th, slot, run, n0);
                 STIME(tp0);
                 L.prefetch_all(run ? slot : 0xFFFFFFFFu);
                 STIME(tl1);
                 STADDL(K_CYC_PF, tl1 - tp0);
                 STADDL(K_CYC_POP, tl1 - tl0);
-                L.step(th, slot, run);
+                L.step(th, slot, run, n0);
                 STIME(th0);
                 L.hash_flush_all();
                 STIME(th1);

@@ -17,7 +17,7 @@ For every tw_run_kernel instantiation:
    run_commit, the LP child staging): N is the number of vector-memory
    instructions the code issues after the load it guards.  Loads and waits
    carry a `; tw:<stream>` comment (pf: the record prefetch, run: a far run's
-   next entry).  A dataflow pass over the kernel's control-flow graph computes,
+   next entry, vic: the throwTo victims' header quads staged at the pop).  A dataflow pass over the kernel's control-flow graph computes,
    per stream, at every such wait, the FEWEST vector-memory instructions issued
    since that stream's most recent LDS-DMA load on any path reaching it (a wait
    that already covered the load ends the concern).  If that count is below N
@@ -79,7 +79,7 @@ def blocks_of(body):
 
 
 TAG = re.compile(r";\s*tw:(\w+)")
-STREAMS = ("pf", "run")
+STREAMS = ("pf", "run", "vic")
 
 
 def transfer(ins, v, checks=None):
