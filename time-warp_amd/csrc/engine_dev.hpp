@@ -174,6 +174,13 @@ enum : uint32_t { LD_NONE, LD_NV, LD_OUT, LD_RL };  // node var / out-link base 
 #define U_NS (1u << 24)
 #define U_TR2 (1u << 25)
 #define U_P2 (1u << 26)
+// END folded into the pass before it (set in the launch prologue from the
+// image): the instruction at pc + 1 / pc + 2 (a fused pair's successor) / its
+// jump target is END.  Not part of the opcode-uniform pass's flag match.
+#define U_NE (1u << 27)
+#define U_NE2 (1u << 28)
+#define U_JE (1u << 29)
+#define U_FOLD (U_NE | U_NE2 | U_JE)
 __host__ __device__ constexpr uint32_t uop_of(uint32_t op) {
     auto u = [](uint32_t alu, uint32_t jm, uint32_t tk) { return alu | (tk << 8) | (jm << 16); };
     switch (op) {
@@ -281,6 +288,10 @@ struct Lane {
     // unless built without them (the compact geometry: far events go to the
     // HBM heap only, and the LDS a lane needs halves)
     static constexpr bool HR = !LP && RUNS;
+    // END folded into the pass before it (U_FOLD): the run geometries only --
+    // the compact and LP kernels measured slower with it (C2 -4 %, C5 -2.6 %:
+    // their register budget, 254-256 VGPRs at two waves per SIMD)
+    static constexpr bool FOLD = HR;
     // per-lane hot passes (lanes at different hot ops share a pass) pay off where
     // lanes diverge -- logical processes and the few-replica sparse geometry; the
     // dense replica geometry runs lock-step programs and keeps the cheaper
@@ -1610,7 +1621,7 @@ struct Lane {
         };
         if (hot) {
             if constexpr (PL) {
-                if (__builtin_expect(__builtin_amdgcn_ballot_w64(at && lfl != fl) == 0, 1))
+                if (__builtin_expect(__builtin_amdgcn_ballot_w64(at && ((lfl ^ fl) & (FOLD ? ~U_FOLD : ~0u)) != 0) == 0, 1))
                     hot_body(BoolC<true>{}, fl);
                 else
                     hot_body(BoolC<false>{}, lfl);
@@ -1919,6 +1930,18 @@ struct Lane {
         if (wr) rs(th, a, wm ? wv : ra);
         (void)lfl;
         if (thr_any) throw_to(th, slot, n, thr, tref, tcode, tval);
+        // END folded into this pass: a lane whose next instruction is END
+        // (U_NE / U_NE2 / U_JE) ends here, with END's count and pc, instead of
+        // in a pass of its own -- launchNode's last END after its `when`
+        // (examples/token-ring/Main.hs:125-131), the kill pair's after its throws
+        if (FOLD && __builtin_amdgcn_ballot_w64(me && (lfl & U_FOLD) != 0)) {
+            const bool fe = me && tc == T_NONE && status == TW_REP_RUNNING && n < TW_STEP_CAP &&
+                            (((lfl & U_NE) && tgt == pc + 1u) || ((lfl & U_NE2) && tgt == pc + 2u) ||
+                             ((lfl & U_JE) && tgt == (uint32_t)imm));
+            n += fe ? 1u : 0u;
+            tgt = fe ? tgt + 1u : tgt;
+            tc = fe ? (uint32_t)T_EXIT : tc;
+        }
         // per-lane epilogue of the pass
         pc = me ? tgt : pc;
         pfail(capped, TW_REP_ERR_INSN);
@@ -2101,7 +2124,7 @@ struct Lane {
             // (opcode-uniform pass: the lanes holding the first lane's opcode and uop
             // flags -- a fused pair's flags depend on b, not only on the opcode)
             const bool at = PL ? (s.running & ((hot & !(lfl & U_FX)) | (!hot & ((in.x & 0xFFu) == op))))
-                               : (s.running && (in.x & 0xFFu) == op && lfl == fl);
+                               : (s.running && (in.x & 0xFFu) == op && ((lfl ^ fl) & (FOLD ? ~U_FOLD : ~0u)) == 0);
             pass(th, slot, s, at, in.x, (int32_t)in.y, op, fl, lfl);
         }
         STIME(ti1);
@@ -2297,7 +2320,14 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
         for (uint32_t i = threadIdx.x; i <= c.n_insns; i += WG * 64 / TPW) {
             const uint2 in = gp(c.insns)[i];
             s_p[i] = in;
-            s_u[i] = uop_insn(in.x);
+            uint32_t u = uop_insn(in.x);
+            auto is_end = [&](uint32_t j) { return j < c.n_insns && (gp(c.insns)[j].x & 0xFFu) == TW_OP_END; };
+            if (HR && i < c.n_insns) {  // (Lane::FOLD)
+                u |= is_end(i + 1u) ? U_NE : 0u;
+                u |= is_end(i + 2u) ? U_NE2 : 0u;
+                u |= (U_JM(u) != JM_NONE && is_end((uint32_t)in.y)) ? U_JE : 0u;
+            }
+            s_u[i] = u;
         }
         for (uint32_t i = threadIdx.x; i < c.n_consts; i += WG * 64 / TPW) s_c[i] = gp(c.consts)[i];
         for (uint32_t i = threadIdx.x; i < c.n_sets * c.n_kinds; i += WG * 64 / TPW) s_l[i] = gp(c.lpc)[i];
