@@ -580,7 +580,15 @@ int tw_lp_run_windows(tw_ctx* ctx, uint64_t max_ticks, tw_lp_state* out);
  * for long enough to outgrow it stops every rank at the same tick with the
  * replica error (tw_lp_state.err bit 8) rather than losing a record.  A local
  * failure on one rank is agreed over the job before the next collective, so
- * every rank returns the same code at the same point.  The multi-GPU
+ * every rank returns the same code at the same point -- a failure the shard
+ * can still report: after a HIP fault that leaves the device unusable (a
+ * kernel fault, a lost device), that rank's next RCCL call fails or never
+ * completes, and the ranks waiting in the collective with it stay stranded
+ * until RCCL's own timeout; nothing in the library can end them sooner.  A
+ * context whose RCCL call failed is marked unusable: every later call that
+ * communicates (tw_run, tw_tie_audit, tw_lp_run, tw_lp_results) returns
+ * TW_ERR_COMM at once, without entering a collective; tw_destroy it and make
+ * a new one.  The multi-GPU
  * replacement of MonadDialog's cross-node send path (MonadDialog.hs:149-166)
  * with runTimedT's loop around it.  The caller-driven primitives
  * (tw_lp_exchange_setup / tw_lp_tick ...) remain for one-device contexts. */

@@ -166,6 +166,32 @@ def test_lp_run_local_failure_agreed(engine_mod, oracle_mod, monkeypatch, mode):
     assert lp.done == 1 and lp.err == 0
 
 
+def test_rccl_failure_marks_the_context_unusable(engine_mod, oracle_mod, monkeypatch):
+    """A failed RCCL call (injected: TW_TEST_FAIL_NCCL=1 fails the next checked
+    call without making it) returns TW_ERR_COMM and marks the context: every
+    later call that communicates returns TW_ERR_COMM at once instead of
+    entering a collective its peers may no longer be in (include/timewarp.h,
+    tw_lp_run).  A fresh context works again."""
+    jid = engine_mod.comm_id()
+    scn = scenarios.token_ring(n_nodes=10, n_replicas=48, launch_duration=25_000_000, drop_log2=4)
+    with engine_mod.Engine(0, comm=(1, 0, jid)) as e:
+        e.load(scn)
+        monkeypatch.setenv("TW_TEST_FAIL_NCCL", "1")
+        with pytest.raises(engine_mod.EngineError, match=r"tw_run failed: -8 "):
+            e.run()
+        monkeypatch.delenv("TW_TEST_FAIL_NCCL")
+        e.reset()
+        with pytest.raises(engine_mod.EngineError, match=r"tw_run failed: -8 "):
+            e.run()
+    with engine_mod.Engine(0, comm=(1, 0, engine_mod.comm_id())) as e:
+        e.load(scn)
+        st = e.run()
+        res, h = e.results(), e.hashes()
+    ores, oh = oracle_mod.run_batch(scn, threads=8)
+    _same_batch(res, h, ores, oh, "rccl x1 after a failed context")
+    assert st.events == int(ores["events"].sum())
+
+
 def test_multi_shard_refuses_caller_loop(engine_mod):
     """The caller-driven window primitives speak for one device only."""
     scn = scenarios.gossip(256, seed=1)

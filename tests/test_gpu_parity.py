@@ -110,3 +110,23 @@ def test_hotspot_bandwidth_aware_delays(engine_mod, oracle_mod):
     scn = scenarios.hotspot(n_senders=8, n_replicas=90, msg_num=30, payload_bytes=1000,
                             bandwidth_bytes_per_s=2_000_000)
     _compare(scn, engine_mod, oracle_mod)
+
+
+@pytest.mark.one_geometry
+def test_ping_pong_benched_shape_compact(engine_mod, oracle_mod):
+    """bench.py's C2 per-replica shape -- 1,000 round trips
+    (examples/ping-pong/Main.hs:53-79) on the compact geometry with forked
+    children in place -- over 2,048 replicas, every field and node hash
+    against the oracle's canonical order."""
+    scn = scenarios.ping_pong(n_replicas=2048, round_trips=1000)
+    with engine_mod.Engine(0) as e:
+        e.load(scn, geometry="compact")
+        assert e.geometry() == "compact"
+        e.reset()
+        st = e.run()
+        res, hashes = e.results(), e.hashes()
+    ores, ohashes = oracle_mod.run_batch(scn, threads=8)
+    for f in FIELDS:
+        assert np.array_equal(res[f], ores[f]), f
+    assert np.array_equal(hashes, ohashes)
+    assert st.events == int(ores["events"].sum()) > 2048 * 4000

@@ -91,6 +91,19 @@ def test_token_ring_c3_nodes_in_pqueue_order(engine_mod, oracle_mod):
     assert o.result["delivered"] >= 3 and o.result["events"] > 30_000
 
 
+def test_token_ring_teardown_in_pqueue_order(engine_mod, oracle_mod):
+    # the whole launchDuration, teardown included: at 120 s each of the 512
+    # kill pairs throws twice and every throwTo rebuilds the ~1.5k-entry queue
+    # with `fromList . map . toList` (TimedT.hs:361-368; examples/token-ring/
+    # Main.hs:124-127), against the oracle's pqueue transcription (mode 1)
+    scn = scenarios.token_ring(n_nodes=512, n_replicas=2, launch_duration=120_000_000, drop_log2=10)
+    res, h = _gpu_pq(engine_mod, scn)
+    for r in range(scn.n_replicas):
+        o = oracle_mod.run(scn, mode=1, replica=r)
+        _check(res, h, o, "token_ring_512_teardown", r)
+        assert o.result["final_t"] == 120_000_000 and o.result["status"] == 1
+
+
 def test_pqueue_mode_needs_the_wave_geometry(engine_mod):
     scn = progs.random_program(0)
     with engine_mod.Engine(0) as e:

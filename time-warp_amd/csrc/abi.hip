@@ -22,6 +22,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -70,6 +71,10 @@ struct tw_ctx {
     std::vector<hipEvent_t> ev_a, ev_b;     // COPY: per shard
     std::vector<void*> scratch;             // per shard: RCCL statistics buffer
     uint32_t xcap = 1u << 14;               // exchange block stride (records per rank pair)
+    // an RCCL call of this context failed: the communicators may hold a
+    // collective the peers are still in, so every later communicating call
+    // returns TW_ERR_COMM without entering another one (timewarp.h, tw_lp_run)
+    bool comm_broken = false;
 };
 
 namespace {
@@ -78,7 +83,28 @@ int comm_fail(ncclResult_t r, const char* what) {
     fprintf(stderr, "timewarp: %s failed: %s\n", what, ncclGetErrorString(r));
     return TW_ERR_COMM;
 }
+// testing hook: with TW_TEST_FAIL_NCCL=k in the environment the k-th checked
+// RCCL call since it was set (counting from 1) fails without being made
+// (one-rank jobs in the tests); the count restarts whenever it is unset
+bool nccl_test_fail() {
+    static std::atomic<long> n{0};
+    const char* e = getenv("TW_TEST_FAIL_NCCL");
+    if (!e) {
+        n = 0;
+        return false;
+    }
+    return ++n == atol(e);
+}
+// (in a function of the context c: a failure marks it unusable)
 #define NCCLCHK(x)                                   \
+    do {                                             \
+        ncclResult_t _r = nccl_test_fail() ? ncclInternalError : (x); \
+        if (_r != ncclSuccess) {                     \
+            c->comm_broken = true;                   \
+            return comm_fail(_r, #x);                \
+        }                                            \
+    } while (0)
+#define NCCLCHK_NC(x)                                \
     do {                                             \
         ncclResult_t _r = (x);                       \
         if (_r != ncclSuccess) return comm_fail(_r, #x); \
@@ -346,7 +372,7 @@ int tw_create(const int* devices, int ndev, tw_ctx** out) {
 int tw_comm_id(uint8_t* id) {
     if (!id) return TW_ERR_INVALID;
     ncclUniqueId u;
-    NCCLCHK(ncclGetUniqueId(&u));
+    NCCLCHK_NC(ncclGetUniqueId(&u));
     static_assert(sizeof(u) == TW_COMM_ID_BYTES, "RCCL unique id size");
     std::memcpy(id, &u, sizeof(u));
     return TW_OK;
@@ -444,6 +470,7 @@ int tw_reset(tw_ctx* c) {
 int tw_run(tw_ctx* c, int64_t t_end_us, uint64_t max_events, tw_stats* out) {
     if (!c) return TW_ERR_INVALID;
     if (single(c) && c->tp == TP_NONE) return sh_run(c->sh[0], t_end_us, max_events, out);
+    if (c->comm_broken) return TW_ERR_COMM;
     const size_t n = c->sh.size();
     std::vector<tw_stats> st(n);
     std::vector<int> rcs(n, TW_OK);
@@ -466,6 +493,7 @@ int tw_run(tw_ctx* c, int64_t t_end_us, uint64_t max_events, tw_stats* out) {
 int tw_tie_audit(tw_ctx* c, int64_t t_end_us, uint64_t max_events, uint32_t probes, tw_stats* out) {
     if (!c) return TW_ERR_INVALID;
     if (single(c) && c->tp == TP_NONE) return sh_tie_audit(c->sh[0], t_end_us, max_events, probes, out);
+    if (c->comm_broken) return TW_ERR_COMM;
     const size_t n = c->sh.size();
     std::vector<tw_stats> st(n);
     std::vector<int> rcs(n, TW_OK);
@@ -692,6 +720,7 @@ int tw_lp_run_windows(tw_ctx* c, uint64_t max_ticks, tw_lp_state* out) {
 int tw_lp_results(tw_ctx* c, tw_replica_result* agg, uint64_t* node_hashes, size_t n_nodes) {
     if (!c || !agg) return TW_ERR_INVALID;
     if (single(c) && c->tp == TP_NONE) return sh_lp_results(c->sh[0], agg, node_hashes, n_nodes);
+    if (c->comm_broken) return TW_ERR_COMM;
     const size_t n = c->sh.size();
     std::vector<std::vector<uint64_t>> sums(n);
     std::vector<std::vector<int64_t>> maxs(n);
@@ -752,6 +781,7 @@ int tw_lp_results(tw_ctx* c, tw_replica_result* agg, uint64_t* node_hashes, size
 // carry buffer.  One host synchronisation per 16 ticks.
 int tw_lp_run(tw_ctx* c, uint64_t max_ticks, tw_lp_state* out) {
     if (!c || !out) return TW_ERR_INVALID;
+    if (c->comm_broken) return TW_ERR_COMM;
     const size_t n = c->sh.size();
     std::vector<int> lrc(n, TW_OK);  // each shard's first local failure
     // the worst local code of the job (RCCL: agreed over every rank first)
