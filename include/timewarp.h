@@ -511,6 +511,15 @@ int tw_lpb_load(tw_ctx* ctx, const tw_scenario_desc* desc, int64_t lookahead_us,
                 uint32_t inbox_cap, uint32_t outbox_cap);
 /* Windows and ticks of the last tw_run in batched mode. */
 int tw_lpb_windows(tw_ctx* ctx, uint64_t* windows, uint64_t* ticks);
+/* Batched mode, since the last tw_reset: the due records (the delivery records
+ * of heavy nodes, sorted per window) and how many of them ran data-parallel --
+ * one per thread, ahead of the node's own chain -- because their handler is
+ * batchable (the fork_-dispatched handler of a (listener set, kind) whose
+ * effects are its own: registers, node-variable reads, links, traces, at most
+ * one send followed by END; bench/Network's Ping handler) and no other event of
+ * the node falls between their events.  Results are those of the sequential
+ * loop either way; TW_LP_BATCH=0 at tw_lpb_load turns the batch off. */
+int tw_lpb_batch(tw_ctx* ctx, uint64_t* batched, uint64_t* due_records);
 
 /* ---- device-driven windows (no host round trip per window)
  * The window loop above costs several host synchronisations per window.  Here

@@ -240,3 +240,64 @@ def test_lpb_per_replica_windows_fewer(engine_mod, oracle_mod, monkeypatch, case
     assert w_rep <= w_glob, (w_rep, w_glob)
     if case == "token_ring_drift":
         assert w_rep < w_glob, (w_rep, w_glob)
+
+
+# ---- batched delivery (tw_lp_due runs a heavy receiver's due run data-parallel)
+
+def _lpb_batched(scn, engine_mod, oracle_mod, threads=8):
+    """The run vs the oracle, plus (batched, due) of tw_lpb_batch."""
+    with engine_mod.Engine(0) as e:
+        e.load(scn, geometry="lpb")
+        e.reset()
+        st = e.run()
+        res, hashes = e.results(), e.hashes()
+        bat = e.lpb_batch()
+    ores, ohashes = oracle_mod.run_batch(scn, threads=threads)
+    for f in RESULT_FIELDS:
+        if f != "tie_flags":
+            assert np.array_equal(res[f], ores[f]), (scn.name, f)
+    assert np.array_equal(hashes, ohashes), scn.name
+    assert st.events == int(ores["events"].sum())
+    return ores, bat
+
+
+def test_lpb_batched_delivery_heavy_receiver(engine_mod, oracle_mod):
+    """bench/Network's Ping handler (Receiver/Main.hs:32-38) is batchable: most
+    of the receiver's due records run one per thread in tw_lp_due, and every
+    field and node hash still equals the sequential oracle."""
+    scn = scenarios.hotspot(n_senders=64, n_replicas=32, msg_num=60)
+    ores, (bat, due) = _lpb_batched(scn, engine_mod, oracle_mod)
+    assert due > 0 and bat >= 0.5 * due, (bat, due)
+
+
+def test_lpb_batched_delivery_off_is_the_chain(engine_mod, oracle_mod, monkeypatch):
+    """TW_LP_BATCH=0: every due record on the receiver's chain; same results."""
+    monkeypatch.setenv("TW_LP_BATCH", "0")
+    scn = scenarios.hotspot(n_senders=64, n_replicas=32, msg_num=60)
+    ores, (bat, due) = _lpb_batched(scn, engine_mod, oracle_mod)
+    assert bat == 0 and due > 0
+
+
+def test_lpb_batched_delivery_refuses_a_stateful_handler(engine_mod, oracle_mod):
+    """A Ping handler that counts its pings in a node variable (NSTORE) is not
+    batchable (classify_batch): the due run stays on the chain."""
+    scn = scenarios.hotspot(n_senders=64, n_replicas=16, msg_num=40, receiver_counter=True)
+    ores, (bat, due) = _lpb_batched(scn, engine_mod, oracle_mod)
+    assert bat == 0 and due > 0
+
+
+def test_lpb_batched_delivery_drops_and_undeliverable(engine_mod, oracle_mod):
+    """Dropped pongs (DROP terms, no resume) and pings that reach the receiver
+    after its `unlisten` at 1 s (undeliverable: the stopper ran first, so the
+    prefix before it and the records after it both batch)."""
+    scn = scenarios.hotspot(n_senders=64, n_replicas=16, msg_num=2000, duration_s=1, drop_log2=2)
+    ores, (bat, due) = _lpb_batched(scn, engine_mod, oracle_mod)
+    assert ores["dropped"].sum() > 0 and ores["undeliverable"].sum() > 0
+    assert bat > 0
+
+
+def test_lpb_batched_delivery_c5_shape(engine_mod, oracle_mod):
+    """The C5 receiver: 256 senders, ~256 pings per 1-ms window."""
+    scn = scenarios.hotspot(n_senders=256, n_replicas=16, msg_num=100)
+    ores, (bat, due) = _lpb_batched(scn, engine_mod, oracle_mod)
+    assert bat >= 0.5 * due

@@ -659,6 +659,21 @@ int tw_lpb_windows(tw_ctx* c, uint64_t* windows, uint64_t* ticks) {
     return TW_OK;
 }
 
+int tw_lpb_batch(tw_ctx* c, uint64_t* batched, uint64_t* due_records) {
+    if (!c) return TW_ERR_INVALID;
+    uint64_t b = 0, d = 0;
+    for (tw_shard* s : c->sh) {
+        uint64_t x = 0, y = 0;
+        int rc = sh_lpb_batch(s, &x, &y);
+        if (rc) return rc;
+        b += x;
+        d += y;
+    }
+    if (batched) *batched = b;
+    if (due_records) *due_records = d;
+    return TW_OK;
+}
+
 // the host-driven window loop and the caller-driven device loop speak for one
 // shard (the caller moves the records between contexts / ranks)
 #define ONE_SHARD(c)                                  \

@@ -337,6 +337,69 @@ static void classify_pcs(const tw_scenario_desc* s, std::vector<uint8_t>& cls) {
     }
 }
 
+// The handlers a heavy lane's due run may execute data-parallel (tw_lp_due,
+// round 5): the fork_-dispatched handler of a (listener set, kind) whose code,
+// on every path from its entry, touches only its own registers, reads its
+// node's variables, computes out-links and reply links, traces, and sends at
+// most once with END right after the send -- bench/Network's Ping handler
+// `reply Pong` (Receiver/Main.hs:32-38; ForkStrategy fork_, MonadDialog.hs:317).
+// Such a handler's effects are its own (hash terms, counters, one record), so
+// records whose events no other event of the lane interleaves with can run one
+// per thread with the totals of the sequential loop.  Forward jumps only (the
+// walk is bounded by the image); no NSTORE, fork, wait, throw, listen or MYTID.
+static void classify_batch(const tw_scenario_desc* s, std::vector<uint8_t>& bat) {
+    const uint32_t n = s->n_insns, nk = s->n_msg_kinds;
+    bat.assign((size_t)s->n_listener_sets * nk, 0);
+    auto op_at = [&](uint32_t q) { return q < n ? s->insns[q].w0 & 0xFFu : 0xFFu; };
+    std::vector<uint32_t> seen(n, 0xFFFFFFFFu), stk;
+    for (size_t e = 0; e < bat.size(); ++e) {
+        const uint32_t lpc = s->listener_pc[e];
+        if (lpc == TW_PC_NONE || (lpc & TW_LPC_INLINE) || lpc >= n) continue;
+        bool ok = true;
+        stk.assign(1, lpc);
+        seen[lpc] = (uint32_t)e;
+        while (!stk.empty() && ok) {
+            const uint32_t q = stk.back();
+            stk.pop_back();
+            const uint32_t w = s->insns[q].w0, op = w & 0xFFu, b = w >> 16;
+            const uint32_t imm = (uint32_t)s->insns[q].imm;
+            uint32_t nx[2] = {q + 1, 0xFFFFFFFFu};
+            switch (op) {
+            case TW_OP_END: nx[0] = 0xFFFFFFFFu; break;
+            case TW_OP_NOP: case TW_OP_MOV: case TW_OP_ADD: case TW_OP_SUB: case TW_OP_NLOAD: case TW_OP_LINK:
+            case TW_OP_RLINK:
+                break;
+            case TW_OP_SETI: case TW_OP_SETK: case TW_OP_ADDI: case TW_OP_MULI: case TW_OP_NOW: case TW_OP_NODE:
+                ok = !(b & TW_ALU_NSTORE);  // (the fused NSTORE writes a node variable)
+                break;
+            case TW_OP_TRACE:
+                if (b & TW_TRACE_PAIR) nx[0] = q + 2;
+                break;
+            case TW_OP_JMP: case TW_OP_JEQ: case TW_OP_JNE: case TW_OP_JLT: case TW_OP_JLE: case TW_OP_JEQI:
+            case TW_OP_JNEI:
+                ok = imm > q && imm < n;
+                nx[0] = imm;
+                nx[1] = op == TW_OP_JMP ? 0xFFFFFFFFu : q + 1;
+                break;
+            case TW_OP_SEND: {
+                // the send yields 1 µs (it forks the deliverer): the thread must end there
+                const uint32_t k = (b & (TW_SEND_VIA_LINK | TW_SEND_VIA_RLINK)) ? q + 2 : q + 1;
+                ok = op_at(k) == TW_OP_END;
+                nx[0] = 0xFFFFFFFFu;
+                break;
+            }
+            default: ok = false; break;
+            }
+            for (uint32_t x : nx) {
+                if (x == 0xFFFFFFFFu || !ok) continue;
+                if (x >= n) { ok = false; break; }
+                if (seen[x] != (uint32_t)e) { seen[x] = (uint32_t)e; stk.push_back(x); }
+            }
+        }
+        bat[e] = ok ? 1 : 0;
+    }
+}
+
 static int load_common(tw_shard* c, const tw_scenario_desc* s, bool lp, uint32_t lp_begin, uint32_t lp_count,
                        int64_t lookahead, uint32_t inbox_cap, uint32_t outbox_cap, bool lpb = false,
                        const uint32_t* node_caps = nullptr) {
@@ -547,6 +610,7 @@ static int load_common(tw_shard* c, const tw_scenario_desc* s, bool lp, uint32_t
         ALLOC(d.due, c->heavy_ok ? ib_entries * 2 : 2);
         ALLOC(d.heavy, c->heavy_ok ? 2 * R : 2);
         ALLOC(d.heavy_n, 2);
+        if (lpb) ALLOC(d.bat_ctr, 2);
         ALLOC(d.pend_min, 1);
         ALLOC(d.inbox_n, 2 * R);
         ALLOC(d.outbox, (size_t)d.out_cap * 2);
@@ -635,6 +699,19 @@ static int load_common(tw_shard* c, const tw_scenario_desc* s, bool lp, uint32_t
         HIPCHK(hipMemcpy(pcl, cls.data(), cls.size(), hipMemcpyHostToDevice));
         d.pc_cls = pcl;
     }
+    d.lpc_bat = nullptr;
+    if (lpb && !c->has_ph1 && d.D == 1 && d.n_sets && !(getenv("TW_LP_BATCH") && getenv("TW_LP_BATCH")[0] == '0')) {
+        std::vector<uint8_t> bat;
+        classify_batch(s, bat);
+        bool any = false;
+        for (uint8_t x : bat) any = any || x;
+        if (any) {
+            uint8_t* bd = nullptr;
+            if ((e = dalloc(c, &bd, bat.size())) != TW_OK) { free_all(c); return e; }
+            HIPCHK(hipMemcpy(bd, bat.data(), bat.size(), hipMemcpyHostToDevice));
+            d.lpc_bat = bd;
+        }
+    }
     d.insns = insns; d.consts = consts; d.lpc = lpc; d.out_off = out_off; d.link_dst = ldst; d.link_rev = lrev;
     d.link_table = ltab;
     c->main_pc = s->main_pc;
@@ -676,6 +753,7 @@ int sh_reset(tw_shard* c) {
     if (c->lp) {
         HIPCHK(hipMemsetAsync(d.hash_g, 0, 8ull * ((size_t)d.Ntot << d.rep_lg), st));
         HIPCHK(hipMemsetAsync(d.heavy_n, 0, 8, st));
+        if (d.bat_ctr) HIPCHK(hipMemsetAsync(d.bat_ctr, 0, 16, st));
         if (d.inlist) HIPCHK(hipMemsetAsync(d.inlist, 0, 4ull * R, st));
         HIPCHK(hipMemsetAsync(d.pend_min, 0xFF, 8, st));
         HIPCHK(hipMemsetAsync(d.out_n, 0, 4, st));
@@ -1196,6 +1274,10 @@ int sh_lp_loop_begin(tw_shard* c) {
     }
     HIPCHK(hipGetLastError());
     HIPCHK(hipMemsetAsync(c->d.lp_err, 0, 4, c->stream));
+    if (c->heavy_ok && c->d.lpc_bat) {  // the due runs' batchable prefixes (after the list: their marks are the next window's)
+        hipLaunchKernelGGL(tw_lp_batch, dim3(TW_DUE_GRID), dim3(256), 0, c->stream, c->dwin());
+        HIPCHK(hipGetLastError());
+    }
     c->loop_ready = true;
     return TW_OK;
 }
@@ -1272,6 +1354,10 @@ int sh_lp_tick_end(tw_shard* c) {
         hipLaunchKernelGGL(tw_lp_compact, dim3(compact_blocks(c->d.R)), dim3(256), 0, c->stream, c->dwin(), 0u, 0u);
     }
     HIPCHK(hipGetLastError());
+    if (c->heavy_ok && c->d.lpc_bat) {  // the due runs' batchable prefixes (after the list: their marks are the next window's)
+        hipLaunchKernelGGL(tw_lp_batch, dim3(TW_DUE_GRID), dim3(256), 0, c->stream, c->dwin());
+        HIPCHK(hipGetLastError());
+    }
     return TW_OK;
 }
 
@@ -1472,6 +1558,20 @@ int sh_lpb_windows(tw_shard* c, uint64_t* windows, uint64_t* ticks) {
     if (!c->loaded || !c->lpb) return TW_ERR_STATE;
     if (windows) *windows = c->lpb_windows;
     if (ticks) *ticks = c->lpb_ticks;
+    return TW_OK;
+}
+
+int sh_lpb_batch(tw_shard* c, uint64_t* batched, uint64_t* due) {
+    if (!c) return TW_ERR_INVALID;
+    if (!c->loaded || !c->lpb) return TW_ERR_STATE;
+    unsigned long long h[2] = {0, 0};
+    if (c->d.bat_ctr) {
+        HIPCHK(hipSetDevice(c->device));
+        HIPCHK(hipMemcpyAsync(h, c->d.bat_ctr, 16, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+    }
+    if (batched) *batched = h[0];
+    if (due) *due = h[1];
     return TW_OK;
 }
 

@@ -3425,6 +3425,193 @@ __device__ __forceinline__ uint32_t wg_excl_scan(uint32_t v, uint32_t* wsum, uin
 __device__ __forceinline__ uint4 due_rec_b(const Dev& c, uint4 b) {
     return make_uint4(b.x, b.y, b.z, b.x < c.L ? gp(c.link_rev)[b.x] : 0u);
 }
+
+// ---------------------------------------------------------------------------
+// Batched delivery of a heavy lane's due run (round 5, Dev::lpc_bat).  A
+// hotspot receiver (bench/Network Receiver/Main.hs:32-38) gets ~256 pings per
+// 1-ms window, and the event kernel runs them one after the other on the
+// lane's chain (a due pop, DELIVER, the handler's passes, the send's record:
+// ≈ 23 µs per message).  When a record's handler is batchable
+// (classify_batch: its effects are its own) and no other event of the lane
+// falls between the record's events, the record runs here instead, one per
+// thread of tw_lp_due's workgroup, with the totals the sequential loop reaches.
+
+// One due record as the event kernel handles it: the deliverer's wake (a
+// phantom pop, counted by the sender); DELIVER's binding check (Lane::pass
+// TW_OP_DELIVER) -- undeliverable, or the fork_ of the handler: the
+// deliverer's resume at t + 1 on the sending node and the handler's first pop
+// at t (TimedT.hs:326-342, MonadDialog.hs:317); the handler's code (the hot
+// classes of Lane::pass; TW_OP_SEND's LP branch); the resume of the send's
+// 1-µs yield, whose instruction is END.  ok = 0: the record runs on the chain.
+// FX: also adds the other nodes' hash terms and emits the send's record.
+struct DueX {
+    uint32_t ok, yld, dl, ud, dr, ev, th, sq, direct;
+    int64_t fin, last;  // final_t candidate, the lane's clock after the record
+    uint64_t h;         // terms of the lane's own node
+};
+// Lane::emit for a record of the batch (the thread's own append: no wave
+// aggregation); returns 1 for a record written straight into a light inbox
+__device__ __forceinline__ uint32_t due_emit(const Dev& c, uint32_t wid, int64_t ta, int64_t payload, uint32_t link,
+                                             uint32_t kind, uint32_t src, uint32_t dst, uint4 dh) {
+    const uint4 q0 = make_uint4((uint32_t)ta, (uint32_t)((uint64_t)ta >> 32), (uint32_t)payload,
+                                (uint32_t)((uint64_t)payload >> 32));
+    const uint4 q1 = make_uint4(link, kind, src, dst);
+    if (c.dpar && c.win && !(dh.x >> 31) && dst - c.lp0 < c.R) {
+        const uint32_t lp = dst - c.lp0;
+        const uint32_t par = (wid + 1u) & 1u;
+        const uint32_t k = __hip_atomic_fetch_add(gp(c.inbox_n) + (size_t)par * c.R + lp, 1u, __ATOMIC_RELAXED,
+                                                  __HIP_MEMORY_SCOPE_AGENT);
+        if (k >= dh.z) {
+            __hip_atomic_fetch_or(gp(c.lp_err), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            return 0u;
+        }
+        const size_t base = c.ib_off ? ((size_t)dh.y << c.rep_lg) + (dst & ((1u << c.rep_lg) - 1u)) : (size_t)lp;
+        uint4 GAS* q = gp(c.inbox) + ((size_t)par * c.ib_total + base + (size_t)k * ib_stride(c)) * 2;
+        q[0] = q0;
+        q[1] = q1;
+        lp_mark(c, lp, wid);
+        return 1u;
+    }
+    const uint32_t i = __hip_atomic_fetch_add(gp(c.out_n), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (i >= c.out_cap) {
+        __hip_atomic_fetch_or(gp(c.lp_err), 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return 0u;
+    }
+    uint4 GAS* o = gp(c.outbox) + (size_t)i * 2;
+    o[0] = q0;
+    o[1] = q1;
+    return 0u;
+}
+template <bool FX>
+__device__ DueX due_exec(const Dev& c, uint32_t r, uint32_t wid, uint32_t set, uint4 a, uint4 b) {
+    DueX o{};
+    const int64_t t = ent_t(a);
+    const int64_t payload = (int64_t)(((uint64_t)a.w << 32) | a.z);
+    const uint32_t link = b.x, kind = b.y, src = b.z;
+    const uint32_t node = (c.lp0 + r) >> c.rep_lg, rho = (c.lp0 + r) & ((1u << c.rep_lg) - 1u);
+    o.last = t;
+    o.fin = INT64_MIN;
+    uint32_t lpc = TW_PC_NONE;
+    size_t e = 0;
+    if (set && kind < c.n_kinds) {
+        e = (size_t)(set - 1u) * c.n_kinds + kind;
+        lpc = gp(c.lpc)[e];
+    }
+    if (lpc == TW_PC_NONE) {  // no listener: undeliverable, the phantom deliverer ends
+        o.ok = 1;
+        o.ud = 1;
+        o.h = term(t, TW_KIND_UNDELIV | kind, payload);
+        return o;
+    }
+    if ((lpc & TW_LPC_INLINE) || !gp(c.lpc_bat)[e]) return o;
+    o.dl = 1;
+    o.ev = 2;
+    o.th = 1;
+    o.sq = 1;
+    o.fin = t + 1;
+    o.h = term(t, TW_KIND_RECV | kind, payload) + term0(t, TW_KIND_RESUME | (lpc & 0xFFFFu));
+    {
+        const uint64_t hs = term0(t + 1, TW_KIND_RESUME | (TW_PC_DELIVER_STUB + 2));
+        if (src == node) o.h += hs;
+        else if (FX)
+            __hip_atomic_fetch_add((unsigned long long GAS*)(gp(c.hash_g) + (((size_t)src << c.rep_lg) | rho)),
+                                   (unsigned long long)hs, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    int64_t rr[4] = {payload, (int64_t)link, (int64_t)src, (int64_t)kind};
+    uint32_t pc = lpc & 0xFFFFu;
+    for (uint32_t n = 0; n <= c.n_insns; ++n) {  // (forward control flow only: classify_batch)
+        if (pc >= c.n_insns) break;
+        const uint2 in = gp(c.insns)[pc];
+        const uint32_t w = in.x, op = w & 0xFFu, ai = (w >> 8) & 3u, b16 = w >> 16;
+        const int32_t imm = (int32_t)in.y;
+        const int64_t ra = rr[ai], rb = rr[b16 & 3u];
+        if (op == TW_OP_END) {
+            o.ok = 1;
+            return o;
+        }
+        uint32_t tgt = pc + 1;
+        if (op == TW_OP_SEND) {
+            uint64_t lk = (uint64_t)ra;
+            bool lbad = false;
+            const bool fz = (b16 & (TW_SEND_VIA_LINK | TW_SEND_VIA_RLINK)) != 0;
+            if (b16 & TW_SEND_VIA_LINK) {
+                lk = (uint64_t)((int64_t)gp(c.out_off)[node] + imm);
+            } else if (b16 & TW_SEND_VIA_RLINK) {
+                const uint64_t rin = (uint64_t)rr[(b16 >> 12) & 3u];
+                lbad = rin >= c.L;
+                if (!lbad) lk = gp(c.link_rev)[rin];
+            }
+            if (lbad || lk >= c.L) break;  // the replica's error: the chain reports it
+            const uint32_t k2 = b16 & 0xFFu, pr = (b16 >> 8) & 3u;
+            const int64_t pay = (fz && pr == ai) ? (int64_t)lk : rr[pr];
+            tgt = fz ? pc + 2 : pc + 1;
+            if (tgt >= c.n_insns || (gp(c.insns)[tgt].x & 0xFFu) != TW_OP_END) break;
+            const uint32_t ent = c.link_table ? gp(c.link_table)[(((size_t)lk * c.D) << c.rep_lg) + rho] : 0u;
+            if (ent & TW_LINK_DROP) {  // dropped: the handler goes on to its END at t
+                o.dr += 1;
+                o.h += term(t, TW_KIND_DROP | k2, pay);
+                pc = tgt;
+                continue;
+            }
+            const int64_t dly = (int64_t)(ent & 0x7FFFFFFFu) + tx_us(c, lk, k2);
+            if (dly < c.lookahead) break;  // (no two-phase windows with lpc_bat)
+            const int64_t ta = t + dly;
+            o.h += term0(t, TW_KIND_RESUME | TW_PC_DELIVER_STUB) + term0(ta, TW_KIND_RESUME | (TW_PC_DELIVER_STUB + 1));
+            o.ev += 2;
+            o.th += 1;
+            o.fin = ta > o.fin ? ta : o.fin;
+            if (FX) {
+                const uint4 dh = gp(c.link_dsth)[lk];
+                o.direct |= due_emit(c, wid, ta, pay, (uint32_t)lk, k2, node,
+                                     ((dh.x & 0x7FFFFFFFu) << c.rep_lg) | rho, dh);
+            }
+            // the send's 1-µs yield (a fork: TimedT.hs:340); the resume runs END
+            o.sq += 1;
+            o.ev += 1;
+            o.yld = 1;
+            o.h += term0(t + 1, TW_KIND_RESUME | (tgt & 0xFFFFu));
+            o.last = t + 1;
+            o.ok = 1;
+            return o;
+        }
+        const uint32_t f = uop_insn(w);
+        if ((f & (U_FX | U_NS)) || U_TK(f) != TK_NONE) break;  // (not admitted by classify_batch)
+        const uint32_t ak = U_ALU(f), ld = U_LD(f), jm = U_JM(f);
+        bool wr = false;
+        int64_t v = 0;
+        if (ak != A_NONE) {
+            if (ak == A_TID) break;
+            v = ak == A_IMM ? (int64_t)imm : ak == A_K ? gp(c.consts)[imm] : ak == A_ADDI ? ra + (int64_t)imm
+                : ak == A_MULI ? ra * (int64_t)imm : ak == A_MOV ? rb : ak == A_ADD ? ra + rb
+                : ak == A_SUB ? ra - rb : ak == A_NOW ? t : (int64_t)node;
+            wr = true;
+        }
+        if (ld == LD_NV) {
+            v = gp(c.nvars)[(size_t)(b16 & 3u) * c.R + r];
+            wr = true;
+        } else if (ld == LD_OUT) {
+            v = (int64_t)gp(c.out_off)[node] + imm;
+            wr = true;
+        } else if (ld == LD_RL) {
+            if ((uint64_t)rb >= c.L) break;
+            v = (int64_t)gp(c.link_rev)[rb];
+            wr = true;
+        }
+        if (f & U_TR) o.h += term(t, TW_KIND_TRACE | ((uint32_t)imm & 0xFFFFu), ra);
+        if (f & U_TR2) o.h += term(t, TW_KIND_TRACE | (b16 & 0x1FFFu), rr[(b16 >> 13) & 3u]);
+        if (f & U_P2) tgt = pc + 2;
+        if (jm != JM_NONE) {
+            const int64_t bb = (int64_t)(int16_t)b16;
+            const uint32_t ci = (ra == rb ? 1u : 0u) | (ra < rb ? 2u : 0u) | (ra == bb ? 4u : 0u);
+            tgt = ((jm >> ci) & 1u) ? (uint32_t)imm : tgt;
+        }
+        if (wr) rr[ai] = v;
+        pc = tgt;
+    }
+    o.ok = 0;  // an error or a path outside the admitted code: the chain runs it
+    return o;
+}
+
 __global__ void __launch_bounds__(256) tw_lp_due(Dev c) {
     const int64_t GAS* w = gp(c.win);
     const int64_t fl = w[WN_FLAGS];
@@ -3566,6 +3753,7 @@ __global__ void __launch_bounds__(256) tw_lp_due(Dev c) {
             sc[SC_DUE_SEQ] = s0;
             sc[SC_DUE_N] = nd;
             sc[SC_DUE_H] = 0;
+            if (c.bat_ctr) atomicAdd(gp(c.bat_ctr) + 1, (unsigned long long)nd);
             if (smin != ~0ull)
                 __hip_atomic_fetch_min(c.rw ? (uint64_t GAS*)rw_at(c, RW_WIN, r) : gp(c.pend_min), (uint64_t)smin,
                                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -3578,6 +3766,237 @@ __global__ void __launch_bounds__(256) tw_lp_due(Dev c) {
                                                           __HIP_MEMORY_SCOPE_AGENT);
                 if (i < c.R) gp(c.heavy)[(size_t)l * c.R + i] = r;
                 else __hip_atomic_fetch_or(gp(c.lp_err), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+        __syncthreads();
+    }
+}
+
+
+// The batch of a window's first tick, after tw_lp_due sorted the heavy lanes'
+// due runs and the work list was built (the senders' inbox marks of this
+// batch are for the next window's list: made before tw_lpb_compact, they would
+// hide the marks it reads).  One workgroup per heavy lane, the due records
+// staged in LDS in due-run order.
+__global__ void __launch_bounds__(256) tw_lp_batch(Dev c) {
+    const int64_t GAS* w = gp(c.win);
+    const int64_t fl = w[WN_FLAGS];
+    if (!(fl & WN_FRESH) || (fl & WN_DONE) || !c.lpc_bat) return;
+    const uint32_t wid = (uint32_t)w[WN_WID];
+    const int64_t T0 = w[WN_T], L = w[WN_L];
+    const uint32_t lst = wid & 1u;
+    uint32_t nh = gp(c.heavy_n)[lst];
+    nh = nh < c.R ? nh : c.R;
+    __shared__ uint4 ea[TW_HEAVY_CAP], eb[TW_HEAVY_CAP];
+    __shared__ uint16_t dix[TW_HEAVY_CAP];  // per record: batchable | yielded << 1
+    __shared__ uint32_t bws[TW_HEAVY_CAP];  // the replayed free stack's pushes
+    __shared__ uint32_t bEl, bSet, bK0, bK, bDirect, bFn, bFtop, bBump, bNd;
+    __shared__ int64_t bTo, cmx[256];
+    __shared__ uint32_t bslot[TW_HEAVY_CAP], bO[32];
+    __shared__ unsigned long long bH, bsum[7];
+    __shared__ long long bFin, bLast;
+    const uint32_t tid = threadIdx.x;
+    const size_t st = ib_stride(c);
+    for (uint32_t hi = blockIdx.x; hi < nh; hi += gridDim.x) {
+        const uint32_t r = gp(c.heavy)[(size_t)lst * c.R + hi];
+        const int64_t T = c.rw ? *rw_at(c, RW_T, r) : T0;
+        if (T == INT64_MAX) continue;
+        const int64_t tend = T + L - 1;
+        if (tid == 0) {
+            const uint64_t GAS* sc = gp(c.scal) + (size_t)r * SC_LP_STRIDE;
+            bNd = sc[SC_DUE_H] == 0 ? (uint32_t)sc[SC_DUE_N] : 0u;  // (tw_lp_due's fresh run)
+        }
+        __syncthreads();
+        const uint32_t nd = bNd;
+        if (!nd) { __syncthreads(); continue; }
+        const size_t ib = ib_base(c, r);
+        for (uint32_t i = tid; i < nd; i += 256) {
+            const uint4 GAS* q = gp(c.due) + (ib + (size_t)i * st) * 2;
+            ea[i] = q[0];
+            eb[i] = q[1];
+        }
+        // ---- the due run's prefix executed data-parallel (due_exec) ----
+        // Every record's events (the wake at t, the handler at t, the send's
+        // resume at t + 1) must precede the lane's next queued event (bTo); the
+        // prefix ends where a record is not batchable, and before a record whose
+        // wake would fall before an earlier record's resume (the alloc / free
+        // order of their slots would interleave).  Within the prefix the slots'
+        // alloc / free order is replayed exactly (thread 0), so the free stack
+        // ends as the chain leaves it.
+        if (tid == 0) {
+            const uint64_t GAS* sc = gp(c.scal) + (size_t)r * SC_LP_STRIDE;
+            bool el = nd && c.trace_cap == 0 && c.tie_mode == TW_TIE_FIFO &&
+                      sc[SC_STATUS] == TW_REP_RUNNING && sc[SC_PENDING_MAIN] == 0 && !(c.lpb && gp(c.spawn_n)[r]) &&
+                      sc[SC_SEQ] + 3ull * nd < 0xFFFFFFFFull && sc[SC_TIDC] + nd < 0xFFFFFFFFull;
+            int64_t to = INT64_MAX;
+            const uint32_t nn = el ? (uint32_t)sc[SC_NEAR_N] : 0u;
+            for (uint32_t j = 0; j < nn; ++j) {
+                const int64_t x = ent_t(gp(c.near_spill)[(size_t)j * c.R + r]);
+                to = x < to ? x : to;
+            }
+            if (el && sc[SC_FAR_N]) {
+                const int64_t x = ent_t(gp(c.far)[r]);
+                to = x < to ? x : to;
+            }
+            const uint32_t own = gp(c.bind_own)[r], rel = gp(c.bind_rel)[r];
+            bSet = own == rel ? 0u : gp(c.bind)[r];
+            bTo = to;
+            bEl = el ? 1u : 0u;
+            bK0 = nd;
+            bK = 0;
+            bDirect = 0;
+            bH = 0;
+            bFin = INT64_MIN;
+            bLast = INT64_MIN;
+            for (int j = 0; j < 7; ++j) bsum[j] = 0;
+            bFn = (uint32_t)sc[SC_FREE_N];
+            bFtop = (uint32_t)sc[SC_FTOP];
+            bBump = (uint32_t)sc[SC_BUMP];
+        }
+        __syncthreads();
+        if (bEl) {
+            // dry run: per record (due order) ok | yielded << 1 into dix
+            for (uint32_t i = tid; i < nd; i += 256) {
+                const DueX x = due_exec<false>(c, r, wid, bSet, ea[i], eb[i]);
+                const bool ok = x.ok && x.last < bTo;
+                dix[i] = (uint16_t)((ok ? 1u : 0u) | (x.yld ? 2u : 0u));
+                if (!ok) atomicMin(&bK0, i);
+            }
+            if (tid < 32u && tid < bFn)  // the free stack's top 32 entries
+                bO[tid] = tid == 0 ? bFtop : gp(c.free_stk)[(size_t)(bFn - 1u - tid) * c.R + r];
+            __syncthreads();
+            const uint32_t K0 = bK0;
+            // the latest resume among records before each position: chunks of 8
+            // per thread, an exclusive prefix max over the chunks (thread 0)
+            int64_t cm = INT64_MIN;
+            for (uint32_t j = 0; j < 8; ++j) {
+                const uint32_t i = tid * 8 + j;
+                if (i < K0 && (dix[i] & 2u)) {
+                    const int64_t x = ent_t(ea[i]) + 1;
+                    cm = x > cm ? x : cm;
+                }
+            }
+            cmx[tid] = cm;
+            __syncthreads();
+            if (tid == 0) {
+                int64_t m = INT64_MIN;
+                for (uint32_t j = 0; j < 256; ++j) {
+                    const int64_t x = cmx[j];
+                    cmx[j] = m;
+                    m = x > m ? x : m;
+                }
+                if (K0 == nd) bK = nd;
+            }
+            __syncthreads();
+            {
+                int64_t m = cmx[tid];
+                for (uint32_t j = 0; j < 8; ++j) {
+                    const uint32_t i = tid * 8 + j;
+                    if (i > K0 || i >= nd) break;
+                    const int64_t ti = ent_t(ea[i]);
+                    if (m < ti) atomicMax(&bK, i);  // (i = 0 always: m = INT64_MIN)
+                    if (i < K0 && (dix[i] & 2u)) m = ti + 1 > m ? ti + 1 : m;
+                }
+            }
+            __syncthreads();
+            if (tid == 0 && bK) {
+                // the slots' alloc (a wake) / free (a thread's end) order of the
+                // prefix, as the chain runs it: a record that yielded holds its
+                // slot until its resume at t + 1 (after every wake at that time:
+                // their seqs are older); the others free it at once
+                const uint32_t K = bK, fn = bFn;
+                uint32_t* ws = bws;
+                uint32_t wsn = 0, used = 0, bump = bBump, rp = 0;
+                bool okk = true;
+                auto pop = [&]() -> uint32_t {
+                    if (wsn) return ws[--wsn];
+                    if (used < fn) {
+                        if (used >= 32u) { okk = false; return 0u; }
+                        return bO[used++];
+                    }
+                    if (bump < c.S) return bump++;
+                    okk = false;
+                    return 0u;
+                };
+                for (uint32_t i = 0; i < K && okk; ++i) {
+                    const int64_t ti = ent_t(ea[i]);
+                    while (rp < i) {
+                        if (!(dix[rp] & 2u)) { ++rp; continue; }
+                        if (ent_t(ea[rp]) + 1 < ti) { ws[wsn++] = bslot[rp]; ++rp; }
+                        else break;
+                    }
+                    const uint32_t sl = pop();
+                    if (dix[i] & 2u) bslot[i] = sl;
+                    else ws[wsn++] = sl;
+                }
+                for (; rp < K && okk; ++rp)
+                    if (dix[rp] & 2u) ws[wsn++] = bslot[rp];
+                if (!okk) {
+                    bK = 0;
+                } else {
+                    // the stack: the untouched bottom fn - used entries, then ws
+                    const uint32_t rest = fn - used;
+                    uint32_t top = bFtop;
+                    if (wsn) {
+                        if (used == 0 && fn) gp(c.free_stk)[(size_t)(fn - 1u) * c.R + r] = bFtop;
+                        for (uint32_t j = 0; j + 1 < wsn; ++j) gp(c.free_stk)[(size_t)(rest + j) * c.R + r] = ws[j];
+                        top = ws[wsn - 1];
+                    } else if (rest) {
+                        top = used < 32u ? bO[used] : gp(c.free_stk)[(size_t)(rest - 1u) * c.R + r];
+                    }
+                    bFn = rest + wsn;
+                    bFtop = top;
+                    bBump = bump;
+                }
+            }
+            __syncthreads();
+            // the prefix for real: other nodes' hash terms, the sends' records
+            const uint32_t K = bK;
+            uint64_t h = 0;
+            uint32_t sm[7] = {0, 0, 0, 0, 0, 0, 0}, dir = 0;
+            int64_t fin = INT64_MIN, last = INT64_MIN;
+            for (uint32_t i = tid; i < K; i += 256) {
+                const DueX x = due_exec<true>(c, r, wid, bSet, ea[i], eb[i]);
+                h += x.h;
+                sm[0] += x.dl; sm[1] += x.ud; sm[2] += x.dr; sm[3] += x.ev; sm[4] += x.th; sm[5] += x.sq;
+                dir |= x.direct;
+                fin = x.fin > fin ? x.fin : fin;
+                last = x.last > last ? x.last : last;
+            }
+            if (K) {
+                if (h) atomicAdd(&bH, (unsigned long long)h);
+                for (int j = 0; j < 6; ++j)
+                    if (sm[j]) atomicAdd(&bsum[j], (unsigned long long)sm[j]);
+                if (dir) bDirect = 1;
+                atomicMax(&bFin, (long long)fin);
+                atomicMax(&bLast, (long long)last);
+            }
+            __syncthreads();
+        }
+        if (tid == 0 && bEl && bK) {
+            uint64_t GAS* sc = gp(c.scal) + (size_t)r * SC_LP_STRIDE;
+            const uint32_t K = bK;
+            sc[SC_SEQ] += bsum[5];  // (after the due run's reserved seqs)
+            sc[SC_DUE_H] = K;
+            if (c.bat_ctr) atomicAdd(gp(c.bat_ctr), (unsigned long long)K);
+            if (K) {  // the batched prefix's totals (due_exec), as its events on the chain add them
+                sc[SC_DELIVERED] += bsum[0];
+                sc[SC_UNDELIV] += bsum[1];
+                sc[SC_DROPPED] += bsum[2];
+                sc[SC_EVENTS] += bsum[3];
+                sc[SC_THREADS] += bsum[4];
+                sc[SC_TIDC] += bsum[0];  // (a thread id per handler)
+                sc[SC_FREE_N] = bFn;
+                sc[SC_FTOP] = bFtop;
+                sc[SC_BUMP] = bBump;
+                if ((int64_t)sc[SC_NOW] < (int64_t)bLast) sc[SC_NOW] = (uint64_t)bLast;
+                if ((int64_t)sc[SC_FINAL_T] < (int64_t)bFin) sc[SC_FINAL_T] = (uint64_t)bFin;
+                if (bH)
+                    __hip_atomic_fetch_add((unsigned long long GAS*)(gp(c.hash_g) + c.lp0 + r), bH, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+                if (bDirect)  // sent records straight into inboxes (Lane::emit, the event kernel's epilogue)
+                    min_hot(c.rw ? (uint64_t GAS*)rw_at(c, RW_WIN, r) : (uint64_t GAS*)(gp(c.win) + WN_REC_MIN),
+                            (uint64_t)(tend + 1));
             }
         }
         __syncthreads();

@@ -49,6 +49,7 @@ TW_HIDDEN int sh_lp_take_outbox(tw_shard* c, tw_lp_record* out, size_t cap, size
 TW_HIDDEN int sh_lp_inject(tw_shard* c, const tw_lp_record* recs, size_t n, int64_t* next_t);
 TW_HIDDEN int sh_lp_results(tw_shard* c, tw_replica_result* agg, uint64_t* node_hashes, size_t n_nodes);
 TW_HIDDEN int sh_lpb_windows(tw_shard* c, uint64_t* windows, uint64_t* ticks);
+TW_HIDDEN int sh_lpb_batch(tw_shard* c, uint64_t* batched, uint64_t* due);
 TW_HIDDEN int sh_set_stream(tw_shard* c, void* hip_stream);
 TW_HIDDEN int sh_lp_exchange_setup(tw_shard* c, uint32_t world, uint32_t rank, const uint32_t* starts, void* send,
                                    void* recv, uint32_t cap, int64_t* red);

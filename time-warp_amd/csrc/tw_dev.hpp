@@ -195,6 +195,11 @@ struct Dev {
     const uint64_t* link_bw;    // [L] or null
     uint32_t tie_mode;          // TW_TIE_*: order of equal-timestamp events
     const uint8_t* pc_cls;      // [n_insns + 1] wave kernel: batch class of each resume pc (classify_pcs)
+    // batched LP: [n_sets * n_kinds] 1 where the fork_-dispatched handler of a
+    // (listener set, kind) may run data-parallel over a heavy lane's due run
+    // (classify_batch, tw_lp_due); null: every due record runs on the lane's chain
+    const uint8_t* lpc_bat;
+    unsigned long long* bat_ctr;  // [2] batched LP since tw_reset: due records run by tw_lp_due, all due records
     uint32_t wave_k;            // wave kernel: near-queue entries per lane (4, 24 or 32), fixed by tw_load
     // wave kernel, tie mode TW_TIE_PQUEUE: each replica's queue is a binomial
     // MinQueue whose nodes are far[r * Q + i] (entries) + pq_link[r * Q + i]

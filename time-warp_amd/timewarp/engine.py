@@ -30,7 +30,7 @@ EXPORTS = ["tw_create", "tw_comm_id", "tw_create_rank", "tw_ctx_info", "tw_lp_ru
            "tw_set_trace", "tw_read_trace", "tw_tie_audit", "tw_set_counter_base", "tw_geometry",
            "tw_set_stream", "tw_lp_exchange_setup", "tw_lp_loop_begin", "tw_lp_tick", "tw_lp_tick_import",
            "tw_lp_tick_end", "tw_lp_progress", "tw_lp_run_windows", "tw_lpb_load", "tw_lpb_windows",
-           "tw_draw_link_table"]
+           "tw_draw_link_table", "tw_lpb_batch"]
 GEOMETRIES = ("dense", "sparse", "half", "wave", "lp", "narrow", "lpb", "compact")  # TW_GEO_* order
 
 # tw_trace_rec (include/timewarp.h)
@@ -104,13 +104,14 @@ def load_library(path: Optional[str] = None):
     lib.tw_lp_run_windows.argtypes = [C.c_void_p, C.c_uint64, C.POINTER(TwLpState)]
     lib.tw_lpb_load.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p, C.c_uint32, C.c_uint32]
     lib.tw_lpb_windows.argtypes = [C.c_void_p, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
+    lib.tw_lpb_batch.argtypes = [C.c_void_p, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
     lib.tw_draw_link_table.argtypes = [C.c_int, C.POINTER(TwTableDraw), C.c_void_p]
     for name in ("tw_create", "tw_comm_id", "tw_create_rank", "tw_ctx_info", "tw_lp_run", "tw_set_tie_mode", "tw_load", "tw_reset", "tw_run", "tw_read_results", "tw_read_hashes", "tw_read_final",
                  "tw_last_launch_ms", "tw_lp_load", "tw_lp_window", "tw_lp_take_outbox", "tw_lp_inject",
                  "tw_lp_results", "tw_set_trace", "tw_read_trace", "tw_tie_audit", "tw_set_counter_base",
                  "tw_geometry", "tw_set_stream", "tw_lp_exchange_setup", "tw_lp_loop_begin", "tw_lp_tick",
                  "tw_lp_tick_import", "tw_lp_tick_end", "tw_lp_progress", "tw_lp_run_windows", "tw_lpb_load",
-                 "tw_lpb_windows", "tw_draw_link_table"):
+                 "tw_lpb_windows", "tw_draw_link_table", "tw_lpb_batch"):
         getattr(lib, name).restype = C.c_int
     if path is None:
         _lib = lib
@@ -279,6 +280,13 @@ class Engine:
         w, t = C.c_uint64(), C.c_uint64()
         _check(self.lib.tw_lpb_windows(self.ctx, C.byref(w), C.byref(t)), "tw_lpb_windows")
         return int(w.value), int(t.value)
+
+    def lpb_batch(self):
+        """(batched, due): batched-LP due records since the last reset that ran
+        data-parallel in tw_lp_due, and all due records (tw_lpb_batch)."""
+        b, d = C.c_uint64(), C.c_uint64()
+        _check(self.lib.tw_lpb_batch(self.ctx, C.byref(b), C.byref(d)), "tw_lpb_batch")
+        return int(b.value), int(d.value)
 
     def geometry(self) -> str:
         """The kernel geometry tw_load chose (GEOMETRIES)."""

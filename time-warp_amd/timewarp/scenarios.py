@@ -267,7 +267,7 @@ def hotspot(n_senders: int = 256, n_replicas: int = 1, msg_num: int = 1000, msg_
             duration_s: int = 10, network_delay=(ms(1), ms(5)), seed_base: int = 0,
             near_horizon_us: int = sec(10), fork_strategy: str = "fork", payload_bytes: int = 0,
             bandwidth_bytes_per_s: float = 0.0, probe_traces: int = 0, probe_loads: int = 0,
-            drawer=None) -> Scenario:
+            drop_log2: int = 0, receiver_counter: bool = False, drawer=None) -> Scenario:
     """bench/Network many-senders -> one-receiver request/response.
 
     Sender (Sender/Main.hs:34-64): listen for Pong, then per message
@@ -284,6 +284,10 @@ def hotspot(n_senders: int = 256, n_replicas: int = 1, msg_num: int = 1000, msg_
     ``probe_traces`` / ``probe_loads`` (diagnostics only, tools/pass_probe.py)
     add that many trace / node-variable load instructions to the Ping handler:
     the receiver's cost per instruction pass and per dependent memory load.
+
+    ``drop_log2 > 0`` drops each send with probability 2^-drop_log2 (tests);
+    ``receiver_counter`` makes the Ping handler count its pings in a node
+    variable (a stateful handler: tests of the batched delivery's classifier).
 
     ``bandwidth_bytes_per_s > 0`` adds each message's transmission time to its
     link delay: the BinaryP wire size of `Ping/Pong MsgId Payload` with a
@@ -320,6 +324,8 @@ def hotspot(n_senders: int = 256, n_replicas: int = 1, msg_num: int = 1000, msg_
         c.trace(TAG_PING, 0)
     for _ in range(int(probe_loads)):
         c.nload(3, 2)
+    if receiver_counter:
+        c.nload(3, 0).addi(3, 1).nstore(3, 0)
     c.trace(TAG_PING, 0)                              # logMeasure PingReceived mid
     c.trace(TAG_PONG_SENT, 0)                         # logMeasure PongSent mid
     c.reply_link(2, 1).send(2, K_PONG, 0)
@@ -351,7 +357,7 @@ def hotspot(n_senders: int = 256, n_replicas: int = 1, msg_num: int = 1000, msg_
     out = [[RECV] for _ in range(S)] + [list(range(S)), []]
     topo = Topology.from_out_lists(S + 2, out)
     table = draw_table(topo.n_links, n_replicas, np.arange(topo.n_links), *network_delay, seed_base=seed_base,
-                       drawer=drawer)
+                       drop_log2=drop_log2, drawer=drawer)
     if bandwidth_bytes_per_s > 0:
         from .wire import bench_message_size, transmission_us
         table[:S] += transmission_us(bench_message_size("Ping", payload_bytes), bandwidth_bytes_per_s)
