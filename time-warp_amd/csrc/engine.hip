@@ -547,8 +547,8 @@ static int load_common(tw_shard* c, const tw_scenario_desc* s, bool lp, uint32_t
         ALLOC(lbw, d.L);
     }
 #ifdef TW_STATS
-    ALLOC(d.prof, 2 * P_COUNT);
-    HIPCHK(hipMemsetAsync(d.prof, 0, 16 * P_COUNT, c->stream));
+    ALLOC(d.prof, 2 * P_COUNT + TW_BPROF);
+    HIPCHK(hipMemsetAsync(d.prof, 0, 8 * (2 * P_COUNT + TW_BPROF), c->stream));
 #endif
     uint32_t* iboff = nullptr;
     std::vector<uint32_t> h_iboff;
@@ -1580,10 +1580,11 @@ int sh_lpb_batch(tw_shard* c, uint64_t* batched, uint64_t* due) {
 int sh_prof_read(tw_shard* c, unsigned long long* out, size_t cap, int reset) {
 #ifdef TW_STATS
     if (!c || !out || !c->loaded || !c->d.prof) return TW_ERR_STATE;
-    size_t n = cap < (size_t)2 * P_COUNT ? cap : (size_t)2 * P_COUNT;  // all lanes, then heavy LP lanes
+    const size_t all = (size_t)2 * P_COUNT + TW_BPROF;  // all lanes, heavy LP lanes, tw_lp_batch's phases
+    size_t n = cap < all ? cap : all;
     HIPCHK(hipSetDevice(c->device));
     HIPCHK(hipMemcpy(out, c->d.prof, 8 * n, hipMemcpyDeviceToHost));
-    if (reset) HIPCHK(hipMemset(c->d.prof, 0, 16 * P_COUNT));
+    if (reset) HIPCHK(hipMemset(c->d.prof, 0, 8 * all));
     return (int)n;
 #else
     (void)c; (void)out; (void)cap; (void)reset;

@@ -78,6 +78,7 @@
 #define TW_LP_WAVES 2
 #endif
 #define P_COUNT 34
+#define TW_BPROF 8  // diagnostic build: tw_lp_batch's phase cycles after the two P_COUNT sets
 // Diagnostic build (-DTW_STATS, lib/libtimewarp_stats.so): per-lane event-path
 // counters summed into Dev::prof at kernel end (tools/stats_probe.py).  The
 // product build compiles every STAT to nothing.
@@ -3443,11 +3444,17 @@ __device__ __forceinline__ uint4 due_rec_b(const Dev& c, uint4 b) {
 // at t (TimedT.hs:326-342, MonadDialog.hs:317); the handler's code (the hot
 // classes of Lane::pass; TW_OP_SEND's LP branch); the resume of the send's
 // 1-µs yield, whose instruction is END.  ok = 0: the record runs on the chain.
-// FX: also adds the other nodes' hash terms and emits the send's record.
+// The effects beyond the lane itself come back as data (due_effects makes
+// them): the deliverer's resume term on the sending node, the send's record.
 struct DueX {
-    uint32_t ok, yld, dl, ud, dr, ev, th, sq, direct;
+    uint32_t ok, yld, dl, ud, dr, ev, th, sq;
     int64_t fin, last;  // final_t candidate, the lane's clock after the record
     uint64_t h;         // terms of the lane's own node
+    uint64_t hs;        // the term of the sending node (0: none or the lane's own)
+    uint32_t hs_lane;   // its lane
+    uint32_t lk, k2, dst;  // the send's record (yld): link, kind, destination lane
+    int64_t ta, pay;
+    uint4 dh;
 };
 // Lane::emit for a record of the batch (the thread's own append: no wave
 // aggregation); returns 1 for a record written straight into a light inbox
@@ -3482,9 +3489,17 @@ __device__ __forceinline__ uint32_t due_emit(const Dev& c, uint32_t wid, int64_t
     o[1] = q1;
     return 0u;
 }
-template <bool FX>
-__device__ DueX due_exec(const Dev& c, uint32_t r, uint32_t wid, uint32_t set, uint4 a, uint4 b) {
+// (the program image, constant pool, listener table and its batchable flags
+// staged in LDS by tw_lp_batch: BP)
+struct BProg {
+    const uint2 LAS* P;
+    const int64_t LAS* K;
+    const uint32_t LAS* LPC;
+    const uint8_t LAS* BAT;
+};
+__device__ DueX due_exec(const Dev& c, const BProg& bp, uint32_t r, uint32_t set, uint4 a, uint4 b) {
     DueX o{};
+    o.hs_lane = 0xFFFFFFFFu;
     const int64_t t = ent_t(a);
     const int64_t payload = (int64_t)(((uint64_t)a.w << 32) | a.z);
     const uint32_t link = b.x, kind = b.y, src = b.z;
@@ -3495,7 +3510,7 @@ __device__ DueX due_exec(const Dev& c, uint32_t r, uint32_t wid, uint32_t set, u
     size_t e = 0;
     if (set && kind < c.n_kinds) {
         e = (size_t)(set - 1u) * c.n_kinds + kind;
-        lpc = gp(c.lpc)[e];
+        lpc = bp.LPC[e];
     }
     if (lpc == TW_PC_NONE) {  // no listener: undeliverable, the phantom deliverer ends
         o.ok = 1;
@@ -3503,7 +3518,7 @@ __device__ DueX due_exec(const Dev& c, uint32_t r, uint32_t wid, uint32_t set, u
         o.h = term(t, TW_KIND_UNDELIV | kind, payload);
         return o;
     }
-    if ((lpc & TW_LPC_INLINE) || !gp(c.lpc_bat)[e]) return o;
+    if ((lpc & TW_LPC_INLINE) || !bp.BAT[e]) return o;
     o.dl = 1;
     o.ev = 2;
     o.th = 1;
@@ -3512,16 +3527,18 @@ __device__ DueX due_exec(const Dev& c, uint32_t r, uint32_t wid, uint32_t set, u
     o.h = term(t, TW_KIND_RECV | kind, payload) + term0(t, TW_KIND_RESUME | (lpc & 0xFFFFu));
     {
         const uint64_t hs = term0(t + 1, TW_KIND_RESUME | (TW_PC_DELIVER_STUB + 2));
-        if (src == node) o.h += hs;
-        else if (FX)
-            __hip_atomic_fetch_add((unsigned long long GAS*)(gp(c.hash_g) + (((size_t)src << c.rep_lg) | rho)),
-                                   (unsigned long long)hs, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (src == node) {
+            o.h += hs;
+        } else {
+            o.hs = hs;
+            o.hs_lane = (src << c.rep_lg) | rho;
+        }
     }
     int64_t rr[4] = {payload, (int64_t)link, (int64_t)src, (int64_t)kind};
     uint32_t pc = lpc & 0xFFFFu;
     for (uint32_t n = 0; n <= c.n_insns; ++n) {  // (forward control flow only: classify_batch)
         if (pc >= c.n_insns) break;
-        const uint2 in = gp(c.insns)[pc];
+        const uint2 in = bp.P[pc];
         const uint32_t w = in.x, op = w & 0xFFu, ai = (w >> 8) & 3u, b16 = w >> 16;
         const int32_t imm = (int32_t)in.y;
         const int64_t ra = rr[ai], rb = rr[b16 & 3u];
@@ -3545,7 +3562,7 @@ __device__ DueX due_exec(const Dev& c, uint32_t r, uint32_t wid, uint32_t set, u
             const uint32_t k2 = b16 & 0xFFu, pr = (b16 >> 8) & 3u;
             const int64_t pay = (fz && pr == ai) ? (int64_t)lk : rr[pr];
             tgt = fz ? pc + 2 : pc + 1;
-            if (tgt >= c.n_insns || (gp(c.insns)[tgt].x & 0xFFu) != TW_OP_END) break;
+            if (tgt >= c.n_insns || (bp.P[tgt].x & 0xFFu) != TW_OP_END) break;
             const uint32_t ent = c.link_table ? gp(c.link_table)[(((size_t)lk * c.D) << c.rep_lg) + rho] : 0u;
             if (ent & TW_LINK_DROP) {  // dropped: the handler goes on to its END at t
                 o.dr += 1;
@@ -3560,11 +3577,12 @@ __device__ DueX due_exec(const Dev& c, uint32_t r, uint32_t wid, uint32_t set, u
             o.ev += 2;
             o.th += 1;
             o.fin = ta > o.fin ? ta : o.fin;
-            if (FX) {
-                const uint4 dh = gp(c.link_dsth)[lk];
-                o.direct |= due_emit(c, wid, ta, pay, (uint32_t)lk, k2, node,
-                                     ((dh.x & 0x7FFFFFFFu) << c.rep_lg) | rho, dh);
-            }
+            o.dh = gp(c.link_dsth)[lk];
+            o.lk = (uint32_t)lk;
+            o.k2 = k2;
+            o.dst = ((o.dh.x & 0x7FFFFFFFu) << c.rep_lg) | rho;
+            o.ta = ta;
+            o.pay = pay;
             // the send's 1-µs yield (a fork: TimedT.hs:340); the resume runs END
             o.sq += 1;
             o.ev += 1;
@@ -3581,7 +3599,7 @@ __device__ DueX due_exec(const Dev& c, uint32_t r, uint32_t wid, uint32_t set, u
         int64_t v = 0;
         if (ak != A_NONE) {
             if (ak == A_TID) break;
-            v = ak == A_IMM ? (int64_t)imm : ak == A_K ? gp(c.consts)[imm] : ak == A_ADDI ? ra + (int64_t)imm
+            v = ak == A_IMM ? (int64_t)imm : ak == A_K ? bp.K[imm] : ak == A_ADDI ? ra + (int64_t)imm
                 : ak == A_MULI ? ra * (int64_t)imm : ak == A_MOV ? rb : ak == A_ADD ? ra + rb
                 : ak == A_SUB ? ra - rb : ak == A_NOW ? t : (int64_t)node;
             wr = true;
@@ -3610,6 +3628,15 @@ __device__ DueX due_exec(const Dev& c, uint32_t r, uint32_t wid, uint32_t set, u
     }
     o.ok = 0;  // an error or a path outside the admitted code: the chain runs it
     return o;
+}
+// The effects of a batched record beyond its lane (due_exec's data): the
+// sending node's term, the send's record; returns 1 for a record written
+// straight into a light inbox
+__device__ __forceinline__ uint32_t due_effects(const Dev& c, uint32_t wid, uint32_t node, const DueX& x) {
+    if (x.hs_lane != 0xFFFFFFFFu)
+        __hip_atomic_fetch_add((unsigned long long GAS*)(gp(c.hash_g) + x.hs_lane), (unsigned long long)x.hs,
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return x.yld ? due_emit(c, wid, x.ta, x.pay, x.lk, x.k2, node, x.dst, x.dh) : 0u;
 }
 
 __global__ void __launch_bounds__(256) tw_lp_due(Dev c) {
@@ -3776,231 +3803,233 @@ __global__ void __launch_bounds__(256) tw_lp_due(Dev c) {
 // The batch of a window's first tick, after tw_lp_due sorted the heavy lanes'
 // due runs and the work list was built (the senders' inbox marks of this
 // batch are for the next window's list: made before tw_lpb_compact, they would
-// hide the marks it reads).  One workgroup per heavy lane, the due records
-// staged in LDS in due-run order.
+// hide the marks it reads).  One workgroup per heavy lane at a time, the first
+// TW_BATCH_CAP records of its due run staged in LDS in due-run order, the
+// program tables staged once per workgroup (a program over the caps is not
+// batched).  Per lane: the eligibility and the lane's next queued event; a dry
+// run of every record -> the longest prefix whose records are batchable,
+// precede that event, and whose resumes precede the next record's wake (a
+// prefix max of the resume times); the prefix's effects (kept from the dry run
+// for each thread's first record); thread 0 adds the totals.
+//
+// The slots: a batched record's phantom and handler thread use a slot from the
+// lane's free stack from its wake to its end on the chain, and the chain's
+// interleaving of those allocations can leave the stack's top entries in
+// another order.  The batch allocates nothing and leaves the stack as it is:
+// the same set of free slots (every batched thread has ended), so capacity
+// failures -- live threads against max_slots -- come out the same, and slot
+// numbers are not observable: a ref (tid << 32 | slot) is an opaque handle
+// whose thread is named by its tid (the oracle's refs carry no slot at all,
+// ref_of in oracle/timedt_oracle.cpp; include/timewarp.h).
+#define TW_BATCH_CAP 1024u    // records per lane and window (the rest stay on the chain)
+#define TW_BATCH_INSNS 512u   // program tables staged in LDS
+#define TW_BATCH_CONSTS 128u
+#define TW_BATCH_LPC 256u
 __global__ void __launch_bounds__(256) tw_lp_batch(Dev c) {
     const int64_t GAS* w = gp(c.win);
     const int64_t fl = w[WN_FLAGS];
     if (!(fl & WN_FRESH) || (fl & WN_DONE) || !c.lpc_bat) return;
+    if (c.n_insns > TW_BATCH_INSNS || c.n_consts > TW_BATCH_CONSTS || c.n_sets * c.n_kinds > TW_BATCH_LPC) return;
     const uint32_t wid = (uint32_t)w[WN_WID];
     const int64_t T0 = w[WN_T], L = w[WN_L];
     const uint32_t lst = wid & 1u;
     uint32_t nh = gp(c.heavy_n)[lst];
     nh = nh < c.R ? nh : c.R;
-    __shared__ uint4 ea[TW_HEAVY_CAP], eb[TW_HEAVY_CAP];
-    __shared__ uint16_t dix[TW_HEAVY_CAP];  // per record: batchable | yielded << 1
-    __shared__ uint32_t bws[TW_HEAVY_CAP];  // the replayed free stack's pushes
-    __shared__ uint32_t bEl, bSet, bK0, bK, bDirect, bFn, bFtop, bBump, bNd;
-    __shared__ int64_t bTo, cmx[256];
-    __shared__ uint32_t bslot[TW_HEAVY_CAP], bO[32];
-    __shared__ unsigned long long bH, bsum[7];
+    if (blockIdx.x >= nh) return;
+    __shared__ uint2 sP[TW_BATCH_INSNS];
+    __shared__ int64_t sK[TW_BATCH_CONSTS];
+    __shared__ uint32_t sL[TW_BATCH_LPC];
+    __shared__ uint8_t sB[TW_BATCH_LPC];
+    __shared__ uint4 ea[TW_BATCH_CAP + 1], eb[TW_BATCH_CAP];
+    __shared__ uint8_t dix[TW_BATCH_CAP];      // per record: batchable | yielded << 1
+    __shared__ int64_t wmx[4], sNear[8];
+    __shared__ uint64_t sS[SC_COUNT];          // the lane's scalar block
+    __shared__ uint32_t bSet, bK0, bK, bDirect, bNd, bNx;
+    __shared__ int64_t bTo;
+    __shared__ unsigned long long bH, bsum[6];
     __shared__ long long bFin, bLast;
-    const uint32_t tid = threadIdx.x;
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
+    for (uint32_t i = tid; i < c.n_insns; i += 256) sP[i] = gp(c.insns)[i];
+    for (uint32_t i = tid; i < c.n_consts; i += 256) sK[i] = gp(c.consts)[i];
+    for (uint32_t i = tid; i < c.n_sets * c.n_kinds; i += 256) {
+        sL[i] = gp(c.lpc)[i];
+        sB[i] = gp(c.lpc_bat)[i];
+    }
+    const BProg bp{(const uint2 LAS*)sP, (const int64_t LAS*)sK, (const uint32_t LAS*)sL, (const uint8_t LAS*)sB};
     const size_t st = ib_stride(c);
+#ifdef TW_STATS
+    uint64_t bp_cyc[6] = {0, 0, 0, 0, 0, 0};
+#define BT(v) const uint64_t v = __builtin_amdgcn_s_memtime()
+#else
+#define BT(v) ((void)0)
+#endif
     for (uint32_t hi = blockIdx.x; hi < nh; hi += gridDim.x) {
         const uint32_t r = gp(c.heavy)[(size_t)lst * c.R + hi];
         const int64_t T = c.rw ? *rw_at(c, RW_T, r) : T0;
-        if (T == INT64_MAX) continue;
+        if (T == INT64_MAX) continue;  // (uniform over the workgroup)
         const int64_t tend = T + L - 1;
+        const uint64_t GAS* sc = gp(c.scal) + (size_t)r * SC_LP_STRIDE;
+        __syncthreads();  // (the previous lane's readers of the shared words are done)
+        BT(bt0);
+        if (tid < SC_COUNT) sS[tid] = sc[tid];
         if (tid == 0) {
-            const uint64_t GAS* sc = gp(c.scal) + (size_t)r * SC_LP_STRIDE;
-            bNd = sc[SC_DUE_H] == 0 ? (uint32_t)sc[SC_DUE_N] : 0u;  // (tw_lp_due's fresh run)
-        }
-        __syncthreads();
-        const uint32_t nd = bNd;
-        if (!nd) { __syncthreads(); continue; }
-        const size_t ib = ib_base(c, r);
-        for (uint32_t i = tid; i < nd; i += 256) {
-            const uint4 GAS* q = gp(c.due) + (ib + (size_t)i * st) * 2;
-            ea[i] = q[0];
-            eb[i] = q[1];
-        }
-        // ---- the due run's prefix executed data-parallel (due_exec) ----
-        // Every record's events (the wake at t, the handler at t, the send's
-        // resume at t + 1) must precede the lane's next queued event (bTo); the
-        // prefix ends where a record is not batchable, and before a record whose
-        // wake would fall before an earlier record's resume (the alloc / free
-        // order of their slots would interleave).  Within the prefix the slots'
-        // alloc / free order is replayed exactly (thread 0), so the free stack
-        // ends as the chain leaves it.
-        if (tid == 0) {
-            const uint64_t GAS* sc = gp(c.scal) + (size_t)r * SC_LP_STRIDE;
-            bool el = nd && c.trace_cap == 0 && c.tie_mode == TW_TIE_FIFO &&
-                      sc[SC_STATUS] == TW_REP_RUNNING && sc[SC_PENDING_MAIN] == 0 && !(c.lpb && gp(c.spawn_n)[r]) &&
-                      sc[SC_SEQ] + 3ull * nd < 0xFFFFFFFFull && sc[SC_TIDC] + nd < 0xFFFFFFFFull;
-            int64_t to = INT64_MAX;
-            const uint32_t nn = el ? (uint32_t)sc[SC_NEAR_N] : 0u;
-            for (uint32_t j = 0; j < nn; ++j) {
-                const int64_t x = ent_t(gp(c.near_spill)[(size_t)j * c.R + r]);
-                to = x < to ? x : to;
-            }
-            if (el && sc[SC_FAR_N]) {
-                const int64_t x = ent_t(gp(c.far)[r]);
-                to = x < to ? x : to;
-            }
             const uint32_t own = gp(c.bind_own)[r], rel = gp(c.bind_rel)[r];
             bSet = own == rel ? 0u : gp(c.bind)[r];
-            bTo = to;
-            bEl = el ? 1u : 0u;
-            bK0 = nd;
             bK = 0;
             bDirect = 0;
             bH = 0;
             bFin = INT64_MIN;
             bLast = INT64_MIN;
-            for (int j = 0; j < 7; ++j) bsum[j] = 0;
-            bFn = (uint32_t)sc[SC_FREE_N];
-            bFtop = (uint32_t)sc[SC_FTOP];
-            bBump = (uint32_t)sc[SC_BUMP];
+            for (int j = 0; j < 6; ++j) bsum[j] = 0;
         }
         __syncthreads();
-        if (bEl) {
-            // dry run: per record (due order) ok | yielded << 1 into dix
-            for (uint32_t i = tid; i < nd; i += 256) {
-                const DueX x = due_exec<false>(c, r, wid, bSet, ea[i], eb[i]);
-                const bool ok = x.ok && x.last < bTo;
-                dix[i] = (uint16_t)((ok ? 1u : 0u) | (x.yld ? 2u : 0u));
-                if (!ok) atomicMin(&bK0, i);
+        if (tid == 0) {
+            const uint32_t nd0 = sS[SC_DUE_H] == 0 ? (uint32_t)sS[SC_DUE_N] : 0u;  // (tw_lp_due's fresh run)
+            const bool el = nd0 && c.trace_cap == 0 && c.tie_mode == TW_TIE_FIFO &&
+                            sS[SC_STATUS] == TW_REP_RUNNING && sS[SC_PENDING_MAIN] == 0 &&
+                            !(c.lpb && gp(c.spawn_n)[r]) && sS[SC_SEQ] + 3ull * nd0 < 0xFFFFFFFFull &&
+                            sS[SC_TIDC] + nd0 < 0xFFFFFFFFull;
+            bNx = nd0;  // the due run's length (records past the cap stay on the chain)
+            bNd = el ? (nd0 < TW_BATCH_CAP ? nd0 : TW_BATCH_CAP) : 0u;
+            bK0 = bNd;
+        }
+        __syncthreads();
+        const uint32_t nd = bNd;
+        if (!nd) continue;  // (uniform)
+        // the records, the lane's next queued event (its near spill and far heap
+        // top, read by eight threads)
+        const size_t ib = ib_base(c, r);
+        const uint32_t nx = bNx > nd ? nd + 1u : nd;  // (+ the first record past the cap: its time)
+        for (uint32_t i = tid; i < nx; i += 256) {
+            const uint4 GAS* q = gp(c.due) + (ib + (size_t)i * st) * 2;
+            ea[i] = q[0];
+            if (i < nd) eb[i] = q[1];
+        }
+        if (tid < 8u) {
+            int64_t x = INT64_MAX;
+            if (tid < (uint32_t)sS[SC_NEAR_N]) x = ent_t(gp(c.near_spill)[(size_t)tid * c.R + r]);
+            if (tid == 0 && sS[SC_FAR_N]) {
+                const int64_t f = ent_t(gp(c.far)[r]);
+                x = f < x ? f : x;
             }
-            if (tid < 32u && tid < bFn)  // the free stack's top 32 entries
-                bO[tid] = tid == 0 ? bFtop : gp(c.free_stk)[(size_t)(bFn - 1u - tid) * c.R + r];
-            __syncthreads();
-            const uint32_t K0 = bK0;
-            // the latest resume among records before each position: chunks of 8
-            // per thread, an exclusive prefix max over the chunks (thread 0)
+            sNear[tid] = x;
+        }
+        __syncthreads();
+        if (tid == 0) {
+            int64_t to = INT64_MAX;
+            for (int j = 0; j < 8; ++j) to = sNear[j] < to ? sNear[j] : to;
+            bTo = to;
+        }
+        __syncthreads();
+        BT(bt1);
+        // dry run: batchable | yielded << 1 per record (due order); each thread
+        // keeps its first record's outcome for the effects
+        DueX x0{};
+        for (uint32_t i = tid; i < nd; i += 256) {
+            const DueX x = due_exec(c, bp, r, bSet, ea[i], eb[i]);
+            const bool ok = x.ok && x.last < bTo;
+            dix[i] = (uint8_t)((ok ? 1u : 0u) | (x.yld ? 2u : 0u));
+            if (!ok) atomicMin(&bK0, i);
+            if (i == tid) x0 = x;
+        }
+        __syncthreads();
+        BT(bt2);
+        const uint32_t K0 = bK0;
+        // the latest resume before each position: four records per thread
+        // (1,024), an inclusive max scan of the thread maxima (wave shuffles,
+        // then the four waves)
+        {
             int64_t cm = INT64_MIN;
-            for (uint32_t j = 0; j < 8; ++j) {
-                const uint32_t i = tid * 8 + j;
+            for (uint32_t j = 0; j < 4; ++j) {
+                const uint32_t i = tid * 4 + j;
                 if (i < K0 && (dix[i] & 2u)) {
-                    const int64_t x = ent_t(ea[i]) + 1;
-                    cm = x > cm ? x : cm;
+                    const int64_t y = ent_t(ea[i]) + 1;
+                    cm = y > cm ? y : cm;
                 }
             }
-            cmx[tid] = cm;
-            __syncthreads();
-            if (tid == 0) {
-                int64_t m = INT64_MIN;
-                for (uint32_t j = 0; j < 256; ++j) {
-                    const int64_t x = cmx[j];
-                    cmx[j] = m;
-                    m = x > m ? x : m;
-                }
-                if (K0 == nd) bK = nd;
+#pragma unroll
+            for (uint32_t d = 1; d < 64; d <<= 1) {
+                const int64_t o = __shfl_up(cm, d, 64);
+                if (lane >= d) cm = o > cm ? o : cm;
             }
+            if (lane == 63) wmx[wv] = cm;
             __syncthreads();
-            {
-                int64_t m = cmx[tid];
-                for (uint32_t j = 0; j < 8; ++j) {
-                    const uint32_t i = tid * 8 + j;
-                    if (i > K0 || i >= nd) break;
-                    const int64_t ti = ent_t(ea[i]);
-                    if (m < ti) atomicMax(&bK, i);  // (i = 0 always: m = INT64_MIN)
-                    if (i < K0 && (dix[i] & 2u)) m = ti + 1 > m ? ti + 1 : m;
-                }
+            int64_t m = __shfl_up(cm, 1, 64);  // (exclusive within the wave)
+            if (lane == 0) m = INT64_MIN;
+            for (uint32_t k = 0; k < wv; ++k) m = wmx[k] > m ? wmx[k] : m;
+            for (uint32_t j = 0; j < 4; ++j) {
+                const uint32_t i = tid * 4 + j;
+                if (i > K0) break;
+                // the prefix [0, i) is kept when its last resume precedes record i's
+                // wake (i = nd: the first record past the cap, or none)
+                if (i == nd && bNx == nd) { atomicMax(&bK, i); break; }
+                const int64_t ti = ent_t(ea[i]);
+                if (m < ti) atomicMax(&bK, i);  // (i = 0 always)
+                if (i < K0 && (dix[i] & 2u)) m = ti + 1 > m ? ti + 1 : m;
             }
-            __syncthreads();
-            if (tid == 0 && bK) {
-                // the slots' alloc (a wake) / free (a thread's end) order of the
-                // prefix, as the chain runs it: a record that yielded holds its
-                // slot until its resume at t + 1 (after every wake at that time:
-                // their seqs are older); the others free it at once
-                const uint32_t K = bK, fn = bFn;
-                uint32_t* ws = bws;
-                uint32_t wsn = 0, used = 0, bump = bBump, rp = 0;
-                bool okk = true;
-                auto pop = [&]() -> uint32_t {
-                    if (wsn) return ws[--wsn];
-                    if (used < fn) {
-                        if (used >= 32u) { okk = false; return 0u; }
-                        return bO[used++];
-                    }
-                    if (bump < c.S) return bump++;
-                    okk = false;
-                    return 0u;
-                };
-                for (uint32_t i = 0; i < K && okk; ++i) {
-                    const int64_t ti = ent_t(ea[i]);
-                    while (rp < i) {
-                        if (!(dix[rp] & 2u)) { ++rp; continue; }
-                        if (ent_t(ea[rp]) + 1 < ti) { ws[wsn++] = bslot[rp]; ++rp; }
-                        else break;
-                    }
-                    const uint32_t sl = pop();
-                    if (dix[i] & 2u) bslot[i] = sl;
-                    else ws[wsn++] = sl;
-                }
-                for (; rp < K && okk; ++rp)
-                    if (dix[rp] & 2u) ws[wsn++] = bslot[rp];
-                if (!okk) {
-                    bK = 0;
-                } else {
-                    // the stack: the untouched bottom fn - used entries, then ws
-                    const uint32_t rest = fn - used;
-                    uint32_t top = bFtop;
-                    if (wsn) {
-                        if (used == 0 && fn) gp(c.free_stk)[(size_t)(fn - 1u) * c.R + r] = bFtop;
-                        for (uint32_t j = 0; j + 1 < wsn; ++j) gp(c.free_stk)[(size_t)(rest + j) * c.R + r] = ws[j];
-                        top = ws[wsn - 1];
-                    } else if (rest) {
-                        top = used < 32u ? bO[used] : gp(c.free_stk)[(size_t)(rest - 1u) * c.R + r];
-                    }
-                    bFn = rest + wsn;
-                    bFtop = top;
-                    bBump = bump;
-                }
-            }
-            __syncthreads();
-            // the prefix for real: other nodes' hash terms, the sends' records
-            const uint32_t K = bK;
+        }
+        __syncthreads();
+        BT(bt3);
+        BT(bt4);
+        // the prefix for real: other nodes' hash terms, the sends' records
+        const uint32_t K = bK;
+        if (!K) continue;  // (uniform)
+        {
+            const uint32_t node = (c.lp0 + r) >> c.rep_lg;
             uint64_t h = 0;
-            uint32_t sm[7] = {0, 0, 0, 0, 0, 0, 0}, dir = 0;
+            uint32_t sm[6] = {0, 0, 0, 0, 0, 0}, dir = 0;
             int64_t fin = INT64_MIN, last = INT64_MIN;
             for (uint32_t i = tid; i < K; i += 256) {
-                const DueX x = due_exec<true>(c, r, wid, bSet, ea[i], eb[i]);
+                const DueX x = i == tid ? x0 : due_exec(c, bp, r, bSet, ea[i], eb[i]);
+                dir |= due_effects(c, wid, node, x);
                 h += x.h;
                 sm[0] += x.dl; sm[1] += x.ud; sm[2] += x.dr; sm[3] += x.ev; sm[4] += x.th; sm[5] += x.sq;
-                dir |= x.direct;
                 fin = x.fin > fin ? x.fin : fin;
                 last = x.last > last ? x.last : last;
             }
-            if (K) {
-                if (h) atomicAdd(&bH, (unsigned long long)h);
-                for (int j = 0; j < 6; ++j)
-                    if (sm[j]) atomicAdd(&bsum[j], (unsigned long long)sm[j]);
-                if (dir) bDirect = 1;
-                atomicMax(&bFin, (long long)fin);
-                atomicMax(&bLast, (long long)last);
-            }
-            __syncthreads();
-        }
-        if (tid == 0 && bEl && bK) {
-            uint64_t GAS* sc = gp(c.scal) + (size_t)r * SC_LP_STRIDE;
-            const uint32_t K = bK;
-            sc[SC_SEQ] += bsum[5];  // (after the due run's reserved seqs)
-            sc[SC_DUE_H] = K;
-            if (c.bat_ctr) atomicAdd(gp(c.bat_ctr), (unsigned long long)K);
-            if (K) {  // the batched prefix's totals (due_exec), as its events on the chain add them
-                sc[SC_DELIVERED] += bsum[0];
-                sc[SC_UNDELIV] += bsum[1];
-                sc[SC_DROPPED] += bsum[2];
-                sc[SC_EVENTS] += bsum[3];
-                sc[SC_THREADS] += bsum[4];
-                sc[SC_TIDC] += bsum[0];  // (a thread id per handler)
-                sc[SC_FREE_N] = bFn;
-                sc[SC_FTOP] = bFtop;
-                sc[SC_BUMP] = bBump;
-                if ((int64_t)sc[SC_NOW] < (int64_t)bLast) sc[SC_NOW] = (uint64_t)bLast;
-                if ((int64_t)sc[SC_FINAL_T] < (int64_t)bFin) sc[SC_FINAL_T] = (uint64_t)bFin;
-                if (bH)
-                    __hip_atomic_fetch_add((unsigned long long GAS*)(gp(c.hash_g) + c.lp0 + r), bH, __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_AGENT);
-                if (bDirect)  // sent records straight into inboxes (Lane::emit, the event kernel's epilogue)
-                    min_hot(c.rw ? (uint64_t GAS*)rw_at(c, RW_WIN, r) : (uint64_t GAS*)(gp(c.win) + WN_REC_MIN),
-                            (uint64_t)(tend + 1));
-            }
+            if (h) atomicAdd(&bH, (unsigned long long)h);
+            for (int j = 0; j < 6; ++j)
+                if (sm[j]) atomicAdd(&bsum[j], (unsigned long long)sm[j]);
+            if (dir) bDirect = 1;
+            if (fin != INT64_MIN) atomicMax(&bFin, (long long)fin);
+            if (last != INT64_MIN) atomicMax(&bLast, (long long)last);
         }
         __syncthreads();
+        BT(bt5);
+        if (tid == 0) {
+            uint64_t GAS* sw = gp(c.scal) + (size_t)r * SC_LP_STRIDE;
+            sw[SC_SEQ] = sS[SC_SEQ] + bsum[5];  // (after the due run's reserved seqs)
+            sw[SC_DUE_H] = K;
+            if (c.bat_ctr) atomicAdd(gp(c.bat_ctr), (unsigned long long)K);
+            // the prefix's totals, as its events on the chain add them
+            sw[SC_DELIVERED] = sS[SC_DELIVERED] + bsum[0];
+            sw[SC_UNDELIV] = sS[SC_UNDELIV] + bsum[1];
+            sw[SC_DROPPED] = sS[SC_DROPPED] + bsum[2];
+            sw[SC_EVENTS] = sS[SC_EVENTS] + bsum[3];
+            sw[SC_THREADS] = sS[SC_THREADS] + bsum[4];
+            sw[SC_TIDC] = sS[SC_TIDC] + bsum[0];  // (a thread id per handler)
+            if ((int64_t)sS[SC_NOW] < (int64_t)bLast) sw[SC_NOW] = (uint64_t)bLast;
+            if ((int64_t)sS[SC_FINAL_T] < (int64_t)bFin) sw[SC_FINAL_T] = (uint64_t)bFin;
+            if (bH)
+                __hip_atomic_fetch_add((unsigned long long GAS*)(gp(c.hash_g) + c.lp0 + r), bH, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+            if (bDirect)  // sent records straight into inboxes (Lane::emit, the event kernel's epilogue)
+                min_hot(c.rw ? (uint64_t GAS*)rw_at(c, RW_WIN, r) : (uint64_t GAS*)(gp(c.win) + WN_REC_MIN),
+                        (uint64_t)(tend + 1));
+        }
+#ifdef TW_STATS
+        BT(bt6);
+        bp_cyc[0] += bt1 - bt0; bp_cyc[1] += bt2 - bt1; bp_cyc[2] += bt3 - bt2;
+        bp_cyc[3] += bt4 - bt3; bp_cyc[4] += bt5 - bt4; bp_cyc[5] += bt6 - bt5;
+#endif
     }
+#ifdef TW_STATS
+    if (tid == 0 && c.prof)
+        for (int j = 0; j < 6; ++j)
+            __hip_atomic_fetch_add(gp(c.prof) + 2 * P_COUNT + j, (unsigned long long)bp_cyc[j], __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+#endif
+#undef BT
 }
 
 // Batched LP: a replica's results = its nodes' lanes (lane = node << rep_lg |
