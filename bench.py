@@ -9,12 +9,15 @@ replica on the device-resident tables and run all of them to quiescence
 PQ.minView pop of the TimedT schedule (TimedT.hs:242); the GPU count equals the
 oracle's (parity-checked on a sample each run).
 
-Multi-GPU: one process per GPU (torchrun).  The replica configs split ONE
-batch of `--replicas` replicas (65,536 for C3) into contiguous blocks
-[g*R/G, (g+1)*R/G), BASELINE config 3 / SURVEY.md 8(e) -- strong scaling, no
-data-path collective; only the statistics are all-reduced over RCCL.
-`--weak` keeps `--replicas` per GPU instead.  C4 (gossip) partitions one
-scenario by node (strong scaling, RCCL all-to-all per window).
+Multi-GPU: one process per GPU (torchrun).  The replica configs shard
+independent replicas over the ranks with no data-path collective (only the
+statistics are all-reduced over RCCL): each rank runs `--replicas` replicas of
+its own (65,536 for C3, BASELINE config 3's per-GPU batch; seeds
+[g*R, (g+1)*R)) -- weak scaling, as the path partitions into independent
+replicas.  `--strong` splits ONE batch of `--replicas` into contiguous blocks
+[g*R/G, (g+1)*R/G) instead (C3's 64k over 8 GPUs: 8,192 per GPU, where a
+replica's own ~45.7k-event chain bounds the step).  C4 (gossip)
+partitions one scenario by node (strong scaling, RCCL all-to-all per window).
 """
 from __future__ import annotations
 
@@ -39,8 +42,8 @@ BYTES_PER_SEND = 8              # link-table entry + ordinal
 
 
 def replica_block(args, rank: int, world: int):
-    """(seed_base, n_replicas) of this rank: a contiguous block of the global
-    batch (strong scaling, the default) or `--replicas` per rank (`--weak`)."""
+    """(seed_base, n_replicas) of this rank: `--replicas` of its own (weak
+    scaling, the default) or a contiguous block of one batch (`--strong`)."""
     from timewarp.dist import strong_block, weak_block
 
     if args.weak:
@@ -285,9 +288,11 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", default="token_ring", choices=["token_ring", "ping_pong", "hotspot", "gossip"])
     ap.add_argument("--replicas", type=int, default=None,
-                    help="replicas in the whole job, split over the GPUs: 65536 (token_ring, C3), "
-                         "1048576 (ping_pong, C2), 4096 (hotspot, C5)")
-    ap.add_argument("--weak", action="store_true", help="--replicas per GPU instead (weak scaling)")
+                    help="replicas per GPU: 65536 (token_ring, C3), 1048576 (ping_pong, C2), 4096 (hotspot, C5); "
+                         "with --strong, the whole job's, split over the GPUs")
+    ap.add_argument("--strong", action="store_true",
+                    help="split one batch of --replicas over the GPUs (strong scaling) instead of --replicas per GPU")
+    ap.add_argument("--weak", action="store_true", help="(the default for the replica configs: --replicas per GPU)")
     ap.add_argument("--nodes", type=int, default=None, help="4096 (token_ring), 256 senders (hotspot), 1M (gossip)")
     ap.add_argument("--duration-s", type=int, default=120)
     ap.add_argument("--drop-log2", type=int, default=10)
@@ -312,6 +317,7 @@ def main():
     ap.add_argument("--workload-key", action="store_true",
                     help="print the workload key and engine digest (tools/pmc.sh provenance) and exit")
     args = ap.parse_args()
+    args.weak = not args.strong
     if args.nodes is None:
         args.nodes = {"token_ring": 4096, "hotspot": 256, "gossip": 1 << 20}.get(args.config, 2)
     if args.replicas is None:
@@ -454,7 +460,9 @@ def main():
                 "replicas_total": args.replicas * (world if args.weak else 1),
                 "replicas_rank0": scn.n_replicas,
                 "events_per_step": int(tot_events / args.steps),
-                "parallelism": f"replica-sharded x{world}, contiguous blocks (no data-path collective)",
+                "parallelism": (f"replica-sharded x{world}: {scn.n_replicas} replicas per GPU, seeds [g*R, (g+1)*R) "
+                                "(no data-path collective)" if args.weak else
+                                f"replica-sharded x{world}: one batch in contiguous blocks (no data-path collective)"),
                 "geometry": eng.geometry(),
                 "tie_order": tie,
             },
