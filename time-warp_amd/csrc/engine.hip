@@ -458,7 +458,7 @@ static int load_common(tw_shard* c, const tw_scenario_desc* s, bool lp, uint32_t
     c->tie_flags.assign(d.R, 0u);
     const size_t R = d.R;
     const size_t Rt = s->n_replicas;  // replica dimension of the host tables
-    const size_t prog_lds = 12ull * (d.n_insns + 1) + 8ull * d.n_consts + 4ull * d.n_sets * d.n_kinds;
+    const size_t prog_lds = 16ull * (d.n_insns + 1) + 8ull * d.n_consts + 4ull * d.n_sets * d.n_kinds;
     // geometry by replica count (TW_GEOMETRY overrides; LP mode is dense):
     // <= 4096: a wavefront per replica (C5: 0.32 G events/s vs 0.25 sparse,
     // 0.20 narrow); < 65536: narrow (C3 at 8192: 2.5 vs 0.99 sparse, 0.74

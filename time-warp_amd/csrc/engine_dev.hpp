@@ -319,6 +319,7 @@ struct Lane {
     uint4 LAS* rq;        // far runs' bookkeeping quads [RQ_*]
     const uint2 LAS* P;   // program image
     const uint32_t LAS* PU;  // its uop flags
+    const uint32_t LAS* PW;  // its pop words (pop_word)
     const int64_t LAS* K; // constant pool
     const uint32_t LAS* LPC;  // listener-set x kind -> handler pc (Dev::lpc), staged in LDS
     // near heap: count, time base, cached root
@@ -1325,14 +1326,15 @@ struct Lane {
     // A thread resumed at an unconditional JMP -- every `schedule`'s stub
     // (`wait spec >> jmp action`, program.py Code.schedule; MonadTimed.hs:162-163)
     // -- goes to the jump's target at the pop: the JMP counts as the step's
-    // first instruction (returns n0 = 1) without an interpreter pass of its own.
-    __device__ __forceinline__ uint32_t jump_at_pop(Th& th, bool run) const {
+    // first instruction (n0 = 1) without an interpreter pass of its own.  The
+    // resume pc's pop word (PW, pop_word: made in the launch prologue) holds the
+    // pc to start at, n0 and the victim staging's throwTo flags, one LDS read.
+    __device__ __forceinline__ uint32_t jump_at_pop(Th& th, bool run, uint32_t& pw) const {
         const uint32_t pc = th_pc(th);
         const bool ok = run && pc < c.n_insns;
-        const uint2 in = P[ok ? pc : 0u];
-        const bool j = ok && (in.x & 0xFFu) == TW_OP_JMP && (uint32_t)in.y < c.n_insns;
-        th.w0 = j ? (th.w0 & 0xFFFF0000u) | (uint32_t)in.y : th.w0;
-        return j ? 1u : 0u;
+        pw = PW[ok ? pc : c.n_insns];  // (entry n_insns: no flags)
+        th.w0 = ok ? (th.w0 & 0xFFFF0000u) | (pw & 0xFFFFu) : th.w0;
+        return ok ? (pw >> 16) & 1u : 0u;
     }
 
     // Victim prefetch (replica kernels).  A step that opens with throwTo -- C3's
@@ -1346,16 +1348,13 @@ struct Lane {
     // so throw_to's counted vmcnt(4) proves they landed without waiting for
     // it.  CW_VS names this pop (d_ev: every counted pop and in-place child
     // changes it), the step's starting instruction count n0 and the staged quads.
-    __device__ __forceinline__ void stage_victims(const Th& th, uint32_t slot, bool run, uint32_t n0) {
-        const uint32_t pc = th_pc(th);
-        const bool ok = run && pc < c.n_insns;
-        const uint32_t w0 = P[ok ? pc : 0u].x, w1 = P[ok ? pc + 1u : 0u].x;  // (the image is padded by one NOP)
-        const bool t0 = ok && (w0 & 0xFFu) == TW_OP_THROW_TO;
+    __device__ __forceinline__ void stage_victims(uint32_t slot, bool run, uint32_t n0, uint32_t pw) {
+        const bool t0 = run && ((pw >> 17) & 1u);
         if (!__builtin_amdgcn_ballot_w64(t0)) return;
-        const uint32_t v0 = (uint32_t)rf[((w0 >> 8) & 3u) * WG];
-        const uint32_t v1 = (uint32_t)rf[((w1 >> 8) & 3u) * WG];
+        const uint32_t v0 = (uint32_t)rf[((pw >> 19) & 3u) * WG];
+        const uint32_t v1 = (uint32_t)rf[((pw >> 21) & 3u) * WG];
         const bool s0 = t0 && v0 < c.S && v0 != slot;
-        const bool s1 = t0 && (w1 & 0xFFu) == TW_OP_THROW_TO && v1 < c.S && v1 != slot && v1 != v0;
+        const bool s1 = t0 && ((pw >> 18) & 1u) && v1 < c.S && v1 != slot && v1 != v0;
         // (readfirstlane: the m0 operand is an SGPR whatever register the value was kept in)
         const uint32_t qw = (uint32_t)__builtin_amdgcn_readfirstlane((int)(pfs_wave + qq_lds_offset<WG, NC, HR>()));
         asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off ; tw:vic" ::"v"(hrec(s0 ? v0 : 0u)),
@@ -2317,6 +2316,7 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
     int64_t LAS* s_c = (int64_t LAS*)(s_p + c.n_insns + 1);
     uint32_t LAS* s_u = (uint32_t LAS*)(s_c + c.n_consts);
     uint32_t LAS* s_l = s_u + c.n_insns + 1;
+    uint32_t LAS* s_w = s_l + c.n_sets * c.n_kinds;  // pop words [n_insns + 1]
     {
         for (uint32_t i = threadIdx.x; i <= c.n_insns; i += WG * 64 / TPW) {
             const uint2 in = gp(c.insns)[i];
@@ -2332,6 +2332,22 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
         }
         for (uint32_t i = threadIdx.x; i < c.n_consts; i += WG * 64 / TPW) s_c[i] = gp(c.consts)[i];
         for (uint32_t i = threadIdx.x; i < c.n_sets * c.n_kinds; i += WG * 64 / TPW) s_l[i] = gp(c.lpc)[i];
+        // pop_word(pc): the pc a resumed thread starts at (an unconditional JMP's
+        // target; bit 16 = the JMP was taken), and whether that pc / the next are
+        // THROW_TOs (bits 17, 18) with their victim registers (bits 19-20, 21-22)
+        for (uint32_t i = threadIdx.x; i <= c.n_insns; i += WG * 64 / TPW) {
+            uint32_t w = i;
+            if (i < c.n_insns) {
+                const uint2 in = gp(c.insns)[i];
+                const bool j = (in.x & 0xFFu) == TW_OP_JMP && (uint32_t)in.y < c.n_insns;
+                const uint32_t t = j ? (uint32_t)in.y : i;
+                const uint32_t w0 = gp(c.insns)[t].x, w1 = gp(c.insns)[t + 1u].x;  // (padded by one NOP)
+                w = t | (j ? 1u << 16 : 0u) | ((w0 & 0xFFu) == TW_OP_THROW_TO ? 1u << 17 : 0u) |
+                    ((w1 & 0xFFu) == TW_OP_THROW_TO ? 1u << 18 : 0u) | (((w0 >> 8) & 3u) << 19) |
+                    (((w1 >> 8) & 3u) << 21);
+            }
+            s_w[i] = w;
+        }
         __syncthreads();
     }
     if (TPW < 64 && (threadIdx.x & 63u) >= TPW) return;
@@ -2393,6 +2409,7 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
             L.pfs_wave = __builtin_amdgcn_readfirstlane((uint32_t)(size_t)(s_pf + wbase));
             L.P = s_p;
             L.PU = s_u;
+            L.PW = s_w;
             L.K = s_c;
             L.LPC = s_l;
             L.pf_slot = 0xFFFFFFFFu;
@@ -2692,8 +2709,9 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
                     }
                 }
                 if (!popping) slot = 0u;  // main's first run is slot 0; idle lanes do not use it
-                const uint32_t n0 = L.jump_at_pop(th, run);
-                if constexpr (!LP) L.stage_victims(th, slot, run, n0);
+                uint32_t pw;
+                const uint32_t n0 = L.jump_at_pop(th, run, pw);
+                if constexpr (!LP) L.stage_victims(slot, run, n0, pw);
                 STIME(tp0);
                 L.prefetch_all(run ? slot : 0xFFFFFFFFu);
                 STIME(tl1);
@@ -3227,7 +3245,9 @@ __global__ void __launch_bounds__(256) tw_lpb_compact(Dev c) {
 // block of TW_CPT * 256 nodes (so the lanes' [field][node] state accesses
 // coalesce); one atomic per block and bucket claims its span.  Device loop
 // (c.win): only at a window's first tick, with mark/list from the window words.
-#define TW_CPT 16
+#ifndef TW_CPT
+#define TW_CPT 4
+#endif
 __global__ void __launch_bounds__(256) tw_lp_compact(Dev c, uint32_t mark, uint32_t dst) {
     int64_t tend = INT64_MIN;  // device loop: lanes whose next event is due in the window are listed too
     int64_t L = 0;

@@ -10,11 +10,13 @@ torch.distributed helpers below remain the thin caller-side pieces (the
 barrier and elapsed-time max of bench.py) and the caller-driven window loops,
 which the gloo tests exercise on CPU.
 
-Strong scaling (the default of bench.py, BASELINE config 3): one batch of R
+Weak scaling (the default of bench.py since round 5): every rank runs R
+replicas of its own, global ids [g*R, (g+1)*R) (weak_block).  Strong scaling
+(`bench.py --strong`, BASELINE config 3 read as one batch): one batch of R
 replicas is split into contiguous blocks, rank g owning [g*R/G, (g+1)*R/G)
-(strong_block) and drawing their link tables from mkStdGen(global replica
-id), so the union over ranks is bit-identical to one process running all R
-replicas.  `bench.py --weak` keeps R replicas per rank instead (weak_block).
+(strong_block).  Either way a rank draws its link tables from
+mkStdGen(global replica id), so the union over ranks is bit-identical to one
+process running all of them.
 """
 from __future__ import annotations
 
