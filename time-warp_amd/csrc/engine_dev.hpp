@@ -77,7 +77,7 @@
 #ifndef TW_LP_WAVES
 #define TW_LP_WAVES 2
 #endif
-#define P_COUNT 34
+#define P_COUNT 36
 #define TW_BPROF 8  // diagnostic build: tw_lp_batch's phase cycles after the two P_COUNT sets
 // Diagnostic build (-DTW_STATS, lib/libtimewarp_stats.so): per-lane event-path
 // counters summed into Dev::prof at kernel end (tools/stats_probe.py).  The
@@ -93,7 +93,7 @@ enum { K_POP, K_SUPERSEDED, K_PEEK_PF, K_PEEK_HBM, K_PUT_HBM, K_PUT_DEAD, K_PF_I
        K_NEAR_PUSH, K_RUN_PUSH, K_FAR_PUSH, K_INSN, K_CYC_POP, K_CYC_INTERP, K_CYC_TAIL,
        K_CYC_SEL, K_CYC_FETCH, K_CYC_QPOP, K_CYC_COMMIT, K_CYC_PF, K_CYC_TERM, K_CYC_STORE, K_CYC_HASH,
        K_CYC_SPAWN, K_CYC_ENQ, K_SPAWN, K_ALLOC_LD, K_ITER, K_CYC_SEND, K_CYC_DELIV, K_CYC_DUE, K_CYC_PRO,
-       K_CYC_EPI };
+       K_CYC_EPI, K_CYC_IP, K_PASS };
 #ifdef TW_STATS
 #define STIME(v) const uint64_t v = __builtin_amdgcn_s_memtime()
 #define STADD(i, v) (st[(i)] += (uint32_t)(v))
@@ -181,7 +181,13 @@ enum : uint32_t { LD_NONE, LD_NV, LD_OUT, LD_RL };  // node var / out-link base 
 #define U_NE (1u << 27)
 #define U_NE2 (1u << 28)
 #define U_JE (1u << 29)
-#define U_FOLD (U_NE | U_NE2 | U_JE)
+// ... and a wait (WAIT_REL / WAIT_ABS) or a jump at pc + 1 folded the same
+// way: the thread yields from this pass (`catch`/`listen` then
+// `sleepForever`), or takes the jump with the registers this pass left (a
+// counted loop's `addi ; jlt`, `node ; jnei`)
+#define U_NW (1u << 30)
+#define U_NJ (1u << 31)
+#define U_FOLD (U_NE | U_NE2 | U_JE | U_NW | U_NJ)
 __host__ __device__ constexpr uint32_t uop_of(uint32_t op) {
     auto u = [](uint32_t alu, uint32_t jm, uint32_t tk) { return alu | (tk << 8) | (jm << 16); };
     switch (op) {
@@ -1941,6 +1947,28 @@ struct Lane {
             n += fe ? 1u : 0u;
             tgt = fe ? tgt + 1u : tgt;
             tc = fe ? (uint32_t)T_EXIT : tc;
+            const bool fw = me && tc == T_NONE && status == TW_REP_RUNNING && n < TW_STEP_CAP && (lfl & U_NW) &&
+                            tgt == pc + 1u;
+            if (__builtin_amdgcn_ballot_w64(fw)) {  // the wait's pass: its count, yield time and resume pc
+                const uint2 wi = P[fw ? pc + 1u : 0u];
+                const int64_t kt = K[fw ? wi.y : 0u];
+                const int64_t w = (wi.x & 0xFFu) == TW_OP_WAIT_ABS ? (kt > now ? kt : now) : now + kt;
+                n += fw ? 1u : 0u;
+                yt = fw ? w : yt;
+                tgt = fw ? pc + 2u : tgt;
+                tc = fw ? (uint32_t)T_YIELD : tc;
+            }
+            const bool fj = me && tc == T_NONE && status == TW_REP_RUNNING && n < TW_STEP_CAP && (lfl & U_NJ) &&
+                            tgt == pc + 1u;
+            if (__builtin_amdgcn_ballot_w64(fj)) {  // the jump's pass, on the registers as this pass left them
+                const uint32_t jp = fj ? pc + 1u : 0u;
+                const uint2 ji = P[jp];
+                const uint32_t jm = U_JM(PU[jp]), jb = ji.x >> 16;
+                const int64_t ja = rg(th, (ji.x >> 8) & 3u), jr = rg(th, jb & 3u);
+                const uint32_t ci = (ja == jr ? 1u : 0u) | (ja < jr ? 2u : 0u) | (ja == (int64_t)(int16_t)jb ? 4u : 0u);
+                n += fj ? 1u : 0u;
+                tgt = fj ? (((jm >> ci) & 1u) ? ji.y : pc + 2u) : tgt;
+            }
         }
         // per-lane epilogue of the pass
         pc = me ? tgt : pc;
@@ -2103,7 +2131,11 @@ struct Lane {
                 // sparse geometry, whose kernel would spill for it (there the
                 // child takes its queue round trip: the same order either way)
                 if constexpr (!LP && !PL && IP) {
-                    if (fork_in_place(th, slot, s)) continue;
+                    STIME(tip0);
+                    const bool more = fork_in_place(th, slot, s);
+                    STIME(tip1);
+                    STADD(K_CYC_IP, tip1 - tip0);
+                    if (more) continue;
                 }
                 break;
             }
@@ -2125,6 +2157,7 @@ struct Lane {
             // flags -- a fused pair's flags depend on b, not only on the opcode)
             const bool at = PL ? (s.running & ((hot & !(lfl & U_FX)) | (!hot & ((in.x & 0xFFu) == op))))
                                : (s.running && (in.x & 0xFFu) == op && ((lfl ^ fl) & (FOLD ? ~U_FOLD : ~0u)) == 0);
+            STAT(K_PASS);
             pass(th, slot, s, at, in.x, (int32_t)in.y, op, fl, lfl);
         }
         STIME(ti1);
@@ -2327,6 +2360,9 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
                 u |= is_end(i + 1u) ? U_NE : 0u;
                 u |= is_end(i + 2u) ? U_NE2 : 0u;
                 u |= (U_JM(u) != JM_NONE && is_end((uint32_t)in.y)) ? U_JE : 0u;
+                const uint32_t nop = i + 1u < c.n_insns ? gp(c.insns)[i + 1u].x & 0xFFu : TW_OP_NOP;
+                u |= (nop == TW_OP_WAIT_REL || nop == TW_OP_WAIT_ABS) ? U_NW : 0u;
+                u |= U_JM(uop_of(nop)) != JM_NONE ? U_NJ : 0u;
             }
             s_u[i] = u;
         }

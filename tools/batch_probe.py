@@ -14,7 +14,7 @@ sys.path.insert(0, os.path.join(ROOT, "time-warp_amd"))
 from timewarp import scenarios  # noqa: E402
 from timewarp.engine import Engine, draw_link_table  # noqa: E402
 
-P_COUNT = 34
+P_COUNT = 36
 S, R, M = (int(x) for x in (sys.argv[1:4] + ["256", "4096", "1000"][len(sys.argv) - 1:]))
 scn = scenarios.hotspot(n_senders=S, n_replicas=R, msg_num=M, drawer=draw_link_table)
 with Engine(0) as e:

@@ -24,7 +24,7 @@ NAMES = ["pop", "superseded", "peek_pf", "peek_hbm", "put_hbm", "put_dead", "pf_
          "near_push", "run_push", "far_push", "insn", "cyc_pop", "cyc_interp", "cyc_step_and_flush",
          "cyc_select", "cyc_fetch", "cyc_qpop", "cyc_commit", "cyc_prefetch", "cyc_terminal", "cyc_store", "cyc_hash",
          "cyc_spawn", "cyc_enqueue", "spawn", "alloc_ld", "iter", "cyc_send", "cyc_deliver", "cyc_due", "cyc_pro",
-         "cyc_epi"]
+         "cyc_epi", "cyc_ip", "pass"]
 
 
 def read(eng, heavy=False):
