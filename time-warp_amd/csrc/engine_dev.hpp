@@ -1966,8 +1966,15 @@ struct Lane {
                 const uint32_t jm = U_JM(PU[jp]), jb = ji.x >> 16;
                 const int64_t ja = rg(th, (ji.x >> 8) & 3u), jr = rg(th, jb & 3u);
                 const uint32_t ci = (ja == jr ? 1u : 0u) | (ja < jr ? 2u : 0u) | (ja == (int64_t)(int16_t)jb ? 4u : 0u);
+                const bool tk = (jm >> ci) & 1u;
                 n += fj ? 1u : 0u;
-                tgt = fj ? (((jm >> ci) & 1u) ? ji.y : pc + 2u) : tgt;
+                tgt = fj ? (tk ? ji.y : pc + 2u) : tgt;
+                // ... and the END it lands on (`when` falling through to the end)
+                const uint32_t jf = PU[jp];
+                const bool je = fj && n < TW_STEP_CAP && (tk ? (jf & U_JE) != 0 : (jf & U_NE) != 0);
+                n += je ? 1u : 0u;
+                tgt = je ? tgt + 1u : tgt;
+                tc = je ? (uint32_t)T_EXIT : tc;
             }
         }
         // per-lane epilogue of the pass
