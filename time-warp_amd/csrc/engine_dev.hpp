@@ -188,7 +188,7 @@ enum : uint32_t { LD_NONE, LD_NV, LD_OUT, LD_RL };  // node var / out-link base 
 #define U_NW (1u << 30)
 #define U_NJ (1u << 31)
 #define U_FOLD (U_NE | U_NE2 | U_JE | U_NW | U_NJ)
-__host__ __device__ constexpr uint32_t uop_of(uint32_t op) {
+__host__ __device__ __forceinline__ constexpr uint32_t uop_of(uint32_t op) {
     auto u = [](uint32_t alu, uint32_t jm, uint32_t tk) { return alu | (tk << 8) | (jm << 16); };
     switch (op) {
     case TW_OP_NOP: return 0;
@@ -221,7 +221,7 @@ __host__ __device__ constexpr uint32_t uop_of(uint32_t op) {
     default: return U_FX;  // every other opcode (and invalid ones) takes the switch
     }
 }
-__host__ __device__ constexpr uint32_t uop_insn(uint32_t w0) {
+__host__ __device__ __forceinline__ constexpr uint32_t uop_insn(uint32_t w0) {
     const uint32_t op = w0 & 0xFFu, b = w0 >> 16;
     uint32_t f = uop_of(op);
     if (b & TW_ALU_NSTORE) {
@@ -633,7 +633,7 @@ struct Lane {
         }
     }
     // Move the near heap to a new time base (keeps (t - nbase) inside 32 bits).
-    __device__ void near_rebase(int64_t nb) {
+    __device__ __forceinline__ void near_rebase(int64_t nb) {
         const uint64_t d = (uint64_t)(nb - nbase) << 32;
 #pragma unroll 16
         for (int i = 0; i < NC; ++i) {
@@ -2099,6 +2099,21 @@ struct Lane {
                 s.fin = s.running ? (uint32_t)T_NONE : (uint32_t)T_STOP;
                 s.n = 0;
                 s.yt = 0;
+                if constexpr (FOLD) {
+                    // a child that starts with a wait (`schedule`'s stub) yields
+                    // here, without an interpreter pass for it
+                    const bool w0 = s.running && ((PW[s.running ? s.pc : c.n_insns] >> 23) & 1u);
+                    if (__builtin_amdgcn_ballot_w64(w0)) {
+                        const uint2 wi = P[w0 ? s.pc : 0u];
+                        const int64_t kt = K[w0 ? wi.y : 0u];
+                        const int64_t w = (wi.x & 0xFFu) == TW_OP_WAIT_ABS ? (kt > now ? kt : now) : now + kt;
+                        s.yt = w0 ? w : s.yt;
+                        s.n = w0 ? 1u : s.n;
+                        s.pc = w0 ? s.pc + 1u : s.pc;
+                        s.fin = w0 ? (uint32_t)T_YIELD : s.fin;
+                        s.running = s.running && !w0;
+                    }
+                }
             } else {
                 s.fin = T_STOP;  // (a slot or counter failure: the terminal stores the parent)
             }
@@ -2377,7 +2392,8 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
         for (uint32_t i = threadIdx.x; i < c.n_sets * c.n_kinds; i += WG * 64 / TPW) s_l[i] = gp(c.lpc)[i];
         // pop_word(pc): the pc a resumed thread starts at (an unconditional JMP's
         // target; bit 16 = the JMP was taken), and whether that pc / the next are
-        // THROW_TOs (bits 17, 18) with their victim registers (bits 19-20, 21-22)
+        // THROW_TOs (bits 17, 18) with their victim registers (bits 19-20, 21-22);
+        // bit 23: the instruction at pc itself is a wait (fork_in_place)
         for (uint32_t i = threadIdx.x; i <= c.n_insns; i += WG * 64 / TPW) {
             uint32_t w = i;
             if (i < c.n_insns) {
@@ -2385,9 +2401,10 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
                 const bool j = (in.x & 0xFFu) == TW_OP_JMP && (uint32_t)in.y < c.n_insns;
                 const uint32_t t = j ? (uint32_t)in.y : i;
                 const uint32_t w0 = gp(c.insns)[t].x, w1 = gp(c.insns)[t + 1u].x;  // (padded by one NOP)
+                const uint32_t op = in.x & 0xFFu;
                 w = t | (j ? 1u << 16 : 0u) | ((w0 & 0xFFu) == TW_OP_THROW_TO ? 1u << 17 : 0u) |
                     ((w1 & 0xFFu) == TW_OP_THROW_TO ? 1u << 18 : 0u) | (((w0 >> 8) & 3u) << 19) |
-                    (((w1 >> 8) & 3u) << 21);
+                    (((w1 >> 8) & 3u) << 21) | ((op == TW_OP_WAIT_REL || op == TW_OP_WAIT_ABS) ? 1u << 23 : 0u);
             }
             s_w[i] = w;
         }
