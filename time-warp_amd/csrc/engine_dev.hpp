@@ -1277,7 +1277,7 @@ struct Lane {
             go = false;
         }
         uint32_t k = 2u;  // the staged quad holding this lane's victim header (2: none)
-        if constexpr (!LP) {
+        if constexpr (HR) {
             if (__builtin_amdgcn_ballot_w64(go && n <= 3u)) {
                 // (CW_VS: d_ev << 3 | the step's first pass count n0 << 2 | quads)
                 const uint32_t vs = cg(CW_VS);
@@ -2769,9 +2769,11 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
                     }
                 }
                 if (!popping) slot = 0u;  // main's first run is slot 0; idle lanes do not use it
-                uint32_t pw;
-                const uint32_t n0 = L.jump_at_pop(th, run, pw);
-                if constexpr (!LP) L.stage_victims(slot, run, n0, pw);
+                // (the compact geometry: neither -- C2's threads resume at no JMP
+                // and throw nothing, and its per-pop cost is the bound)
+                uint32_t pw = 0, n0 = 0;
+                if constexpr (RUNS) n0 = L.jump_at_pop(th, run, pw);
+                if constexpr (HR) L.stage_victims(slot, run, n0, pw);
                 STIME(tp0);
                 L.prefetch_all(run ? slot : 0xFFFFFFFFu);
                 STIME(tl1);
