@@ -74,6 +74,9 @@
 #ifndef TW_DMA_BUILTIN
 #define TW_DMA_BUILTIN 0
 #endif
+#ifndef TW_LP_FOLDJ
+#define TW_LP_FOLDJ 1  // the LP kernels fold a jump into the pass before it (Lane::FOLDJ; 0: the A/B baseline)
+#endif
 #ifndef TW_LP_WAVES
 #define TW_LP_WAVES 2
 #endif
@@ -299,6 +302,10 @@ struct Lane {
     // the compact and LP kernels measured slower with it (C2 -4 %, C5 -2.6 %:
     // their register budget, 254-256 VGPRs at two waves per SIMD)
     static constexpr bool FOLD = HR;
+    // the LP kernels fold only a jump (U_NJ): a main thread's counted fork loop
+    // (`forM_ [1..N] fork`, examples/token-ring/Main.hs:65-68) takes two passes
+    // per fork instead of three
+    static constexpr bool FOLDJ = HR || (LP && TW_LP_FOLDJ);
     // per-lane hot passes (lanes at different hot ops share a pass) pay off where
     // lanes diverge -- logical processes and the few-replica sparse geometry; the
     // dense replica geometry runs lock-step programs and keeps the cheaper
@@ -1627,7 +1634,7 @@ struct Lane {
         };
         if (hot) {
             if constexpr (PL) {
-                if (__builtin_expect(__builtin_amdgcn_ballot_w64(at && ((lfl ^ fl) & (FOLD ? ~U_FOLD : ~0u)) != 0) == 0, 1))
+                if (__builtin_expect(__builtin_amdgcn_ballot_w64(at && ((lfl ^ fl) & (FOLDJ ? ~U_FOLD : ~0u)) != 0) == 0, 1))
                     hot_body(BoolC<true>{}, fl);
                 else
                     hot_body(BoolC<false>{}, lfl);
@@ -1940,7 +1947,8 @@ struct Lane {
         // (U_NE / U_NE2 / U_JE) ends here, with END's count and pc, instead of
         // in a pass of its own -- launchNode's last END after its `when`
         // (examples/token-ring/Main.hs:125-131), the kill pair's after its throws
-        if (FOLD && __builtin_amdgcn_ballot_w64(me && (lfl & U_FOLD) != 0)) {
+        if (FOLDJ && __builtin_amdgcn_ballot_w64(me && (lfl & U_FOLD) != 0)) {
+          if constexpr (FOLD) {
             const bool fe = me && tc == T_NONE && status == TW_REP_RUNNING && n < TW_STEP_CAP &&
                             (((lfl & U_NE) && tgt == pc + 1u) || ((lfl & U_NE2) && tgt == pc + 2u) ||
                              ((lfl & U_JE) && tgt == (uint32_t)imm));
@@ -1958,6 +1966,7 @@ struct Lane {
                 tgt = fw ? pc + 2u : tgt;
                 tc = fw ? (uint32_t)T_YIELD : tc;
             }
+          }
             const bool fj = me && tc == T_NONE && status == TW_REP_RUNNING && n < TW_STEP_CAP && (lfl & U_NJ) &&
                             tgt == pc + 1u;
             if (__builtin_amdgcn_ballot_w64(fj)) {  // the jump's pass, on the registers as this pass left them
@@ -2178,7 +2187,7 @@ struct Lane {
             // (opcode-uniform pass: the lanes holding the first lane's opcode and uop
             // flags -- a fused pair's flags depend on b, not only on the opcode)
             const bool at = PL ? (s.running & ((hot & !(lfl & U_FX)) | (!hot & ((in.x & 0xFFu) == op))))
-                               : (s.running && (in.x & 0xFFu) == op && ((lfl ^ fl) & (FOLD ? ~U_FOLD : ~0u)) == 0);
+                               : (s.running && (in.x & 0xFFu) == op && ((lfl ^ fl) & (FOLDJ ? ~U_FOLD : ~0u)) == 0);
             STAT(K_PASS);
             pass(th, slot, s, at, in.x, (int32_t)in.y, op, fl, lfl);
         }
@@ -2378,6 +2387,10 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
             s_p[i] = in;
             uint32_t u = uop_insn(in.x);
             auto is_end = [&](uint32_t j) { return j < c.n_insns && (gp(c.insns)[j].x & 0xFFu) == TW_OP_END; };
+            if (LP && TW_LP_FOLDJ && i < c.n_insns) {  // (Lane::FOLDJ: a jump only)
+                const uint32_t nop = i + 1u < c.n_insns ? gp(c.insns)[i + 1u].x & 0xFFu : TW_OP_NOP;
+                u |= U_JM(uop_of(nop)) != JM_NONE ? U_NJ : 0u;
+            }
             if (HR && i < c.n_insns) {  // (Lane::FOLD)
                 u |= is_end(i + 1u) ? U_NE : 0u;
                 u |= is_end(i + 2u) ? U_NE2 : 0u;
