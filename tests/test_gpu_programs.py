@@ -7,6 +7,7 @@ import pytest
 
 import progs
 from test_golden_c1 import GOLD, c1_table_scenario
+from timewarp import isa
 from timewarp.abi import RESULT_DTYPE, RESULT_FIELDS
 
 pytestmark = pytest.mark.gpu
@@ -100,3 +101,41 @@ def test_run_in_pieces_equals_one_run(engine_mod, oracle_mod):
     ores, oh = oracle_mod.run_batch(scn, threads=8)
     _same(scn, res, h, ores, oh)
     _same(scn, res2, h2, ores, oh)
+
+
+def _cap_prog(kind: str, k: int):
+    """A step that runs into the 2^22-instruction cap (TW_REP_ERR_INSN) or just
+    fits under it, with the boundary on an instruction the run geometries fold
+    into the pass before it (Lane::FOLD, DESIGN 3h): the loop's jump after its
+    `addi` (U_NJ) and its END after the loop (U_NE); or a `catch` followed by a
+    wait (U_NW).  The folded step must count exactly as the oracle does."""
+    from timewarp.program import Program
+    from timewarp.timeunits import for_
+    p = Program()
+    c = p.function("main")
+    c.seti(0, 0).seti(1, k)
+    top = c.here()
+    c.addi(0, 1).jlt(0, 1, top)
+    if kind == "wait":
+        c.catch_(1 << 4, "h")
+        c.wait(for_(5))
+        c.uncatch()
+    c.end()
+    c = p.function("h")
+    c.end()
+    return progs.single(p, name=f"cap_{kind}_{k}")
+
+
+@pytest.mark.one_geometry
+@pytest.mark.parametrize("geometry", ["dense", "compact"])
+@pytest.mark.parametrize("kind,k", [("jump", 2097150), ("jump", 2097151), ("wait", 2097150), ("wait", 2097151)])
+def test_step_cap_on_folded_instructions(engine_mod, oracle_mod, geometry, kind, k):
+    scn = _cap_prog(kind, k)
+    st, res, h = engine_mod.run_scenario(scn, geometry=geometry)
+    o = oracle_mod.run(scn)
+    for f in FIELDS:
+        assert res[f][0] == o.result[f], (kind, k, f, res[f][0], o.result[f])
+    assert np.array_equal(h[0], o.hashes)
+    # 2 + 2k + 1 (END) or 2 + 2k + 2 (catch, wait) against the cap of 2^22
+    n = 2 + 2 * k + (1 if kind == "jump" else 2)
+    assert (int(o.result["status"]) == isa.REP_ERR_INSN) == (n > 1 << 22), (kind, k, o.result["status"])
