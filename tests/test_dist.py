@@ -1,8 +1,9 @@
 """Multi-rank replica sharding with world_size 2 over gloo (CPU).
 
 Each rank owns a contiguous block of one global batch (strong scaling,
-bench.py's default: dist.strong_block, uneven here so the remainder rule is
-exercised); the per-rank run (here the oracle, standing in for the per-GPU
+`bench.py --strong`: dist.strong_block, uneven here so the remainder rule is
+exercised; bench.py's default since round 5 is weak scaling, each rank a batch
+of its own: dist.weak_block, test_bench_replica_blocks); the per-rank run (here the oracle, standing in for the per-GPU
 engine which needs a device) is reduced with timewarp.dist exactly as bench.py
 does over RCCL.  The union must equal a single-process run of all replicas,
 replica for replica."""
@@ -112,3 +113,26 @@ def test_record_exchange_all_to_all(tmp_path):
         got = np.sort(r[rank]["got"], order=["src", "payload"])
         assert np.array_equal(exp, got)
         assert int(r[rank]["m"]) == int(sent["t_arr"].min())
+
+
+def test_bench_replica_blocks():
+    """bench.py's rank blocks: weak scaling by default (rank g runs global
+    replicas [g*R, (g+1)*R), its tables drawn from mkStdGen(g*R + i)), one
+    batch split with --strong; the workload key names the choice, so a PMC
+    summary of one is never used for the other."""
+    import argparse
+    import importlib.util
+    import pathlib
+
+    root = pathlib.Path(__file__).resolve().parents[1]
+    spec = importlib.util.spec_from_file_location("bench_mod", root / "bench.py")
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    args = argparse.Namespace(replicas=65536, weak=True, config="token_ring", nodes=4096, duration_s=120,
+                              drop_log2=10, round_trips=1000, msg_num=1000, geometry=None, tie="auto")
+    assert [bench.replica_block(args, g, 8) for g in range(3)] == [(0, 65536), (65536, 65536), (131072, 65536)]
+    assert ":weak=1:" in bench.workload_key(args)
+    args.weak = False
+    blocks = [bench.replica_block(args, g, 8) for g in range(8)]
+    assert blocks[0] == (0, 8192) and blocks[7] == (57344, 8192) and sum(n for _, n in blocks) == 65536
+    assert ":weak=0:" in bench.workload_key(args)
