@@ -11,13 +11,14 @@ oracle's (parity-checked on a sample each run).
 
 Multi-GPU: one process per GPU (torchrun).  The replica configs shard
 independent replicas over the ranks with no data-path collective (only the
-statistics are all-reduced over RCCL): each rank runs `--replicas` replicas of
-its own (65,536 for C3, BASELINE config 3's per-GPU batch; seeds
-[g*R, (g+1)*R)) -- weak scaling, as the path partitions into independent
-replicas.  `--strong` splits ONE batch of `--replicas` into contiguous blocks
-[g*R/G, (g+1)*R/G) instead (C3's 64k over 8 GPUs: 8,192 per GPU, where a
-replica's own ~45.7k-event chain bounds the step).  C4 (gossip)
-partitions one scenario by node (strong scaling, RCCL all-to-all per window).
+statistics are all-reduced over RCCL).  By default ONE batch of `--replicas`
+is split into contiguous blocks [g*R/G, (g+1)*R/G) -- BASELINE config 3, "64k
+replicas sharded across 1/2/4/8 GPUs" (8,192 per GPU at 8, where a replica's
+own ~45.7k-event chain bounds the step) -- and for the token
+ring at N > 1 the weak figure (every rank a 64k batch of its own, seeds
+[g*R, (g+1)*R)) is measured after it and reported beside it as `weak_line`.
+`--weak` makes the weak split the line itself.  C4 (gossip) partitions one
+scenario by node (strong scaling, RCCL all-to-all per window).
 """
 from __future__ import annotations
 
@@ -61,19 +62,20 @@ def build_scenario(args, rank: int, world: int, drawer=None, max_replicas=None):
     base, R = replica_block(args, rank, world)
     if max_replicas is not None:
         R = min(R, max_replicas)
+    per = "/GPU" if args.weak else "" if world == 1 else f" (rank {rank} of {world}: [{base}, {base + R}) of {args.replicas})"
     if args.config == "token_ring":
         return scenarios.token_ring(n_nodes=args.nodes, n_replicas=R, launch_duration=args.duration_s * 1_000_000,
                                     drop_log2=args.drop_log2, seed_base=base, drawer=drawer), (
-            f"token-ring (examples/token-ring) {args.nodes} nodes x {R} replicas/GPU, delay U[1,5] ms, "
+            f"token-ring (examples/token-ring) {args.nodes} nodes x {R} replicas{per}, delay U[1,5] ms, "
             f"drop 2^-{args.drop_log2}, launchDuration {args.duration_s} s")
     if args.config == "ping_pong":
         return scenarios.ping_pong(n_replicas=R, round_trips=args.round_trips, seed_base=base, drawer=drawer), (
-            f"ping-pong (examples/ping-pong) 2 nodes x {R} replicas/GPU, {args.round_trips} round trips, "
+            f"ping-pong (examples/ping-pong) 2 nodes x {R} replicas{per}, {args.round_trips} round trips, "
             "per-link delay U[1,5] ms")
     if args.config == "hotspot":
         return scenarios.hotspot(n_senders=args.nodes, n_replicas=R, msg_num=args.msg_num, seed_base=base,
                                  drawer=drawer), (
-            f"hotspot (bench/Network) {args.nodes} senders -> 1 receiver x {R} replicas/GPU, "
+            f"hotspot (bench/Network) {args.nodes} senders -> 1 receiver x {R} replicas{per}, "
             f"{args.msg_num} msgs @1000/s")
     if args.config == "gossip":
         return scenarios.gossip(n_nodes=args.nodes, seed=0), (
@@ -282,6 +284,40 @@ def bench_gossip(args, scn, workload, world, rank, local, dist_on, barrier):
     eng.close()
 
 
+def pick_geometry(args, world):
+    """The default kernel geometry of a replica config for this rank's share."""
+    if args.geometry is None and args.config == "hotspot":
+        # C5: a replica is one long chain in the replica geometries (0.32 G
+        # events/s, wave); its nodes as logical processes run it in parallel
+        args.geometry = "lpb"
+    if args.geometry is None and args.config == "token_ring":
+        # C3 split 8 ways (8,192 replicas per GPU): a replica's ~45.7k-event
+        # chain bounds the replica geometries (narrow 2.5 G events/s); its
+        # (node, replica) pairs as logical processes run it at 3.6 G.  From
+        # 16,384 replicas per GPU up, narrow/dense win (5.3 vs 4.2 G at 16k).
+        per = args.replicas if args.weak else args.replicas // max(world, 1)
+        if per <= 8192 and per & (per - 1) == 0 and args.replicas % max(world, 1) == 0:
+            args.geometry = "lpb"
+
+
+def parity_sample(scn, gpu_res, gpu_hashes, seconds: float):
+    """(bit_exact, n): the oracle on replicas [0, n) of this rank's batch,
+    about `seconds` of host work (N > 1: no CPU baseline is timed, but every
+    run still checks a sample of its own replicas)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle  # the parity checker -- never the measured GPU path
+
+    threads, _ = host_cpu()
+    t0 = time.perf_counter()
+    oracle.run_batch(scn, 0, 1, threads=1)
+    one = max(time.perf_counter() - t0, 1e-4)
+    n = int(max(1, min(scn.n_replicas, seconds * threads / one)))
+    res, hashes = oracle.run_batch(scn, 0, n, threads=threads)
+    ok = all(np.array_equal(res[f], gpu_res[f][:n]) for f in res.dtype.names) and \
+        np.array_equal(hashes, gpu_hashes[:n])
+    return ok, n
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -289,11 +325,15 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", default="token_ring", choices=["token_ring", "ping_pong", "hotspot", "gossip"])
     ap.add_argument("--replicas", type=int, default=None,
-                    help="replicas per GPU: 65536 (token_ring, C3), 1048576 (ping_pong, C2), 4096 (hotspot, C5); "
-                         "with --strong, the whole job's, split over the GPUs")
-    ap.add_argument("--strong", action="store_true",
-                    help="split one batch of --replicas over the GPUs (strong scaling) instead of --replicas per GPU")
-    ap.add_argument("--weak", action="store_true", help="(the default for the replica configs: --replicas per GPU)")
+                    help="replicas of the job: 65536 (token_ring, C3), 1048576 (ping_pong, C2), 4096 (hotspot, "
+                         "C5), split over the GPUs (BASELINE config 3: 64k replicas sharded across 1/2/4/8 GPUs); "
+                         "with --weak, per GPU")
+    ap.add_argument("--strong", action="store_true", help="(the default: one batch of --replicas split over the GPUs)")
+    ap.add_argument("--weak", action="store_true",
+                    help="--replicas per GPU (weak scaling) instead of one batch split over the GPUs")
+    ap.add_argument("--no-weak-line", action="store_true",
+                    help="token_ring at N > 1: skip the weak-scaling figure (a 64k batch per GPU) that is "
+                         "measured after the strong split and reported beside it as weak_line")
     ap.add_argument("--nodes", type=int, default=None, help="4096 (token_ring), 256 senders (hotspot), 1M (gossip)")
     ap.add_argument("--duration-s", type=int, default=120)
     ap.add_argument("--drop-log2", type=int, default=10)
@@ -318,24 +358,13 @@ def main():
     ap.add_argument("--workload-key", action="store_true",
                     help="print the workload key and engine digest (tools/pmc.sh provenance) and exit")
     args = ap.parse_args()
-    args.weak = not args.strong
+    args.weak = args.weak and not args.strong
     if args.nodes is None:
         args.nodes = {"token_ring": 4096, "hotspot": 256, "gossip": 1 << 20}.get(args.config, 2)
     if args.replicas is None:
         args.replicas = {"token_ring": 65536, "ping_pong": 1 << 20, "hotspot": 4096}.get(args.config, 1)
-    if args.geometry is None and args.config == "hotspot":
-        # C5: a replica is one long chain in the replica geometries (0.32 G
-        # events/s, wave); its nodes as logical processes run it in parallel
-        args.geometry = "lpb"
-    if args.geometry is None and args.config == "token_ring":
-        # C3 split 8 ways (8,192 replicas per GPU): a replica's ~45.7k-event
-        # chain bounds the replica geometries (narrow 2.5 G events/s); its
-        # (node, replica) pairs as logical processes run it at 3.2-3.3 G.  From
-        # 16,384 replicas per GPU up, narrow/dense win (5.0 vs 4.4 G at 16k).
-        world0 = int(os.environ.get("WORLD_SIZE", "1"))
-        per = args.replicas if args.weak else args.replicas // max(world0, 1)
-        if per <= 8192 and per & (per - 1) == 0 and args.replicas % max(world0, 1) == 0:
-            args.geometry = "lpb"
+    args.geometry_auto = args.geometry is None
+    pick_geometry(args, int(os.environ.get("WORLD_SIZE", "1")))
     if args.workload_key:
         print(json.dumps({"bench_workload": workload_key(args), "engine_sha": engine_sha()}))
         return
@@ -356,16 +385,38 @@ def main():
         if dist_on:
             dist.barrier()
 
-    from timewarp import dist as twd
-    from timewarp.engine import Engine
+    if args.config == "gossip":
+        scn, workload, setup = setup_scenario(args, rank, world, local)
+        return bench_gossip(args, scn, workload, world, rank, local, dist_on, barrier)
+    m = measure_replicas(args, rank, world, local, dist_on, barrier)
+    print_line = replica_line(args, world, m) if rank == 0 else None
+    # BASELINE config 3 is one 64k batch split over the GPUs (the line above);
+    # the weak figure -- every GPU a 64k batch of its own -- is measured after
+    # it and sits beside it, never in its place
+    if world > 1 and args.config == "token_ring" and not args.weak and not args.no_weak_line:
+        wa = argparse.Namespace(**vars(args))
+        wa.weak = True
+        wa.geometry = None if args.geometry_auto else args.geometry
+        pick_geometry(wa, world)
+        w = measure_replicas(wa, rank, world, local, dist_on, barrier, parity=False)
+        if rank == 0:
+            print_line["weak_line"] = {
+                "value": w["value"], "ms_per_step": w["ms_per_step"], "scaling": "weak",
+                "replicas_per_gpu": w["scn_replicas"], "replicas_total": w["scn_replicas"] * world,
+                "geometry": w["geometry"], "tie_order": w["tie"],
+                "note": "each GPU its own 65,536-replica batch (seeds [g*R, (g+1)*R)); not BASELINE config 3's "
+                        "split, reported beside it"}
+    if rank == 0:
+        print(json.dumps(print_line), flush=True)
+        if "parity_sample" in print_line and not print_line["parity_sample"]["bit_exact"]:
+            raise SystemExit("parity_sample: the GPU results differ from the oracle's")
+    if dist_on:
+        dist.destroy_process_group()
 
-    if args.geometry == "lpb" and args.config != "gossip":
-        _, r_rank = replica_block(args, rank, world)
-        if r_rank & (r_rank - 1):
-            raise SystemExit(f"--geometry lpb needs a power-of-two replica count per GPU (lanes are node << log2(R) "
-                             f"| replica); rank {rank} of {world} would get {r_rank} of {args.replicas} replicas")
-    # scenario set-up (outside the timed region): the link table drawn on the
-    # GPU, checked against the host StdGen draw on its first replicas
+
+def setup_scenario(args, rank, world, local):
+    """This rank's scenario (outside the timed region): the link table drawn on
+    the GPU, checked against the host StdGen draw on its first replicas."""
     drawer = None
     if not args.host_tables and args.config != "gossip":
         from timewarp.engine import draw_link_table
@@ -381,8 +432,24 @@ def main():
         setup["host_check_equal"] = bool(np.array_equal(scn.link_table[:, :, :n_chk], ref.link_table))
         if not setup["host_check_equal"]:
             raise SystemExit("device-drawn link table differs from the host StdGen draw")
-    if args.config == "gossip":
-        return bench_gossip(args, scn, workload, world, rank, local, dist_on, barrier)
+    return scn, workload, setup
+
+
+def measure_replicas(args, rank, world, local, dist_on, barrier, parity=True):
+    """W warm-up and K timed steps of the replica configs on this rank; the
+    parity sample (rank 0: the CPU baseline at N = 1, a smaller oracle check of
+    its own replicas at N > 1)."""
+    import torch
+
+    from timewarp import dist as twd
+    from timewarp.engine import Engine
+
+    if args.geometry == "lpb":
+        _, r_rank = replica_block(args, rank, world)
+        if r_rank & (r_rank - 1):
+            raise SystemExit(f"--geometry lpb needs a power-of-two replica count per GPU (lanes are node << log2(R) "
+                             f"| replica); rank {rank} of {world} would get {r_rank} of {args.replicas} replicas")
+    scn, workload, setup = setup_scenario(args, rank, world, local)
     # one rank of the job: the library's RCCL communicator over the ranks
     # (tw_create_rank) all-reduces every tw_run's statistics
     comm = twd.library_comm(world, rank) if dist_on else None
@@ -406,6 +473,7 @@ def main():
     msg = {"delivered": 0, "dropped": 0, "undeliverable": 0}
     kernel_ms = 0.0
     launches = 0
+    lpb_wt = None
     for _ in range(args.steps):
         eng.reset()
         barrier()
@@ -432,89 +500,105 @@ def main():
     hashes = eng.hashes()
     # st.* are the job's (tw_run's statistics, all-reduced by the library over
     # the ranks); this rank's own share is in its replicas' results
-    loc_events = int(res["events"].sum()) * args.steps
-    loc_sends = int((res["delivered"] + res["dropped"] + res["undeliverable"]).sum()) * args.steps
-    tot_events = events
-    max_elapsed = (twd.reduce_stats({"elapsed_s": elapsed}, device=f"cuda:{local}")["elapsed_s"]
-                   if dist_on else elapsed)
-
-    if rank == 0:
-        value = tot_events / max_elapsed
-        alg_bytes = BYTES_PER_EVENT * loc_events + BYTES_PER_SEND * loc_sends   # this rank, K steps
-        achieved = alg_bytes / (kernel_ms / 1e3) / 1e9 if kernel_ms > 0 else 0.0
-        out = {
-            "metric": "committed events/sec (whole node) + % HBM roofline, token-ring 64k replicas"
-            if args.config == "token_ring" else f"committed events/sec (whole node), {args.config}",
-            "value": value,
-            "unit": "events/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": max_elapsed * 1e3 / args.steps,
-            "higher_is_better": True,
-            "scaling": "weak" if args.weak else "strong",
-            "vs_baseline": None,
-            "dtype": "int64",
-            "data": "synthetic (scenario tables drawn from random-1.1 StdGen, seed = replica id)",
-            "config": {
-                "workload": workload,
-                "replicas_total": args.replicas * (world if args.weak else 1),
-                "replicas_rank0": scn.n_replicas,
-                "events_per_step": int(tot_events / args.steps),
-                "parallelism": (f"replica-sharded x{world}: {scn.n_replicas} replicas per GPU, seeds [g*R, (g+1)*R) "
-                                "(no data-path collective)" if args.weak else
-                                f"replica-sharded x{world}: one batch in contiguous blocks (no data-path collective)"),
-                "geometry": eng.geometry(),
-                "tie_order": tie,
-            },
-            "roofline": {
-                "bound": "hbm",
-                "achieved": achieved,
-                "peak": HBM_PEAK_GBS,
-                "unit": "GB/s",
-                "frac": achieved / HBM_PEAK_GBS,
-                "traffic": None,
-                "kernel": "tw_run_kernel" if eng.geometry() != "lpb" else "tw_run_kernel<LP> window loop",
-                "launches": launches,
-                "avg_launch_ms": kernel_ms / max(1, launches),
-                "algorithmic_bytes": "64 B/event + 8 B/send (SURVEY.md 8d)",
-            },
-        }
-        out["roofline"]["algorithmic_per_event"] = alg_bytes / max(1, loc_events)
-        out["setup"] = setup
-        if eng.geometry() == "lpb":
-            out["config"]["parallelism"] = (f"replica-sharded x{world}; inside a GPU every (node, replica) pair is a "
-                                            "logical process: one device window loop, lookahead = min link delay")
-            out["config"]["windows"], out["config"]["ticks"] = lpb_wt
-            out["roofline"]["kernel_ms_note"] = ("one launch = the whole device window loop (event kernels + "
-                                                 "due/pack/compact/advance kernels), HIP events")
-        # what the timed events are (the job, per step): message sends, arrivals
-        # (delivered / dropped / no listener), threads forked, and the rest
-        # (waits, wake-ups, kills, timeouts)
-        per = {k: v // args.steps for k, v in msg.items()}
-        per["sends"] = sends // args.steps
-        per["threads_forked"] = int(res["threads"].sum())
-        per["events"] = events // args.steps
-        arrivals = per["delivered"] + per["dropped"] + per["undeliverable"]
-        # arrival pops over all pops (each delivered message also forks a
-        # handler thread and wakes its receiver: DESIGN.md section 6)
-        per["arrivals_frac"] = arrivals / max(1, per["events"])
-        out["events_breakdown"] = per
-        mt = (measured_traffic(args, launches / args.steps, loc_events / args.steps, eng.geometry() == "lpb")
-              if world == 1 else None)
-        if mt:
-            out["roofline"].update(mt)
-        if not args.no_cpu_baseline and world == 1:  # (the CPU baseline: rank 0 at N=1 only)
-            cb, parity, n = cpu_baseline(scn, res, hashes, args.cpu_seconds)
-            out["cpu_baseline"] = cb
-            out["parity_sample"] = {"replicas": n, "bit_exact": bool(parity),
-                                    "against": "oracle canonical (t, seq) order"}
-        print(json.dumps(out), flush=True)
-        if "parity_sample" in out and not out["parity_sample"]["bit_exact"]:
-            raise SystemExit("parity_sample: the GPU results differ from the oracle's")
+    m = {"scn_replicas": scn.n_replicas, "workload": workload, "setup": setup, "tie": tie,
+         "geometry": eng.geometry(), "lpb_wt": lpb_wt, "steps": args.steps,
+         "loc_events": int(res["events"].sum()) * args.steps,
+         "loc_sends": int((res["delivered"] + res["dropped"] + res["undeliverable"]).sum()) * args.steps,
+         "tot_events": events, "sends": sends, "msg": msg, "kernel_ms": kernel_ms, "launches": launches,
+         "threads_forked": int(res["threads"].sum())}
+    m["max_elapsed"] = (twd.reduce_stats({"elapsed_s": elapsed}, device=f"cuda:{local}")["elapsed_s"]
+                        if dist_on else elapsed)
+    m["value"] = events / m["max_elapsed"]
+    m["ms_per_step"] = m["max_elapsed"] * 1e3 / args.steps
     eng.close()
-    if dist_on:
-        dist.destroy_process_group()
+    if rank == 0 and parity and not args.no_cpu_baseline:
+        if world == 1:  # the CPU baseline: rank 0 at N=1 only; its results double as the parity sample
+            cb, ok, n = cpu_baseline(scn, res, hashes, args.cpu_seconds)
+            m["cpu_baseline"] = cb
+        else:  # N > 1: no CPU timing, but still an oracle check of this rank's own replicas
+            ok, n = parity_sample(scn, res, hashes, args.cpu_seconds / 2)
+        m["parity_sample"] = {"replicas": n, "bit_exact": bool(ok),
+                              "against": "oracle canonical (t, seq) order"
+                                         + ("" if world == 1 else f", rank 0's replicas [0,{n}) of its block")}
+    return m
+
+
+def replica_line(args, world, m):
+    """The bench JSON line of a replica config from measure_replicas' numbers."""
+    value = m["value"]
+    alg_bytes = BYTES_PER_EVENT * m["loc_events"] + BYTES_PER_SEND * m["loc_sends"]   # this rank, K steps
+    kernel_ms, launches = m["kernel_ms"], m["launches"]
+    achieved = alg_bytes / (kernel_ms / 1e3) / 1e9 if kernel_ms > 0 else 0.0
+    geometry = m["geometry"]
+    out = {
+        "metric": "committed events/sec (whole node) + % HBM roofline, token-ring 64k replicas"
+        if args.config == "token_ring" else f"committed events/sec (whole node), {args.config}",
+        "value": value,
+        "unit": "events/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": m["ms_per_step"],
+        "higher_is_better": True,
+        "scaling": "weak" if args.weak else "strong",
+        "vs_baseline": None,
+        "dtype": "int64",
+        "data": "synthetic (scenario tables drawn from random-1.1 StdGen, seed = replica id)",
+        "config": {
+            "workload": m["workload"],
+            "baseline_config": ("BASELINE config 3: one batch of 65,536 replicas split over the GPUs"
+                                if args.config == "token_ring" and not args.weak and args.replicas == 65536 else None),
+            "replicas_total": args.replicas * (world if args.weak else 1),
+            "replicas_rank0": m["scn_replicas"],
+            "events_per_step": int(m["tot_events"] / args.steps),
+            "parallelism": (f"replica-sharded x{world}: {m['scn_replicas']} replicas per GPU, seeds [g*R, (g+1)*R) "
+                            "(no data-path collective)" if args.weak else
+                            f"replica-sharded x{world}: one batch in contiguous blocks (no data-path collective)"),
+            "geometry": geometry,
+            "tie_order": m["tie"],
+        },
+        "roofline": {
+            "bound": "hbm",
+            "achieved": achieved,
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS,
+            "traffic": None,
+            "kernel": "tw_run_kernel" if geometry != "lpb" else "tw_run_kernel<LP> window loop",
+            "launches": launches,
+            "avg_launch_ms": kernel_ms / max(1, launches),
+            "algorithmic_bytes": "64 B/event + 8 B/send (SURVEY.md 8d)",
+        },
+    }
+    out["roofline"]["algorithmic_per_event"] = alg_bytes / max(1, m["loc_events"])
+    out["setup"] = m["setup"]
+    if geometry == "lpb":
+        out["config"]["parallelism"] = (f"replica-sharded x{world}; inside a GPU every (node, replica) pair is a "
+                                        "logical process: one device window loop, lookahead = min link delay")
+        out["config"]["windows"], out["config"]["ticks"] = m["lpb_wt"]
+        out["roofline"]["kernel_ms_note"] = ("one launch = the whole device window loop (event kernels + "
+                                             "due/pack/compact/advance kernels), HIP events")
+    # what the timed events are (the job, per step): message sends, arrivals
+    # (delivered / dropped / no listener), threads forked, and the rest
+    # (waits, wake-ups, kills, timeouts)
+    per = {k: v // args.steps for k, v in m["msg"].items()}
+    per["sends"] = m["sends"] // args.steps
+    per["threads_forked"] = m["threads_forked"]
+    per["events"] = m["tot_events"] // args.steps
+    arrivals = per["delivered"] + per["dropped"] + per["undeliverable"]
+    # arrival pops over all pops (each delivered message also forks a
+    # handler thread and wakes its receiver: DESIGN.md section 6)
+    per["arrivals_frac"] = arrivals / max(1, per["events"])
+    out["events_breakdown"] = per
+    mt = (measured_traffic(args, launches / args.steps, m["loc_events"] / args.steps, geometry == "lpb")
+          if world == 1 else None)
+    if mt:
+        out["roofline"].update(mt)
+    if "cpu_baseline" in m:
+        out["cpu_baseline"] = m["cpu_baseline"]
+    if "parity_sample" in m:
+        out["parity_sample"] = m["parity_sample"]
+    return out
 
 
 if __name__ == "__main__":

@@ -1,9 +1,10 @@
 """Multi-rank replica sharding with world_size 2 over gloo (CPU).
 
 Each rank owns a contiguous block of one global batch (strong scaling,
-`bench.py --strong`: dist.strong_block, uneven here so the remainder rule is
-exercised; bench.py's default since round 5 is weak scaling, each rank a batch
-of its own: dist.weak_block, test_bench_replica_blocks); the per-rank run (here the oracle, standing in for the per-GPU
+bench.py's default -- BASELINE config 3's 64k over the GPUs: dist.strong_block,
+uneven here so the remainder rule is exercised; `bench.py --weak` and the
+token ring's weak_line give each rank a batch of its own: dist.weak_block,
+test_bench_replica_blocks); the per-rank run (here the oracle, standing in for the per-GPU
 engine which needs a device) is reduced with timewarp.dist exactly as bench.py
 does over RCCL.  The union must equal a single-process run of all replicas,
 replica for replica."""
@@ -116,10 +117,13 @@ def test_record_exchange_all_to_all(tmp_path):
 
 
 def test_bench_replica_blocks():
-    """bench.py's rank blocks: weak scaling by default (rank g runs global
-    replicas [g*R, (g+1)*R), its tables drawn from mkStdGen(g*R + i)), one
-    batch split with --strong; the workload key names the choice, so a PMC
-    summary of one is never used for the other."""
+    """bench.py's rank blocks: --weak (rank g runs global
+    replicas [g*R, (g+1)*R), its tables drawn from mkStdGen(g*R + i)), or
+    one batch split (the default since round 6: BASELINE config 3's 64k over
+    the GPUs); the workload key names the choice, so a PMC summary of one is
+    never used for the other.  The default geometry follows the per-GPU share:
+    batched logical processes at 8,192 replicas per GPU (8 GPUs), the replica
+    kernels from 16,384 up, and the weak line's 64k per GPU."""
     import argparse
     import importlib.util
     import pathlib
@@ -136,3 +140,11 @@ def test_bench_replica_blocks():
     blocks = [bench.replica_block(args, g, 8) for g in range(8)]
     assert blocks[0] == (0, 8192) and blocks[7] == (57344, 8192) and sum(n for _, n in blocks) == 65536
     assert ":weak=0:" in bench.workload_key(args)
+    for world, geo in ((1, None), (2, None), (4, None), (8, "lpb")):
+        a = argparse.Namespace(**vars(args))
+        bench.pick_geometry(a, world)
+        assert a.geometry == geo, (world, a.geometry)
+    a = argparse.Namespace(**vars(args))
+    a.weak = True
+    bench.pick_geometry(a, 8)
+    assert a.geometry is None

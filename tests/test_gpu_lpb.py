@@ -301,3 +301,57 @@ def test_lpb_batched_delivery_c5_shape(engine_mod, oracle_mod):
     scn = scenarios.hotspot(n_senders=256, n_replicas=16, msg_num=100)
     ores, (bat, due) = _lpb_batched(scn, engine_mod, oracle_mod)
     assert bat >= 0.5 * due
+
+
+def test_lpb_batched_delivery_benched_shape_256(engine_mod, oracle_mod):
+    """C5's full message count on a 256-replica batch: 256 senders x 1,000
+    messages each, every replica against the sequential oracle (the bench's
+    own check samples ~1k of 4,096 replicas; tools/parity_all.py runs all)."""
+    scn = scenarios.hotspot(n_senders=256, n_replicas=256, msg_num=1000)
+    ores, (bat, due) = _lpb_batched(scn, engine_mod, oracle_mod, threads=16)
+    assert ores["delivered"].sum() == 2 * 256 * 1000 * 256
+    assert bat >= 0.5 * due, (bat, due)
+
+
+def test_lpb_batched_delivery_over_the_cap(engine_mod, oracle_mod):
+    """More than TW_BATCH_CAP (1,024) due records per lane and window: 100
+    senders at one ping per 80 µs over 1-ms links put ~1,250 pings in each
+    window's due run; the batch takes at most the cap and the rest runs on the
+    chain, bit-exact against the oracle."""
+    scn = scenarios.hotspot(n_senders=100, n_replicas=8, msg_num=60, msg_rate=12_500, duration_s=1,
+                            network_delay=(1000, 1000))
+    # (the builder sizes a tick's outbox for one ping per sender and window;
+    # here each sender sends 12.5 per 1-ms window)
+    caps = np.array(scn.meta["lp_inbox_cap"], np.uint32)
+    caps[100] = 2048  # the receiver: every ping of a window in flight (tw_lp_due stages up to 2,048)
+    scn.meta = dict(scn.meta, lp_outbox_cap=1 << 16, lp_inbox_cap=caps)
+    ores, (bat, due) = _lpb_batched(scn, engine_mod, oracle_mod)
+    assert due > 1024 and bat > 0, (bat, due)
+
+
+def test_lpb_batched_delivery_full_lane_fails_like_the_chain(engine_mod, oracle_mod, monkeypatch):
+    """A lane with no free thread slot: on the chain the first due pop fails
+    the replica with TW_REP_ERR_SLOTS (alloc_slot), so the batch must leave
+    such a lane's due run to the chain.  One slot per lane: every
+    node's own thread fills it; batched and chain runs end the same."""
+    import copy
+
+    base = scenarios.hotspot(n_senders=64, n_replicas=16, msg_num=40)
+    scn = copy.copy(base)
+    scn.meta = dict(base.meta, lp_max_slots=1)
+    out = {}
+    for mode in ("1", "0"):
+        monkeypatch.setenv("TW_LP_BATCH", mode)
+        with engine_mod.Engine(0) as e:
+            e.load(scn, geometry="lpb")
+            e.reset()
+            with pytest.raises(engine_mod.EngineError):
+                e.run()
+            out[mode] = (e.results(), e.hashes(), e.lpb_batch())
+    (r1, h1, (b1, _)), (r0, h0, (b0, _)) = out["1"], out["0"]
+    assert b0 == 0 and b1 == 0, (b1, b0)
+    assert (r1["status"] == 3).all()  # TW_REP_ERR_SLOTS
+    for f in RESULT_FIELDS:
+        if f != "tie_flags":
+            assert np.array_equal(r1[f], r0[f]), f
+    assert np.array_equal(h1, h0)

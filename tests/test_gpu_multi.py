@@ -166,20 +166,26 @@ def test_lp_run_local_failure_agreed(engine_mod, oracle_mod, monkeypatch, mode):
     assert lp.done == 1 and lp.err == 0
 
 
-def test_rccl_failure_marks_the_context_unusable(engine_mod, oracle_mod, monkeypatch):
-    """A failed RCCL call (injected: TW_TEST_FAIL_NCCL=1 fails the next checked
-    call without making it) returns TW_ERR_COMM and marks the context: every
+@pytest.mark.parametrize("k", [1, 2, 3, 4])
+def test_rccl_failure_marks_the_context_unusable(engine_mod, oracle_mod, monkeypatch, k):
+    """A failed RCCL call returns TW_ERR_COMM and marks the context: every
     later call that communicates returns TW_ERR_COMM at once instead of
     entering a collective its peers may no longer be in (include/timewarp.h,
-    tw_lp_run).  A fresh context works again."""
-    jid = engine_mod.comm_id()
+    tw_lp_run).  Injected with TW_TEST_FAIL_NCCL=k, read when the context is
+    made: its k-th checked RCCL call fails without being made -- tw_run's
+    statistics reduction is ncclGroupStart (1), two ncclAllReduce calls (2, 3)
+    and ncclGroupEnd (4), so k = 2, 3 fail inside the group, which the library
+    must close before it returns, and k = 4 fails at the close itself.  The
+    broken context is aborted (ncclCommAbort) at tw_destroy, and a fresh
+    context made afterwards on the same thread -- its own group not folded
+    into a half-open one -- works again."""
     scn = scenarios.token_ring(n_nodes=10, n_replicas=48, launch_duration=25_000_000, drop_log2=4)
-    with engine_mod.Engine(0, comm=(1, 0, jid)) as e:
+    monkeypatch.setenv("TW_TEST_FAIL_NCCL", str(k))
+    with engine_mod.Engine(0, comm=(1, 0, engine_mod.comm_id())) as e:
+        monkeypatch.delenv("TW_TEST_FAIL_NCCL")  # (read once, at tw_create_rank)
         e.load(scn)
-        monkeypatch.setenv("TW_TEST_FAIL_NCCL", "1")
         with pytest.raises(engine_mod.EngineError, match=r"tw_run failed: -8 "):
             e.run()
-        monkeypatch.delenv("TW_TEST_FAIL_NCCL")
         e.reset()
         with pytest.raises(engine_mod.EngineError, match=r"tw_run failed: -8 "):
             e.run()

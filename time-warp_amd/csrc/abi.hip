@@ -75,6 +75,10 @@ struct tw_ctx {
     // collective the peers are still in, so every later communicating call
     // returns TW_ERR_COMM without entering another one (timewarp.h, tw_lp_run)
     bool comm_broken = false;
+    // testing hook (nccl_test_fail): TW_TEST_FAIL_NCCL as it was when the
+    // context was made (0: off), and the checked RCCL calls made since
+    long test_fail_at = 0;
+    std::atomic<long> test_calls{0};
 };
 
 namespace {
@@ -83,25 +87,46 @@ int comm_fail(ncclResult_t r, const char* what) {
     fprintf(stderr, "timewarp: %s failed: %s\n", what, ncclGetErrorString(r));
     return TW_ERR_COMM;
 }
-// testing hook: with TW_TEST_FAIL_NCCL=k in the environment the k-th checked
-// RCCL call since it was set (counting from 1) fails without being made
-// (one-rank jobs in the tests); the count restarts whenever it is unset
-bool nccl_test_fail() {
-    static std::atomic<long> n{0};
+// testing hook: a context made with TW_TEST_FAIL_NCCL=k in the environment
+// fails its k-th checked RCCL call (counting from 1) without making it
+// (one-rank jobs in the tests).  The variable is read once, when the context
+// is made (test_hook_init), not on every call.
+void test_hook_init(tw_ctx* c) {
     const char* e = getenv("TW_TEST_FAIL_NCCL");
-    if (!e) {
-        n = 0;
-        return false;
-    }
-    return ++n == atol(e);
+    c->test_fail_at = e ? atol(e) : 0;
 }
+bool nccl_test_fail(tw_ctx* c) { return c->test_fail_at > 0 && ++c->test_calls == c->test_fail_at; }
 // (in a function of the context c: a failure marks it unusable)
 #define NCCLCHK(x)                                   \
     do {                                             \
-        ncclResult_t _r = nccl_test_fail() ? ncclInternalError : (x); \
+        ncclResult_t _r = nccl_test_fail(c) ? ncclInternalError : (x); \
         if (_r != ncclSuccess) {                     \
             c->comm_broken = true;                   \
             return comm_fail(_r, #x);                \
+        }                                            \
+    } while (0)
+// ... between ncclGroupStart and ncclGroupEnd: a failure closes the group
+// first, so the thread is not left inside it (a later group of this thread --
+// a fresh context's -- would be folded into the open one); the broken
+// communicators are then aborted, not destroyed (destroy_parts)
+#define NCCLCHK_G(x)                                 \
+    do {                                             \
+        ncclResult_t _r = nccl_test_fail(c) ? ncclInternalError : (x); \
+        if (_r != ncclSuccess) {                     \
+            (void)ncclGroupEnd();                    \
+            c->comm_broken = true;                   \
+            return comm_fail(_r, #x);                \
+        }                                            \
+    } while (0)
+// ... the group's end: an injected failure still closes the group
+#define NCCLCHK_GEND()                               \
+    do {                                             \
+        const bool _inj = nccl_test_fail(c);         \
+        ncclResult_t _r = ncclGroupEnd();            \
+        if (_inj) _r = ncclInternalError;            \
+        if (_r != ncclSuccess) {                     \
+            c->comm_broken = true;                   \
+            return comm_fail(_r, "ncclGroupEnd()");  \
         }                                            \
     } while (0)
 #define NCCLCHK_NC(x)                                \
@@ -170,11 +195,11 @@ int job_reduce(tw_ctx* c, std::vector<std::vector<uint64_t>>& sums, std::vector<
     }
     NCCLCHK(ncclGroupStart());
     for (size_t i = 0; i < n; ++i) {
-        NCCLCHK(ncclAllReduce(buf[i], buf[i], ns, ncclUint64, ncclSum, c->comm[i], nullptr));
-        NCCLCHK(ncclAllReduce((char*)buf[i] + 8 * ns, (char*)buf[i] + 8 * ns, nm, ncclInt64, ncclMax, c->comm[i],
+        NCCLCHK_G(ncclAllReduce(buf[i], buf[i], ns, ncclUint64, ncclSum, c->comm[i], nullptr));
+        NCCLCHK_G(ncclAllReduce((char*)buf[i] + 8 * ns, (char*)buf[i] + 8 * ns, nm, ncclInt64, ncclMax, c->comm[i],
                               nullptr));
     }
-    NCCLCHK(ncclGroupEnd());
+    NCCLCHK_GEND();
     for (size_t i = 0; i < n; ++i) {
         HIPCHK_A(hipSetDevice(c->dev[i]));
         HIPCHK_A(hipStreamSynchronize(nullptr));
@@ -282,8 +307,10 @@ void split(uint32_t total, uint32_t parts, uint32_t i, uint32_t& b0, uint32_t& n
 }
 
 int destroy_parts(tw_ctx* c) {
+    // (a failed call may have left a collective the peers never joined:
+    // abort, which does not wait for it, instead of destroy)
     for (size_t i = 0; i < c->comm.size(); ++i)
-        if (c->comm[i]) (void)ncclCommDestroy(c->comm[i]);
+        if (c->comm[i]) (void)(c->comm_broken ? ncclCommAbort(c->comm[i]) : ncclCommDestroy(c->comm[i]));
     c->comm.clear();
     for (size_t i = 0; i < c->sh.size(); ++i) {
         (void)hipSetDevice(c->dev[i]);
@@ -347,6 +374,7 @@ int tw_create(const int* devices, int ndev, tw_ctx** out) {
     }
     c->world = ndev;
     c->rank0 = 0;
+    test_hook_init(c);
     if (ndev > 1) {
         std::vector<int> sorted(c->dev);
         std::sort(sorted.begin(), sorted.end());
@@ -395,6 +423,7 @@ int tw_create_rank(int device, int nranks, int rank, const uint8_t* id, tw_ctx**
     c->world = nranks;
     c->rank0 = rank;
     c->tp = TP_RCCL;
+    test_hook_init(c);
     ncclUniqueId u;
     std::memcpy(&u, id, sizeof(u));
     c->comm.assign(1, nullptr);
@@ -766,8 +795,8 @@ int tw_lp_results(tw_ctx* c, tw_replica_result* agg, uint64_t* node_hashes, size
             }
             NCCLCHK(ncclGroupStart());
             for (size_t i = 0; i < n; ++i)
-                NCCLCHK(ncclAllReduce(buf[i], buf[i], n_nodes, ncclUint64, ncclSum, c->comm[i], nullptr));
-            NCCLCHK(ncclGroupEnd());
+                NCCLCHK_G(ncclAllReduce(buf[i], buf[i], n_nodes, ncclUint64, ncclSum, c->comm[i], nullptr));
+            NCCLCHK_GEND();
             for (size_t i = 0; i < n; ++i) {
                 HIPCHK_A(hipSetDevice(c->dev[i]));
                 HIPCHK_A(hipStreamSynchronize(nullptr));
@@ -914,10 +943,10 @@ int tw_lp_run(tw_ctx* c, uint64_t max_ticks, tw_lp_state* out) {
                 NCCLCHK(ncclGroupStart());
                 for (size_t i = 0; i < n; ++i)
                     for (int g = 0; g < c->world; ++g) {
-                        NCCLCHK(ncclSend((char*)x[i].send + g * stride_b, bytes, ncclUint8, g, c->comm[i], x[i].stream));
-                        NCCLCHK(ncclRecv((char*)x[i].recv + g * stride_b, bytes, ncclUint8, g, c->comm[i], x[i].stream));
+                        NCCLCHK_G(ncclSend((char*)x[i].send + g * stride_b, bytes, ncclUint8, g, c->comm[i], x[i].stream));
+                        NCCLCHK_G(ncclRecv((char*)x[i].recv + g * stride_b, bytes, ncclUint8, g, c->comm[i], x[i].stream));
                     }
-                NCCLCHK(ncclGroupEnd());
+                NCCLCHK_GEND();
             } else {
                 for (size_t i = 0; i < n; ++i) {
                     HIPCHK_A(hipSetDevice(c->dev[i]));
@@ -942,8 +971,8 @@ int tw_lp_run(tw_ctx* c, uint64_t max_ticks, tw_lp_state* out) {
             if (c->tp == TP_RCCL) {
                 NCCLCHK(ncclGroupStart());
                 for (size_t i = 0; i < n; ++i)
-                    NCCLCHK(ncclAllReduce(x[i].red, x[i].red, RD_N, ncclInt64, ncclMin, c->comm[i], x[i].stream));
-                NCCLCHK(ncclGroupEnd());
+                    NCCLCHK_G(ncclAllReduce(x[i].red, x[i].red, RD_N, ncclInt64, ncclMin, c->comm[i], x[i].stream));
+                NCCLCHK_GEND();
             } else {
                 for (size_t i = 0; i < n; ++i) {
                     HIPCHK_A(hipSetDevice(c->dev[i]));

@@ -77,6 +77,12 @@
 #ifndef TW_LP_FOLDJ
 #define TW_LP_FOLDJ 1  // the LP kernels fold a jump into the pass before it (Lane::FOLDJ; 0: the A/B baseline)
 #endif
+// the run geometries' lock-step fast path (Lane::fast_run): measured slower
+// (C3 138.8 -> 144.3 ms per step), so off -- 1 builds it for A/B
+#ifndef TW_FAST
+#define TW_FAST 0
+#endif
+#define TW_FAST_MAX 32u  // instructions per fast_run entry
 #ifndef TW_LP_WAVES
 #define TW_LP_WAVES 2
 #endif
@@ -306,6 +312,8 @@ struct Lane {
     // (`forM_ [1..N] fork`, examples/token-ring/Main.hs:65-68) takes two passes
     // per fork instead of three
     static constexpr bool FOLDJ = HR || (LP && TW_LP_FOLDJ);
+    // the lock-step fast path (fast_run): the run geometries
+    static constexpr bool FAST = HR && TW_FAST;
     // per-lane hot passes (lanes at different hot ops share a pass) pay off where
     // lanes diverge -- logical processes and the few-replica sparse geometry; the
     // dense replica geometry runs lock-step programs and keeps the cheaper
@@ -2038,6 +2046,138 @@ struct Lane {
         fin = at ? tc : fin;
         running = running && !(at && tc != T_NONE);
     }
+    // Lock-step fast path (round 6, the run geometries: TW_FAST).  When every
+    // running lane of the wave is at the same pc -- the replicas of one
+    // scenario step through the same code, e.g. C3's start-up: main's `forM_
+    // fork launchNode`, launchNode's forks, the worker's `catch ; sleepForever`,
+    // the server's `listen ; sleepForever` (examples/token-ring/Main.hs:
+    // 65-68,104-135) -- the instruction is one scalar word: it is read once
+    // (an LDS broadcast) and decoded in SGPRs, and its body is the op's own
+    // few vector instructions.  Consecutive instructions run in one loop, and
+    // the step's terminal (a wait's yield, END, FORK) leaves it, with no
+    // general pass -- whose per-lane decode, opcode-uniform lane match, class
+    // branches, fold checks and epilogue cost ~2.4k cycles per instruction
+    // (tools/stats_probe.py).  The semantics are the pass's,
+    // instruction for instruction: the same counts n (the 2^22 cap), register
+    // writes, node variable / binding / frame stores, hash terms and terminal
+    // staging.  Anything else -- a rare op, a fused pair, a jump the lanes
+    // take differently, an instruction that would fail (a bad node, frames
+    // over the cap, an out-of-range target, the step cap) -- leaves the lanes
+    // at its pc for the general pass, which executes it exactly as before.
+    __device__ __forceinline__ void fast_run(Th& th, uint32_t slot, St& s) {
+        const uint64_t rm = __builtin_amdgcn_ballot_w64(s.running);
+        if (!rm) return;
+        uint32_t fp = __builtin_amdgcn_readlane(s.pc, (uint32_t)__builtin_ctzll(rm));
+        if (__builtin_amdgcn_ballot_w64(s.running && s.pc != fp)) return;  // lanes at different pcs
+        const bool run = s.running;
+        for (uint32_t k = 0; k < TW_FAST_MAX; ++k) {
+            // (the image's last instruction goes to the general pass: running off
+            // the end is its error, counted as it counts it)
+            if (fp + 1u >= c.n_insns || __builtin_amdgcn_ballot_w64(run && s.n >= TW_STEP_CAP)) break;
+            const uint2 in = P[fp];
+            const uint32_t w = __builtin_amdgcn_readfirstlane(in.x);
+            const int32_t imm = (int32_t)__builtin_amdgcn_readfirstlane(in.y);
+            const uint32_t op = w & 0xFFu, a = (w >> 8) & 3u, b = w >> 16;
+            uint32_t nx = fp + 1u;      // the next pc (uniform)
+            uint32_t fin = T_NONE;      // a terminal: every running lane leaves the step
+            if (op == TW_OP_FORK) {     // r[a] <- ref(child) at the terminal (TimedT.hs:326-342)
+                const uint32_t node = b == 0xFFFFu ? th.w1 : (uint32_t)rg(th, b & 3u);
+                if (__builtin_amdgcn_ballot_w64(run && node >= c.N)) break;
+                csp(run, CW_CPC, (uint32_t)imm);
+                csp(run, CW_CNODE, node);
+                csp(run, CW_CRA, a);
+                csp(run, CW_CDEL, 2u);  // the child's registers are the parent's
+                fin = T_SPAWN;
+            } else if (op == TW_OP_WAIT_REL || op == TW_OP_WAIT_ABS || op == TW_OP_WAIT_REG) {
+                int64_t wt;
+                if (op == TW_OP_WAIT_REG) {
+                    const int64_t ra = rg(th, a);
+                    wt = now + (ra > 0 ? ra : 0);
+                } else {
+                    const int64_t kt = K[imm];
+                    wt = op == TW_OP_WAIT_REL ? now + kt : (kt > now ? kt : now);
+                }
+                s.yt = run ? wt : s.yt;
+                fin = T_YIELD;
+            } else if (op == TW_OP_END) {
+                fin = T_EXIT;
+            } else if (op == TW_OP_JMP) {
+                if ((uint32_t)imm >= c.n_insns) break;
+                nx = (uint32_t)imm;
+            } else if (op >= TW_OP_JEQ && op <= TW_OP_JNEI) {
+                if ((uint32_t)imm >= c.n_insns) break;
+                const int64_t ra = rg(th, a), rb = rg(th, b & 3u), bi = (int64_t)(int16_t)b;
+                const bool tk = op == TW_OP_JEQ ? ra == rb : op == TW_OP_JNE ? ra != rb : op == TW_OP_JLT ? ra < rb
+                              : op == TW_OP_JLE ? ra <= rb : op == TW_OP_JEQI ? ra == bi : ra != bi;
+                const uint64_t tm = __builtin_amdgcn_ballot_w64(run && tk);
+                if (tm != 0 && tm != rm) break;  // the lanes part ways: the general pass
+                nx = tm ? (uint32_t)imm : nx;
+            } else if (op == TW_OP_SETI || op == TW_OP_SETK || op == TW_OP_ADDI || op == TW_OP_MULI ||
+                       op == TW_OP_MOV || op == TW_OP_ADD || op == TW_OP_SUB || op == TW_OP_NOW ||
+                       op == TW_OP_NODE || op == TW_OP_MYTID) {
+                const bool two = op == TW_OP_MOV || op == TW_OP_ADD || op == TW_OP_SUB;
+                if (!two && op != TW_OP_MYTID && (b & TW_ALU_NSTORE)) break;  // a fused pair
+                const int64_t ra = rg(th, a);
+                const int64_t rb = two ? rg(th, b & 3u) : 0;
+                int64_t v;
+                if (op == TW_OP_SETI) v = imm;
+                else if (op == TW_OP_SETK) v = K[imm];
+                else if (op == TW_OP_ADDI) v = ra + (int64_t)imm;
+                else if (op == TW_OP_MULI) v = ra * (int64_t)imm;
+                else if (op == TW_OP_MOV) v = rb;
+                else if (op == TW_OP_ADD) v = ra + rb;
+                else if (op == TW_OP_SUB) v = ra - rb;
+                else if (op == TW_OP_NOW) v = now;
+                else if (op == TW_OP_NODE) v = (int64_t)th.w1;
+                else v = (int64_t)(((uint64_t)th.w2 << 32) | slot);
+                rs(th, a, run ? v : ra);
+            } else if (op == TW_OP_NLOAD) {
+                const int64_t x = gp(c.nvars)[nix(run ? th.w1 : 0u, b & 3u)];
+                tw_vm_drain();
+                if (run) rs(th, a, x);
+            } else if (op == TW_OP_NSTORE) {
+                const int64_t ra = rg(th, a);
+                if (run) gp(c.nvars)[nix(th.w1, b & 3u)] = ra;
+            } else if (op == TW_OP_TRACE) {
+                if (c.trace_cap || (b & TW_TRACE_PAIR)) break;
+                const int64_t ra = rg(th, a);
+                hacc += run ? term(now, TW_KIND_TRACE | ((uint32_t)imm & 0xFFFFu), ra) : 0ull;
+            } else if (op == TW_OP_CATCH) {
+                const uint32_t nf = th_nfr(th);
+                if (__builtin_amdgcn_ballot_w64(run && nf >= c.max_frames)) break;
+                const uint32_t fv = (b << 16) | ((uint32_t)imm & 0xFFFFu);
+                th.f0 = (run && nf == 0) ? fv : th.f0;
+                th.f1 = (run && nf == 1) ? fv : th.f1;
+                q1d = q1d || (run && nf < 2);
+                if (run && nf >= 2) *fxp(slot, nf) = fv;  // deeper frames: the overflow area
+                th.w0 = run ? (th.w0 & ~(15u << 16)) | ((nf + 1) << 16) : th.w0;
+            } else if (op == TW_OP_LISTEN) {
+                if ((uint32_t)imm >= c.n_sets) break;
+                if (run) {
+                    gp(c.bind)[bix(th.w1)] = (uint32_t)imm + 1;
+                    gp(c.bind_own)[bix(th.w1)] = b ? th.w2 : 0xFFFFFFFFu;
+                }
+                th.w0 = (run && b) ? th.w0 | (F_OWNS << FL_SHIFT) : th.w0;
+            } else if (op == TW_OP_UNLISTEN) {
+                if (run) {
+                    gp(c.bind)[bix(th.w1)] = 0;
+                    gp(c.bind_own)[bix(th.w1)] = 0xFFFFFFFFu;
+                }
+            } else if (op != TW_OP_NOP) {
+                break;  // a rare op: the general pass
+            }
+            STAT(K_INSN);
+            s.n += run ? 1u : 0u;
+            fp = nx;
+            if (fin != T_NONE) {
+                s.fin = run ? fin : s.fin;
+                s.running = false;
+                break;
+            }
+        }
+        s.pc = run ? fp : s.pc;
+    }
+
     // A fork whose child is the very next pop runs the child in place, in this
     // iteration (replica kernels).  TimedT's fork queues the child at now and
     // the parent at now + 1 (TimedT.hs:326-342); the child is PQ.minView's
@@ -2170,7 +2310,11 @@ struct Lane {
                 }
                 break;
             }
-            const uint32_t first = (uint32_t)__builtin_ctzll(mask);
+            if constexpr (FAST) {
+                fast_run(th, slot, s);
+                if (!__builtin_amdgcn_ballot_w64(s.running)) continue;
+            }
+            const uint32_t first = (uint32_t)__builtin_ctzll(__builtin_amdgcn_ballot_w64(s.running));
             // every lane fetches its own instruction; the pass runs the first running
             // lane's opcode in all lanes holding that opcode (their operands and
             // immediates stay per lane), so divergent lanes at different pcs still
@@ -3980,7 +4124,13 @@ __global__ void __launch_bounds__(256) tw_lp_batch(Dev c) {
         __syncthreads();
         if (tid == 0) {
             const uint32_t nd0 = sS[SC_DUE_H] == 0 ? (uint32_t)sS[SC_DUE_N] : 0u;  // (tw_lp_due's fresh run)
+            // a free slot: on the chain each record's phantom takes one at its
+            // wake (due_pop -> alloc_slot) and its handler keeps it (DELIVER's
+            // in-place fork_); a batched prefix never overlaps two records, so
+            // one free slot is what the chain needs -- a full lane stays on the
+            // chain, which fails it with TW_REP_ERR_SLOTS at the first due pop
             const bool el = nd0 && c.trace_cap == 0 && c.tie_mode == TW_TIE_FIFO &&
+                            (sS[SC_FREE_N] > 0 || sS[SC_BUMP] < (uint64_t)c.S) &&
                             sS[SC_STATUS] == TW_REP_RUNNING && sS[SC_PENDING_MAIN] == 0 &&
                             !(c.lpb && gp(c.spawn_n)[r]) && sS[SC_SEQ] + 3ull * nd0 < 0xFFFFFFFFull &&
                             sS[SC_TIDC] + nd0 < 0xFFFFFFFFull;
@@ -4052,7 +4202,10 @@ __global__ void __launch_bounds__(256) tw_lp_batch(Dev c) {
             int64_t m = __shfl_up(cm, 1, 64);  // (exclusive within the wave)
             if (lane == 0) m = INT64_MIN;
             for (uint32_t k = 0; k < wv; ++k) m = wmx[k] > m ? wmx[k] : m;
-            for (uint32_t j = 0; j < 4; ++j) {
+            // (the last thread also checks position TW_BATCH_CAP: a due run of
+            // exactly the cap, or the first record past it, may close the prefix)
+            const uint32_t jn = tid == 255u ? 5u : 4u;
+            for (uint32_t j = 0; j < jn; ++j) {
                 const uint32_t i = tid * 4 + j;
                 if (i > K0) break;
                 // the prefix [0, i) is kept when its last resume precedes record i's

@@ -10,11 +10,12 @@ torch.distributed helpers below remain the thin caller-side pieces (the
 barrier and elapsed-time max of bench.py) and the caller-driven window loops,
 which the gloo tests exercise on CPU.
 
-Weak scaling (the default of bench.py since round 5): every rank runs R
-replicas of its own, global ids [g*R, (g+1)*R) (weak_block).  Strong scaling
-(`bench.py --strong`, BASELINE config 3 read as one batch): one batch of R
-replicas is split into contiguous blocks, rank g owning [g*R/G, (g+1)*R/G)
-(strong_block).  Either way a rank draws its link tables from
+Strong scaling (bench.py's default, BASELINE config 3: "64k replicas
+sharded across 1/2/4/8 GPUs"): one batch of R replicas is split into
+contiguous blocks, rank g owning [g*R/G, (g+1)*R/G) (strong_block).  Weak
+scaling (`bench.py --weak`, and the token ring's `weak_line` beside the
+strong line at N > 1): every rank runs R replicas of its own, global ids
+[g*R, (g+1)*R) (weak_block).  Either way a rank draws its link tables from
 mkStdGen(global replica id), so the union over ranks is bit-identical to one
 process running all of them.
 """

@@ -24,6 +24,7 @@ for s in "$@"; do
     micro)  step micro 300 python tools/micro_probe.py 65536 8 ;;
     probe)  step probe 300 env TW_LIB=$PWD/time-warp_amd/lib/libtimewarp_prof.so python tools/kernel_probe.py 65536 4096 ;;
     stats) step stats 300 env TW_LIB=$PWD/time-warp_amd/lib/libtimewarp_stats.so python tools/stats_probe.py 65536 4096 ;;
+    stats_base) step stats_base 300 env TW_LIB=$PWD/time-warp_amd/lib/libtimewarp_stats_base.so python tools/stats_probe.py 65536 4096 ;;
     stats_c4) step stats_c4 300 env TW_LIB=$PWD/time-warp_amd/lib/libtimewarp_stats.so python -u tools/stats_probe.py gossip ;;
     stats_c5) step stats_c5 400 env TW_LIB=$PWD/time-warp_amd/lib/libtimewarp_stats.so python -u tools/stats_probe.py hotspot 4096 256 ;;
     probe2) step probe2 300 env TW_LIB=$PWD/time-warp_amd/lib/libtimewarp_prof2.so python tools/kernel_probe.py 65536 4096 ;;
@@ -61,6 +62,12 @@ for s in "$@"; do
     multi_tests) step multi_tests 400 python -u -m pytest tests/test_gpu_multi.py -x -v --timeout 200 --timeout-method thread ;;
     fusion_tests) step fusion_tests 400 python -u -m pytest tests/test_send_fusion.py -x -q -m gpu --timeout 200 --timeout-method thread ;;
     throw_tests) step throw_tests 300 python -u -m pytest tests/test_gpu_throw_sequences.py -x -q -m gpu --timeout 120 --timeout-method thread ;;
+    parity_all) step parity_all 900 python -u tools/parity_all.py c3 c2 c5 ;;
+    parity_c3) step parity_c3 600 python -u tools/parity_all.py c3 ;;
+    parity_c5) step parity_c5 600 python -u tools/parity_all.py c5 ;;
+    lpb_new) step lpb_new 600 python -u -m pytest tests/test_gpu_lpb.py -x -v --timeout 300 --timeout-method thread -k "benched_shape_256 or over_the_cap or full_lane" ;;
+    core_tests) step core_tests 900 python -u -m pytest tests/test_gpu_programs.py tests/test_gpu_tie_orders.py tests/test_gpu_parity.py tests/test_gpu_throw_sequences.py -x -q -m gpu --timeout 300 --timeout-method thread ;;
+    ab_c3) bash tools/ab_session.sh token_ring; rc=$?; echo "ab_c3=$rc"; [ $rc -eq 0 ] || exit $rc ;;
     lpb_tests) step lpb_tests 500 python -u -m pytest tests/test_gpu_lpb.py -x -v --timeout 200 --timeout-method thread ;;
     stats_c3_lpb) step stats_c3_lpb 400 env TW_LIB=$PWD/time-warp_amd/lib/libtimewarp_stats.so python -u tools/stats_probe.py lpb_token 8192 ;;
     stats_c5_lpb) step stats_c5_lpb 400 env TW_LIB=$PWD/time-warp_amd/lib/libtimewarp_stats.so python -u tools/stats_probe.py lpb_hotspot 4096 256 ;;
