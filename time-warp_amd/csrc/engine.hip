@@ -611,6 +611,16 @@ static int load_common(tw_shard* c, const tw_scenario_desc* s, bool lp, uint32_t
         ALLOC(d.heavy, c->heavy_ok ? 2 * R : 2);
         ALLOC(d.heavy_n, 2);
         if (lpb) ALLOC(d.bat_ctr, 2);
+        // tw_lp_due_batch's deferred marks: at most one per batched reply, and a
+        // window's replies fit its outbox
+        d.dmk = nullptr;
+        d.dmk_n = nullptr;
+        d.dmk_cap = 0;
+        if (lpb && c->heavy_ok) {
+            d.dmk_cap = d.out_cap;
+            ALLOC(d.dmk, (size_t)2 * d.dmk_cap);
+            ALLOC(d.dmk_n, 2);
+        }
         ALLOC(d.pend_min, 1);
         ALLOC(d.inbox_n, 2 * R);
         ALLOC(d.outbox, (size_t)d.out_cap * 2);
@@ -754,6 +764,7 @@ int sh_reset(tw_shard* c) {
         HIPCHK(hipMemsetAsync(d.hash_g, 0, 8ull * ((size_t)d.Ntot << d.rep_lg), st));
         HIPCHK(hipMemsetAsync(d.heavy_n, 0, 8, st));
         if (d.bat_ctr) HIPCHK(hipMemsetAsync(d.bat_ctr, 0, 16, st));
+        if (d.dmk_n) HIPCHK(hipMemsetAsync(d.dmk_n, 0, 8, st));
         if (d.inlist) HIPCHK(hipMemsetAsync(d.inlist, 0, 4ull * R, st));
         HIPCHK(hipMemsetAsync(d.pend_min, 0xFF, 8, st));
         HIPCHK(hipMemsetAsync(d.out_n, 0, 4, st));
@@ -821,7 +832,12 @@ int sh_run(tw_shard* c, int64_t t_end_us, uint64_t max_events, tw_stats* out) {
         HIPCHK(hipGetLastError());
         c->d.wid += 1u;
     }
-    const uint32_t budget = 1u << 14;  // pops per lane per launch: bounded kernel time
+    // loop iterations (pops) per lane per launch: bounded kernel time
+    static const uint32_t budget = [] {
+        const char* b = getenv("TW_LAUNCH_BUDGET");
+        const long v = b ? strtol(b, nullptr, 10) : 0;
+        return v >= 1 && v <= (1L << 24) ? (uint32_t)v : (1u << 14);
+    }();
     // launches between host checks: a replica run needs several budgets; an LP
     // window is almost always done after one launch
     const int per_check = c->lp ? 1 : 4;
@@ -1235,6 +1251,44 @@ int sh_lp_clear_xmax(tw_shard* c) {
     return TW_OK;
 }
 
+
+// A fresh window's start (every tick launches it; the kernels return unless
+// the window is fresh): the heavy lanes' due runs (tw_lp_due), the work list
+// from the last window's marks (tw_lpb_compact / tw_lp_compact), then the
+// due runs' batchable prefixes (tw_lp_batch: its replies' marks are the next
+// window's, so after the list).  Where the batch runs, tw_lp_due_batch does
+// both in one pass over each heavy lane's records (round 6) and tw_lp_dmark
+// makes its marks after the list -- measured slower (C5 1,463 -> 1,708 ms per
+// step: one 89-KB workgroup per CU runs the batch's dry runs that the separate
+// tw_lp_batch runs three workgroups per CU wide), so only with
+// TW_LP_FUSED=1 (A/B).
+static int lp_window_start(tw_shard* c) {
+    static const bool fused = getenv("TW_LP_FUSED") && getenv("TW_LP_FUSED")[0] == '1';
+    const bool bat = c->heavy_ok && c->d.lpc_bat;
+    const bool fuse = bat && fused && c->d.dmk;
+    if (c->heavy_ok) {
+        if (fuse) hipLaunchKernelGGL(tw_lp_due_batch, dim3(TW_DUE_GRID), dim3(256), 0, c->stream, c->dwin());
+        else hipLaunchKernelGGL(tw_lp_due, dim3(TW_DUE_GRID), dim3(256), 0, c->stream, c->dwin());
+        HIPCHK(hipGetLastError());
+    }
+    if (c->d.rw) {  // per-replica windows: tiles of 64 replicas x one chunk of nodes, four per workgroup
+        const uint32_t nk = ((c->d.R >> c->d.rep_lg) + (1u << TW_CHUNK_LG) - 1u) >> TW_CHUNK_LG;
+        const uint32_t tiles = nk * (((1u << c->d.rep_lg) + 63u) >> 6);
+        hipLaunchKernelGGL(tw_lpb_compact, dim3((tiles + 3) / 4), dim3(256), 0, c->stream, c->dwin());
+    } else {
+        hipLaunchKernelGGL(tw_lp_compact, dim3(compact_blocks(c->d.R)), dim3(256), 0, c->stream, c->dwin(), 0u, 0u);
+    }
+    HIPCHK(hipGetLastError());
+    if (fuse) {
+        hipLaunchKernelGGL(tw_lp_dmark, dim3(64), dim3(256), 0, c->stream, c->dwin());
+        HIPCHK(hipGetLastError());
+    } else if (bat) {
+        hipLaunchKernelGGL(tw_lp_batch, dim3(TW_DUE_GRID), dim3(256), 0, c->stream, c->dwin());
+        HIPCHK(hipGetLastError());
+    }
+    return TW_OK;
+}
+
 int sh_lp_loop_begin(tw_shard* c) {
     if (!c) return TW_ERR_INVALID;
     if (!c->loaded || !c->lp) return TW_ERR_STATE;
@@ -1261,23 +1315,10 @@ int sh_lp_loop_begin(tw_shard* c) {
         HIPCHK(hipMemsetAsync(c->d.rw + RW_T * nrep, 0, 8 * nrep, c->stream));
         HIPCHK(hipMemsetAsync(c->d.rw + RW_TICK * nrep, 0xFF, 8 * nrep * (RW_COUNT - RW_TICK), c->stream));
     }
-    if (c->heavy_ok) {
-        hipLaunchKernelGGL(tw_lp_due, dim3(TW_DUE_GRID), dim3(256), 0, c->stream, c->dwin());
-        HIPCHK(hipGetLastError());
-    }
-    if (c->d.rw) {  // per-replica windows: tiles of 64 replicas x one chunk of nodes, four per workgroup
-        const uint32_t nk = ((c->d.R >> c->d.rep_lg) + (1u << TW_CHUNK_LG) - 1u) >> TW_CHUNK_LG;
-        const uint32_t tiles = nk * (((1u << c->d.rep_lg) + 63u) >> 6);
-        hipLaunchKernelGGL(tw_lpb_compact, dim3((tiles + 3) / 4), dim3(256), 0, c->stream, c->dwin());
-    } else {
-        hipLaunchKernelGGL(tw_lp_compact, dim3(compact_blocks(c->d.R)), dim3(256), 0, c->stream, c->dwin(), 0u, 0u);
-    }
-    HIPCHK(hipGetLastError());
     HIPCHK(hipMemsetAsync(c->d.lp_err, 0, 4, c->stream));
-    if (c->heavy_ok && c->d.lpc_bat) {  // the due runs' batchable prefixes (after the list: their marks are the next window's)
-        hipLaunchKernelGGL(tw_lp_batch, dim3(TW_DUE_GRID), dim3(256), 0, c->stream, c->dwin());
-        HIPCHK(hipGetLastError());
-    }
+    if (c->d.dmk_n) HIPCHK(hipMemsetAsync(c->d.dmk_n, 0, 8, c->stream));
+    int rc = lp_window_start(c);
+    if (rc) return rc;
     c->loop_ready = true;
     return TW_OK;
 }
@@ -1342,23 +1383,7 @@ int sh_lp_tick_end(tw_shard* c) {
         hipLaunchKernelGGL(tw_lpb_fin, dim3(1), dim3(1), 0, c->stream, c->dwin());
         HIPCHK(hipGetLastError());
     }
-    if (c->heavy_ok) {
-        hipLaunchKernelGGL(tw_lp_due, dim3(TW_DUE_GRID), dim3(256), 0, c->stream, c->dwin());
-        HIPCHK(hipGetLastError());
-    }
-    if (c->d.rw) {  // per-replica windows: tiles of 64 replicas x one chunk of nodes, four per workgroup
-        const uint32_t nk = ((c->d.R >> c->d.rep_lg) + (1u << TW_CHUNK_LG) - 1u) >> TW_CHUNK_LG;
-        const uint32_t tiles = nk * (((1u << c->d.rep_lg) + 63u) >> 6);
-        hipLaunchKernelGGL(tw_lpb_compact, dim3((tiles + 3) / 4), dim3(256), 0, c->stream, c->dwin());
-    } else {
-        hipLaunchKernelGGL(tw_lp_compact, dim3(compact_blocks(c->d.R)), dim3(256), 0, c->stream, c->dwin(), 0u, 0u);
-    }
-    HIPCHK(hipGetLastError());
-    if (c->heavy_ok && c->d.lpc_bat) {  // the due runs' batchable prefixes (after the list: their marks are the next window's)
-        hipLaunchKernelGGL(tw_lp_batch, dim3(TW_DUE_GRID), dim3(256), 0, c->stream, c->dwin());
-        HIPCHK(hipGetLastError());
-    }
-    return TW_OK;
+    return lp_window_start(c);
 }
 
 // the window words + lp_err into the pinned host copy (stream-ordered)

@@ -82,6 +82,9 @@
 #ifndef TW_FAST
 #define TW_FAST 0
 #endif
+#ifndef TW_FAST_COMPACT
+#define TW_FAST_COMPACT 0  // ... in the compact geometry (C2)
+#endif
 #define TW_FAST_MAX 32u  // instructions per fast_run entry
 #ifndef TW_LP_WAVES
 #define TW_LP_WAVES 2
@@ -313,7 +316,7 @@ struct Lane {
     // per fork instead of three
     static constexpr bool FOLDJ = HR || (LP && TW_LP_FOLDJ);
     // the lock-step fast path (fast_run): the run geometries
-    static constexpr bool FAST = HR && TW_FAST;
+    static constexpr bool FAST = (HR && TW_FAST) || (!LP && !RUNS && TW_FAST_COMPACT);
     // per-lane hot passes (lanes at different hot ops share a pass) pay off where
     // lanes diverge -- logical processes and the few-replica sparse geometry; the
     // dense replica geometry runs lock-step programs and keeps the cheaper
@@ -3698,7 +3701,7 @@ struct DueX {
 // Lane::emit for a record of the batch (the thread's own append: no wave
 // aggregation); returns 1 for a record written straight into a light inbox
 __device__ __forceinline__ uint32_t due_emit(const Dev& c, uint32_t wid, int64_t ta, int64_t payload, uint32_t link,
-                                             uint32_t kind, uint32_t src, uint32_t dst, uint4 dh) {
+                                             uint32_t kind, uint32_t src, uint32_t dst, uint4 dh, bool defer = false) {
     const uint4 q0 = make_uint4((uint32_t)ta, (uint32_t)((uint64_t)ta >> 32), (uint32_t)payload,
                                 (uint32_t)((uint64_t)payload >> 32));
     const uint4 q1 = make_uint4(link, kind, src, dst);
@@ -3715,7 +3718,14 @@ __device__ __forceinline__ uint32_t due_emit(const Dev& c, uint32_t wid, int64_t
         uint4 GAS* q = gp(c.inbox) + ((size_t)par * c.ib_total + base + (size_t)k * ib_stride(c)) * 2;
         q[0] = q0;
         q[1] = q1;
-        lp_mark(c, lp, wid);
+        if (defer) {  // (tw_lp_due_batch runs before the window's list is built: tw_lp_dmark marks it after)
+            const uint32_t j = __hip_atomic_fetch_add(gp(c.dmk_n) + (wid & 1u), 1u, __ATOMIC_RELAXED,
+                                                      __HIP_MEMORY_SCOPE_AGENT);
+            if (j < c.dmk_cap) gp(c.dmk)[(size_t)(wid & 1u) * c.dmk_cap + j] = lp;
+            else __hip_atomic_fetch_or(gp(c.lp_err), 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            lp_mark(c, lp, wid);
+        }
         return 1u;
     }
     const uint32_t i = __hip_atomic_fetch_add(gp(c.out_n), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -3871,11 +3881,12 @@ __device__ DueX due_exec(const Dev& c, const BProg& bp, uint32_t r, uint32_t set
 // The effects of a batched record beyond its lane (due_exec's data): the
 // sending node's term, the send's record; returns 1 for a record written
 // straight into a light inbox
-__device__ __forceinline__ uint32_t due_effects(const Dev& c, uint32_t wid, uint32_t node, const DueX& x) {
+__device__ __forceinline__ uint32_t due_effects(const Dev& c, uint32_t wid, uint32_t node, const DueX& x,
+                                                bool defer = false) {
     if (x.hs_lane != 0xFFFFFFFFu)
         __hip_atomic_fetch_add((unsigned long long GAS*)(gp(c.hash_g) + x.hs_lane), (unsigned long long)x.hs,
                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return x.yld ? due_emit(c, wid, x.ta, x.pay, x.lk, x.k2, node, x.dst, x.dh) : 0u;
+    return x.yld ? due_emit(c, wid, x.ta, x.pay, x.lk, x.k2, node, x.dst, x.dh, defer) : 0u;
 }
 
 __global__ void __launch_bounds__(256) tw_lp_due(Dev c) {
@@ -4278,6 +4289,349 @@ __global__ void __launch_bounds__(256) tw_lp_batch(Dev c) {
                                    __HIP_MEMORY_SCOPE_AGENT);
 #endif
 #undef BT
+}
+
+// ---------------------------------------------------------------------------
+// tw_lp_due + tw_lp_batch in one pass over a heavy lane's records (round 6,
+// DESIGN §3i; TW_LP_FUSED=1 -- measured slower than the two kernels, so not
+// the default).  A heavy lane's inbox is staged in LDS once: the records
+// due in the window are sorted into the due run as tw_lp_due sorts them
+// (timestamp bins, then rec_less inside a bin), their reply links looked up
+// once, and the batch's dry run, prefix and effects (tw_lp_batch) run on the
+// sorted records in LDS -- no second read of the due run, no second launch,
+// and only the records the batch leaves (positions [K, nd)) are written back
+// as the due run.  The one ordering the two kernels kept: the window's work
+// list (tw_lpb_compact) is built from the marks of the window before, and a
+// batched reply delivered straight into a light lane's inbox marks that lane
+// for the window after -- made now, before the list is built, the mark would
+// hide the one the list reads.  So those lanes are recorded (Dev::dmk, by
+// window parity) and marked by tw_lp_dmark right after the list is built.
+// Everything else is tw_lp_due's and tw_lp_batch's code path for path: the
+// reserved seqs of the due run, the records left for later windows and their
+// minimum, the heavy list of the next window, the batch's eligibility and
+// totals.
+__global__ void __launch_bounds__(256) tw_lp_due_batch(Dev c) {
+    const int64_t GAS* w = gp(c.win);
+    const int64_t fl = w[WN_FLAGS];
+    if (!(fl & WN_FRESH) || (fl & WN_DONE)) return;
+    const uint32_t wid = (uint32_t)w[WN_WID];
+    const int64_t T0 = w[WN_T], L = w[WN_L];
+    const bool radix = L <= TW_DUE_BINS;
+    const uint32_t nb = radix ? (uint32_t)L : 0u;
+    const uint32_t lst = wid & 1u;
+    uint32_t nh = gp(c.heavy_n)[lst];
+    nh = nh < c.R ? nh : c.R;  // (an over-full list has set lp_err)
+    if (blockIdx.x >= nh) return;
+    // the batch needs the program tables in LDS (a program over the caps is
+    // only sorted, as tw_lp_due alone would)
+    const bool tables = c.lpc_bat && c.n_insns <= TW_BATCH_INSNS && c.n_consts <= TW_BATCH_CONSTS &&
+                        c.n_sets * c.n_kinds <= TW_BATCH_LPC;
+    __shared__ uint4 ea[TW_HEAVY_CAP], eb[TW_HEAVY_CAP];
+    __shared__ uint16_t dix[TW_HEAVY_CAP];  // entry index of the i-th due record (arrival order); then batch flags
+    __shared__ uint16_t srt[TW_HEAVY_CAP];  // ... of the i-th due record in due-run order
+    __shared__ uint32_t bins[TW_DUE_BINS];
+    __shared__ uint32_t wsum[4];
+    __shared__ unsigned long long smin;
+    __shared__ uint2 sP[TW_BATCH_INSNS];
+    __shared__ int64_t sK[TW_BATCH_CONSTS];
+    __shared__ uint32_t sL[TW_BATCH_LPC];
+    __shared__ uint8_t sB[TW_BATCH_LPC];
+    __shared__ int64_t wmx[4], sNear[8];
+    __shared__ uint64_t sS[SC_COUNT];
+    __shared__ uint32_t bSet, bK0, bK, bDirect, bNd;
+    __shared__ int64_t bTo;
+    __shared__ unsigned long long bH, bsum[6];
+    __shared__ long long bFin, bLast;
+    static_assert(TW_HEAVY_CAP == 256 * 8, "eight entries per thread");
+    static_assert(TW_DUE_BINS == 256 * 8, "eight bins per thread");
+    static_assert(TW_BATCH_CAP == 256 * 4, "four prefix positions per thread");
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
+    if (tables) {
+        for (uint32_t i = tid; i < c.n_insns; i += 256) sP[i] = gp(c.insns)[i];
+        for (uint32_t i = tid; i < c.n_consts; i += 256) sK[i] = gp(c.consts)[i];
+        for (uint32_t i = tid; i < c.n_sets * c.n_kinds; i += 256) {
+            sL[i] = gp(c.lpc)[i];
+            sB[i] = gp(c.lpc_bat)[i];
+        }
+    }
+    const BProg bp{(const uint2 LAS*)sP, (const int64_t LAS*)sK, (const uint32_t LAS*)sL, (const uint8_t LAS*)sB};
+    uint8_t* bfl = (uint8_t*)dix;  // (batch flags per due position, once dix is consumed)
+    const size_t st = ib_stride(c);
+    for (uint32_t hi = blockIdx.x; hi < nh; hi += gridDim.x) {
+        const uint32_t r = gp(c.heavy)[(size_t)lst * c.R + hi];
+        const int64_t T = c.rw ? *rw_at(c, RW_T, r) : T0;
+        if (T == INT64_MAX) continue;  // (a finished replica has no records; uniform)
+        const int64_t tend = T + L - 1;
+        uint64_t* sc = gp(c.scal) + (size_t)r * SC_LP_STRIDE;  // (LP: the lane's block)
+        __syncthreads();  // (the previous lane's readers of the shared words are done)
+        uint32_t n = gp(c.inbox_n)[r];
+        const uint32_t cap = ib_cap(c, r);
+        n = n < cap ? n : cap;
+        const size_t ib = ib_base(c, r);
+        for (uint32_t k = tid; k < n; k += 256) {
+            const uint4 GAS* q = gp(c.inbox) + (ib + (size_t)k * st) * 2;
+            ea[k] = q[0];
+            eb[k] = q[1];
+        }
+        if (tid < SC_COUNT) sS[tid] = sc[tid];
+        if (tid == 0) {
+            smin = ~0ull;
+            const uint32_t own = gp(c.bind_own)[r], rel = gp(c.bind_rel)[r];
+            bSet = own == rel ? 0u : gp(c.bind)[r];
+            bK = 0;
+            bDirect = 0;
+            bH = 0;
+            bFin = INT64_MIN;
+            bLast = INT64_MIN;
+            for (int j = 0; j < 6; ++j) bsum[j] = 0;
+        }
+        if (tid < 8u) {  // the lane's next queued event: its near spill and far heap top
+            int64_t x = INT64_MAX;
+            if (tid < (uint32_t)sc[SC_NEAR_N]) x = ent_t(gp(c.near_spill)[(size_t)tid * c.R + r]);
+            if (tid == 0 && sc[SC_FAR_N]) {
+                const int64_t f = ent_t(gp(c.far)[r]);
+                x = f < x ? f : x;
+            }
+            sNear[tid] = x;
+        }
+        for (uint32_t i = tid; i < nb; i += 256) bins[i] = 0;
+        __syncthreads();
+        // ---- tw_lp_due: due flags, a scan, the due records' arrival indices
+        // and timestamp bins, the rest compacted back into the inbox
+        uint32_t my = 0;
+        for (uint32_t j = 0; j < 8; ++j) {
+            const uint32_t k = tid * 8 + j;
+            my += (k < n && ent_t(ea[k]) <= tend) ? 1u : 0u;
+        }
+        uint32_t nd = 0;
+        uint32_t before = wg_excl_scan(my, wsum, &nd);
+        unsigned long long mn = ~0ull;
+        for (uint32_t j = 0; j < 8; ++j) {
+            const uint32_t k = tid * 8 + j;
+            if (k >= n) break;
+            const int64_t t = ent_t(ea[k]);
+            if (t <= tend) {
+                dix[before++] = (uint16_t)k;
+                if (radix) atomicAdd(&bins[t > T ? (uint32_t)(t - T) : 0u], 1u);
+            } else {
+                uint4 GAS* q = gp(c.inbox) + (ib + (size_t)(k - before) * st) * 2;
+                q[0] = ea[k];
+                q[1] = eb[k];
+                mn = (unsigned long long)t < mn ? (unsigned long long)t : mn;
+            }
+        }
+        if (mn != ~0ull) atomicMin(&smin, mn);
+        __syncthreads();
+        if (radix) {
+            uint32_t cnt8[8], sum = 0;
+            for (uint32_t j = 0; j < 8; ++j) {
+                const uint32_t bi = tid * 8 + j;
+                cnt8[j] = bi < nb ? bins[bi] : 0u;
+                sum += cnt8[j];
+            }
+            uint32_t tot = 0;
+            uint32_t off = wg_excl_scan(sum, wsum, &tot);
+            for (uint32_t j = 0; j < 8; ++j) {
+                const uint32_t bi = tid * 8 + j;
+                if (bi < nb) bins[bi] = off;
+                off += cnt8[j];
+            }
+            __syncthreads();
+            for (uint32_t i = tid; i < nd; i += 256) {
+                const uint32_t k = dix[i];
+                const int64_t t = ent_t(ea[k]);
+                const uint32_t pos = atomicAdd(&bins[t > T ? (uint32_t)(t - T) : 0u], 1u);
+                srt[pos] = (uint16_t)k;
+            }
+            __syncthreads();
+            for (uint32_t bi = tid; bi < nb; bi += 256) {
+                const uint32_t s0 = bi ? bins[bi - 1] : 0u, s1 = bins[bi];
+                for (uint32_t x = s0 + 1; x < s1; ++x) {
+                    const uint16_t k = srt[x];
+                    uint32_t y = x;
+                    while (y > s0 && rec_less(ea[k], eb[k], ea[srt[y - 1]], eb[srt[y - 1]])) {
+                        srt[y] = srt[y - 1];
+                        --y;
+                    }
+                    srt[y] = k;
+                }
+            }
+        } else {
+            // long windows: rank of every due record among the due ones (ties by arrival)
+            for (uint32_t i = tid; i < nd; i += 256) {
+                const uint32_t k = dix[i];
+                const uint4 a = ea[k], b = eb[k];
+                uint32_t rank = 0;
+                for (uint32_t j = 0; j < nd; ++j) {
+                    const uint32_t m = dix[j];
+                    rank += (rec_less(ea[m], eb[m], a, b) || (j < i && !rec_less(a, b, ea[m], eb[m]))) ? 1u : 0u;
+                }
+                srt[rank] = (uint16_t)k;
+            }
+        }
+        __syncthreads();
+        // the due-run format of each due record: its reply link in place of the destination
+        for (uint32_t i = tid; i < nd; i += 256) {
+            const uint32_t k = srt[i];
+            eb[k] = due_rec_b(c, eb[k]);
+        }
+        // ---- tw_lp_batch's eligibility (the due run is fresh: seqs reserved below)
+        const uint64_t s0 = sS[SC_SEQ];
+        const bool ctr_ok = s0 + nd < 0xFFFFFFFFull;
+        if (tid == 0) {
+            const uint64_t sq = s0 + nd;  // (SC_SEQ after the due run's reservation)
+            const bool el = tables && nd && ctr_ok && c.trace_cap == 0 && c.tie_mode == TW_TIE_FIFO &&
+                            (sS[SC_FREE_N] > 0 || sS[SC_BUMP] < (uint64_t)c.S) &&
+                            sS[SC_STATUS] == TW_REP_RUNNING && sS[SC_PENDING_MAIN] == 0 &&
+                            !(c.lpb && gp(c.spawn_n)[r]) && sq + 3ull * nd < 0xFFFFFFFFull &&
+                            sS[SC_TIDC] + nd < 0xFFFFFFFFull;
+            bNd = el ? (nd < TW_BATCH_CAP ? nd : TW_BATCH_CAP) : 0u;
+            bK0 = bNd;
+            int64_t to = INT64_MAX;
+            for (int j = 0; j < 8; ++j) to = sNear[j] < to ? sNear[j] : to;
+            bTo = to;
+        }
+        __syncthreads();
+        const uint32_t nbt = bNd;  // (uniform)
+        uint32_t K = 0;
+        DueX x0{};
+        if (nbt) {
+            // dry run: batchable | yielded << 1 per record (due order)
+            for (uint32_t i = tid; i < nbt; i += 256) {
+                const uint32_t k = srt[i];
+                const DueX x = due_exec(c, bp, r, bSet, ea[k], eb[k]);
+                const bool ok = x.ok && x.last < bTo;
+                bfl[i] = (uint8_t)((ok ? 1u : 0u) | (x.yld ? 2u : 0u));
+                if (!ok) atomicMin(&bK0, i);
+                if (i == tid) x0 = x;
+            }
+            __syncthreads();
+            const uint32_t K0 = bK0;
+            // the latest resume before each position (an inclusive max scan)
+            int64_t cm = INT64_MIN;
+            for (uint32_t j = 0; j < 4; ++j) {
+                const uint32_t i = tid * 4 + j;
+                if (i < K0 && (bfl[i] & 2u)) {
+                    const int64_t y = ent_t(ea[srt[i]]) + 1;
+                    cm = y > cm ? y : cm;
+                }
+            }
+#pragma unroll
+            for (uint32_t d = 1; d < 64; d <<= 1) {
+                const int64_t o = __shfl_up(cm, d, 64);
+                if (lane >= d) cm = o > cm ? o : cm;
+            }
+            if (lane == 63) wmx[wv] = cm;
+            __syncthreads();
+            int64_t m = __shfl_up(cm, 1, 64);
+            if (lane == 0) m = INT64_MIN;
+            for (uint32_t k = 0; k < wv; ++k) m = wmx[k] > m ? wmx[k] : m;
+            // (the last thread also checks position TW_BATCH_CAP: the first record
+            // past the cap may close the prefix)
+            const uint32_t jn = tid == 255u ? 5u : 4u;
+            for (uint32_t j = 0; j < jn; ++j) {
+                const uint32_t i = tid * 4 + j;
+                if (i > K0) break;
+                // the prefix [0, i) is kept when its last resume precedes record
+                // i's wake (i = nbt: the first record past the cap, or none)
+                if (i == nbt && nd == nbt) { atomicMax(&bK, i); break; }
+                const int64_t ti = ent_t(ea[srt[i]]);
+                if (m < ti) atomicMax(&bK, i);
+                if (i < K0 && (bfl[i] & 2u)) m = ti + 1 > m ? ti + 1 : m;
+            }
+            __syncthreads();
+            K = bK;
+        }
+        // ---- the due run the chain pops: positions [K, nd) (the batch took [0, K))
+        for (uint32_t i = K + tid; i < nd; i += 256) {
+            const uint32_t k = srt[i];
+            uint4 GAS* q = gp(c.due) + (ib + (size_t)i * st) * 2;
+            q[0] = ea[k];
+            q[1] = eb[k];
+        }
+        // ---- the prefix for real: other nodes' hash terms, the sends' records
+        if (K) {
+            const uint32_t node = (c.lp0 + r) >> c.rep_lg;
+            uint64_t h = 0;
+            uint32_t sm[6] = {0, 0, 0, 0, 0, 0}, dir = 0;
+            int64_t fin = INT64_MIN, last = INT64_MIN;
+            for (uint32_t i = tid; i < K; i += 256) {
+                const uint32_t k = srt[i];
+                const DueX x = i == tid ? x0 : due_exec(c, bp, r, bSet, ea[k], eb[k]);
+                dir |= due_effects(c, wid, node, x, true);
+                h += x.h;
+                sm[0] += x.dl; sm[1] += x.ud; sm[2] += x.dr; sm[3] += x.ev; sm[4] += x.th; sm[5] += x.sq;
+                fin = x.fin > fin ? x.fin : fin;
+                last = x.last > last ? x.last : last;
+            }
+            if (h) atomicAdd(&bH, (unsigned long long)h);
+            for (int j = 0; j < 6; ++j)
+                if (sm[j]) atomicAdd(&bsum[j], (unsigned long long)sm[j]);
+            if (dir) bDirect = 1;
+            if (fin != INT64_MIN) atomicMax(&bFin, (long long)fin);
+            if (last != INT64_MIN) atomicMax(&bLast, (long long)last);
+        }
+        __syncthreads();
+        if (tid == 0) {
+            // tw_lp_due's bookkeeping
+            const uint32_t left = n - nd;
+            gp(c.inbox_n)[r] = left;
+            if (!ctr_ok) {
+                if (sS[SC_STATUS] == TW_REP_RUNNING) sc[SC_STATUS] = TW_REP_ERR_COUNTER;
+            } else {
+                sc[SC_SEQ] = s0 + nd + bsum[5];  // the due run's seqs s0 + 1 .. s0 + nd, then the batch's
+            }
+            sc[SC_DUE_SEQ] = s0;
+            sc[SC_DUE_N] = nd;
+            sc[SC_DUE_H] = K;
+            if (c.bat_ctr) {
+                atomicAdd(gp(c.bat_ctr) + 1, (unsigned long long)nd);
+                if (K) atomicAdd(gp(c.bat_ctr), (unsigned long long)K);
+            }
+            if (smin != ~0ull)
+                __hip_atomic_fetch_min(c.rw ? (uint64_t GAS*)rw_at(c, RW_WIN, r) : gp(c.pend_min), (uint64_t)smin,
+                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (nd) lp_mark(c, r, wid - 1u);
+            if (left) {
+                const uint32_t l = lst ^ 1u;
+                const uint32_t i = __hip_atomic_fetch_add(gp(c.heavy_n) + l, 1u, __ATOMIC_RELAXED,
+                                                          __HIP_MEMORY_SCOPE_AGENT);
+                if (i < c.R) gp(c.heavy)[(size_t)l * c.R + i] = r;
+                else __hip_atomic_fetch_or(gp(c.lp_err), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            // tw_lp_batch's totals, as the prefix's events on the chain add them
+            if (K) {
+                sc[SC_DELIVERED] = sS[SC_DELIVERED] + bsum[0];
+                sc[SC_UNDELIV] = sS[SC_UNDELIV] + bsum[1];
+                sc[SC_DROPPED] = sS[SC_DROPPED] + bsum[2];
+                sc[SC_EVENTS] = sS[SC_EVENTS] + bsum[3];
+                sc[SC_THREADS] = sS[SC_THREADS] + bsum[4];
+                sc[SC_TIDC] = sS[SC_TIDC] + bsum[0];  // (a thread id per handler)
+                if ((int64_t)sS[SC_NOW] < (int64_t)bLast) sc[SC_NOW] = (uint64_t)bLast;
+                if ((int64_t)sS[SC_FINAL_T] < (int64_t)bFin) sc[SC_FINAL_T] = (uint64_t)bFin;
+                if (bH)
+                    __hip_atomic_fetch_add((unsigned long long GAS*)(gp(c.hash_g) + c.lp0 + r), bH, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+                if (bDirect)
+                    min_hot(c.rw ? (uint64_t GAS*)rw_at(c, RW_WIN, r) : (uint64_t GAS*)(gp(c.win) + WN_REC_MIN),
+                            (uint64_t)(tend + 1));
+            }
+        }
+    }
+}
+// The light lanes tw_lp_due_batch delivered batched replies to, marked for the
+// next window now that this window's list is built; the other parity's list
+// (the window before's, already marked) is emptied for the next window.
+__global__ void __launch_bounds__(256) tw_lp_dmark(Dev c) {
+    const int64_t GAS* w = gp(c.win);
+    const int64_t fl = w[WN_FLAGS];
+    if (!(fl & WN_FRESH) || (fl & WN_DONE)) return;
+    const uint32_t wid = (uint32_t)w[WN_WID], p = wid & 1u;
+    uint32_t n = gp(c.dmk_n)[p];
+    n = n < c.dmk_cap ? n : c.dmk_cap;
+    for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256)
+        lp_mark(c, gp(c.dmk)[(size_t)p * c.dmk_cap + i], wid);
+    if (blockIdx.x == 0 && threadIdx.x == 0) gp(c.dmk_n)[p ^ 1u] = 0;
 }
 
 // Batched LP: a replica's results = its nodes' lanes (lane = node << rep_lg |

@@ -200,6 +200,12 @@ struct Dev {
     // (classify_batch, tw_lp_due); null: every due record runs on the lane's chain
     const uint8_t* lpc_bat;
     unsigned long long* bat_ctr;  // [2] batched LP since tw_reset: due records run by tw_lp_due, all due records
+    // tw_lp_due_batch (round 6): the light lanes its batched replies were
+    // delivered to, marked for the next window only after the window's work
+    // list is built (tw_lp_dmark): [2][dmk_cap] by window parity, counts [2]
+    uint32_t* dmk;
+    uint32_t* dmk_n;
+    uint32_t dmk_cap;
     uint32_t wave_k;            // wave kernel: near-queue entries per lane (4, 24 or 32), fixed by tw_load
     // wave kernel, tie mode TW_TIE_PQUEUE: each replica's queue is a binomial
     // MinQueue whose nodes are far[r * Q + i] (entries) + pq_link[r * Q + i]
