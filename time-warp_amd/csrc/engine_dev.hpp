@@ -86,6 +86,9 @@
 #define TW_FAST_COMPACT 0  // ... in the compact geometry (C2)
 #endif
 #define TW_FAST_MAX 32u  // instructions per fast_run entry
+#ifndef TW_LP_FORKN
+#define TW_LP_FORKN 1  // the LP kernels run a counted cross-node fork loop in one pass (Lane::fork_loop; 0: A/B)
+#endif
 #ifndef TW_LP_WAVES
 #define TW_LP_WAVES 2
 #endif
@@ -200,6 +203,9 @@ enum : uint32_t { LD_NONE, LD_NV, LD_OUT, LD_RL };  // node var / out-link base 
 #define U_NW (1u << 30)
 #define U_NJ (1u << 31)
 #define U_FOLD (U_NE | U_NE2 | U_JE | U_NW | U_NJ)
+// (LP prologue) a counted fork loop's head: FORK onto a register's node, then
+// `ADDI x,k ; J* .., pc` back to it (`forM_ [..] $ fork ...`, Lane::fork_loop)
+#define U_FL (1u << 4)
 __host__ __device__ __forceinline__ constexpr uint32_t uop_of(uint32_t op) {
     auto u = [](uint32_t alu, uint32_t jm, uint32_t tk) { return alu | (tk << 8) | (jm << 16); };
     switch (op) {
@@ -1628,6 +1634,8 @@ struct Lane {
                             }
                             tc = go ? (uint32_t)T_YIELD : tc;
                             yt = go ? now + 1 : yt;
+                            if (TW_LP_FORKN && __builtin_amdgcn_ballot_w64(go && (lfl & U_FL)))
+                                if (go && (lfl & U_FL)) fork_loop(th, n, pc, (uint32_t)imm, a, b, tgt, tc, yt);
                         }
                     }
                 }
@@ -2049,6 +2057,75 @@ struct Lane {
         fin = at ? tc : fin;
         running = running && !(at && tc != T_NONE);
     }
+    // A counted loop of forks onto other nodes in one pass (LP kernels, round
+    // 6: U_FL).  `forM_ [1..N] $ fork (launchNode ..)` (examples/token-ring/
+    // Main.hs:65-68) lowers to `L: FORK a, pc, node r[b] ; ADDI x, k ; J* .., L`,
+    // and in batched LP each fork is a spawn record plus the parent's 1-µs
+    // yield, which the inline continuation resumes when nothing on the lane is
+    // due first: two passes per fork (FOLDJ), ≈ 3 µs per fork on main's lane,
+    // the chain of C3's start-up windows at 8,192 replicas per GPU (DESIGN
+    // §3g).  Called after the pass emitted the first spawn, this runs the
+    // loop's iterations as those passes would, one after the other: the
+    // inline continuation of the yield at now + 1 (the epilogue's conditions,
+    // count, clock, insertion-counter step and resume term; n restarts), the
+    // ADDI, the jump (their counts), and while the jump goes back, the next
+    // fork's spawn (its node checked first; a bad one is left to the next
+    // pass at that pc, which fails it as it always has).  It stops where a
+    // pass would leave the step or the loop: the yield not resumable (the
+    // window's end, a queued event first, the event budget) -- the thread
+    // yields at now + 1 from here -- or the jump falling through.
+    __device__ __forceinline__ void fork_loop(Th& th, uint32_t& n, uint32_t pc, uint32_t imm, uint32_t a, uint32_t b,
+                                           uint32_t& tgt, uint32_t& tc, int64_t& yt) {
+        const uint2 ia = P[pc + 1u], ij = P[pc + 2u];
+        const uint32_t x = (ia.x >> 8) & 3u, ja = (ij.x >> 8) & 3u, jb16 = ij.x >> 16;
+        const uint32_t jm = U_JM(uop_of(ij.x & 0xFFu));
+        for (;;) {
+            // the parent's `wait (for 1 mcs)`, resumed inline (the pass epilogue's rule)
+            if (status != TW_REP_RUNNING || seq == 0xFFFFFFFFu) break;
+            if (far_dirty) far_min();
+            const int64_t y = now + 1;
+            const uint32_t sn = c.tie_mode ? seq_key(c.tie_mode, seq + 1) : seq + 1;
+            bool has = near_n != 0;
+            int64_t qt = nbase + (int64_t)(nrk >> 32);
+            uint32_t qs = (uint32_t)nrk;
+            const bool uf = fsrc >= 0 && (!has || tless(fmt, fms, qt, qs));
+            qt = uf ? fmt : qt;
+            qs = uf ? fms : qs;
+            has = has || fsrc >= 0;
+            if (!(y <= t_end && d_ev < ev_room && (!has || tless(y, sn, qt, qs)))) break;
+            STAT(K_POP);
+            ++seq;
+            now = y;
+            ++d_ev;
+            final_t = y > final_t ? y : final_t;
+            hacc += term0(y, TW_KIND_RESUME | ((pc + 1u) & 0xFFFFu));
+            if (now - nbase > (int64_t)0x7FFFFFFF) near_rebase(now);
+            // ADDI x, k ; J* (n restarted at the resume: two counts, never near the cap)
+            rs(th, x, rg(th, x) + (int64_t)(int32_t)ia.y);
+            const int64_t va = rg(th, ja), vb = rg(th, jb16 & 3u);
+            const uint32_t ci = (va == vb ? 1u : 0u) | (va < vb ? 2u : 0u) | (va == (int64_t)(int16_t)jb16 ? 4u : 0u);
+            n = 2;
+            if (!((jm >> ci) & 1u)) {  // the loop ends: the pass goes on after the jump
+                tc = T_NONE;
+                tgt = pc + 3u;
+                return;
+            }
+            // the next fork: its node checked as the pass checks it
+            const uint32_t node = (uint32_t)rg(th, b & 3u);
+            if (node >= c.Ntot || node == th.w1) {  // (a bad or own node: the next pass at pc)
+                tc = T_NONE;
+                tgt = pc;
+                return;
+            }
+            n = 3;
+            emit_spawn(now, imm, lane_of(node), rg(th, 0), rg(th, 1), rg(th, 2), rg(th, 3));
+            rs(th, a, -1);
+        }
+        tc = T_YIELD;
+        yt = now + 1;
+        tgt = pc + 1u;
+    }
+
     // Lock-step fast path (round 6, the run geometries: TW_FAST).  When every
     // running lane of the wave is at the same pc -- the replicas of one
     // scenario step through the same code, e.g. C3's start-up: main's `forM_
@@ -2537,6 +2614,14 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
             if (LP && TW_LP_FOLDJ && i < c.n_insns) {  // (Lane::FOLDJ: a jump only)
                 const uint32_t nop = i + 1u < c.n_insns ? gp(c.insns)[i + 1u].x & 0xFFu : TW_OP_NOP;
                 u |= U_JM(uop_of(nop)) != JM_NONE ? U_NJ : 0u;
+            }
+            if (LP && TW_LP_FORKN && c.lpb && i + 2u < c.n_insns && (in.x & 0xFFu) == TW_OP_FORK &&
+                (in.x >> 16) != 0xFFFFu) {  // (Lane::fork_loop)
+                const uint32_t w1 = gp(c.insns)[i + 1u].x;
+                const uint2 j2 = gp(c.insns)[i + 2u];
+                const uint32_t op2 = j2.x & 0xFFu;
+                u |= ((w1 & 0xFFu) == TW_OP_ADDI && !((w1 >> 16) & TW_ALU_NSTORE) && op2 >= TW_OP_JEQ &&
+                      op2 <= TW_OP_JNEI && j2.y == i) ? U_FL : 0u;
             }
             if (HR && i < c.n_insns) {  // (Lane::FOLD)
                 u |= is_end(i + 1u) ? U_NE : 0u;

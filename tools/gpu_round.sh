@@ -66,6 +66,7 @@ for s in "$@"; do
     parity_c3) step parity_c3 600 python -u tools/parity_all.py c3 ;;
     parity_c2c5) step parity_c2c5 900 python -u tools/parity_all.py c2 c5 ;;
     parity_c5) step parity_c5 600 python -u tools/parity_all.py c5 ;;
+    lpb_batch_tests) step lpb_batch_tests 600 python -u -m pytest tests/test_gpu_lpb.py -x -v --timeout 300 --timeout-method thread -k "batched" ;;
     lpb_new) step lpb_new 600 python -u -m pytest tests/test_gpu_lpb.py -x -v --timeout 300 --timeout-method thread -k "benched_shape_256 or over_the_cap or full_lane" ;;
     core_tests) step core_tests 900 python -u -m pytest tests/test_gpu_programs.py tests/test_gpu_tie_orders.py tests/test_gpu_parity.py tests/test_gpu_throw_sequences.py -x -q -m gpu --timeout 300 --timeout-method thread ;;
     ab_c3) bash tools/ab_session.sh token_ring; rc=$?; echo "ab_c3=$rc"; [ $rc -eq 0 ] || exit $rc ;;
