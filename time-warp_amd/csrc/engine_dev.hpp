@@ -2499,12 +2499,55 @@ __global__ void __launch_bounds__(TW_WG) tw_init_kernel(Dev c, uint32_t main_pc,
                                                        const uint32_t* listen_init, int lp_mode, uint32_t seq0,
                                                        uint32_t tid0) {
     uint32_t r = blockIdx.x * TW_WG + threadIdx.x;
+    // LP contexts keep a lane's scalar block and thread records contiguous
+    // ([lane][SC_LP_STRIDE] words, 4 quads per slot): written one lane per
+    // thread, every store of a wave would touch 64 lines (a batched C3 share
+    // of 8,192 replicas has 33.6M lanes: 13 ms of a 97-ms step).  The
+    // workgroup writes its 256 lanes' blocks and slot-0 records as one
+    // contiguous span instead, word k*256 + t by thread t.
+    if (lp_mode && c.sc_lp) {
+        const size_t l0 = (size_t)blockIdx.x * TW_WG;
+        uint64_t GAS* scb = gp(c.scal) + l0 * SC_LP_STRIDE;
+        for (uint32_t k = 0; k < SC_LP_STRIDE; ++k) {
+            const uint32_t w = k * TW_WG + threadIdx.x;
+            const uint32_t f = w % SC_LP_STRIDE;
+            const size_t l = l0 + w / SC_LP_STRIDE;
+            if (l >= c.R || f >= SC_COUNT) continue;
+            const bool hm = ((c.lp0 + (uint32_t)l) >> c.rep_lg) == main_node;
+            uint64_t v = 0;
+            v = (f == SC_THREADS || f == SC_PENDING_MAIN || f == SC_BUMP) ? (hm ? 1u : 0u) : v;
+            v = f == SC_TIDC ? tid0 : v;  // main is tid 0 (TimedT.hs:272-280)
+            v = f == SC_SEQ ? seq0 : v;
+            v = f == SC_STATUS ? (uint64_t)TW_REP_RUNNING : v;
+            scb[w] = v;
+        }
+        if (c.RQ == 1) {  // slot 0 (Lane::hrec): quad j of lane l at l * 4 + j (else below)
+            uint4 GAS* pb = gp(c.slots) + l0 * 4;
+            for (uint32_t k = 0; k < 4; ++k) {
+                const uint32_t w = k * TW_WG + threadIdx.x;
+                const uint32_t j = w & 3u;
+                const size_t l = l0 + (w >> 2);
+                if (l >= c.R) continue;
+                const uint32_t gl = (c.lp0 + (uint32_t)l) >> c.rep_lg;
+                const uint32_t rl = (c.lp0 + (uint32_t)l) & ((1u << c.rep_lg) - 1u);
+                const bool hm = gl == main_node;
+                uint4 q = make_uint4(0u, 0u, 0u, 0u);
+                if (j == 0) q = make_uint4((main_pc & 0xFFFFu) | (F_MAIN << FL_SHIFT), main_node, hm ? 0u : 0xFFFFFFFFu, 0u);
+                if (j >= 2 && main_regs && hm) {
+                    const int64_t m0 = main_regs[(size_t)rl * 4 + (j - 2) * 2], m1 = main_regs[(size_t)rl * 4 + (j - 2) * 2 + 1];
+                    q = make_uint4((uint32_t)m0, (uint32_t)((uint64_t)m0 >> 32), (uint32_t)m1, (uint32_t)((uint64_t)m1 >> 32));
+                }
+                pb[w] = q;
+            }
+        }
+    }
     if (r >= c.R) return;
     // LP mode: lane r runs global node g (of replica rho, batched mode); only
     // the main node's lane holds the main thread
     const uint32_t g = lp_mode ? (c.lp0 + r) >> c.rep_lg : 0u;
     const uint32_t rho = lp_mode ? (c.lp0 + r) & ((1u << c.rep_lg) - 1u) : r;
     const bool has_main = !lp_mode || g == main_node;
+    if (!(lp_mode && c.sc_lp && c.RQ == 1)) {  // (LP contexts: written above)
     for (uint32_t f = 0; f < SC_COUNT; ++f) gp(c.scal)[sc_ix(c, f, r)] = 0;
     gp(c.scal)[sc_ix(c, SC_THREADS, r)] = has_main ? 1 : 0;
     gp(c.scal)[sc_ix(c, SC_TIDC, r)] = tid0;  // main is tid 0 (TimedT.hs:272-280)
@@ -2521,6 +2564,7 @@ __global__ void __launch_bounds__(TW_WG) tw_init_kernel(Dev c, uint32_t main_pc,
         for (int i = 0; i < 4; ++i) m[i] = main_regs[(size_t)rho * 4 + i];
     p[2 * c.RQ] = make_uint4((uint32_t)m[0], (uint32_t)((uint64_t)m[0] >> 32), (uint32_t)m[1], (uint32_t)((uint64_t)m[1] >> 32));
     p[3 * c.RQ] = make_uint4((uint32_t)m[2], (uint32_t)((uint64_t)m[2] >> 32), (uint32_t)m[3], (uint32_t)((uint64_t)m[3] >> 32));
+    }
     if (lp_mode) {
         if (nv_init)
             for (uint32_t i = 0; i < 4; ++i) gp(c.nvars)[(size_t)i * c.R + r] = nv_init[(size_t)g * 4 + i];
@@ -3186,15 +3230,20 @@ __device__ __forceinline__ void lp_spawn(const Dev& c, const uint4 GAS* o, uint6
     // this tick's earliest spawn: one in the current window reruns it (tw_lp_fill),
     // with the target lane appended to the running window's work list (once)
     (void)tmin;
+    // (one store / append per wave on the window's shared words: a start-up
+    // window of batched C3 packs a spawn per node per replica -- 8.2M records
+    // at 8,192 replicas -- and same-address writes serialise in the L2)
     if (c.rw && c.win) {  // per-replica windows: the spawn bounds its replica's next window, or reruns this one
         min_hot((uint64_t GAS*)rw_at(c, RW_TICK, lp), (uint64_t)ent_t(a));
-        if (ent_t(a) <= rw_tend(c, lp, gp(c.win)[WN_L])) gp(c.win)[WN_SPN_HERE] = 1;
+        const bool here = ent_t(a) <= rw_tend(c, lp, gp(c.win)[WN_L]);
+        const uint64_t hm = __builtin_amdgcn_ballot_w64(here);
+        if (here && __builtin_amdgcn_mbcnt_hi((uint32_t)(hm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)hm, 0u)) == 0)
+            gp(c.win)[WN_SPN_HERE] = 1;
     } else {
         min_hot((uint64_t GAS*)(gp(c.win) + WN_SPN_MIN), (uint64_t)ent_t(a));
     }
     if (__hip_atomic_exchange(gp(c.inlist) + lp, c.wid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != c.wid) {
-        const uint32_t i = __hip_atomic_fetch_add(gp(c.act_n) + c.act_cur * TW_LP_NB, 1u, __ATOMIC_RELAXED,
-                                                  __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t i = wave_append(gp(c.act_n) + c.act_cur * TW_LP_NB, 1u);
         if (i < c.R) gp(c.act)[(size_t)c.act_cur * TW_LP_NB * c.R + i] = lp;  // (inlist: once per window)
         else __hip_atomic_fetch_or(gp(c.lp_err), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
@@ -3988,13 +4037,20 @@ __global__ void __launch_bounds__(256) tw_lp_due(Dev c) {
     __shared__ uint4 ea[TW_HEAVY_CAP], eb[TW_HEAVY_CAP];
     __shared__ uint16_t dix[TW_HEAVY_CAP];  // entry index of the i-th due record (arrival order)
     __shared__ uint16_t srt[TW_HEAVY_CAP];  // ... of the i-th due record in due-run order
-    __shared__ uint32_t bins[TW_DUE_BINS];  // counts -> segment offsets -> segment ends
+    // counts -> segment offsets -> segment ends, two 16-bit bins per word (bin
+    // b in half b & 1: every value is <= TW_HEAVY_CAP, so a half never carries
+    // into the other).  Unpacked, the kernel held 24 B more than half of the
+    // CU's 160 KB of LDS and ran one workgroup per CU; packed it runs two.
+    __shared__ uint32_t bins[TW_DUE_BINS / 2];
     __shared__ uint32_t wsum[4];
     __shared__ unsigned long long smin;
     static_assert(TW_HEAVY_CAP == 256 * 8, "eight entries per thread");
     static_assert(TW_DUE_BINS == 256 * 8, "eight bins per thread");
     const uint32_t tid = threadIdx.x;
     const size_t st = ib_stride(c);
+    auto bsh = [](uint32_t b) { return (b & 1u) * 16u; };
+    auto bget = [&](uint32_t b) { return (bins[b >> 1] >> bsh(b)) & 0xFFFFu; };
+    auto binc = [&](uint32_t b) { return (atomicAdd(&bins[b >> 1], 1u << bsh(b)) >> bsh(b)) & 0xFFFFu; };
     for (uint32_t hi = blockIdx.x; hi < nh; hi += gridDim.x) {
         const uint32_t r = gp(c.heavy)[(size_t)lst * c.R + hi];
         // the lane's window: the batch's, or its replica's own (per-replica windows)
@@ -4011,7 +4067,7 @@ __global__ void __launch_bounds__(256) tw_lp_due(Dev c) {
             eb[k] = q[1];
         }
         if (tid == 0) smin = ~0ull;
-        for (uint32_t i = tid; i < nb; i += 256) bins[i] = 0;
+        for (uint32_t i = tid; i < (nb + 1) / 2; i += 256) bins[i] = 0;
         __syncthreads();
         // thread tid owns entries [8 tid, 8 tid + 8): due flags, then a scan
         uint32_t my = 0;
@@ -4031,7 +4087,7 @@ __global__ void __launch_bounds__(256) tw_lp_due(Dev c) {
             const int64_t t = ent_t(ea[k]);
             if (t <= tend) {
                 dix[before++] = (uint16_t)k;
-                if (radix) atomicAdd(&bins[t > T ? (uint32_t)(t - T) : 0u], 1u);
+                if (radix) (void)binc(t > T ? (uint32_t)(t - T) : 0u);
             } else {
                 uint4 GAS* q = gp(c.inbox) + (ib + (size_t)(k - before) * st) * 2;
                 q[0] = ea[k];
@@ -4046,15 +4102,16 @@ __global__ void __launch_bounds__(256) tw_lp_due(Dev c) {
             uint32_t cnt8[8], sum = 0;
             for (uint32_t j = 0; j < 8; ++j) {
                 const uint32_t bi = tid * 8 + j;
-                cnt8[j] = bi < nb ? bins[bi] : 0u;
+                cnt8[j] = bi < nb ? bget(bi) : 0u;
                 sum += cnt8[j];
             }
             uint32_t tot = 0;
             uint32_t off = wg_excl_scan(sum, wsum, &tot);
-            for (uint32_t j = 0; j < 8; ++j) {
+            for (uint32_t j = 0; j < 8; j += 2) {  // (the thread's bins are four whole words)
                 const uint32_t bi = tid * 8 + j;
-                if (bi < nb) bins[bi] = off;
-                off += cnt8[j];
+                const uint32_t o0 = off, o1 = off + cnt8[j];
+                off = o1 + cnt8[j + 1];
+                if (bi < nb) bins[bi >> 1] = o0 | (bi + 1 < nb ? o1 << 16 : 0u);
             }
             __syncthreads();
             // scatter by timestamp (positions inside a segment in any order);
@@ -4062,13 +4119,13 @@ __global__ void __launch_bounds__(256) tw_lp_due(Dev c) {
             for (uint32_t i = tid; i < nd; i += 256) {
                 const uint32_t k = dix[i];
                 const int64_t t = ent_t(ea[k]);
-                const uint32_t pos = atomicAdd(&bins[t > T ? (uint32_t)(t - T) : 0u], 1u);
+                const uint32_t pos = binc(t > T ? (uint32_t)(t - T) : 0u);
                 srt[pos] = (uint16_t)k;
             }
             __syncthreads();
             // each segment of equal timestamps into rec_less order
             for (uint32_t bi = tid; bi < nb; bi += 256) {
-                const uint32_t s0 = bi ? bins[bi - 1] : 0u, s1 = bins[bi];
+                const uint32_t s0 = bi ? bget(bi - 1) : 0u, s1 = bget(bi);
                 for (uint32_t x = s0 + 1; x < s1; ++x) {
                     const uint16_t k = srt[x];
                     uint32_t y = x;
