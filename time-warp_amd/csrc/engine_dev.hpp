@@ -2607,6 +2607,11 @@ __host__ __device__ constexpr size_t fixed_lds_bytes() {
 // RUNS = false (the compact geometry): no far runs, and built for two waves
 // per SIMD (<= 256 registers, half the LDS of a dense lane), so 1M-replica
 // batches keep two workgroups per CU
+// LP lanes' prologue: the near spill's entries and the far heap's top loaded
+// together (round 6: C5 1,366 -> 1,341 ms, C4 flat; TW_LP_PRO=0 for the A/B)
+#ifndef TW_LP_PRO
+#define TW_LP_PRO 1
+#endif
 template <bool LP, int WG, int NC, int TPW = 64, bool RUNS = true, bool GS = false, bool PRW = false, bool IP = false>
 __global__ void __launch_bounds__(WG * 64 / TPW)
     __attribute__((amdgpu_waves_per_eu(LP ? TW_LP_WAVES : !RUNS ? 2 : (WG * 64 / TPW + 255) / 256,
@@ -2783,7 +2788,14 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
             L.ev_room = ev_room;
             L.d_ev = 0;
             L.d_th = 0;
-            if (L.far_n) L.set_ftop(L.far_ld(0));
+            if constexpr (LP && TW_LP_PRO) {
+                // (loaded whether or not the heap holds anything, so the load
+                // goes out with the scalar block's instead of after it; CW_FT*
+                // are read only while far_n > 0)
+                L.set_ftop(c.Q ? L.far_ld(0) : make_uint4(0u, 0u, 0u, 0u));
+            } else {
+                if (L.far_n) L.set_ftop(L.far_ld(0));
+            }
             L.rlc_link = 0xFFFFFFFFu;
             L.rlc_rev = 0;
             L.oo = 0;
@@ -2831,7 +2843,39 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
             // ahead for a 32-bit key (or an oversized spill) takes the pushing path.
             L.nbase = L.now;
             L.near_init();
-            {
+            if constexpr (LP && TW_LP_PRO) {
+                // (an LP lane reloads its spill every window: its entries are
+                // loaded together, one round trip, instead of one after another)
+                uint4 se[NC];
+                bool fits = near_n0 <= (uint32_t)NC;
+        #pragma unroll
+                for (uint32_t j = 0; j < (uint32_t)NC; ++j)
+                    se[j] = (fits && j < near_n0) ? gp(c.near_spill)[(size_t)j * R + r] : make_uint4(0u, 0u, 0u, 0u);
+        #pragma unroll
+                for (uint32_t j = 0; j < (uint32_t)NC; ++j)
+                    fits = fits && (j >= near_n0 || (uint64_t)(ent_t(se[j]) - L.nbase) < 0xFFFFFFFFull);
+                if (fits) {
+        #pragma unroll
+                    for (uint32_t j = 0; j < (uint32_t)NC; ++j) {
+                        if (j < near_n0) {
+                            L.nk[j * WG] = L.nkey(ent_t(se[j]), se[j].w);
+                            L.ns[j * WG] = se[j].z;
+                        }
+                    }
+                    L.near_n = near_n0;
+                    L.nrk = near_n0 ? L.nkey(ent_t(se[0]), se[0].w) : ~0ull;
+                    L.nrs = near_n0 ? se[0].z : 0u;
+                } else {
+                    for (uint32_t j = 0; j < near_n0; ++j) {
+                        uint4 e = gp(c.near_spill)[(size_t)j * R + r];
+                        if (L.near_n < NC && (uint64_t)(ent_t(e) - L.nbase) < 0xFFFFFFFFull) {
+                            L.near_push(ent_t(e), e.w, e.z);
+                            continue;
+                        }
+                        L.push_far(ent_t(e), e.w, e.z);
+                    }
+                }
+            } else {
                 bool fits = near_n0 <= (uint32_t)NC;
                 for (uint32_t j = 0; j < near_n0 && fits; ++j)
                     fits = (uint64_t)(ent_t(gp(c.near_spill)[(size_t)j * R + r]) - L.nbase) < 0xFFFFFFFFull;
@@ -3109,6 +3153,9 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
             sc[SC_FREE_N * SR] = L.free_n; sc[SC_FTOP * SR] = L.ftop; sc[SC_BUMP * SR] = L.bump;
             sc[SC_TMO_CTR * SR] = L.cg(CW_TMO);
             sc[SC_TRACE_N * SR] = L.cg(CW_TRN);
+            // (LP lanes: the sums below as no-return atomics, without the drain
+            // above, measured slower -- C5 1,366 -> 1,448 ms, C4 7.05 -> 7.30 ms:
+            // round 6, profiles/r06c/ab_lp_epi_*)
             if constexpr (KEEP) sc[SC_EVENTS * SR] = events0 + L.d_ev;
             else sc[SC_EVENTS * SR] += L.d_ev;
             if (LP) {
@@ -3167,7 +3214,7 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
             }
         #endif
         } while (0);
-        if (!(LP && GS) || (size_t)(blk + gridDim.x) * WG >= lp_n) break;
+        if (!(LP && GS) || (size_t)(blk + gridDim.x) * WG >= lp_n) break;  // vmcnt(0): the last block's LDS-DMA landed before LDS is reused
     }
 }
 
