@@ -3986,7 +3986,9 @@ __device__ DueX due_exec(const Dev& c, const BProg& bp, uint32_t r, uint32_t set
             } else if (b16 & TW_SEND_VIA_RLINK) {
                 const uint64_t rin = (uint64_t)rr[(b16 >> 12) & 3u];
                 lbad = rin >= c.L;
-                if (!lbad) lk = gp(c.link_rev)[rin];
+                // (the reply to the record's own link: link_rev[link] is the
+                // due record's fourth word, due_rec_b -- no load)
+                if (!lbad) lk = rin == (uint64_t)link ? (uint64_t)b.w : gp(c.link_rev)[rin];
             }
             if (lbad || lk >= c.L) break;  // the replica's error: the chain reports it
             const uint32_t k2 = b16 & 0xFFu, pr = (b16 >> 8) & 3u;
@@ -3994,6 +3996,9 @@ __device__ DueX due_exec(const Dev& c, const BProg& bp, uint32_t r, uint32_t set
             tgt = fz ? pc + 2 : pc + 1;
             if (tgt >= c.n_insns || (bp.P[tgt].x & 0xFFu) != TW_OP_END) break;
             const uint32_t ent = c.link_table ? gp(c.link_table)[(((size_t)lk * c.D) << c.rep_lg) + rho] : 0u;
+            // (the destination entry goes out with the table entry: one round trip)
+            const uint4 dh = gp(c.link_dsth)[lk];
+            asm volatile("" ::"v"(dh.x));
             if (ent & TW_LINK_DROP) {  // dropped: the handler goes on to its END at t
                 o.dr += 1;
                 o.h += term(t, TW_KIND_DROP | k2, pay);
@@ -4007,7 +4012,7 @@ __device__ DueX due_exec(const Dev& c, const BProg& bp, uint32_t r, uint32_t set
             o.ev += 2;
             o.th += 1;
             o.fin = ta > o.fin ? ta : o.fin;
-            o.dh = gp(c.link_dsth)[lk];
+            o.dh = dh;
             o.lk = (uint32_t)lk;
             o.k2 = k2;
             o.dst = ((o.dh.x & 0x7FFFFFFFu) << c.rep_lg) | rho;
@@ -4042,7 +4047,7 @@ __device__ DueX due_exec(const Dev& c, const BProg& bp, uint32_t r, uint32_t set
             wr = true;
         } else if (ld == LD_RL) {
             if ((uint64_t)rb >= c.L) break;
-            v = (int64_t)gp(c.link_rev)[rb];
+            v = rb == (int64_t)link ? (int64_t)b.w : (int64_t)gp(c.link_rev)[rb];
             wr = true;
         }
         if (f & U_TR) o.h += term(t, TW_KIND_TRACE | ((uint32_t)imm & 0xFFFFu), ra);
@@ -4284,7 +4289,8 @@ __global__ void __launch_bounds__(256) tw_lp_batch(Dev c) {
     __shared__ int64_t wmx[4], sNear[8];
     __shared__ uint64_t sS[SC_COUNT];          // the lane's scalar block
     __shared__ uint32_t bSet, bK0, bK, bDirect, bNd, bNx;
-    __shared__ int64_t bTo;
+    __shared__ int64_t bTo, bFarT;
+    __shared__ uint32_t bSpn;
     __shared__ unsigned long long bH, bsum[6];
     __shared__ long long bFin, bLast;
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
@@ -4310,10 +4316,16 @@ __global__ void __launch_bounds__(256) tw_lp_batch(Dev c) {
         const uint64_t GAS* sc = gp(c.scal) + (size_t)r * SC_LP_STRIDE;
         __syncthreads();  // (the previous lane's readers of the shared words are done)
         BT(bt0);
+        // (one round of independent loads: the scalar block, the binding, the
+        // lane's near spill and far-heap top -- the lane's next queued event --
+        // and its spawn count, whether or not they turn out to be needed)
         if (tid < SC_COUNT) sS[tid] = sc[tid];
+        if (tid >= 64u && tid < 64u + TW_NEAR_LP) sNear[tid - 64u] = ent_t(gp(c.near_spill)[(size_t)(tid - 64u) * c.R + r]);
+        if (tid == 64u + TW_NEAR_LP) bFarT = c.Q ? ent_t(gp(c.far)[r]) : INT64_MAX;
+        if (tid == 65u + TW_NEAR_LP) bSpn = c.lpb ? gp(c.spawn_n)[r] : 0u;
         if (tid == 0) {
-            const uint32_t own = gp(c.bind_own)[r], rel = gp(c.bind_rel)[r];
-            bSet = own == rel ? 0u : gp(c.bind)[r];
+            const uint32_t own = gp(c.bind_own)[r], rel = gp(c.bind_rel)[r], bd = gp(c.bind)[r];
+            bSet = own == rel ? 0u : bd;
             bK = 0;
             bDirect = 0;
             bH = 0;
@@ -4332,38 +4344,27 @@ __global__ void __launch_bounds__(256) tw_lp_batch(Dev c) {
             const bool el = nd0 && c.trace_cap == 0 && c.tie_mode == TW_TIE_FIFO &&
                             (sS[SC_FREE_N] > 0 || sS[SC_BUMP] < (uint64_t)c.S) &&
                             sS[SC_STATUS] == TW_REP_RUNNING && sS[SC_PENDING_MAIN] == 0 &&
-                            !(c.lpb && gp(c.spawn_n)[r]) && sS[SC_SEQ] + 3ull * nd0 < 0xFFFFFFFFull &&
+                            !bSpn && sS[SC_SEQ] + 3ull * nd0 < 0xFFFFFFFFull &&
                             sS[SC_TIDC] + nd0 < 0xFFFFFFFFull;
             bNx = nd0;  // the due run's length (records past the cap stay on the chain)
             bNd = el ? (nd0 < TW_BATCH_CAP ? nd0 : TW_BATCH_CAP) : 0u;
             bK0 = bNd;
+            int64_t to = INT64_MAX;  // the lane's next queued event
+            for (uint32_t j = 0; j < TW_NEAR_LP; ++j)
+                if (j < (uint32_t)sS[SC_NEAR_N]) to = sNear[j] < to ? sNear[j] : to;
+            if (sS[SC_FAR_N]) to = bFarT < to ? bFarT : to;
+            bTo = to;
         }
         __syncthreads();
         const uint32_t nd = bNd;
         if (!nd) continue;  // (uniform)
-        // the records, the lane's next queued event (its near spill and far heap
-        // top, read by eight threads)
+        // the records
         const size_t ib = ib_base(c, r);
         const uint32_t nx = bNx > nd ? nd + 1u : nd;  // (+ the first record past the cap: its time)
         for (uint32_t i = tid; i < nx; i += 256) {
             const uint4 GAS* q = gp(c.due) + (ib + (size_t)i * st) * 2;
             ea[i] = q[0];
             if (i < nd) eb[i] = q[1];
-        }
-        if (tid < 8u) {
-            int64_t x = INT64_MAX;
-            if (tid < (uint32_t)sS[SC_NEAR_N]) x = ent_t(gp(c.near_spill)[(size_t)tid * c.R + r]);
-            if (tid == 0 && sS[SC_FAR_N]) {
-                const int64_t f = ent_t(gp(c.far)[r]);
-                x = f < x ? f : x;
-            }
-            sNear[tid] = x;
-        }
-        __syncthreads();
-        if (tid == 0) {
-            int64_t to = INT64_MAX;
-            for (int j = 0; j < 8; ++j) to = sNear[j] < to ? sNear[j] : to;
-            bTo = to;
         }
         __syncthreads();
         BT(bt1);
