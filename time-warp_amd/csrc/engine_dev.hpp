@@ -3549,6 +3549,7 @@ __global__ void __launch_bounds__(256) tw_lpb_rctl(Dev c) {
             // the replica's lanes' next events: the minimum over its chunks
             const uint32_t nk = ((c.R >> c.rep_lg) + (1u << TW_CHUNK_LG) - 1u) >> TW_CHUNK_LG;
             const uint64_t GAS* cm = (const uint64_t GAS*)gp(c.cw_min) + q;
+#pragma unroll 16
             for (uint32_t k = 0; k < nk; ++k) {
                 const uint64_t v = cm[(size_t)k * nrep];
                 t = v < t ? v : t;
@@ -3606,15 +3607,25 @@ __global__ void __launch_bounds__(256) tw_lpb_compact(Dev c) {
     const uint32_t n0 = k << TW_CHUNK_LG;
     const uint32_t nn = n0 + (1u << TW_CHUNK_LG) < nloc ? 1u << TW_CHUNK_LG : nloc - n0;
     if (due || mk) {
-        for (uint32_t j = 0; j < nn; ++j) {
-            const uint32_t r = ((n0 + j) << c.rep_lg) | q;
-            bool b = mk && gp(c.listed)[r] == mark;
-            if (due) {
-                const int64_t wk = gp(c.wake)[r];
-                b = b || wk <= te;
-                if (!b && wk < nm) nm = wk;
+        // (16 nodes' words in flight at a time: one after another, the 64
+        // nodes of a chunk were 64 dependent round trips per tile)
+        for (uint32_t jb = 0; jb < nn; jb += 16) {
+            uint32_t ls[16];
+            int64_t wks[16];
+#pragma unroll
+            for (uint32_t i = 0; i < 16; ++i) {
+                const uint32_t j = jb + i;
+                const uint32_t r = ((n0 + (j < nn ? j : 0u)) << c.rep_lg) | q;
+                ls[i] = (mk && j < nn) ? gp(c.listed)[r] : ~mark;
+                wks[i] = (due && j < nn) ? gp(c.wake)[r] : INT64_MAX;
             }
-            bits |= (uint64_t)b << j;
+#pragma unroll
+            for (uint32_t i = 0; i < 16; ++i) {
+                const uint32_t j = jb + i;
+                const bool b = j < nn && ((mk && ls[i] == mark) || (due && wks[i] <= te));
+                if (due && j < nn && !b && wks[i] < nm) nm = wks[i];
+                bits |= (uint64_t)b << (j & 63u);
+            }
         }
     }
     // pass 2: one append per tile, then node-major positions
