@@ -1283,7 +1283,7 @@ static int lp_window_start(tw_shard* c) {
         hipLaunchKernelGGL(tw_lp_dmark, dim3(64), dim3(256), 0, c->stream, c->dwin());
         HIPCHK(hipGetLastError());
     } else if (bat) {
-        hipLaunchKernelGGL(tw_lp_batch, dim3(TW_DUE_GRID), dim3(256), 0, c->stream, c->dwin());
+        hipLaunchKernelGGL(tw_lp_batch, dim3(TW_DUE_GRID), dim3(TW_BAT_T), 0, c->stream, c->dwin());
         HIPCHK(hipGetLastError());
     }
     return TW_OK;

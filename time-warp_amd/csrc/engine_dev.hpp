@@ -4280,7 +4280,16 @@ __global__ void __launch_bounds__(256) tw_lp_due(Dev c) {
 #define TW_BATCH_INSNS 512u   // program tables staged in LDS
 #define TW_BATCH_CONSTS 128u
 #define TW_BATCH_LPC 256u
-__global__ void __launch_bounds__(256) tw_lp_batch(Dev c) {
+// threads per workgroup: two waves, so four workgroups (40.7 KB of LDS each)
+// share a CU at the kernel's two waves per SIMD -- a heavy lane's pass is a
+// chain of round trips and barriers, and twice the lanes in flight halve the
+// rounds (four waves per workgroup: two per CU)
+#ifndef TW_BAT_T
+#define TW_BAT_T 128u
+#endif
+#define TW_BAT_RPT (TW_BATCH_CAP / TW_BAT_T)  // records per thread in the prefix scan
+static_assert(TW_BAT_T % 64 == 0 && TW_BAT_T <= 256 && TW_BATCH_CAP % TW_BAT_T == 0, "batch workgroup shape");
+__global__ void __launch_bounds__(TW_BAT_T) tw_lp_batch(Dev c) {
     const int64_t GAS* w = gp(c.win);
     const int64_t fl = w[WN_FLAGS];
     if (!(fl & WN_FRESH) || (fl & WN_DONE) || !c.lpc_bat) return;
@@ -4305,9 +4314,9 @@ __global__ void __launch_bounds__(256) tw_lp_batch(Dev c) {
     __shared__ unsigned long long bH, bsum[6];
     __shared__ long long bFin, bLast;
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
-    for (uint32_t i = tid; i < c.n_insns; i += 256) sP[i] = gp(c.insns)[i];
-    for (uint32_t i = tid; i < c.n_consts; i += 256) sK[i] = gp(c.consts)[i];
-    for (uint32_t i = tid; i < c.n_sets * c.n_kinds; i += 256) {
+    for (uint32_t i = tid; i < c.n_insns; i += TW_BAT_T) sP[i] = gp(c.insns)[i];
+    for (uint32_t i = tid; i < c.n_consts; i += TW_BAT_T) sK[i] = gp(c.consts)[i];
+    for (uint32_t i = tid; i < c.n_sets * c.n_kinds; i += TW_BAT_T) {
         sL[i] = gp(c.lpc)[i];
         sB[i] = gp(c.lpc_bat)[i];
     }
@@ -4372,7 +4381,7 @@ __global__ void __launch_bounds__(256) tw_lp_batch(Dev c) {
         // the records
         const size_t ib = ib_base(c, r);
         const uint32_t nx = bNx > nd ? nd + 1u : nd;  // (+ the first record past the cap: its time)
-        for (uint32_t i = tid; i < nx; i += 256) {
+        for (uint32_t i = tid; i < nx; i += TW_BAT_T) {
             const uint4 GAS* q = gp(c.due) + (ib + (size_t)i * st) * 2;
             ea[i] = q[0];
             if (i < nd) eb[i] = q[1];
@@ -4382,7 +4391,7 @@ __global__ void __launch_bounds__(256) tw_lp_batch(Dev c) {
         // dry run: batchable | yielded << 1 per record (due order); each thread
         // keeps its first record's outcome for the effects
         DueX x0{};
-        for (uint32_t i = tid; i < nd; i += 256) {
+        for (uint32_t i = tid; i < nd; i += TW_BAT_T) {
             const DueX x = due_exec(c, bp, r, bSet, ea[i], eb[i]);
             const bool ok = x.ok && x.last < bTo;
             dix[i] = (uint8_t)((ok ? 1u : 0u) | (x.yld ? 2u : 0u));
@@ -4392,13 +4401,13 @@ __global__ void __launch_bounds__(256) tw_lp_batch(Dev c) {
         __syncthreads();
         BT(bt2);
         const uint32_t K0 = bK0;
-        // the latest resume before each position: four records per thread
-        // (1,024), an inclusive max scan of the thread maxima (wave shuffles,
-        // then the four waves)
+        // the latest resume before each position: TW_BAT_RPT records per
+        // thread (1,024), an inclusive max scan of the thread maxima (wave
+        // shuffles, then the waves)
         {
             int64_t cm = INT64_MIN;
-            for (uint32_t j = 0; j < 4; ++j) {
-                const uint32_t i = tid * 4 + j;
+            for (uint32_t j = 0; j < TW_BAT_RPT; ++j) {
+                const uint32_t i = tid * TW_BAT_RPT + j;
                 if (i < K0 && (dix[i] & 2u)) {
                     const int64_t y = ent_t(ea[i]) + 1;
                     cm = y > cm ? y : cm;
@@ -4416,9 +4425,9 @@ __global__ void __launch_bounds__(256) tw_lp_batch(Dev c) {
             for (uint32_t k = 0; k < wv; ++k) m = wmx[k] > m ? wmx[k] : m;
             // (the last thread also checks position TW_BATCH_CAP: a due run of
             // exactly the cap, or the first record past it, may close the prefix)
-            const uint32_t jn = tid == 255u ? 5u : 4u;
+            const uint32_t jn = tid == TW_BAT_T - 1u ? TW_BAT_RPT + 1u : TW_BAT_RPT;
             for (uint32_t j = 0; j < jn; ++j) {
-                const uint32_t i = tid * 4 + j;
+                const uint32_t i = tid * TW_BAT_RPT + j;
                 if (i > K0) break;
                 // the prefix [0, i) is kept when its last resume precedes record i's
                 // wake (i = nd: the first record past the cap, or none)
@@ -4439,7 +4448,7 @@ __global__ void __launch_bounds__(256) tw_lp_batch(Dev c) {
             uint64_t h = 0;
             uint32_t sm[6] = {0, 0, 0, 0, 0, 0}, dir = 0;
             int64_t fin = INT64_MIN, last = INT64_MIN;
-            for (uint32_t i = tid; i < K; i += 256) {
+            for (uint32_t i = tid; i < K; i += TW_BAT_T) {
                 const DueX x = i == tid ? x0 : due_exec(c, bp, r, bSet, ea[i], eb[i]);
                 dir |= due_effects(c, wid, node, x);
                 h += x.h;
