@@ -1200,6 +1200,35 @@ struct Lane {
             ds(DW_IB, dg(DW_IB) | 0x80000000u);
             return;
         }
+        if (c.dpar && c.win && (dh.x >> 31) && dst - c.lp0 < c.R) {
+            // a heavy local lane: straight into its inbox too (buffer 0, which
+            // tw_lp_due reads at the next window's first tick, before any event
+            // kernel of that window), with tw_lp_pack's bookkeeping: the next
+            // window's heavy list on the first pending record, the mark, and
+            // the window-minimum bound of the light path above
+            const uint32_t lp = dst - c.lp0;
+            const uint32_t k = __hip_atomic_fetch_add(gp(c.inbox_n) + lp, 1u, __ATOMIC_RELAXED,
+                                                      __HIP_MEMORY_SCOPE_AGENT);
+            if (k >= dh.z) {
+                __hip_atomic_fetch_or(gp(c.lp_err), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                return;
+            }
+            const size_t base = c.ib_off ? ((size_t)dh.y << c.rep_lg) + (dst & ((1u << c.rep_lg) - 1u)) : (size_t)lp;
+            uint4 GAS* q = gp(c.inbox) + (base + (size_t)k * ib_stride(c)) * 2;
+            q[0] = make_uint4((uint32_t)ta, (uint32_t)((uint64_t)ta >> 32), (uint32_t)payload,
+                              (uint32_t)((uint64_t)payload >> 32));
+            q[1] = make_uint4(link, kind, src, dst);
+            if (k == 0) {
+                const uint32_t l = (c.wid + 1u) & 1u;
+                const uint32_t j = __hip_atomic_fetch_add(gp(c.heavy_n) + l, 1u, __ATOMIC_RELAXED,
+                                                          __HIP_MEMORY_SCOPE_AGENT);
+                if (j < c.R) gp(c.heavy)[(size_t)l * c.R + j] = lp;
+                else __hip_atomic_fetch_or(gp(c.lp_err), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            lp_list_next(c, lp);
+            ds(DW_IB, dg(DW_IB) | 0x80000000u);
+            return;
+        }
         const uint32_t i = wave_append(gp(c.out_n), 1u);
         if (i >= c.out_cap) {
             __hip_atomic_fetch_or(gp(c.lp_err), 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
