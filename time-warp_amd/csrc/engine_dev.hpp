@@ -2652,21 +2652,25 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
     bool fresh = true;
     uint32_t ph = 0;
     int64_t lwin = 0;  // the lookahead (per-replica windows: t_end is the lane's replica's)
+    // LP: the window's work list (workgroups past it leave before staging the program)
+    static_assert(TW_LP_NB == 1, "the LP grid serves one work-list bucket");
+    uint32_t lp_n = 0;
     if (LP && c.win) {
+        // (both lists' lengths load with the window words: a workgroup past the
+        // list -- most of a light tick's grid -- leaves after one round trip)
+        const uint32_t n0 = gp(c.act_n)[0], n1 = gp(c.act_n)[TW_LP_NB];
         const int64_t GAS* w = gp(c.win);
         const int64_t fl = w[WN_FLAGS];
-        if (fl & WN_DONE) return;
         lwin = w[WN_L];
         t_end = w[WN_T] + w[WN_L] - 1;
         c.act_cur = (uint32_t)w[WN_ACT];
         c.wid = (uint32_t)w[WN_WID];
         ph = (uint32_t)w[WN_PHASE];
+        if (fl & WN_DONE) return;
         fresh = (fl & (ph ? WN_PH1FRESH : WN_FRESH)) != 0;
-    }
-    // LP: the window's work list (workgroups past it leave before staging the program)
-    static_assert(TW_LP_NB == 1, "the LP grid serves one work-list bucket");
-    uint32_t lp_n = 0;
-    if (LP) {
+        lp_n = c.act_cur ? n1 : n0;
+        if ((size_t)blockIdx.x * WG >= lp_n) return;
+    } else if (LP) {
         lp_n = gp(c.act_n)[c.act_cur * TW_LP_NB];
         if ((size_t)blockIdx.x * WG >= lp_n) return;
     }
