@@ -146,12 +146,18 @@ enum {
     CW_FTH, CW_FS, CW_FSL,
     CW_DL, CW_DR, CW_UD, CW_MAINEXC, CW_TMO,          // counters
     CW_CPC, CW_CNODE, CW_CRA, CW_CDEL,                 // step staging: the child (its registers: Lane::qq)
-    CW_F2L, CW_F2H, CW_F2S,  // the far sources' runner-up key (t, seq): the least but the chosen source's
-    CW_VS,                   // victim headers staged at this pop: d_ev << 3 | n0 << 2 | quads (stage_victims)
-    CW_TRN,                                            // TRACE records emitted (tw_set_trace)
     CW_DUMMY,                                          // target of idle lanes' predicated stores
+    CW_LP_COUNT,  // (LP lanes keep the words above only: the ones below are the replica kernels')
+    CW_F2L = CW_LP_COUNT, CW_F2H, CW_F2S,  // the far sources' runner-up key (t, seq): the least but the chosen source's
+    CW_VS,                   // victim headers staged at this pop: d_ev << 3 | n0 << 2 | quads (stage_victims)
+    CW_TRN,                                            // TRACE records emitted (tw_set_trace: replica contexts)
     CW_COUNT
 };
+// cold words per lane: LP lanes have no far runs, victim staging or TRACE
+// records, and five words less per lane (2.5 KB per 128-lane workgroup) let
+// four LP workgroups share a CU's LDS instead of three
+template <bool LP>
+__host__ __device__ constexpr int cw_count() { return LP ? CW_LP_COUNT : CW_COUNT; }
 // byte offset of the child-register quads (Lane::qq) from the record staging
 template <int WG, int NC, bool HR>
 __host__ __device__ constexpr uint32_t qq_lds_offset() {
@@ -408,8 +414,8 @@ struct Lane {
         return LP ? (i << c.rep_lg) + rho() : ix(i);
     }
     // LP cold words (DW_*)
-    __device__ __forceinline__ uint32_t dg(int w) const { return cw[(CW_COUNT + w) * WG]; }
-    __device__ __forceinline__ void ds(int w, uint32_t v) { cw[(CW_COUNT + w) * WG] = v; }
+    __device__ __forceinline__ uint32_t dg(int w) const { return cw[(cw_count<LP>() + w) * WG]; }
+    __device__ __forceinline__ void ds(int w, uint32_t v) { cw[(cw_count<LP>() + w) * WG] = v; }
     // cold words
     __device__ __forceinline__ uint32_t cg(int w) const {
         if constexpr (CWR) return cwr[w];
@@ -1488,6 +1494,7 @@ struct Lane {
 
     // TRACE record (tw_set_trace): appended in this replica's execution order
     __device__ __forceinline__ void trace_rec(uint32_t node, int32_t tag, int64_t val) {
+        if constexpr (LP) return;  // (tw_set_trace refuses LP contexts: trace_cap is 0)
         const uint32_t n = cg(CW_TRN);
         cs(CW_TRN, n + 1);
         if (n < c.trace_cap) {
@@ -2628,7 +2635,7 @@ __global__ void __launch_bounds__(TW_WG) tw_init_kernel(Dev c, uint32_t main_pc,
 template <int WG, int NC, bool LP = false, bool RUNS = true>
 __host__ __device__ constexpr size_t fixed_lds_bytes() {
     return (size_t)(LP || !RUNS ? 4 : 5) * WG * 16 + (size_t)(LP || !RUNS ? 0 : RQ_COUNT) * WG * 16 + (size_t)NC * WG * 12 +
-           (size_t)4 * WG * 8 + (size_t)2 * WG * 16 + (size_t)(CW_COUNT + (LP ? DW_COUNT : 0)) * WG * 4;
+           (size_t)4 * WG * 8 + (size_t)2 * WG * 16 + (size_t)(cw_count<LP>() + (LP ? DW_COUNT : 0)) * WG * 4;
 }
 
 // WG replicas per workgroup share its LDS; TPW of each wave's 64 lanes carry a
@@ -2682,7 +2689,7 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
     uint4 LAS* s_q = (uint4 LAS*)((uint8_t LAS*)s_pf + qq_lds_offset<WG, NC, HR>());  // (= s_rf + 4 * WG)
     uint32_t LAS* s_s = (uint32_t LAS*)(s_q + 2 * WG);
     uint32_t LAS* s_cw = s_s + NC * WG;
-    uint2 LAS* s_p = (uint2 LAS*)(s_cw + (CW_COUNT + (LP ? DW_COUNT : 0)) * WG);
+    uint2 LAS* s_p = (uint2 LAS*)(s_cw + (cw_count<LP>() + (LP ? DW_COUNT : 0)) * WG);
     int64_t LAS* s_c = (int64_t LAS*)(s_p + c.n_insns + 1);
     uint32_t LAS* s_u = (uint32_t LAS*)(s_c + c.n_consts);
     uint32_t LAS* s_l = s_u + c.n_insns + 1;
@@ -2810,10 +2817,10 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
             L.status = (uint32_t)sc[SC_STATUS * SR];
             L.free_n = (uint32_t)sc[SC_FREE_N * SR]; L.ftop = (uint32_t)sc[SC_FTOP * SR]; L.bump = (uint32_t)sc[SC_BUMP * SR];
         #pragma unroll
-            for (int w = 0; w < CW_COUNT; ++w) L.cs(w, 0);
+            for (int w = 0; w < cw_count<LP>(); ++w) L.cs(w, 0);
             L.cs(CW_MAINEXC, (uint32_t)sc[SC_MAIN_EXC * SR]);
             L.cs(CW_TMO, (uint32_t)sc[SC_TMO_CTR * SR]);
-            L.cs(CW_TRN, (uint32_t)sc[SC_TRACE_N * SR]);
+            if constexpr (!LP) L.cs(CW_TRN, (uint32_t)sc[SC_TRACE_N * SR]);
             const uint64_t events0 = sc[SC_EVENTS * SR];
             const uint64_t ev_room64 = max_events > events0 ? max_events - events0 : 0;
             const uint32_t ev_room = ev_room64 > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)ev_room64;
@@ -3185,7 +3192,7 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
             sc[SC_STATUS * SR] = L.status; sc[SC_MAIN_EXC * SR] = L.cg(CW_MAINEXC);
             sc[SC_FREE_N * SR] = L.free_n; sc[SC_FTOP * SR] = L.ftop; sc[SC_BUMP * SR] = L.bump;
             sc[SC_TMO_CTR * SR] = L.cg(CW_TMO);
-            sc[SC_TRACE_N * SR] = L.cg(CW_TRN);
+            if constexpr (!LP) sc[SC_TRACE_N * SR] = L.cg(CW_TRN);
             // (LP lanes: the sums below as no-return atomics, without the drain
             // above, measured slower -- C5 1,366 -> 1,448 ms, C4 7.05 -> 7.30 ms:
             // round 6, profiles/r06c/ab_lp_epi_*)
