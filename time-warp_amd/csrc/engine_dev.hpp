@@ -145,7 +145,7 @@ enum {
     CW_FTL = 0,                     // far heap top (t, seq, slot)
     CW_FTH, CW_FS, CW_FSL,
     CW_DL, CW_DR, CW_UD, CW_MAINEXC, CW_TMO,          // counters
-    CW_CPC, CW_CNODE, CW_CRA, CW_CDEL,                 // step staging: the child (its registers: Lane::qq)
+    CW_CSP, CW_CNODE,  // step staging: the child's pc | ref register << 16 | registers' source << 20 (csp_word), its node
     CW_DUMMY,                                          // target of idle lanes' predicated stores
     CW_LP_COUNT,  // (LP lanes keep the words above only: the ones below are the replica kernels')
     CW_F2L = CW_LP_COUNT, CW_F2H, CW_F2S,  // the far sources' runner-up key (t, seq): the least but the chosen source's
@@ -158,6 +158,12 @@ enum {
 // four LP workgroups share a CU's LDS instead of three
 template <bool LP>
 __host__ __device__ constexpr int cw_count() { return LP ? CW_LP_COUNT : CW_COUNT; }
+// the spawn staging word: the child's pc (16 bits, as a thread record keeps
+// it), the parent register its ref goes to (4: none) and where the child's
+// registers come from (2: the parent's; 0: Lane::qq; 1: LP's deliverer)
+__host__ __device__ constexpr uint32_t csp_word(uint32_t pc, uint32_t ra, uint32_t del) {
+    return (pc & 0xFFFFu) | (ra << 16) | (del << 20);
+}
 // byte offset of the child-register quads (Lane::qq) from the record staging
 template <int WG, int NC, bool HR>
 __host__ __device__ constexpr uint32_t qq_lds_offset() {
@@ -1641,10 +1647,8 @@ struct Lane {
                     pfail(me && bad, TW_REP_ERR_INSN);
                     tc = fk ? (bad ? (uint32_t)T_STOP : (uint32_t)T_SPAWN) : tc;
                     const bool p = me && fk && !bad;
-                    csp(p, CW_CPC, (uint32_t)imm);
+                    csp(p, CW_CSP, csp_word((uint32_t)imm, a, 2u));  // the child's registers are the parent's
                     csp(p, CW_CNODE, node);
-                    csp(p, CW_CRA, a);
-                    csp(p, CW_CDEL, 2u);  // the child's registers are the parent's
                     if constexpr (LP) {
                         // batched LP, a fork onto another node of the replica
                         // (TimedT.hs:326-342): the child goes out as a spawn record
@@ -1828,7 +1832,7 @@ struct Lane {
                             tc = T_YIELD;
                         }
                     } else {
-                        cs(CW_CPC, TW_PC_DELIVER_STUB); cs(CW_CNODE, th.w1); cs(CW_CRA, 4); cs(CW_CDEL, 0);
+                        cs(CW_CSP, csp_word(TW_PC_DELIVER_STUB, 4u, 0u)); cs(CW_CNODE, th.w1);
                         qset(payload, (int64_t)link, (int64_t)(e & 0x7FFFFFFFu) + tx_us(c, link, kind), (int64_t)kind);
                         tc = T_SPAWN;
                     }
@@ -1911,7 +1915,7 @@ struct Lane {
                 } else {
                     cinc(CW_DL);
                     hash(dst, TW_KIND_RECV | kind, r0);
-                    cs(CW_CPC, lpc); cs(CW_CNODE, dst); cs(CW_CRA, 4); cs(CW_CDEL, LP ? 1u : 0u);
+                    cs(CW_CSP, csp_word(lpc, 4u, LP ? 1u : 0u)); cs(CW_CNODE, dst);
                     qset(r0, (int64_t)link, LP ? r2 : (int64_t)th.w1, (int64_t)kind);
                     tc = T_SPAWN;
                 }
@@ -1957,7 +1961,7 @@ struct Lane {
                     cs(CW_TMO, tmo + 1);
                     gp(c.tmo_done)[ix(tmo)] = 0;
                     rs(th, a, tmo);
-                    cs(CW_CPC, TW_PC_WATCHDOG_STUB); cs(CW_CNODE, th.w1); cs(CW_CRA, 4); cs(CW_CDEL, 0);
+                    cs(CW_CSP, csp_word(TW_PC_WATCHDOG_STUB, 4u, 0u)); cs(CW_CNODE, th.w1);
                     qset((int64_t)(((uint64_t)th.w2 << 32) | slot), (int64_t)tmo, K[imm], 0);
                     tc = T_SPAWN;
                 }
@@ -2199,10 +2203,8 @@ struct Lane {
             if (op == TW_OP_FORK) {     // r[a] <- ref(child) at the terminal (TimedT.hs:326-342)
                 const uint32_t node = b == 0xFFFFu ? th.w1 : (uint32_t)rg(th, b & 3u);
                 if (__builtin_amdgcn_ballot_w64(run && node >= c.N)) break;
-                csp(run, CW_CPC, (uint32_t)imm);
+                csp(run, CW_CSP, csp_word((uint32_t)imm, a, 2u));  // the child's registers are the parent's
                 csp(run, CW_CNODE, node);
-                csp(run, CW_CRA, a);
-                csp(run, CW_CDEL, 2u);  // the child's registers are the parent's
                 fin = T_SPAWN;
             } else if (op == TW_OP_WAIT_REL || op == TW_OP_WAIT_ABS || op == TW_OP_WAIT_REG) {
                 int64_t wt;
@@ -2327,16 +2329,16 @@ struct Lane {
         if (!__builtin_amdgcn_ballot_w64(ip)) return false;
         if (ip) {
             STAT(K_SPAWN);
-            const uint32_t cdel = cg(CW_CDEL), cra = cg(CW_CRA);
+            const uint32_t csw = cg(CW_CSP), cdel = (csw >> 20) & 3u, cra = (csw >> 16) & 7u, cpc = csw & 0xFFFFu;
             int64_t ref;
             Th ch;
             uint32_t cslot = 0xFFFFFFFFu;
             bool ok;
             if (cdel & 2u) {
-                ok = spawn(cg(CW_CPC), cg(CW_CNODE), rg(th, 0), rg(th, 1), rg(th, 2), rg(th, 3), ref, ch, cslot, false);
+                ok = spawn(cpc, cg(CW_CNODE), rg(th, 0), rg(th, 1), rg(th, 2), rg(th, 3), ref, ch, cslot, false);
             } else {
                 const uint4 a = qq[0], b = qq[WG];
-                ok = spawn(cg(CW_CPC), cg(CW_CNODE), qa(a), qb(a), qa(b), qb(b), ref, ch, cslot, false);
+                ok = spawn(cpc, cg(CW_CNODE), qa(a), qb(a), qa(b), qb(b), ref, ch, cslot, false);
             }
             if (ok) {
                 // the parent: `wait (for 1 mcs)` (TimedT.hs:340) -- queued, record stored
@@ -2463,7 +2465,7 @@ struct Lane {
         // fork (TimedT.hs:326-342): the child is queued at now, then the parent waits 1 µs
         if (fin == T_SPAWN) {
             STAT(K_SPAWN);
-            const uint32_t cdel = cg(CW_CDEL), cra = cg(CW_CRA);
+            const uint32_t csw = cg(CW_CSP), cdel = (csw >> 20) & 3u, cra = (csw >> 16) & 7u, cpc = csw & 0xFFFFu;
             int64_t ref;
             bool ok;
             if (LP && c.lpb && (cdel & 2u) && cg(CW_CNODE) != th.w1) {
@@ -2472,14 +2474,14 @@ struct Lane {
                 // outside LP mode anyway).  Not from a phase-1 node: the window's
                 // phase 0 has finished by then.
                 ok = !(c.phase && gp(c.phase)[th.w1]);
-                if (ok) emit_spawn(now, cg(CW_CPC), lane_of(cg(CW_CNODE)), rg(th, 0), rg(th, 1), rg(th, 2), rg(th, 3));
+                if (ok) emit_spawn(now, cpc, lane_of(cg(CW_CNODE)), rg(th, 0), rg(th, 1), rg(th, 2), rg(th, 3));
                 else fail(TW_REP_ERR_INSN);
                 ref = -1;
             } else if (cdel & 2u) {
-                ok = spawn(cg(CW_CPC), cg(CW_CNODE), rg(th, 0), rg(th, 1), rg(th, 2), rg(th, 3), ref, ch, cslot);
+                ok = spawn(cpc, cg(CW_CNODE), rg(th, 0), rg(th, 1), rg(th, 2), rg(th, 3), ref, ch, cslot);
             } else {
                 const uint4 a = qq[0], b = qq[WG];
-                ok = spawn(cg(CW_CPC), cg(CW_CNODE), qa(a), qb(a), qa(b), qb(b), ref, ch, cslot);
+                ok = spawn(cpc, cg(CW_CNODE), qa(a), qb(a), qa(b), qb(b), ref, ch, cslot);
             }
             if (!ok) {
                 fin = T_STOP;
