@@ -506,12 +506,14 @@ struct Lane {
         kb = m ? kc : ka; sb = m ? sc : sa; ib = m ? ic : ia;
     }
     // Place (k, s) at the root hole and sift it down.
-    __device__ __forceinline__ void near_down(uint64_t k, uint32_t s) {
+    __device__ __forceinline__ void near_down(uint64_t k, uint32_t s, bool deep = true) {
         uint64_t k1; uint32_t s1, c1;
         near_kids(0, k1, s1, c1);                // c1 in 1..4
         const bool mv1 = k1 < k;                 // the smallest child rises into the root
-        uint64_t k2; uint32_t s2, c2;
-        near_kids(c1, k2, s2, c2);
+        // (the second level holds nothing while every lane's heap has at most
+        // five entries: no read of it)
+        uint64_t k2 = ~0ull; uint32_t s2 = 0u, c2 = c1;
+        if (__builtin_amdgcn_ballot_w64(deep)) near_kids(c1, k2, s2, c2);
         const bool mv2 = mv1 && k2 < k;          // ... and its smallest child into c1
         // root <- c1's entry or k; c1 <- c2's entry, k, or itself; c2 <- k (or
         // c1's new value again when nothing moved that far: a repeated store)
@@ -613,7 +615,7 @@ struct Lane {
             nrk = nk[0];
             nrs = ns[0];
         } else {
-            near_down(lk, ls);
+            near_down(lk, ls, n > 5u);
         }
     }
     // Re-key the live near entry with seq `old_seq` (seqs are unique) to (t, sq),
