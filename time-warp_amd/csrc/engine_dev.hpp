@@ -1206,7 +1206,7 @@ struct Lane {
                 return;
             }
             const size_t base = c.ib_off ? ((size_t)dh.y << c.rep_lg) + (dst & ((1u << c.rep_lg) - 1u)) : (size_t)lp;
-            uint4 GAS* q = gp(c.inbox) + ((size_t)par * c.ib_total + base + (size_t)k * ib_stride(c)) * 2;
+            uint4 GAS* q = gp(c.inbox) + ((size_t)par * c.ib_total + base + (size_t)k * ib_stride(c, false)) * 2;
             q[0] = make_uint4((uint32_t)ta, (uint32_t)((uint64_t)ta >> 32), (uint32_t)payload,
                               (uint32_t)((uint64_t)payload >> 32));
             q[1] = make_uint4(link, kind, src, dst);
@@ -1227,8 +1227,8 @@ struct Lane {
                 __hip_atomic_fetch_or(gp(c.lp_err), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 return;
             }
-            const size_t base = c.ib_off ? ((size_t)dh.y << c.rep_lg) + (dst & ((1u << c.rep_lg) - 1u)) : (size_t)lp;
-            uint4 GAS* q = gp(c.inbox) + (base + (size_t)k * ib_stride(c)) * 2;
+            const size_t base = c.ib_off ? ib_heavy_base(c, dh.y, dh.z, dst) : (size_t)lp;
+            uint4 GAS* q = gp(c.inbox) + (base + (size_t)k * ib_stride(c, true)) * 2;
             q[0] = make_uint4((uint32_t)ta, (uint32_t)((uint64_t)ta >> 32), (uint32_t)payload,
                               (uint32_t)((uint64_t)payload >> 32));
             q[1] = make_uint4(link, kind, src, dst);
@@ -1275,7 +1275,7 @@ struct Lane {
     // exactly as if it had been queued at the window's start.
     __device__ __forceinline__ void due_pop(Th& th, uint32_t& slot, uint32_t sq) {
         const uint32_t hn = dg(DW_HN), h = hn & 0xFFFFu, n = hn >> 16;
-        const size_t ib = dg(DW_IB) & 0x7FFFFFFFu, st = ib_stride(c);
+        const size_t ib = dg(DW_IB) & 0x7FFFFFFFu, st = ib_stride(c, true);  // (a due run: a heavy lane's)
         const uint4 GAS* q = gp(c.due) + (ib + (size_t)h * st) * 2;
         const uint4 a = q[0], b = q[1];
         const uint4 nx = gp(c.due)[(ib + (size_t)(h + 1 < n ? h + 1 : h) * st) * 2];
@@ -2851,7 +2851,7 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
                 L.ds(DW_HN, dh | (dn << 16));
                 L.ds(DW_SQ0, (uint32_t)sc[SC_DUE_SEQ * SR]);
                 uint4 h = make_uint4(0, 0, 0, 0);
-                if (dh < dn) h = gp(c.due)[(ib + (size_t)dh * ib_stride(c)) * 2];
+                if (dh < dn) h = gp(c.due)[(ib + (size_t)dh * ib_stride(c, !ilight)) * 2];
                 L.ds(DW_TL, h.x);
                 L.ds(DW_TH, h.y);
                 L.ds(DW_BSET, gp(c.bind)[r]);  // (LP: bix(node) = the lane itself)
@@ -2949,7 +2949,7 @@ tw_run_kernel(Dev c, int64_t t_end, uint64_t max_events, uint32_t budget) {
                 // threads, inserted in (t, link, payload, src, kind) order (rec_less, the
                 // order tw_lp_due gives a heavy lane's due run) so queue seqs are
                 // deterministic whatever order the records arrived in
-                const size_t ib = (size_t)ipar * c.ib_total + ib_base(c, r), ist = ib_stride(c);
+                const size_t ib = (size_t)ipar * c.ib_total + ib_base(c, r), ist = ib_stride(c, false);
                 const uint32_t cap = ib_cap(c, r);  // (an overflowed inbox -- lp_err set -- keeps its first cap)
                 if (n_in > cap) {
                     L.fail(TW_REP_ERR_QUEUE);
@@ -3277,7 +3277,7 @@ __device__ __forceinline__ void lp_deliver(const Dev& c, uint4 a, uint4 b, uint6
         __hip_atomic_fetch_or(gp(c.lp_err), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         return;
     }
-    uint4 GAS* q = gp(c.inbox) + ((size_t)par * c.ib_total + ib_base(c, lp) + (size_t)k * ib_stride(c)) * 2;
+    uint4 GAS* q = gp(c.inbox) + ((size_t)par * c.ib_total + ib_base(c, lp) + (size_t)k * ib_stride(c, cap > TW_LIGHT)) * 2;
     q[0] = a;
     q[1] = b;
     // (a record due in this window, t < wend -- a short link into a phase-1
@@ -3951,7 +3951,7 @@ __device__ __forceinline__ uint32_t due_emit(const Dev& c, uint32_t wid, int64_t
             return 0u;
         }
         const size_t base = c.ib_off ? ((size_t)dh.y << c.rep_lg) + (dst & ((1u << c.rep_lg) - 1u)) : (size_t)lp;
-        uint4 GAS* q = gp(c.inbox) + ((size_t)par * c.ib_total + base + (size_t)k * ib_stride(c)) * 2;
+        uint4 GAS* q = gp(c.inbox) + ((size_t)par * c.ib_total + base + (size_t)k * ib_stride(c, false)) * 2;
         q[0] = q0;
         q[1] = q1;
         if (defer) {  // (tw_lp_due_batch runs before the window's list is built: tw_lp_dmark marks it after)
@@ -4154,7 +4154,7 @@ __global__ void __launch_bounds__(256) tw_lp_due(Dev c) {
     static_assert(TW_HEAVY_CAP == 256 * 8, "eight entries per thread");
     static_assert(TW_DUE_BINS == 256 * 8, "eight bins per thread");
     const uint32_t tid = threadIdx.x;
-    const size_t st = ib_stride(c);
+    const size_t st = ib_stride(c, true);  // (heavy lanes only)
     auto bsh = [](uint32_t b) { return (b & 1u) * 16u; };
     auto bget = [&](uint32_t b) { return (bins[b >> 1] >> bsh(b)) & 0xFFFFu; };
     auto binc = [&](uint32_t b) { return (atomicAdd(&bins[b >> 1], 1u << bsh(b)) >> bsh(b)) & 0xFFFFu; };
@@ -4365,7 +4365,7 @@ __global__ void __launch_bounds__(TW_BAT_T) tw_lp_batch(Dev c) {
         sB[i] = gp(c.lpc_bat)[i];
     }
     const BProg bp{(const uint2 LAS*)sP, (const int64_t LAS*)sK, (const uint32_t LAS*)sL, (const uint8_t LAS*)sB};
-    const size_t st = ib_stride(c);
+    const size_t st = ib_stride(c, true);  // (heavy lanes only)
 #ifdef TW_STATS
     uint64_t bp_cyc[6] = {0, 0, 0, 0, 0, 0};
 #define BT(v) const uint64_t v = __builtin_amdgcn_s_memtime()
@@ -4610,7 +4610,7 @@ __global__ void __launch_bounds__(256) tw_lp_due_batch(Dev c) {
     }
     const BProg bp{(const uint2 LAS*)sP, (const int64_t LAS*)sK, (const uint32_t LAS*)sL, (const uint8_t LAS*)sB};
     uint8_t* bfl = (uint8_t*)dix;  // (batch flags per due position, once dix is consumed)
-    const size_t st = ib_stride(c);
+    const size_t st = ib_stride(c, true);  // (heavy lanes only)
     for (uint32_t hi = blockIdx.x; hi < nh; hi += gridDim.x) {
         const uint32_t r = gp(c.heavy)[(size_t)lst * c.R + hi];
         const int64_t T = c.rw ? *rw_at(c, RW_T, r) : T0;

@@ -277,12 +277,25 @@ enum : int64_t { WN_FRESH = 1, WN_DONE = 2, WN_PH1FRESH = 4 };
 #define TW_LIGHT 32u   // a lane with at most this many pending records drains them in the event kernel
 #define TW_SPN 4u      // spawn records per lane per tick
 #define TW_HEAVY_CAP 2048u  // largest per-node inbox (tw_lp_due stages a lane's records in LDS)
+// Batched LP: node n's inbox region holds cap(n) records of each of its 2^rep_lg
+// replicas.  A light node's records are replica-interleaved (entry k of every
+// replica side by side: the event kernel's waves drain 64 replicas' inboxes
+// at once); a heavy node's are one contiguous run per replica (entry k at
+// rep * cap + k: tw_lp_due and tw_lp_batch read and write one lane's hundreds
+// of records as whole cache lines, instead of one 128-KB-strided record each).
+__device__ __forceinline__ size_t ib_heavy_base(const Dev& c, uint32_t off, uint32_t cap, uint32_t g) {
+    return ((size_t)off << c.rep_lg) + (size_t)(g & ((1u << c.rep_lg) - 1u)) * cap;
+}
 __device__ __forceinline__ size_t ib_base(const Dev& c, uint32_t r) {
     if (!c.ib_off) return r;
     const uint32_t g = c.lp0 + r, n = (g >> c.rep_lg) - (c.lp0 >> c.rep_lg);
-    return ((size_t)gp(c.ib_off)[n] << c.rep_lg) + (g & ((1u << c.rep_lg) - 1u));
+    const uint32_t o0 = gp(c.ib_off)[n], cap = gp(c.ib_off)[n + 1] - o0;
+    if (cap > TW_LIGHT) return ib_heavy_base(c, o0, cap, g);
+    return ((size_t)o0 << c.rep_lg) + (g & ((1u << c.rep_lg) - 1u));
 }
-__device__ __forceinline__ size_t ib_stride(const Dev& c) { return c.ib_off ? (size_t)1 << c.rep_lg : (size_t)c.R; }
+__device__ __forceinline__ size_t ib_stride(const Dev& c, bool heavy) {
+    return c.ib_off ? (heavy ? (size_t)1 : (size_t)1 << c.rep_lg) : (size_t)c.R;
+}
 // the inbox buffer a delivery to a light lane goes to during window wid
 __device__ __forceinline__ uint32_t ib_par_in(const Dev& c, bool light) {
     return (c.dpar && c.win && light) ? ((c.wid + 1u) & 1u) : 0u;
