@@ -29,14 +29,17 @@ NAMES = ["pop", "superseded", "peek_pf", "peek_hbm", "put_hbm", "put_dead", "pf_
 
 def read(eng, heavy=False):
     """the counters of every lane (heavy=True: of heavy-inbox LP lanes alone)"""
-    buf = (C.c_ulonglong * (2 * len(NAMES)))()
+    buf = (C.c_ulonglong * (2 * len(NAMES) + 8))()
     fn = eng.lib.tw_prof_read
     fn.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]
-    n = fn(eng.ctx, buf, 2 * len(NAMES), 1)
+    n = fn(eng.ctx, buf, 2 * len(NAMES) + 8, 1)
     if n < 0:
         raise RuntimeError(f"tw_prof_read: {n}")
     o = len(NAMES) if heavy else 0
-    return {k: buf[o + i] for i, k in enumerate(NAMES)}
+    d = {k: buf[o + i] for i, k in enumerate(NAMES)}
+    if n >= 2 * len(NAMES) + 6:  # tw_lp_batch's phase cycles (staging, dry run, scan, -, effects, tail)
+        d["bat_phase_cyc"] = [buf[2 * len(NAMES) + j] for j in range(6)]
+    return d
 
 
 def main():
@@ -57,7 +60,7 @@ def main():
         pops = max(d["pop"], 1)
         print(json.dumps({"phase": "gossip", "windows": st.windows, "ticks": st.ticks,
                           "lane_efficiency": d["pop"] / max(d["iter"], 1),
-                          "per_pop": {k: round(v / pops, 4) for k, v in d.items() if k != "pop"}, "counters": d}))
+                          "per_pop": {k: round(v / pops, 4) for k, v in d.items() if k not in ("pop", "bat_phase_cyc")}, "counters": d}))
         return
     if len(sys.argv) > 1 and sys.argv[1] in ("lpb_hotspot", "lpb_token"):  # C5 / C3 as logical processes
         R = int(sys.argv[2]) if len(sys.argv) > 2 else (4096 if sys.argv[1] == "lpb_hotspot" else 8192)
@@ -74,7 +77,7 @@ def main():
             d = read(eng, heavy=True)
             pops = max(d["pop"], 1)
             print(json.dumps({"phase": "lpb_hotspot_receivers", "lane_efficiency": d["pop"] / max(d["iter"], 1),
-                              "per_pop": {k: round(v / pops, 4) for k, v in d.items() if k != "pop"},
+                              "per_pop": {k: round(v / pops, 4) for k, v in d.items() if k not in ("pop", "bat_phase_cyc")},
                               "counters": d}))
             eng.reset()
             st = eng.run()
@@ -83,7 +86,7 @@ def main():
         w, t = eng.lpb_windows()
         print(json.dumps({"phase": sys.argv[1], "events": st.events, "loop_ms": st.kernel_ms, "windows": w,
                           "ticks": t, "lane_efficiency": d["pop"] / max(d["iter"], 1),
-                          "per_pop": {k: round(v / pops, 4) for k, v in d.items() if k != "pop"}, "counters": d}))
+                          "per_pop": {k: round(v / pops, 4) for k, v in d.items() if k not in ("pop", "bat_phase_cyc")}, "counters": d}))
         return
     if len(sys.argv) > 1 and sys.argv[1] == "hotspot":  # config 5: one phase per 0.25 s of virtual time
         R = int(sys.argv[2]) if len(sys.argv) > 2 else 4096
@@ -110,7 +113,7 @@ def main():
         pops = max(d["pop"], 1)
         rec = {"phase": name, "events": st.events, "kernel_ms": round(ms, 3),
                "ev_per_s": st.events / max(ms, 1e-9) * 1e3,
-               "per_pop": {k: round(v / pops, 4) for k, v in d.items() if k != "pop"}, "counters": d}
+               "per_pop": {k: round(v / pops, 4) for k, v in d.items() if k not in ("pop", "bat_phase_cyc")}, "counters": d}
         print(json.dumps(rec), flush=True)
 
 
